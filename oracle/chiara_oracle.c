@@ -1,0 +1,369 @@
+/*
+ * chiara_oracle.c -- TEST INFRASTRUCTURE ONLY (see chiara_oracle.h).
+ *
+ * A bulk-synchronous, single-process restatement of every rank of CHiArA's
+ * all_reduce_radix_batch / reduce_scatter_radix_batch.  Each block of code cites the
+ * reference lines it follows (paths relative to /root/reference/Fugaku_experiments/).
+ * All arithmetic goes through orc_reduce_local, the MPI_Reduce_local restatement.
+ *
+ * Why a bulk-synchronous simulation reproduces the MPI program exactly: inside one
+ * recexch phase a participant only writes its own region R(phase, me) and only reads
+ * its neighbours' copies of that same region, which those neighbours do not write in
+ * that phase (neighbours differ in base-k digit `phase`, so their regions are
+ * disjoint: all_reduce_radix_batch.cpp:106-131, :348-364).  Phase-2 roots only write
+ * their own lane chunk, and read the other nodes' copies of it.  So executing the
+ * ranks one after another per phase gives the same operands, in the same order, as
+ * the message-passing program.  tests/test_oracle_golden.py pins this against the
+ * real reference's outputs.
+ */
+#include "chiara_oracle.h"
+
+#include <stdlib.h>
+
+size_t orc_dtype_size(int dtype) {
+    switch (dtype) {
+    case ORC_F32: return 4;
+    case ORC_F64: return 8;
+    case ORC_I32: return 4;
+    case ORC_BF16: return 2;
+    default: return 0;
+    }
+}
+
+void orc_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int rank,
+              uint64_t count_for_seq) {
+    size_t i;
+    for (i = 0; i < n; ++i) {
+        if (pattern == ORC_PAT_SEQ) {
+            /* Fugaku_experiments/Allreduce/main.cpp:48-49 (int wraps as on the reference). */
+            uint32_t v = (uint32_t)((uint64_t)rank * count_for_seq + i);
+            switch (dtype) {
+            case ORC_F32: ((float*)buf)[i] = (float)(int32_t)v; break;
+            case ORC_F64: ((double*)buf)[i] = (double)(int32_t)v; break;
+            case ORC_I32: ((int32_t*)buf)[i] = (int32_t)v; break;
+            case ORC_BF16: ((uint16_t*)buf)[i] = orc_f32_to_bf16((float)(int32_t)v); break;
+            }
+        } else {
+            switch (dtype) {
+            case ORC_F32: ((float*)buf)[i] = orc_gen_f32(seed, (uint64_t)rank, i); break;
+            case ORC_F64: ((double*)buf)[i] = orc_gen_f64(seed, (uint64_t)rank, i); break;
+            case ORC_I32: ((int32_t*)buf)[i] = (int32_t)(uint32_t)(orc_key(seed, (uint64_t)rank, i) >> 32); break;
+            case ORC_BF16:
+                ((uint16_t*)buf)[i] = orc_f32_to_bf16(orc_gen_f32(seed, (uint64_t)rank, i));
+                break;
+            }
+        }
+    }
+}
+
+/* MPICH 3.3.2 predefined ops (src/mpi/coll/op/opsum.c, opmax.c, ...): the loop is
+ * `b[i] = MPIR_OP(a[i], b[i])` with a = inbuf, b = inoutbuf; MAX(a,b) = a > b ? a : b. */
+#define ORC_LOOP(T, EXPR)                                     \
+    do {                                                      \
+        const T* a = (const T*)in;                            \
+        T* b = (T*)inout;                                     \
+        size_t i;                                             \
+        for (i = 0; i < n; ++i) { T x = a[i], y = b[i]; b[i] = (EXPR); } \
+    } while (0)
+
+void orc_reduce_local(const void* in, void* inout, size_t n, int dtype, int op) {
+    switch (dtype) {
+    case ORC_F32:
+        if (op == ORC_SUM) ORC_LOOP(float, x + y);
+        else if (op == ORC_PROD) ORC_LOOP(float, x * y);
+        else if (op == ORC_MAX) ORC_LOOP(float, x > y ? x : y);
+        else ORC_LOOP(float, x < y ? x : y);
+        break;
+    case ORC_F64:
+        if (op == ORC_SUM) ORC_LOOP(double, x + y);
+        else if (op == ORC_PROD) ORC_LOOP(double, x * y);
+        else if (op == ORC_MAX) ORC_LOOP(double, x > y ? x : y);
+        else ORC_LOOP(double, x < y ? x : y);
+        break;
+    case ORC_I32:
+        if (op == ORC_SUM) ORC_LOOP(int32_t, (int32_t)((uint32_t)x + (uint32_t)y));
+        else if (op == ORC_PROD) ORC_LOOP(int32_t, (int32_t)((uint32_t)x * (uint32_t)y));
+        else if (op == ORC_MAX) ORC_LOOP(int32_t, x > y ? x : y);
+        else ORC_LOOP(int32_t, x < y ? x : y);
+        break;
+    case ORC_BF16:
+        /* The reference has no bf16; the golden driver runs it as a user-defined op on
+         * MPI_Type_contiguous(2, MPI_BYTE) computing bf16_rne(f32(a) op f32(b)). */
+        if (op == ORC_SUM)
+            ORC_LOOP(uint16_t, orc_f32_to_bf16(orc_bf16_to_f32(x) + orc_bf16_to_f32(y)));
+        else if (op == ORC_PROD)
+            ORC_LOOP(uint16_t, orc_f32_to_bf16(orc_bf16_to_f32(x) * orc_bf16_to_f32(y)));
+        else if (op == ORC_MAX)
+            ORC_LOOP(uint16_t, orc_bf16_to_f32(x) > orc_bf16_to_f32(y) ? x : y);
+        else
+            ORC_LOOP(uint16_t, orc_bf16_to_f32(x) < orc_bf16_to_f32(y) ? x : y);
+        break;
+    }
+}
+
+void orc_reduce_multi(void* acc, const void* const* ins, int m, size_t n, int dtype, int op) {
+    int j;
+    for (j = 0; j < m; ++j) orc_reduce_local(ins[j], acc, n, dtype, op);
+}
+
+/* ---- recexch tables: all_reduce_radix_batch.cpp:11-198 ---------------------------- */
+
+int orc_recexch_neighbors(int rank, int nranks, int k, orc_recexch_t* o) {
+    int i, j, p_of_k = 1, log_p_of_k = 0, rem, T, newrank;
+    memset(o, 0, sizeof(*o));
+    if (k < 2) return 1;
+    if (nranks < k) k = (nranks > 2) ? nranks : 2;                       /* :19-21 */
+    if (k > 64) return 1;
+    o->k = k;
+    while (p_of_k <= nranks) { p_of_k *= k; log_p_of_k++; }               /* :23-28 */
+    p_of_k /= k;
+    log_p_of_k--;
+    if (log_p_of_k > 32) return 1;
+    o->step2_nphases = log_p_of_k;                                         /* :45 */
+    rem = nranks - p_of_k;                                                 /* :47 */
+    T = (rem * k) / (k - 1);                                               /* :49 */
+    o->T = T;
+    o->p_of_k = p_of_k;
+    o->rem = rem;
+    o->step1_nrecvs = 0;
+    o->step1_sendto = -1;
+    if (rank < T) {                                                        /* :56-70 */
+        if (rank % k != (k - 1)) {
+            o->step1_sendto = rank + (k - 1 - rank % k);
+            if (o->step1_sendto > T - 1) o->step1_sendto = T;
+            newrank = -1;
+        } else {
+            for (i = 0; i < k - 1; i++) o->step1_recvfrom[i] = rank - i - 1;
+            o->step1_nrecvs = k - 1;
+            newrank = rank / k;
+        }
+    } else {                                                               /* :71-82 */
+        newrank = rank - rem;
+        if (rank == T && (T - 1) % k != k - 1 && T >= 1) {
+            int nsenders = (T - 1) % k + 1;
+            for (j = nsenders - 1; j >= 0; j--) o->step1_recvfrom[nsenders - 1 - j] = T - nsenders + j;
+            o->step1_nrecvs = nsenders;
+        }
+    }
+    if (o->step1_sendto == -1) {                                           /* :84-134 */
+        int digit[32];
+        int temprank = newrank, mask = 1, phase = 0, i_digit = 0;
+        for (i = 0; i < log_p_of_k; i++) digit[i] = 0;
+        while (temprank != 0) {
+            digit[i_digit++] = temprank % k;
+            temprank /= k;
+        }
+        while (mask < p_of_k) {
+            int cbit = digit[phase], cnt = 0;
+            for (i = 0; i < k; i++) {
+                if (i != cbit) {
+                    int nbr = 0, power = 1;
+                    digit[phase] = i;
+                    for (j = 0; j < log_p_of_k; j++) { nbr += digit[j] * power; power *= k; }
+                    o->step2_nbrs[phase][cnt++] = (nbr < rem / (k - 1)) ? (nbr * k) + (k - 1) : nbr + rem;
+                }
+            }
+            digit[phase] = cbit;
+            phase++;
+            mask *= k;
+        }
+    }
+    return 0;
+}
+
+static int orc_step2_to_orig(int r, int rem, int k) {                      /* :152-161 */
+    return (r < rem / (k - 1)) ? (r * k) + (k - 1) : r + rem;
+}
+
+void orc_recexch_count_offset(int nranks, int max_phases, int k, int* count, int* offset) {
+    int p_of_k = 1, rem, T, phase, rank, kpp = 1;                          /* :163-198 */
+    while (p_of_k <= nranks) p_of_k *= k;
+    p_of_k /= k;
+    rem = nranks - p_of_k;
+    T = (rem * k) / (k - 1);
+    for (phase = 0; phase < max_phases; phase++) {
+        for (rank = 0; rank < nranks; rank++) {
+            int s2 = (rank < T) ? rank / k : rank - rem;                   /* :140-149 */
+            int mn = ((s2 / kpp) * kpp) - 1;
+            int mx = mn + kpp;
+            int omn = (mn >= 0) ? orc_step2_to_orig(mn, rem, k) : mn;
+            int omx = orc_step2_to_orig(mx, rem, k);
+            count[phase * nranks + rank] = omx - omn;
+            offset[phase * nranks + rank] = omn + 1;
+        }
+        kpp *= k;
+    }
+}
+
+/* ---- phases 0-2, shared by allreduce and reduce-scatter ---------------------------- */
+
+typedef struct {
+    int nranks, b, k, nnodes, nstages, nu_count, nph;
+    size_t recvcount, irc, total, es;
+    orc_recexch_t* rx; /* per lane */
+    int *cnt, *off;
+    char **tres, **trecv; /* per-rank tmp_results / tmp_recvbuf */
+} orc_state;
+
+static void orc_free_state(orc_state* s) {
+    int r;
+    if (s->tres)
+        for (r = 0; r < s->nranks; r++) free(s->tres[r]);
+    if (s->trecv)
+        for (r = 0; r < s->nranks; r++) free(s->trecv[r]);
+    free(s->tres);
+    free(s->trecv);
+    free(s->rx);
+    free(s->cnt);
+    free(s->off);
+}
+
+#define ORC_AT(buf, elem) ((buf) + (size_t)(elem) * s->es)
+
+/* Runs phases 0-2 (all_reduce_radix_batch.cpp:234-539 ==
+ * reduce_scatter_radix_batch.cpp:228-562).  Afterwards the fully reduced chunk N
+ * (IRC elements) lives at trecv[N*b + N%b] + (N/b)*IRC. */
+static int orc_phases_0_2(orc_state* s, int nranks, int k_in, int b, size_t recvcount,
+                          int dtype, int op, const void* const* send, void* const* recv) {
+    int r, l, node, st, ph, i;
+    memset(s, 0, sizeof(*s));
+    if (b < 1 || nranks < 1 || nranks % b != 0 || k_in < 2) return 1;
+    s->es = orc_dtype_size(dtype);
+    if (!s->es || op < ORC_SUM || op > ORC_MIN) return 1;
+    s->nranks = nranks;
+    s->b = b;
+    s->recvcount = recvcount;
+    s->nnodes = nranks / b;                                                /* :241-244 */
+    s->nstages = s->nnodes / b;
+    s->nu_count = s->nnodes % b;                                           /* :258 */
+    s->irc = recvcount * (size_t)b;                                        /* :249 */
+    s->total = recvcount * (size_t)nranks;                                 /* :254 */
+    s->rx = (orc_recexch_t*)calloc((size_t)b, sizeof(orc_recexch_t));
+    for (l = 0; l < b; l++)
+        if (orc_recexch_neighbors(l, b, k_in, &s->rx[l])) return 1;     /* :283 */
+    s->k = s->rx[0].k;
+    s->nph = s->rx[0].step2_nphases;
+    s->cnt = (int*)calloc((size_t)(s->nph * b + 1), sizeof(int));
+    s->off = (int*)calloc((size_t)(s->nph * b + 1), sizeof(int));
+    orc_recexch_count_offset(b, s->nph, s->k, s->cnt, s->off);            /* :288 */
+    s->tres = (char**)calloc((size_t)nranks, sizeof(char*));
+    s->trecv = (char**)calloc((size_t)nranks, sizeof(char*));
+    for (r = 0; r < nranks; r++) {
+        s->tres[r] = (char*)calloc(s->total + 1, s->es);                   /* :296-297 */
+        s->trecv[r] = (char*)calloc(s->total + 1, s->es);
+        if (!s->tres[r] || !s->trecv[r]) return 3;
+    }
+#define SB(rr) ((const char*)(send[rr] ? send[rr] : recv[rr]))
+    /* Phase 0 (:306-312): participants copy their input into tmp_results. */
+    for (r = 0; r < nranks; r++)
+        if (s->rx[r % b].step1_sendto == -1) memcpy(s->tres[r], SB(r), s->total * s->es);
+    /* Phase 1a step-1 fold (:315-335): reduce the whole buffers of the non-participants,
+     * in step1_recvfrom order. */
+    for (r = 0; r < nranks; r++) {
+        const orc_recexch_t* x = &s->rx[r % b];
+        node = r / b;
+        if (x->step1_sendto != -1) continue;
+        for (i = 0; i < x->step1_nrecvs; i++)
+            orc_reduce_local(SB(x->step1_recvfrom[i] + b * node), s->tres[r], s->total, dtype, op);
+    }
+    /* Phase 1b: full stages (:339-400) and 1c: the truncated leftover stage (:404-478). */
+    for (st = 0; st <= s->nstages; st++) {
+        size_t base = (size_t)st * b * s->irc;
+        int leftover = (st == s->nstages);
+        if (leftover && s->nu_count == 0) break;
+        for (ph = s->nph - 1; ph >= 0; ph--) {
+            for (r = 0; r < nranks; r++) {
+                const orc_recexch_t* x = &s->rx[r % b];
+                l = r % b;
+                node = r / b;
+                if (x->step1_sendto != -1) continue;
+                for (i = 0; i < s->k - 1; i++) {
+                    int dst = x->step2_nbrs[ph][i];
+                    int rc = s->cnt[ph * b + l], o = s->off[ph * b + l];
+                    if (leftover) {                                        /* :432-446 */
+                        int mrc = rc < (s->nu_count - o) ? rc : (s->nu_count - o);
+                        if (!(o < s->nu_count && mrc > 0)) continue;
+                        rc = mrc;
+                    }
+                    /* :364 / :446 -- MPI_Reduce_local(tmp_recvbuf, tmp_results + off). */
+                    orc_reduce_local(ORC_AT(s->tres[dst + b * node], base + (size_t)o * s->irc),
+                                     ORC_AT(s->tres[r], base + (size_t)o * s->irc),
+                                     (size_t)rc * s->irc, dtype, op);
+                }
+            }
+        }
+        /* phase_buf[st] (:372-385, :459-473): own block for participants, block returned
+         * by the step-1 partner for non-participants. */
+        for (r = 0; r < nranks; r++) {
+            const orc_recexch_t* x = &s->rx[r % b];
+            l = r % b;
+            node = r / b;
+            if (leftover && l >= s->nu_count) continue;
+            if (x->step1_sendto == -1)
+                memcpy(ORC_AT(s->trecv[r], (size_t)st * s->irc),
+                       ORC_AT(s->tres[r], base + (size_t)l * s->irc), s->irc * s->es);
+            else
+                memcpy(ORC_AT(s->trecv[r], (size_t)st * s->irc),
+                       ORC_AT(s->tres[x->step1_sendto + b * node], base + (size_t)l * s->irc),
+                       s->irc * s->es);
+        }
+    }
+    /* Phase 2 inter-node linear reduce to rotating lane roots (:498-539). */
+    {
+        int nIters = (s->nu_count == 0) ? s->nstages : 1 + s->nstages;
+        for (l = 0; l < b; l++) {
+            for (i = 0; i < nIters; i++) {
+                int root_node = i * b + l, X;
+                char* acc;
+                if (root_node >= s->nnodes) break;
+                acc = ORC_AT(s->trecv[root_node * b + l], (size_t)i * s->irc);
+                for (X = 0; X < s->nnodes; X++) {
+                    if (X == root_node) continue;
+                    /* :529 MPI_Reduce_local(incoming stage X chunk, tmp_recvbuf + i*IRC) */
+                    orc_reduce_local(ORC_AT(s->trecv[X * b + l], (size_t)i * s->irc), acc, s->irc,
+                                     dtype, op);
+                }
+            }
+        }
+    }
+#undef SB
+    return 0;
+}
+
+static const char* orc_chunk(const orc_state* s, int N) {
+    int b = s->b;
+    return s->trecv[N * b + N % b] + (size_t)(N / b) * s->irc * s->es;
+}
+
+int orc_allreduce_radix_batch(int nranks, int k, int b, size_t count, int dtype, int op,
+                              const void* const* send, void* const* recv) {
+    orc_state st;
+    int rc, R, N;
+    if (nranks < 1 || count % (size_t)nranks != 0) return 2; /* :239 truncates silently */
+    rc = orc_phases_0_2(&st, nranks, k, b, count / (size_t)nranks, dtype, op, send, recv);
+    if (rc) { orc_free_state(&st); return rc; }
+    /* Phases 3-4 (:552-756) are pure data movement: lane roots broadcast their chunk
+     * across nodes, then a k-Bruck allgather inside each node; every rank ends with
+     * chunk N at recvbuf + N*IRC.  (Golden vectors confirm the reference does exactly
+     * that on every geometry in the grid.) */
+    for (R = 0; R < nranks; R++)
+        for (N = 0; N < st.nnodes; N++)
+            memcpy((char*)recv[R] + (size_t)N * st.irc * st.es, orc_chunk(&st, N), st.irc * st.es);
+    orc_free_state(&st);
+    return 0;
+}
+
+int orc_reduce_scatter_radix_batch(int nranks, int k, int b, size_t recvcount, int dtype,
+                                   int op, const void* const* send, void* const* recv) {
+    orc_state st;
+    int rc, N, j;
+    rc = orc_phases_0_2(&st, nranks, k, b, recvcount, dtype, op, send, recv);
+    if (rc) { orc_free_state(&st); return rc; }
+    /* Root re-layout + intra k-nomial scatter + own-block copy (:572-627): rank N*b+j
+     * receives sub-block j of reduced chunk N. */
+    for (N = 0; N < st.nnodes; N++)
+        for (j = 0; j < b; j++)
+            memcpy(recv[N * b + j], orc_chunk(&st, N) + (size_t)j * recvcount * st.es, recvcount * st.es);
+    orc_free_state(&st);
+    return 0;
+}

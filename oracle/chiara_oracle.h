@@ -1,0 +1,117 @@
+/*
+ * chiara_oracle.h -- TEST INFRASTRUCTURE ONLY (the checker, never the product).
+ *
+ * CPU restatement of CHiArA's hierarchical radix/batch reduce-scatter and allreduce
+ * (reference: /root/reference/Fugaku_experiments/{Allreduce/all_reduce_radix_batch.cpp,
+ * Reduce-scatter/reduce_scatter_radix_batch.cpp}) and of the MPICH 3.3.2 predefined
+ * reduction loop behind MPI_Reduce_local, which is where the reference does all of its
+ * arithmetic.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this library.  The product (libchiara.so) never links or calls it.
+ *
+ * Parity pinning: tests/golden/ holds outputs of the REAL reference (its two algorithm
+ * files compiled unchanged against the container's MPICH by oracle/Makefile target
+ * `ref`, driven by oracle/ref_driver.cpp).  tests/test_oracle_golden.py checks this
+ * restatement bit-exactly against them.
+ *
+ * The synthetic input generator below is shared by the golden driver, the oracle, the
+ * numpy test helpers and the product's device fill kernel (same formula everywhere).
+ */
+#ifndef CHIARA_ORACLE_H
+#define CHIARA_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Same numbering as include/chiara.h (chr_dtype / chr_op). */
+enum { ORC_F32 = 0, ORC_F64 = 1, ORC_I32 = 2, ORC_BF16 = 3 };
+enum { ORC_SUM = 0, ORC_PROD = 1, ORC_MAX = 2, ORC_MIN = 3 };
+
+/* Input patterns for the generator. */
+enum {
+    ORC_PAT_UNIFORM = 0,  /* f32/f64/bf16: U[-1,1); i32: full-range random 32-bit ints */
+    ORC_PAT_SEQ = 1       /* the reference harness pattern: rank*count + i
+                             (Fugaku_experiments/Allreduce/main.cpp:48-49) */
+};
+
+static inline uint64_t orc_splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+static inline uint64_t orc_key(uint64_t seed, uint64_t rank, uint64_t i) {
+    return orc_splitmix64(seed ^ (rank << 40) ^ i);
+}
+
+/* f32 -> bf16 round-to-nearest-even, NaN kept a (quiet) NaN. */
+static inline uint16_t orc_f32_to_bf16(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x007FFFFFu)) return (uint16_t)((u >> 16) | 0x40u);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+static inline float orc_bf16_to_f32(uint16_t h) {
+    uint32_t u = (uint32_t)h << 16;
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+
+/* Uniform value in [-1, 1) with 24 random bits: exactly representable in f32. */
+static inline float orc_gen_f32(uint64_t seed, uint64_t rank, uint64_t i) {
+    uint64_t u = orc_key(seed, rank, i);
+    return (float)(u >> 40) * (1.0f / 8388608.0f) - 1.0f;
+}
+static inline double orc_gen_f64(uint64_t seed, uint64_t rank, uint64_t i) {
+    uint64_t u = orc_key(seed, rank, i);
+    return (double)(u >> 11) * (1.0 / 4503599627370496.0) - 1.0;
+}
+
+size_t orc_dtype_size(int dtype);
+
+/* Fill `n` elements of rank `rank`'s buffer.  `count_for_seq` is the per-rank element
+ * count used by the SEQ pattern (value = rank*count_for_seq + i, wrapping int32). */
+void orc_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int rank,
+              uint64_t count_for_seq);
+
+/* MPI_Reduce_local restated (MPICH 3.3.2 predefined ops): inout[i] = in[i] (op) inout[i].
+ * int32 arithmetic wraps; bf16 is computed in f32 and rounded to bf16 RNE per call. */
+void orc_reduce_local(const void* in, void* inout, size_t n, int dtype, int op);
+
+/* Fused left-to-right form: acc = (((acc op ins[0]) op ins[1]) ... op ins[m-1]). */
+void orc_reduce_multi(void* acc, const void* const* ins, int m, size_t n, int dtype, int op);
+
+/* Recexch tables (all_reduce_radix_batch.cpp:11-198) for one group of `nranks` (= b). */
+typedef struct {
+    int k;               /* possibly clamped (:19-21) */
+    int p_of_k, rem, T;
+    int step1_sendto;    /* -1 for participants */
+    int step1_nrecvs;
+    int step1_recvfrom[64];
+    int step2_nphases;
+    int step2_nbrs[32][64];
+} orc_recexch_t;
+
+int orc_recexch_neighbors(int rank, int nranks, int k, orc_recexch_t* out);
+void orc_recexch_count_offset(int nranks, int max_phases, int k, int* count, int* offset);
+
+/* Whole-collective simulation of every rank of the communicator in one process.
+ * send[r] / recv[r] point at rank r's buffers.  send[r] may be NULL for in-place
+ * (then recv[r] holds the input, MPI_IN_PLACE semantics).
+ * Return 0 on success, nonzero for the preconditions the reference leaves unchecked. */
+int orc_allreduce_radix_batch(int nranks, int k, int b, size_t count, int dtype, int op,
+                              const void* const* send, void* const* recv);
+int orc_reduce_scatter_radix_batch(int nranks, int k, int b, size_t recvcount, int dtype,
+                                   int op, const void* const* send, void* const* recv);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,102 @@
+"""pyoracle -- TEST INFRASTRUCTURE ONLY: ctypes view of oracle/liboracle.so.
+
+The CPU restatement of CHiArA's radix/batch collectives and of MPI_Reduce_local
+(see chiara_oracle.h).  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import this module; the product never does.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+DTYPES = {"f32": 0, "f64": 1, "i32": 2, "bf16": 3}
+OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3}
+NP_DTYPES = {"f32": np.float32, "f64": np.float64, "i32": np.int32, "bf16": np.uint16}
+PAT_UNIFORM, PAT_SEQ = 0, 1
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE, "liboracle.so"])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        vp, sz, i, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
+        L.orc_fill.argtypes = [vp, sz, i, i, u64, i, u64]
+        L.orc_reduce_local.argtypes = [vp, vp, sz, i, i]
+        L.orc_reduce_multi.argtypes = [vp, ctypes.POINTER(vp), i, sz, i, i]
+        L.orc_allreduce_radix_batch.argtypes = [i, i, i, sz, i, i, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+        L.orc_allreduce_radix_batch.restype = i
+        L.orc_reduce_scatter_radix_batch.argtypes = [i, i, i, sz, i, i, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+        L.orc_reduce_scatter_radix_batch.restype = i
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def fill(n, dtype, pattern, seed, rank, count_for_seq=None):
+    """Rank `rank`'s synthetic input (same formula as the golden driver and the device fill)."""
+    a = np.empty(n, dtype=NP_DTYPES[dtype])
+    lib().orc_fill(_ptr(a), n, DTYPES[dtype], pattern, seed, rank, n if count_for_seq is None else count_for_seq)
+    return a
+
+
+def reduce_local(inp, inout, dtype, op):
+    """MPI_Reduce_local restated: inout = inp (op) inout, in place."""
+    assert inp.size == inout.size
+    lib().orc_reduce_local(_ptr(inp), _ptr(inout), inout.size, DTYPES[dtype], OPS[op])
+    return inout
+
+
+def reduce_multi(acc, ins, dtype, op):
+    arr = (ctypes.c_void_p * max(1, len(ins)))(*[x.ctypes.data for x in ins])
+    lib().orc_reduce_multi(_ptr(acc), arr, len(ins), acc.size, DTYPES[dtype], OPS[op])
+    return acc
+
+
+def _ptr_array(bufs):
+    return (ctypes.c_void_p * len(bufs))(*[(b.ctypes.data if b is not None else None) for b in bufs])
+
+
+def allreduce_radix_batch(sends, k, b, dtype, op, inplace=False):
+    """All ranks' outputs of all_reduce_radix_batch.  sends: list (one per rank)."""
+    n = len(sends)
+    count = sends[0].size
+    if inplace:
+        recvs = [s.copy() for s in sends]
+        sp = _ptr_array([None] * n)
+    else:
+        recvs = [np.zeros_like(s) for s in sends]
+        sp = _ptr_array(sends)
+    rc = lib().orc_allreduce_radix_batch(n, k, b, count, DTYPES[dtype], OPS[op], sp, _ptr_array(recvs))
+    if rc:
+        raise ValueError(f"oracle allreduce rejected geometry (rc={rc})")
+    return recvs
+
+
+def reduce_scatter_radix_batch(sends, k, b, dtype, op, inplace=False):
+    n = len(sends)
+    recvcount = sends[0].size // n
+    if inplace:
+        recvs = [s.copy() for s in sends]
+        sp = _ptr_array([None] * n)
+    else:
+        recvs = [np.zeros(recvcount, dtype=s.dtype) for s in sends]
+        sp = _ptr_array(sends)
+    rc = lib().orc_reduce_scatter_radix_batch(n, k, b, recvcount, DTYPES[dtype], OPS[op], sp, _ptr_array(recvs))
+    if rc:
+        raise ValueError(f"oracle reduce_scatter rejected geometry (rc={rc})")
+    return [r[:recvcount] for r in recvs]

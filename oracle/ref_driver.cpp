@@ -1,0 +1,142 @@
+// ref_driver.cpp -- TEST INFRASTRUCTURE ONLY, container-only.
+//
+// Drives the REAL reference algorithms, compiled unchanged from where they lie:
+//   /root/reference/Fugaku_experiments/Allreduce/all_reduce_radix_batch.cpp
+//   /root/reference/Fugaku_experiments/Reduce-scatter/reduce_scatter_radix_batch.cpp
+// against the container's MPICH 3.3.2 (/opt/conda), to produce golden vectors for
+// tests/golden/.  Build: `make -C oracle ref`; run: tests/golden/gen_golden.py.
+// Nothing from /root/reference is copied; this file only declares the two entry points
+// with the signatures at all_reduce_radix_batch.cpp:202-204 and
+// reduce_scatter_radix_batch.cpp:200-202.
+//
+// Usage: mpiexec -n N ref_driver <cases.txt> <outdir>
+//   one case per line: id mode(ar|rs|rl) k b count dtype op pattern seed inplace
+//   mode rl = a single MPI_Reduce_local timing/semantics probe on rank 0.
+// For each case rank 0 writes <outdir>/<id>.out (all ranks' outputs, rank-major) and
+// <outdir>/<id>.lib (the MPI library collective's result on the same inputs).
+#include <mpi.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "chiara_oracle.h"
+
+int all_reduce_radix_batch(char* sendbuf, char* recvbuf, int aCount, MPI_Datatype datatype,
+                           MPI_Op op, MPI_Comm comm, int k, int b);
+int reduce_scatter_radix_batch(const void* sendbuf, void* recvbuf, MPI_Aint recvcount,
+                               MPI_Datatype datatype, MPI_Op op, MPI_Comm comm, int k, int b);
+
+// orc_reduce_local is the single definition of the bf16 op semantics.
+static void bf16_user_op(void* in, void* inout, int* len, MPI_Datatype*) {
+    orc_reduce_local(in, inout, (size_t)*len, ORC_BF16, ORC_SUM);
+}
+static void bf16_user_max(void* in, void* inout, int* len, MPI_Datatype*) {
+    orc_reduce_local(in, inout, (size_t)*len, ORC_BF16, ORC_MAX);
+}
+static void bf16_user_min(void* in, void* inout, int* len, MPI_Datatype*) {
+    orc_reduce_local(in, inout, (size_t)*len, ORC_BF16, ORC_MIN);
+}
+static void bf16_user_prod(void* in, void* inout, int* len, MPI_Datatype*) {
+    orc_reduce_local(in, inout, (size_t)*len, ORC_BF16, ORC_PROD);
+}
+
+static int parse_dtype(const std::string& s) {
+    if (s == "f32") return ORC_F32;
+    if (s == "f64") return ORC_F64;
+    if (s == "i32") return ORC_I32;
+    if (s == "bf16") return ORC_BF16;
+    return -1;
+}
+static int parse_op(const std::string& s) {
+    if (s == "sum") return ORC_SUM;
+    if (s == "prod") return ORC_PROD;
+    if (s == "max") return ORC_MAX;
+    if (s == "min") return ORC_MIN;
+    return -1;
+}
+
+int main(int argc, char** argv) {
+    MPI_Init(&argc, &argv);
+    int rank, nprocs;
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    MPI_Comm_size(MPI_COMM_WORLD, &nprocs);
+    if (argc != 3) {
+        if (rank == 0) fprintf(stderr, "usage: ref_driver cases.txt outdir\n");
+        MPI_Finalize();
+        return 1;
+    }
+    MPI_Datatype bf16_t;
+    MPI_Type_contiguous(2, MPI_BYTE, &bf16_t);
+    MPI_Type_commit(&bf16_t);
+    MPI_Op bf16_ops[4];
+    MPI_Op_create(bf16_user_op, 1, &bf16_ops[ORC_SUM]);
+    MPI_Op_create(bf16_user_prod, 1, &bf16_ops[ORC_PROD]);
+    MPI_Op_create(bf16_user_max, 1, &bf16_ops[ORC_MAX]);
+    MPI_Op_create(bf16_user_min, 1, &bf16_ops[ORC_MIN]);
+    const MPI_Op std_ops[4] = {MPI_SUM, MPI_PROD, MPI_MAX, MPI_MIN};
+
+    std::ifstream cases(argv[1]);
+    std::string line;
+    while (std::getline(cases, line)) {
+        if (line.empty() || line[0] == '#') continue;
+        std::istringstream is(line);
+        std::string id, mode, dts, ops;
+        int k, b, pattern, inplace;
+        long long count;
+        unsigned long long seed;
+        is >> id >> mode >> k >> b >> count >> dts >> ops >> pattern >> seed >> inplace;
+        int dtype = parse_dtype(dts), op = parse_op(ops);
+        if (dtype < 0 || op < 0) {
+            if (rank == 0) fprintf(stderr, "bad case: %s\n", line.c_str());
+            continue;
+        }
+        size_t es = orc_dtype_size(dtype);
+        MPI_Datatype mdt = dtype == ORC_F32 ? MPI_FLOAT
+                           : dtype == ORC_F64 ? MPI_DOUBLE
+                           : dtype == ORC_I32 ? MPI_INT
+                                              : bf16_t;
+        MPI_Op mop = dtype == ORC_BF16 ? bf16_ops[op] : std_ops[op];
+
+        size_t in_n = (mode == "ar") ? (size_t)count : (size_t)count * nprocs;
+        size_t out_n = (size_t)count;
+        std::vector<char> send(in_n * es), recv(in_n * es, 0), lib(out_n * es, 0);
+        orc_fill(send.data(), in_n, dtype, pattern, seed, rank, in_n);
+
+        if (mode == "ar") {
+            MPI_Allreduce(send.data(), lib.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
+            if (inplace) memcpy(recv.data(), send.data(), in_n * es);
+            MPI_Barrier(MPI_COMM_WORLD);
+            all_reduce_radix_batch(inplace ? (char*)MPI_IN_PLACE : send.data(), recv.data(), (int)count,
+                                   mdt, mop, MPI_COMM_WORLD, k, b);
+        } else {
+            MPI_Reduce_scatter_block(send.data(), lib.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
+            if (inplace) memcpy(recv.data(), send.data(), in_n * es);
+            MPI_Barrier(MPI_COMM_WORLD);
+            reduce_scatter_radix_batch(inplace ? MPI_IN_PLACE : (const void*)send.data(), recv.data(),
+                                       (MPI_Aint)count, mdt, mop, MPI_COMM_WORLD, k, b);
+        }
+        MPI_Barrier(MPI_COMM_WORLD);
+        std::vector<char> all(rank == 0 ? out_n * es * nprocs : 1), all_lib(rank == 0 ? out_n * es * nprocs : 1);
+        MPI_Gather(recv.data(), (int)(out_n * es), MPI_BYTE, all.data(), (int)(out_n * es), MPI_BYTE, 0,
+                   MPI_COMM_WORLD);
+        MPI_Gather(lib.data(), (int)(out_n * es), MPI_BYTE, all_lib.data(), (int)(out_n * es), MPI_BYTE, 0,
+                   MPI_COMM_WORLD);
+        if (rank == 0) {
+            std::string base = std::string(argv[2]) + "/" + id;
+            FILE* f = fopen((base + ".out").c_str(), "wb");
+            fwrite(all.data(), 1, out_n * es * nprocs, f);
+            fclose(f);
+            f = fopen((base + ".lib").c_str(), "wb");
+            fwrite(all_lib.data(), 1, out_n * es * nprocs, f);
+            fclose(f);
+        }
+    }
+    MPI_Finalize();
+    return 0;
+}

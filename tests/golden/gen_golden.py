@@ -1,0 +1,153 @@
+#!/usr/bin/env python3
+"""Generate golden vectors from the REAL reference (container-only).
+
+Builds oracle/_ref/ref_driver (the reference's two algorithm files, compiled unchanged
+from /root/reference against the container's MPICH 3.3.2) and runs it under
+`mpiexec -n N` for a grid of (mode, n, k, b, count, dtype, op, pattern, inplace) cases.
+Writes:
+  tests/golden/manifest.json  one record per case: parameters, sha256 of all ranks'
+                              outputs (rank-major), sha256 of the MPI library collective,
+                              and the library-vs-reference difference statistics
+  tests/golden/outputs.npz    full outputs (rank-major) for the small cases
+Inputs are not stored: they are regenerated from (dtype, pattern, seed, rank) with the
+shared generator (oracle/chiara_oracle.h).  Rerun: python tests/golden/gen_golden.py
+"""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+ORACLE = os.path.join(REPO, "oracle")
+sys.path.insert(0, ORACLE)
+import pyoracle  # noqa: E402
+
+MPIEXEC = "/opt/conda/bin/mpiexec"
+SEED = 0xC41A5EED
+STORE_LIMIT = 64 * 1024  # bytes of rank-major output stored in full
+
+
+def divisors(n):
+    return [d for d in range(1, n + 1) if n % d == 0]
+
+
+def cases_for(n):
+    """Case grid for communicator size n (ids are unique across the whole grid)."""
+    out = []
+    ks = [2, 3, 4, 5, 8]
+
+    def add(mode, k, b, count, dt, op, pat, inplace):
+        cid = f"{mode}_n{n}_k{k}_b{b}_c{count}_{dt}_{op}_p{pat}_ip{inplace}"
+        out.append(dict(id=cid, mode=mode, n=n, k=k, b=b, count=count, dtype=dt, op=op,
+                        pattern=pat, seed=SEED, inplace=inplace))
+
+    for b in divisors(n):
+        for k in ks:
+            if k > max(b, 2) + 1 and k != 2:
+                continue  # k is clamped to b (all_reduce_radix_batch.cpp:19-21); keep one clamp probe
+            # allreduce: the reference harness's own int32 pattern, plus fp32/bf16/f64 uniform
+            add("ar", k, b, n * 3, "i32", "sum", pyoracle.PAT_SEQ, 0)
+            add("ar", k, b, n * 64, "f32", "sum", pyoracle.PAT_UNIFORM, 0)
+            add("ar", k, b, n * 5, "bf16", "sum", pyoracle.PAT_UNIFORM, 0)
+            # reduce-scatter (block): recvcount odd and even
+            add("rs", k, b, 7, "i32", "sum", pyoracle.PAT_SEQ, 0)
+            add("rs", k, b, 33, "f32", "sum", pyoracle.PAT_UNIFORM, 0)
+        # a few extra dtypes / ops / in-place per geometry at k = 2 and 3
+        for k in (2, 3):
+            add("ar", k, b, n * 16, "f64", "sum", pyoracle.PAT_UNIFORM, 0)
+            add("ar", k, b, n * 16, "i32", "sum", pyoracle.PAT_UNIFORM, 0)
+            add("ar", k, b, n * 16, "f32", "max", pyoracle.PAT_UNIFORM, 0)
+            add("ar", k, b, n * 16, "f32", "min", pyoracle.PAT_UNIFORM, 1)
+            add("ar", k, b, n * 16, "f32", "prod", pyoracle.PAT_UNIFORM, 0)
+            add("ar", k, b, n * 16, "f32", "sum", pyoracle.PAT_UNIFORM, 1)
+            add("rs", k, b, 16, "bf16", "sum", pyoracle.PAT_UNIFORM, 0)
+            add("rs", k, b, 16, "f32", "sum", pyoracle.PAT_UNIFORM, 1)
+            add("rs", k, b, 16, "i32", "max", pyoracle.PAT_UNIFORM, 0)
+    return out
+
+
+LARGE = [
+    # BASELINE geometries at sizes the reference finishes in seconds (hash-only)
+    dict(mode="ar", n=8, k=4, b=4, count=1 << 20, dtype="f32", op="sum"),
+    dict(mode="ar", n=8, k=4, b=4, count=1 << 20, dtype="bf16", op="sum"),
+    dict(mode="ar", n=8, k=2, b=2, count=1 << 20, dtype="f32", op="sum"),
+    dict(mode="ar", n=8, k=4, b=8, count=1 << 20, dtype="f32", op="sum"),
+    dict(mode="ar", n=8, k=3, b=4, count=1 << 20, dtype="bf16", op="sum"),
+    dict(mode="ar", n=8, k=2, b=4, count=1 << 20, dtype="bf16", op="sum"),
+    dict(mode="ar", n=2, k=2, b=1, count=1024, dtype="f32", op="sum"),
+    dict(mode="ar", n=2, k=2, b=2, count=1024, dtype="f32", op="sum"),
+    dict(mode="rs", n=2, k=2, b=1, count=1 << 18, dtype="f32", op="sum"),
+    dict(mode="rs", n=2, k=2, b=2, count=1 << 18, dtype="f32", op="sum"),
+    dict(mode="ar", n=4, k=2, b=2, count=1 << 18, dtype="f32", op="sum"),
+    dict(mode="ar", n=4, k=4, b=4, count=1 << 18, dtype="f32", op="sum"),
+]
+
+
+def run_n(n, cases, tmp):
+    cf = os.path.join(tmp, f"cases_{n}.txt")
+    with open(cf, "w") as f:
+        for c in cases:
+            f.write(f"{c['id']} {c['mode']} {c['k']} {c['b']} {c['count']} {c['dtype']} {c['op']} "
+                    f"{c['pattern']} {c['seed']} {c['inplace']}\n")
+    cmd = [MPIEXEC, "-n", str(n)]
+    if n <= os.cpu_count():
+        cmd[1:1] = ["-bind-to", "core"]
+    cmd += [os.path.join(ORACLE, "_ref", "ref_driver"), cf, tmp]
+    subprocess.check_call(cmd, timeout=600)
+
+
+def main():
+    subprocess.check_call(["make", "-s", "-C", ORACLE, "ref", "liboracle.so"])
+    all_cases = []
+    for n in (1, 2, 3, 4, 5, 6, 8, 9, 12, 16):
+        all_cases += cases_for(n)
+    for c in LARGE:
+        c = dict(c, pattern=pyoracle.PAT_UNIFORM, seed=SEED, inplace=0)
+        c["id"] = (f"{c['mode']}_n{c['n']}_k{c['k']}_b{c['b']}_c{c['count']}_{c['dtype']}_{c['op']}"
+                   f"_p{c['pattern']}_ip0_large")
+        all_cases.append(c)
+    manifest, arrays = [], {}
+    with tempfile.TemporaryDirectory() as tmp:
+        by_n = {}
+        for c in all_cases:
+            by_n.setdefault(c["n"], []).append(c)
+        for n, cs in sorted(by_n.items()):
+            print(f"n={n}: {len(cs)} cases", flush=True)
+            run_n(n, cs, tmp)
+        for c in all_cases:
+            out = open(os.path.join(tmp, c["id"] + ".out"), "rb").read()
+            libb = open(os.path.join(tmp, c["id"] + ".lib"), "rb").read()
+            rec = dict(c)
+            rec["sha256"] = hashlib.sha256(out).hexdigest()
+            rec["sha256_lib"] = hashlib.sha256(libb).hexdigest()
+            npdt = pyoracle.NP_DTYPES[c["dtype"]]
+            a = np.frombuffer(out, dtype=npdt)
+            lb = np.frombuffer(libb, dtype=npdt)
+            if c["dtype"] == "bf16":
+                af = (a.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+                lf = (lb.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+            else:
+                af, lf = a.astype(np.float64), lb.astype(np.float64)
+            rec["n_diff_vs_lib"] = int(np.count_nonzero(a != lb))
+            rec["max_abs_diff_vs_lib"] = float(np.max(np.abs(af - lf))) if a.size else 0.0
+            rec["stored"] = len(out) <= STORE_LIMIT
+            if rec["stored"]:
+                arrays[c["id"]] = a.copy()
+                arrays[c["id"] + "__lib"] = lb.copy()
+            manifest.append(rec)
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump({"generator": "tests/golden/gen_golden.py",
+                   "reference": "Fugaku_experiments/{Allreduce/all_reduce_radix_batch.cpp,"
+                                "Reduce-scatter/reduce_scatter_radix_batch.cpp} @ 2025-11-21, MPICH 3.3.2",
+                   "seed": SEED, "cases": manifest}, f, indent=0)
+    np.savez_compressed(os.path.join(HERE, "outputs.npz"), **arrays)
+    print(f"{len(manifest)} cases, {len(arrays) // 2} stored in full")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,86 @@
+"""Pin the oracle (CPU restatement) against the real reference's golden vectors.
+
+tests/golden/ was produced by tests/golden/gen_golden.py, which runs the reference's
+all_reduce_radix_batch.cpp / reduce_scatter_radix_batch.cpp unchanged under MPICH.
+Every case must match bit-for-bit (sha256 of all ranks' outputs).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import pyoracle as po
+
+
+def _run_oracle(c):
+    n = c["n"]
+    in_n = c["count"] if c["mode"] == "ar" else c["count"] * n
+    sends = [po.fill(in_n, c["dtype"], c["pattern"], c["seed"], r) for r in range(n)]
+    f = po.allreduce_radix_batch if c["mode"] == "ar" else po.reduce_scatter_radix_batch
+    return f(sends, c["k"], c["b"], c["dtype"], c["op"], inplace=bool(c["inplace"]))
+
+
+def test_golden_manifest_is_complete(golden):
+    cases, arrays = golden
+    assert len(cases) > 1000
+    assert len({c["id"] for c in cases}) == len(cases)
+    modes = {(c["mode"], c["dtype"], c["op"]) for c in cases}
+    for need in [("ar", "i32", "sum"), ("ar", "f32", "sum"), ("ar", "bf16", "sum"), ("rs", "f32", "sum"),
+                 ("ar", "f32", "max"), ("ar", "f64", "sum"), ("rs", "bf16", "sum")]:
+        assert need in modes
+
+
+def test_oracle_matches_reference_bit_exact(golden):
+    cases, arrays = golden
+    bad = []
+    for c in cases:
+        outs = _run_oracle(c)
+        h = hashlib.sha256(b"".join(o.tobytes() for o in outs)).hexdigest()
+        if h != c["sha256"]:
+            bad.append(c["id"])
+        elif c["stored"]:
+            np.testing.assert_array_equal(np.concatenate(outs), arrays[c["id"]])
+    assert not bad, f"{len(bad)} oracle/reference mismatches, e.g. {bad[:5]}"
+
+
+def test_reference_exact_on_integers(golden):
+    """The reference harness's own is_correct: int32 results equal MPI's collective."""
+    cases, _ = golden
+    ints = [c for c in cases if c["dtype"] == "i32"]
+    assert ints and all(c["n_diff_vs_lib"] == 0 for c in ints)
+
+
+def test_float_tolerance_vs_library(golden):
+    """fp32 SUM vs MPI_Allreduce is not bit-exact for n>2 (different association);
+    bound: |x - lib| <= (n-1) * 2^-23 * sum|x_i|, with |x_i| < 1 here."""
+    cases, _ = golden
+    for c in cases:
+        if c["dtype"] == "f32" and c["op"] == "sum":
+            assert c["max_abs_diff_vs_lib"] <= (c["n"] - 1) * 2.0 ** -23 * c["n"] * 2
+            if c["n"] <= 2:
+                assert c["n_diff_vs_lib"] == 0
+
+
+def test_reduce_local_semantics():
+    # MPICH loop: inout = in op inout; MAX picks `in` only when strictly greater.
+    a = np.array([1.0, -0.0, np.nan, 3.0], dtype=np.float32)
+    b = np.array([2.0, 0.0, 1.0, np.nan], dtype=np.float32)
+    out = po.reduce_local(a, b.copy(), "f32", "max")
+    assert out[0] == 2.0 and np.signbit(out[1]) == np.signbit(np.float32(0.0))
+    assert out[2] == 1.0 and np.isnan(out[3])
+    i = np.array([2**31 - 1], dtype=np.int32)
+    j = np.array([1], dtype=np.int32)
+    assert po.reduce_local(i, j, "i32", "sum")[0] == -(2**31)  # wraps
+    # bf16: f32 add then RNE per call
+    x = np.array([0x3F80], dtype=np.uint16)  # 1.0
+    y = np.array([0x3B80], dtype=np.uint16)  # 2^-8: 1 + 2^-8 is a tie -> even (1.0)
+    assert po.reduce_local(x, y, "bf16", "sum")[0] == 0x3F80
+
+
+def test_preconditions_rejected():
+    sends = [po.fill(131, "f32", 0, 1, r) for r in range(8)]
+    with pytest.raises(ValueError):  # count % nranks != 0: reference silently wrong
+        po.allreduce_radix_batch(sends, 2, 2, "f32", "sum")
+    sends = [po.fill(12, "f32", 0, 1, r) for r in range(6)]
+    with pytest.raises(ValueError):  # nranks % b != 0: reference aborts in MPI_Irecv
+        po.allreduce_radix_batch(sends, 2, 4, "f32", "sum")
