@@ -1,0 +1,273 @@
+#!/usr/bin/env python3
+"""bench.py -- CHiArA hot path on MI355X.
+
+N=1 (default): BASELINE config C2, the device-resident fp32 bucket reduction with k=2
+(one incoming 64 MiB bucket reduced into a 64 MiB accumulator = one MPI_Reduce_local
+call site of the reference, all_reduce_radix_batch.cpp:364).  One step = one call.
+Inputs are resident in HBM before the timed region; NSETS distinct (acc, in) pairs are
+cycled so the 768 MiB working set streams from HBM and not from the 256 MiB Infinity
+Cache.  value = algorithmic bytes (3 x 64 MiB per call) / wall time per step.
+
+N>1 (torchrun, one rank per GPU): the whole hierarchical allreduce over RCCL/xGMI
+(C4 geometry: fp32, 1 GiB per rank, k=4, b=4 at N=8; k=b=min(4,N) otherwise).
+value = aggregate input bytes reduced per second (N x 1 GiB per step / time).
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.join(REPO, "configurable-hierarchical-allreduce-algorithms_amd")
+sys.path[:0] = [PKG_DIR, os.path.join(REPO, "oracle")]
+
+METRIC = "device-resident bucket-reduction GB/s (fp32); allreduce GB/s at 2/4/8 GPUs"
+HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+XGMI_LINK_GBPS = 153.0       # per link, per the task statement; 7 links per GPU
+C2_ELEMS = 16 << 20          # 64 MiB fp32 per bucket
+NSETS = 4                    # 4 x 192 MiB working set > 256 MiB Infinity Cache
+SEED = 0xC41A5EED
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--no-cpu-baseline", action="store_true", help="skip the CPU baseline (profiling runs)")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--sweep", action="store_true", help="N=1: bucket sizes 1 KiB..1 GiB, m=1/3/7 (table to stderr)")
+    p.add_argument("--count", type=int, default=None, help="N>1: elements per rank (default 2^28)")
+    p.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
+    return p.parse_args()
+
+
+# ---- CPU baseline (rank 0, N=1 only; runs BEFORE the GPU is touched) ------------------------
+
+def cpu_baseline(seconds):
+    ref_bin = os.path.join(REPO, "oracle", "_ref", "ref_reduce_local")
+    if os.path.exists(ref_bin):
+        try:
+            out = subprocess.run([ref_bin, str(C2_ELEMS), str(seconds)], capture_output=True, text=True,
+                                 timeout=seconds + 60)
+            if out.returncode == 0:
+                r = json.loads(out.stdout.strip().splitlines()[-1])
+                return {"value": round(r["gbps"], 3), "unit": "GB/s", "cores": 1, "kind": "reference",
+                        "sample": f"MPICH 3.3.2 MPI_Reduce_local(MPI_FLOAT, MPI_SUM) on a 64 MiB bucket, m=1, "
+                                  f"{r['calls']} calls in {r['seconds']:.1f} s, 1 thread "
+                                  f"(oracle/_ref/ref_reduce_local; nproc={os.cpu_count()})"}
+        except Exception:
+            pass
+    import numpy as np
+
+    import pyoracle as po
+
+    a = po.fill(C2_ELEMS, "f32", 0, SEED, 1)
+    b = po.fill(C2_ELEMS, "f32", 0, SEED, 0)
+    po.reduce_local(a, b, "f32", "sum")
+    calls, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        po.reduce_local(a, b, "f32", "sum")
+        calls += 1
+    dt = time.perf_counter() - t0
+    np.asarray(b).sum()
+    return {"value": round(3 * 4 * C2_ELEMS * calls / dt / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"oracle orc_reduce_local (MPI_Reduce_local restated), 64 MiB fp32 bucket, m=1, "
+                      f"{calls} calls in {dt:.1f} s, 1 thread (nproc={os.cpu_count()})"}
+
+
+def pmc_traffic(kernel_key):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if any."""
+    path = os.path.join(REPO, "profiles", "pmc_latest.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d["kernels"][kernel_key]
+        return e["hbm_bytes_per_launch"]
+    except Exception:
+        return None
+
+
+# ---- N = 1: bucket reduction (C2) ----------------------------------------------------------------
+
+def bench_bucket(args, cpu):
+    import torch
+
+    import chiara_amd as ca
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    stream = torch.cuda.current_stream(dev)
+    n = C2_ELEMS
+    accs = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(NSETS)]
+    ins = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(NSETS)]
+    for i in range(NSETS):
+        ca.check(ca.fill(accs[i], n, ca.FLOAT32, 0, SEED, 2 * i, stream=stream))
+        ca.check(ca.fill(ins[i], n, ca.FLOAT32, 0, SEED, 2 * i + 1, stream=stream))
+    torch.cuda.synchronize()
+
+    def step(i):
+        s = i % NSETS
+        return ca.reduce_local(ins[s], accs[s], n, ca.FLOAT32, ca.SUM, stream)
+
+    for i in range(args.warmup):
+        ca.check(step(i))
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t_start, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    wall0 = time.perf_counter()
+    t_start.record(stream)
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        rc = step(i)
+        ev[i][1].record(stream)
+        if rc:
+            ca.check(rc)
+    t_end.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - wall0
+    total_ms = t_start.elapsed_time(t_end)
+    kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
+    avg_kern_ms = sum(kern_ms) / len(kern_ms)
+    bytes_per_step = 3 * 4 * n
+    ms_per_step = total_ms / args.steps
+    achieved = bytes_per_step / (avg_kern_ms * 1e-3) / 1e9
+    traffic = pmc_traffic("reduce_f32_sum_m1_64MiB")
+    line = {
+        "metric": METRIC, "value": round(bytes_per_step / (ms_per_step * 1e-3) / 1e9, 2), "unit": "GB/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "C2 bucket reduction: k=2 (m=1 incoming bucket), 64 MiB fp32 per bucket, "
+                               "device-resident, MPI_Reduce_local semantics", "bucket_bytes": 4 * n, "m": 1,
+                   "buffer_sets": NSETS, "parallelism": "replicas"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                     "kernel": "chr::k_reduce_vec<f32,SUM,M=1,U=4>", "algorithmic_bytes_per_launch": bytes_per_step,
+                     "avg_kernel_ms": round(avg_kern_ms, 5), "median_kernel_ms": round(kern_ms[len(kern_ms) // 2], 5)},
+        "cpu_baseline": cpu,
+        "host_wall_s": round(wall, 4),
+    }
+    if cpu:
+        line["gpu_vs_cpu"] = round(line["value"] / cpu["value"], 1)
+    if args.sweep:
+        line["sweep"] = sweep(ca, torch, dev, stream)
+    print(json.dumps(line), flush=True)
+
+
+def sweep(ca, torch, dev, stream):
+    """Bucket sizes 1 KiB .. 1 GiB, m = 1, 3, 7: kernel-time GB/s (HIP events)."""
+    rows = []
+    for m in (1, 3, 7):
+        for lg in range(10, 31, 2):
+            nbytes = 1 << lg
+            n = nbytes // 4
+            sets = max(1, min(8, (768 << 20) // ((m + 2) * nbytes)))
+            bufs = [[torch.empty(n, dtype=torch.float32, device=dev) for _ in range(m + 1)] for _ in range(sets)]
+            for s in bufs:
+                for j, t in enumerate(s):
+                    ca.fill(t, n, ca.FLOAT32, 0, SEED, j, stream=stream)
+            reps = max(5, min(200, (4 << 30) // ((m + 2) * nbytes)))
+
+            def go(i):
+                s = bufs[i % sets]
+                return ca.reduce_multi(s[0], s[0], s[1:], n, ca.FLOAT32, ca.SUM, stream)
+
+            for i in range(3):
+                go(i)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record(stream)
+            for i in range(reps):
+                go(i)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / reps
+            gbps = (m + 2) * nbytes / (ms * 1e-3) / 1e9
+            rows.append({"m": m, "bucket_bytes": nbytes, "us": round(ms * 1e3, 2), "GBps": round(gbps, 1),
+                         "frac": round(gbps / HBM_PEAK_GBPS, 4)})
+            print(f"sweep m={m} bucket={nbytes:>11d} B  {ms * 1e3:9.2f} us  {gbps:8.1f} GB/s", file=sys.stderr,
+                  flush=True)
+            del bufs
+    torch.cuda.empty_cache()
+    return rows
+
+
+# ---- N > 1: hierarchical allreduce over RCCL ---------------------------------------------------
+
+def bench_allreduce(args):
+    import torch
+    import torch.distributed as dist
+
+    import chiara_amd as ca
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    comm = ca.Comm.from_torch_distributed(device=local)
+    b = 4 if world % 4 == 0 else world
+    k = min(4, b) if b > 1 else 2
+    dt = ca.FLOAT32 if args.dtype == "f32" else ca.BFLOAT16
+    es = 4 if args.dtype == "f32" else 2
+    count = args.count or ((1 << 30) // es)
+    count -= count % world
+    stream = comm.stream
+    send = torch.empty(count * es, dtype=torch.uint8, device=dev)
+    recv = torch.empty(count * es, dtype=torch.uint8, device=dev)
+    ca.check(ca.fill(send, count, dt, 0, SEED, rank, stream=stream))
+    torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        ca.check(ca.all_reduce_radix_batch(send, recv, count, dt, ca.SUM, comm, k, b, async_op=True))
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ca.check(ca.all_reduce_radix_batch(send, recv, count, dt, ca.SUM, comm, k, b, async_op=True))
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    S = count * es
+    algbw = S * args.steps / el / 1e9
+    busbw = algbw * 2 * (world - 1) / world
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(world * S * args.steps / el / 1e9, 2), "unit": "GB/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
+            "config": {"workload": f"all_reduce_radix_batch, {S >> 20} MiB per rank, k={k}, b={b}, RCCL p2p over "
+                                   f"xGMI, device-resident", "k": k, "b": b, "count": count,
+                       "parallelism": f"collective x{world}"},
+            "algbw_GBps": round(algbw, 2), "busbw_GBps": round(busbw, 2),
+            "xgmi_roofline": {"per_link_GBps": XGMI_LINK_GBPS, "aggregate_GBps": 7 * XGMI_LINK_GBPS,
+                              "busbw_frac_per_link": round(busbw / XGMI_LINK_GBPS, 4),
+                              "busbw_frac_aggregate": round(busbw / (7 * XGMI_LINK_GBPS), 4)},
+            "roofline": None, "cpu_baseline": None,
+        }
+        print(json.dumps(line), flush=True)
+    comm.destroy()
+    dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        bench_allreduce(args)
+        return
+    cpu = None if args.no_cpu_baseline else cpu_baseline(args.cpu_seconds)
+    bench_bucket(args, cpu)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,13 @@
+"""chiara_amd -- MI355X-native hot path of CHiArA (Configurable Hierarchical Allreduce
+Algorithms): fused bucket-reduction HIP kernels + radix/batch schedules over RCCL.
+
+The compute lives in libchiara.so (hand-written gfx950 HIP + host C++ schedule); this
+package is the Python mirror of the reference's operator interface over its C ABI.
+"""
+from ._lib import EXPORTED, ChiaraError, lib  # noqa: F401  (fails loudly without libchiara.so)
+from .collectives import (  # noqa: F401
+    BFLOAT16, DOUBLE, DTYPE_SIZE, FLOAT, FLOAT32, FLOAT64, IN_PLACE, INT, INT32, MAX, MIN,
+    MODE_ALLREDUCE, MODE_REDUCE_SCATTER, PROD, SUCCESS, SUM, Comm, LocalGroup, all_reduce_radix_batch,
+    check, describe_plan, fill, get_unique_id, parse_plan, reduce_local, reduce_multi,
+    reduce_scatter_radix_batch,
+)

@@ -1,0 +1,79 @@
+"""Loader for libchiara.so (the in-tree MI355X build of the CHiArA hot path).
+
+There is no CPU fallback: if the library is missing, importing the package fails
+loudly with the build command to run.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "libchiara.so")
+
+
+class ChiaraError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = code
+        msg = _lib.chr_error_string(code).decode() if _lib is not None else str(code)
+        super().__init__(f"{what}: chiara error {code} ({msg})" if what else f"chiara error {code} ({msg})")
+
+
+class UniqueId(ctypes.Structure):
+    _fields_ = [("internal", ctypes.c_char * 128)]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libchiara.so not found at {LIB_PATH}; build it with "
+            f"`make -C {PKG_ROOT}` (hipcc --offload-arch=gfx950) or __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, i, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
+    pp = ctypes.POINTER(ctypes.c_void_p)
+    sig = {
+        "chr_abi_version": ([], i),
+        "chr_error_string": ([i], ctypes.c_char_p),
+        "chr_reduce_local": ([vp, vp, sz, i, i, vp], i),
+        "chr_reduce_multi": ([vp, vp, pp, i, sz, i, i, vp], i),
+        "chr_fill": ([vp, sz, i, i, u64, i, u64, vp], i),
+        "chr_get_unique_id": ([ctypes.POINTER(UniqueId)], i),
+        "chr_comm_init_rank": ([ctypes.POINTER(vp), i, ctypes.POINTER(UniqueId), i, i], i),
+        "chr_comm_destroy": ([vp], i),
+        "chr_comm_rank": ([vp, ctypes.POINTER(i)], i),
+        "chr_comm_size": ([vp, ctypes.POINTER(i)], i),
+        "chr_comm_stream": ([vp, pp], i),
+        "chr_allreduce_radix_batch": ([vp, vp, sz, i, i, vp, i, i], i),
+        "chr_reduce_scatter_radix_batch": ([vp, vp, sz, i, i, vp, i, i], i),
+        "chr_allreduce_radix_batch_async": ([vp, vp, sz, i, i, vp, i, i], i),
+        "chr_reduce_scatter_radix_batch_async": ([vp, vp, sz, i, i, vp, i, i], i),
+        "chr_local_group_create": ([ctypes.POINTER(vp), i, i], i),
+        "chr_local_group_destroy": ([vp], i),
+        "chr_local_group_stream": ([vp, pp], i),
+        "chr_local_allreduce_radix_batch": ([vp, pp, pp, sz, i, i, i, i], i),
+        "chr_local_reduce_scatter_radix_batch": ([vp, pp, pp, sz, i, i, i, i], i),
+        "chr_plan_describe": ([i, i, i, i, i, sz, ctypes.c_char_p, sz], ctypes.c_long),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    return L
+
+
+_lib = None
+_lib = _load()
+
+
+def lib():
+    return _lib
+
+
+# Every symbol include/chiara.h declares (checked by tests/test_abi.py).
+EXPORTED = [
+    "chr_reduce_local", "chr_reduce_multi", "chr_get_unique_id", "chr_comm_init_rank", "chr_comm_destroy",
+    "chr_comm_rank", "chr_comm_size", "chr_comm_stream", "chr_allreduce_radix_batch",
+    "chr_reduce_scatter_radix_batch", "chr_allreduce_radix_batch_async", "chr_reduce_scatter_radix_batch_async",
+    "chr_local_group_create", "chr_local_group_destroy", "chr_local_group_stream",
+    "chr_local_allreduce_radix_batch", "chr_local_reduce_scatter_radix_batch", "chr_plan_describe", "chr_fill",
+    "chr_error_string", "chr_abi_version",
+]

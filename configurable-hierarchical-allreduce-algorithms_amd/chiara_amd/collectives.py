@@ -1,0 +1,231 @@
+"""Host-side mirror of CHiArA's operator interface, over the libchiara C ABI.
+
+Same names, argument meaning and status-code behaviour as the reference:
+  all_reduce_radix_batch(sendbuf, recvbuf, count, datatype, op, comm, k, b) -> int
+      Fugaku_experiments/Allreduce/all_reduce_radix_batch.cpp:202-204
+  reduce_scatter_radix_batch(sendbuf, recvbuf, recvcount, datatype, op, comm, k, b) -> int
+      Fugaku_experiments/Reduce-scatter/reduce_scatter_radix_batch.cpp:200-202
+  reduce_local(inbuf, inoutbuf, count, datatype, op) -> int      (MPI_Reduce_local)
+Return value 0 == MPI_SUCCESS.  Unlike the reference (which always returns MPI_SUCCESS)
+the preconditions it leaves unchecked come back as nonzero codes (CHR_ERR_*).
+
+Buffers may be torch tensors (device: device-resident path; CPU: staged through HBM),
+numpy arrays (host) or raw integer addresses.  PyTorch is only plumbing here.
+"""
+import ctypes
+import os
+
+from ._lib import ChiaraError, UniqueId, lib
+
+# datatypes (chr_dtype) with MPI-style aliases
+FLOAT32 = FLOAT = 0
+FLOAT64 = DOUBLE = 1
+INT32 = INT = 2
+BFLOAT16 = 3
+# ops (chr_op)
+SUM, PROD, MAX, MIN = 0, 1, 2, 3
+SUCCESS = 0
+IN_PLACE = object()  # MPI_IN_PLACE analogue
+_IN_PLACE_PTR = 1     # CHR_IN_PLACE
+
+DTYPE_SIZE = {FLOAT32: 4, FLOAT64: 8, INT32: 4, BFLOAT16: 2}
+MODE_ALLREDUCE, MODE_REDUCE_SCATTER = 0, 1
+
+
+def _addr(buf):
+    """Raw address of a buffer (torch tensor, numpy array, ctypes object or int)."""
+    if buf is None:
+        return None
+    if buf is IN_PLACE:
+        return _IN_PLACE_PTR
+    if isinstance(buf, int):
+        return buf
+    if hasattr(buf, "data_ptr"):
+        return buf.data_ptr()
+    if hasattr(buf, "ctypes"):
+        return buf.ctypes.data
+    if isinstance(buf, ctypes.Array):
+        return ctypes.addressof(buf)
+    raise TypeError(f"unsupported buffer type {type(buf)!r}")
+
+
+def _stream(stream):
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    if hasattr(stream, "cuda_stream"):
+        return stream.cuda_stream
+    raise TypeError(f"unsupported stream {type(stream)!r}")
+
+
+def check(code, what=""):
+    if code != SUCCESS:
+        raise ChiaraError(code, what)
+    return code
+
+
+# ---- kernel boundary ------------------------------------------------------------------------
+
+def reduce_local(inbuf, inoutbuf, count, datatype, op, stream=None):
+    """MPI_Reduce_local on device buffers: inout = in (op) inout (enqueued on `stream`)."""
+    return lib().chr_reduce_local(_addr(inbuf), _addr(inoutbuf), count, datatype, op, _stream(stream))
+
+
+def reduce_multi(out, acc, ins, count, datatype, op, stream=None):
+    """Fused left-to-right reduction of len(ins) incoming buckets into acc (written to out)."""
+    arr = (ctypes.c_void_p * max(1, len(ins)))(*[_addr(x) for x in ins])
+    return lib().chr_reduce_multi(_addr(out), _addr(acc), arr, len(ins), count, datatype, op, _stream(stream))
+
+
+def fill(buf, count, datatype, pattern, seed, rank, count_for_seq=None, stream=None):
+    """Device-side synthetic inputs (same generator as the oracle)."""
+    cfs = count if count_for_seq is None else count_for_seq
+    return lib().chr_fill(_addr(buf), count, datatype, pattern, seed, rank, cfs, _stream(stream))
+
+
+# ---- communicators --------------------------------------------------------------------------
+
+def get_unique_id():
+    uid = UniqueId()
+    check(lib().chr_get_unique_id(ctypes.byref(uid)), "chr_get_unique_id")
+    return bytes(uid.internal)
+
+
+class Comm:
+    """RCCL-backed communicator (one rank per process, one MI355X per rank)."""
+
+    def __init__(self, nranks, unique_id, rank, device):
+        uid = UniqueId()
+        ctypes.memmove(ctypes.byref(uid), unique_id, 128)
+        h = ctypes.c_void_p()
+        check(lib().chr_comm_init_rank(ctypes.byref(h), nranks, ctypes.byref(uid), rank, device),
+              "chr_comm_init_rank")
+        self._h = h
+        self.rank, self.nranks, self.device = rank, nranks, device
+
+    @classmethod
+    def from_torch_distributed(cls, group=None, device=None):
+        """Bootstrap over an initialised torch.distributed group (gloo is enough): rank 0
+        creates the RCCL unique id and broadcasts its 128 bytes."""
+        import torch
+        import torch.distributed as dist
+
+        rank, n = dist.get_rank(group), dist.get_world_size(group)
+        buf = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            buf.copy_(torch.frombuffer(bytearray(get_unique_id()), dtype=torch.uint8))
+        dist.broadcast(buf, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        return cls(n, bytes(buf.numpy().tobytes()), rank, device)
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def stream(self):
+        s = ctypes.c_void_p()
+        check(lib().chr_comm_stream(self._h, ctypes.byref(s)))
+        return s.value
+
+    def destroy(self):
+        if self._h:
+            lib().chr_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+class LocalGroup:
+    """n virtual ranks on ONE device (loopback transport, same plans and kernels)."""
+
+    def __init__(self, nranks, device=0):
+        h = ctypes.c_void_p()
+        check(lib().chr_local_group_create(ctypes.byref(h), nranks, device), "chr_local_group_create")
+        self._h = h
+        self.nranks, self.device = nranks, device
+
+    @property
+    def stream(self):
+        s = ctypes.c_void_p()
+        check(lib().chr_local_group_stream(self._h, ctypes.byref(s)))
+        return s.value
+
+    def all_reduce_radix_batch(self, sendbufs, recvbufs, count, datatype, op, k, b):
+        S = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in sendbufs])
+        R = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in recvbufs])
+        return lib().chr_local_allreduce_radix_batch(self._h, S, R, count, datatype, op, k, b)
+
+    def reduce_scatter_radix_batch(self, sendbufs, recvbufs, recvcount, datatype, op, k, b):
+        S = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in sendbufs])
+        R = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in recvbufs])
+        return lib().chr_local_reduce_scatter_radix_batch(self._h, S, R, recvcount, datatype, op, k, b)
+
+    def destroy(self):
+        if self._h:
+            lib().chr_local_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+# ---- schedule boundary (the reference's entry points) ------------------------------------------
+
+def all_reduce_radix_batch(sendbuf, recvbuf, count, datatype, op, comm, k, b, async_op=False):
+    fn = lib().chr_allreduce_radix_batch_async if async_op else lib().chr_allreduce_radix_batch
+    return fn(_addr(sendbuf), _addr(recvbuf), count, datatype, op, comm.handle, k, b)
+
+
+def reduce_scatter_radix_batch(sendbuf, recvbuf, recvcount, datatype, op, comm, k, b, async_op=False):
+    fn = lib().chr_reduce_scatter_radix_batch_async if async_op else lib().chr_reduce_scatter_radix_batch
+    return fn(_addr(sendbuf), _addr(recvbuf), recvcount, datatype, op, comm.handle, k, b)
+
+
+# ---- plan introspection (host only) --------------------------------------------------------------
+
+def describe_plan(mode, nranks, rank, k, b, count):
+    n = lib().chr_plan_describe(mode, nranks, rank, k, b, count, None, 0)
+    if n < 0:
+        raise ValueError("bad plan request")
+    buf = ctypes.create_string_buffer(n + 1)
+    lib().chr_plan_describe(mode, nranks, rank, k, b, count, buf, n + 1)
+    return buf.value.decode()
+
+
+def parse_plan(text):
+    """Parse describe_plan() output into {'header':{...}, 'pre':[...], 'steps':[...]}."""
+    lines = text.strip().split("\n")
+    head = dict(kv.split("=") for kv in lines[0].split()[1:])
+    header = {k: int(v) for k, v in head.items()}
+    plan = {"header": header, "pre": [], "steps": []}
+    cur = None
+
+    def local(tok):
+        if tok[0] == "copy":
+            return ("copy", (tok[1], int(tok[2])), (tok[3], int(tok[4])), int(tok[5]), [])
+        m = int(tok[6])
+        ins = [(tok[7 + 2 * j], int(tok[8 + 2 * j])) for j in range(m)]
+        return ("reduce", (tok[1], int(tok[2])), (tok[3], int(tok[4])), int(tok[5]), ins)
+
+    for ln in lines[1:]:
+        tok = ln.split()
+        if tok[0] == "pre":
+            plan["pre"].append(local(tok[1:]))
+        elif tok[0] == "step":
+            cur = {"label": tok[2], "sends": [], "recvs": [], "post": []}
+            plan["steps"].append(cur)
+        elif tok[0] in ("send", "recv"):
+            cur[tok[0] + "s"].append((int(tok[1]), (tok[2], int(tok[3])), int(tok[4])))
+        else:
+            cur["post"].append(local(tok))
+    return plan

@@ -1,0 +1,71 @@
+// api.cpp -- C ABI glue for the kernel boundary, plan introspection and utilities.
+#include <hip/hip_runtime_api.h>
+
+#include <cstring>
+#include <string>
+
+#include "chr_internal.hpp"
+#include "schedule.hpp"
+
+extern "C" {
+
+int chr_abi_version(void) { return CHR_ABI_VERSION; }
+
+const char* chr_error_string(int code) {
+    switch (code) {
+    case CHR_SUCCESS: return "success";
+    case CHR_ERR_INVALID_ARG: return "invalid argument";
+    case CHR_ERR_COUNT_NOT_DIVISIBLE: return "count is not a multiple of the number of ranks";
+    case CHR_ERR_BATCH_NOT_DIVISOR: return "batch b does not divide the number of ranks";
+    case CHR_ERR_HIP: return "HIP runtime error";
+    case CHR_ERR_RCCL: return "RCCL error";
+    case CHR_ERR_NO_DEVICE: return "no HIP device";
+    case CHR_ERR_OUT_OF_MEMORY: return "out of device memory";
+    case CHR_ERR_UNSUPPORTED: return "unsupported";
+    default: return "unknown error";
+    }
+}
+
+static int status(hipError_t e) {
+    if (e == hipSuccess) return CHR_SUCCESS;
+    return e == hipErrorOutOfMemory ? CHR_ERR_OUT_OF_MEMORY : CHR_ERR_HIP;
+}
+
+int chr_reduce_local(const void* in, void* inout, size_t n, chr_dtype dtype, chr_op op, hipStream_t stream) {
+    if (!chr::valid_dtype_op(dtype, op)) return CHR_ERR_INVALID_ARG;
+    if (n == 0) return CHR_SUCCESS;
+    if (!in || !inout) return CHR_ERR_INVALID_ARG;
+    const void* ins[1] = {in};
+    return status(chr::launch_reduce(inout, inout, ins, 1, n, dtype, op, stream));
+}
+
+int chr_reduce_multi(void* out, const void* acc, const void* const* ins, int m, size_t n, chr_dtype dtype, chr_op op,
+                     hipStream_t stream) {
+    if (!chr::valid_dtype_op(dtype, op) || m < 0) return CHR_ERR_INVALID_ARG;
+    if (n == 0) return CHR_SUCCESS;
+    if (!out || !acc || (m > 0 && !ins)) return CHR_ERR_INVALID_ARG;
+    for (int j = 0; j < m; ++j)
+        if (!ins[j]) return CHR_ERR_INVALID_ARG;
+    return status(chr::launch_reduce(out, acc, ins, m, n, dtype, op, stream));
+}
+
+int chr_fill(void* buf, size_t n, chr_dtype dtype, int pattern, uint64_t seed, int rank, uint64_t count_for_seq,
+             hipStream_t stream) {
+    if (!chr::dtype_size(dtype) || (pattern != 0 && pattern != 1)) return CHR_ERR_INVALID_ARG;
+    if (n == 0) return CHR_SUCCESS;
+    if (!buf) return CHR_ERR_INVALID_ARG;
+    return status(chr::launch_fill(buf, n, dtype, pattern, seed, rank, count_for_seq, stream));
+}
+
+long chr_plan_describe(chr_mode mode, int nranks, int rank, int k, int b, size_t count, char* buf, size_t len) {
+    if (mode != CHR_MODE_ALLREDUCE && mode != CHR_MODE_REDUCE_SCATTER) return -1;
+    const std::string s = chr::describe(chr::build_plan((chr::Mode)mode, nranks, rank, k, b, count));
+    if (buf && len) {
+        const size_t c = s.size() < len - 1 ? s.size() : len - 1;
+        std::memcpy(buf, s.data(), c);
+        buf[c] = '\0';
+    }
+    return (long)s.size();
+}
+
+}  // extern "C"

@@ -1,0 +1,33 @@
+// chr_internal.hpp -- declarations shared by the libchiara translation units.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "chiara.h"
+
+namespace chr {
+
+size_t dtype_size(int dtype);
+bool valid_dtype_op(int dtype, int op);
+
+// Fused bucket reduction: out = (...((acc op ins[0]) op ins[1])...) op ins[m-1].
+// Device pointers.  m may exceed the kernel's fan-in: chained left to right.
+hipError_t launch_reduce(void* out, const void* acc, const void* const* ins, int m, size_t n,
+                         int dtype, int op, hipStream_t stream);
+
+hipError_t launch_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int rank,
+                       uint64_t count_for_seq, hipStream_t stream);
+
+// Tunables (read once from the environment):
+//   CHR_REDUCE_MAX_BLOCKS  cap on the grid (default 2048 = 8 per CU)
+//   CHR_REDUCE_NT          1: non-temporal stores of the result
+struct ReduceTuning {
+    int max_blocks;
+    int nt_store;
+};
+ReduceTuning& reduce_tuning();
+
+}  // namespace chr

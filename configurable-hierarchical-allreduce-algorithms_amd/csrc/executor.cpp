@@ -1,0 +1,405 @@
+// executor.cpp -- runs compiled radix/batch plans on MI355X.
+//
+// Two transports behind one executor:
+//  * chr_comm: one rank per process/GPU, messages = RCCL ncclSend/ncclRecv over xGMI.
+//    All k-1 neighbour exchanges of a recexch phase (and all nnodes-1 lane messages of
+//    the inter-node phase) go into ONE ncclGroupStart/End, so the phase drives several
+//    xGMI links at once (the reference serialises them: all_reduce_radix_batch.cpp:343-367),
+//    then ONE fused reduction kernel consumes all incoming buckets.
+//  * chr_local_group: n virtual ranks on one device, messages = device-to-device copies.
+//    Same plans, same kernels; used to check multi-rank schedules on a single MI355X.
+// Everything is enqueued on one HIP stream per communicator; scratch (ACC, STAGE) is
+// allocated once and reused (the reference mallocs 2x the buffer per call, :296-297).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "chr_internal.hpp"
+#include "schedule.hpp"
+
+namespace {
+
+using chr::Plan;
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    // Grows (never shrinks).  The caller has synchronised the stream before a regrow.
+    hipError_t reserve(size_t want, hipStream_t s) {
+        if (want <= bytes) return hipSuccess;
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return e;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        e = hipMalloc(&p, want);
+        if (e == hipSuccess) bytes = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+struct Bufs {
+    const char* send;
+    char* recv;
+    char* acc;
+    char* stage;
+    size_t es;
+    char* ptr(const chr::Ref& r) const {
+        char* base = r.buf == chr::BUF_SEND   ? const_cast<char*>(send)
+                     : r.buf == chr::BUF_RECV ? recv
+                     : r.buf == chr::BUF_ACC  ? acc
+                                              : stage;
+        return base + r.off * es;
+    }
+};
+
+int hip_code(hipError_t e) {
+    if (e == hipSuccess) return CHR_SUCCESS;
+    if (e == hipErrorOutOfMemory) return CHR_ERR_OUT_OF_MEMORY;
+    if (std::getenv("CHR_DEBUG")) std::fprintf(stderr, "[chiara] HIP error: %s\n", hipGetErrorString(e));
+    return CHR_ERR_HIP;
+}
+
+int nccl_code(ncclResult_t r) {
+    if (r == ncclSuccess) return CHR_SUCCESS;
+    if (std::getenv("CHR_DEBUG")) std::fprintf(stderr, "[chiara] RCCL error: %s\n", ncclGetErrorString(r));
+    return CHR_ERR_RCCL;
+}
+
+int run_local(const chr::LocalOp& op, const Bufs& B, int dtype, int rop, hipStream_t s) {
+    if (op.count == 0) return CHR_SUCCESS;
+    if (op.kind == chr::L_COPY) {
+        char* d = B.ptr(op.dst);
+        const char* src = B.ptr(op.acc);
+        if (d == src) return CHR_SUCCESS;
+        return hip_code(hipMemcpyAsync(d, src, op.count * B.es, hipMemcpyDeviceToDevice, s));
+    }
+    std::vector<const void*> ins(op.ins.size());
+    for (size_t j = 0; j < op.ins.size(); ++j) ins[j] = B.ptr(op.ins[j]);
+    return hip_code(chr::launch_reduce(B.ptr(op.dst), B.ptr(op.acc), ins.data(), (int)ins.size(), op.count, dtype,
+                                       rop, s));
+}
+
+bool is_device_ptr(const void* p) {
+    hipPointerAttribute_t attr;
+    std::memset(&attr, 0, sizeof(attr));
+    hipError_t e = hipPointerGetAttributes(&attr, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+using PlanKey = std::tuple<int, int, int, int, uint64_t>;  // mode, rank, k, b, count
+
+}  // namespace
+
+struct chr_comm {
+    int rank = 0, nranks = 0, device = 0;
+    ncclComm_t nccl = nullptr;
+    hipStream_t stream = nullptr;
+    DevBuf acc, stage, hsend, hrecv;
+    std::map<PlanKey, std::unique_ptr<Plan>> plans;
+
+    const Plan& plan(int mode, int k, int b, uint64_t count) {
+        PlanKey key{mode, rank, k, b, count};
+        auto it = plans.find(key);
+        if (it == plans.end())
+            it = plans.emplace(key, std::make_unique<Plan>(chr::build_plan((chr::Mode)mode, nranks, rank, k, b, count)))
+                     .first;
+        return *it->second;
+    }
+};
+
+struct chr_local_group {
+    int nranks = 0, device = 0;
+    hipStream_t stream = nullptr;
+    std::vector<DevBuf> acc, stage;
+    std::map<std::tuple<int, int, int, uint64_t>, std::vector<Plan>> plans;
+};
+
+namespace {
+
+int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int dtype, int op) {
+    const size_t es = chr::dtype_size(dtype);
+    hipError_t e = c->acc.reserve(p.acc_elems * es, c->stream);
+    if (e == hipSuccess) e = c->stage.reserve(p.stage_elems * es, c->stream);
+    if (e != hipSuccess) return hip_code(e);
+    Bufs B{(const char*)send, (char*)recv, (char*)c->acc.p, (char*)c->stage.p, es};
+    int rc;
+    for (const auto& op_ : p.pre)
+        if ((rc = run_local(op_, B, dtype, op, c->stream))) return rc;
+    for (const chr::Step& s : p.steps) {
+        if (!s.sends.empty() || !s.recvs.empty()) {
+            if ((rc = nccl_code(ncclGroupStart()))) return rc;
+            for (const chr::Xfer& x : s.sends)
+                if ((rc = nccl_code(ncclSend(B.ptr(x.ref), x.count * es, ncclUint8, x.peer, c->nccl, c->stream)))) {
+                    (void)ncclGroupEnd();
+                    return rc;
+                }
+            for (const chr::Xfer& x : s.recvs)
+                if ((rc = nccl_code(ncclRecv(B.ptr(x.ref), x.count * es, ncclUint8, x.peer, c->nccl, c->stream)))) {
+                    (void)ncclGroupEnd();
+                    return rc;
+                }
+            if ((rc = nccl_code(ncclGroupEnd()))) return rc;
+        }
+        for (const auto& op_ : s.post)
+            if ((rc = run_local(op_, B, dtype, op, c->stream))) return rc;
+    }
+    return CHR_SUCCESS;
+}
+
+int collective(chr_comm* c, int mode, const void* send, void* recv, size_t count, int dtype, int op, int k, int b,
+               bool sync) {
+    if (!c || !chr::valid_dtype_op(dtype, op)) return CHR_ERR_INVALID_ARG;
+    const Plan& p = c->plan(mode, k, b, count);
+    if (p.error) return p.error;
+    if (p.g.total == 0) return CHR_SUCCESS;
+    if (!recv) return CHR_ERR_INVALID_ARG;
+    const size_t es = chr::dtype_size(dtype);
+    const bool inplace = send == CHR_IN_PLACE;
+    const void* input = inplace ? (const void*)recv : send;
+    if (!input) return CHR_ERR_INVALID_ARG;
+    hipError_t e = hipSetDevice(c->device);
+    if (e != hipSuccess) return hip_code(e);
+    const bool dev_in = is_device_ptr(input), dev_out = is_device_ptr(recv);
+    if (dev_in && dev_out) {
+        int rc = enqueue_rccl(c, p, input, recv, dtype, op);
+        if (rc || !sync) return rc;
+        return hip_code(hipStreamSynchronize(c->stream));
+    }
+    if (!sync) return CHR_ERR_UNSUPPORTED;  // async needs device-resident buffers
+    // Host-memory contract of the reference: stage through HBM (PCIe H2D / D2H).
+    const void* dsend = input;
+    void* drecv = recv;
+    if (!dev_in) {
+        if ((e = c->hsend.reserve(p.send_elems * es, c->stream)) != hipSuccess) return hip_code(e);
+        if ((e = hipMemcpyAsync(c->hsend.p, input, p.send_elems * es, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+            return hip_code(e);
+        dsend = c->hsend.p;
+    }
+    if (!dev_out) {
+        if ((e = c->hrecv.reserve(p.recv_elems * es, c->stream)) != hipSuccess) return hip_code(e);
+        drecv = c->hrecv.p;
+    }
+    int rc = enqueue_rccl(c, p, dsend, drecv, dtype, op);
+    if (rc) return rc;
+    if (!dev_out &&
+        (e = hipMemcpyAsync(recv, drecv, p.recv_elems * es, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+        return hip_code(e);
+    return hip_code(hipStreamSynchronize(c->stream));
+}
+
+int local_collective(chr_local_group* g, int mode, const void* const* sends, void* const* recvs, size_t count,
+                     int dtype, int op, int k, int b) {
+    if (!g || !sends || !recvs || !chr::valid_dtype_op(dtype, op)) return CHR_ERR_INVALID_ARG;
+    const int n = g->nranks;
+    auto key = std::make_tuple(mode, k, b, (uint64_t)count);
+    auto it = g->plans.find(key);
+    if (it == g->plans.end()) {
+        std::vector<Plan> v;
+        for (int r = 0; r < n; ++r) v.push_back(chr::build_plan((chr::Mode)mode, n, r, k, b, count));
+        it = g->plans.emplace(key, std::move(v)).first;
+    }
+    const std::vector<Plan>& P = it->second;
+    if (P[0].error) return P[0].error;
+    if (P[0].g.total == 0) return CHR_SUCCESS;
+    const size_t es = chr::dtype_size(dtype);
+    hipError_t e = hipSetDevice(g->device);
+    if (e != hipSuccess) return hip_code(e);
+    std::vector<Bufs> B(n);
+    for (int r = 0; r < n; ++r) {
+        if (!recvs[r]) return CHR_ERR_INVALID_ARG;
+        if ((e = g->acc[r].reserve(P[r].acc_elems * es, g->stream)) != hipSuccess) return hip_code(e);
+        if ((e = g->stage[r].reserve(P[r].stage_elems * es, g->stream)) != hipSuccess) return hip_code(e);
+        const void* in = sends[r] == CHR_IN_PLACE ? recvs[r] : sends[r];
+        if (!in || !is_device_ptr(in) || !is_device_ptr(recvs[r])) return CHR_ERR_INVALID_ARG;
+        B[r] = Bufs{(const char*)in, (char*)recvs[r], (char*)g->acc[r].p, (char*)g->stage[r].p, es};
+    }
+    int rc;
+    for (int r = 0; r < n; ++r)
+        for (const auto& op_ : P[r].pre)
+            if ((rc = run_local(op_, B[r], dtype, op, g->stream))) return rc;
+    const size_t nsteps = P[0].steps.size();
+    for (size_t si = 0; si < nsteps; ++si) {
+        // Loopback transport: each receive takes the next unmatched send of its peer to
+        // this rank in the same step (RCCL's per-pair ordering).
+        std::vector<std::vector<char>> used(n);
+        for (int r = 0; r < n; ++r) used[r].assign(P[r].steps[si].sends.size(), 0);
+        for (int r = 0; r < n; ++r) {
+            for (const chr::Xfer& rv : P[r].steps[si].recvs) {
+                const int q = rv.peer;
+                const auto& qs = P[q].steps[si].sends;
+                size_t j = 0;
+                while (j < qs.size() && (used[q][j] || qs[j].peer != r)) ++j;
+                if (j == qs.size() || qs[j].count != rv.count) {
+                    std::fprintf(stderr, "[chiara] plan mismatch: step %zu rank %d <- %d\n", si, r, q);
+                    return CHR_ERR_UNSUPPORTED;
+                }
+                used[q][j] = 1;
+                if ((e = hipMemcpyAsync(B[r].ptr(rv.ref), B[q].ptr(qs[j].ref), rv.count * es, hipMemcpyDeviceToDevice,
+                                        g->stream)) != hipSuccess)
+                    return hip_code(e);
+            }
+        }
+        for (int r = 0; r < n; ++r)
+            for (size_t j = 0; j < used[r].size(); ++j)
+                if (!used[r][j]) {
+                    std::fprintf(stderr, "[chiara] plan mismatch: unmatched send step %zu rank %d\n", si, r);
+                    return CHR_ERR_UNSUPPORTED;
+                }
+        for (int r = 0; r < n; ++r)
+            for (const auto& op_ : P[r].steps[si].post)
+                if ((rc = run_local(op_, B[r], dtype, op, g->stream))) return rc;
+    }
+    return hip_code(hipStreamSynchronize(g->stream));
+}
+
+}  // namespace
+
+extern "C" {
+
+int chr_get_unique_id(chr_unique_id* id) {
+    static_assert(sizeof(chr_unique_id) == sizeof(ncclUniqueId), "unique id size");
+    if (!id) return CHR_ERR_INVALID_ARG;
+    ncclUniqueId u;
+    int rc = nccl_code(ncclGetUniqueId(&u));
+    if (!rc) std::memcpy(id, &u, sizeof(u));
+    return rc;
+}
+
+int chr_comm_init_rank(chr_comm** out, int nranks, const chr_unique_id* id, int rank, int device) {
+    if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks) return CHR_ERR_INVALID_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return CHR_ERR_NO_DEVICE;
+    if (device < 0 || device >= ndev) return CHR_ERR_INVALID_ARG;
+    auto c = std::make_unique<chr_comm>();
+    c->rank = rank;
+    c->nranks = nranks;
+    c->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_code(e);
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    int rc = nccl_code(ncclCommInitRank(&c->nccl, nranks, u, rank));
+    if (rc) {
+        (void)hipStreamDestroy(c->stream);
+        return rc;
+    }
+    *out = c.release();
+    return CHR_SUCCESS;
+}
+
+int chr_comm_destroy(chr_comm* c) {
+    if (!c) return CHR_SUCCESS;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->nccl) (void)ncclCommDestroy(c->nccl);
+    c->acc.release();
+    c->stage.release();
+    c->hsend.release();
+    c->hrecv.release();
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return CHR_SUCCESS;
+}
+
+int chr_comm_rank(const chr_comm* c, int* rank) {
+    if (!c || !rank) return CHR_ERR_INVALID_ARG;
+    *rank = c->rank;
+    return CHR_SUCCESS;
+}
+
+int chr_comm_size(const chr_comm* c, int* n) {
+    if (!c || !n) return CHR_ERR_INVALID_ARG;
+    *n = c->nranks;
+    return CHR_SUCCESS;
+}
+
+int chr_comm_stream(const chr_comm* c, hipStream_t* s) {
+    if (!c || !s) return CHR_ERR_INVALID_ARG;
+    *s = c->stream;
+    return CHR_SUCCESS;
+}
+
+int chr_allreduce_radix_batch(const void* send, void* recv, size_t count, chr_dtype dtype, chr_op op, chr_comm* comm,
+                              int k, int b) {
+    return collective(comm, chr::MODE_ALLREDUCE, send, recv, count, dtype, op, k, b, true);
+}
+
+int chr_reduce_scatter_radix_batch(const void* send, void* recv, size_t recvcount, chr_dtype dtype, chr_op op,
+                                   chr_comm* comm, int k, int b) {
+    return collective(comm, chr::MODE_REDUCE_SCATTER, send, recv, recvcount, dtype, op, k, b, true);
+}
+
+int chr_allreduce_radix_batch_async(const void* send, void* recv, size_t count, chr_dtype dtype, chr_op op,
+                                    chr_comm* comm, int k, int b) {
+    return collective(comm, chr::MODE_ALLREDUCE, send, recv, count, dtype, op, k, b, false);
+}
+
+int chr_reduce_scatter_radix_batch_async(const void* send, void* recv, size_t recvcount, chr_dtype dtype, chr_op op,
+                                         chr_comm* comm, int k, int b) {
+    return collective(comm, chr::MODE_REDUCE_SCATTER, send, recv, recvcount, dtype, op, k, b, false);
+}
+
+int chr_local_group_create(chr_local_group** out, int nranks, int device) {
+    if (!out || nranks < 1) return CHR_ERR_INVALID_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return CHR_ERR_NO_DEVICE;
+    if (device < 0 || device >= ndev) return CHR_ERR_INVALID_ARG;
+    auto g = std::make_unique<chr_local_group>();
+    g->nranks = nranks;
+    g->device = device;
+    g->acc.resize(nranks);
+    g->stage.resize(nranks);
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_code(e);
+    *out = g.release();
+    return CHR_SUCCESS;
+}
+
+int chr_local_group_destroy(chr_local_group* g) {
+    if (!g) return CHR_SUCCESS;
+    (void)hipSetDevice(g->device);
+    if (g->stream) (void)hipStreamSynchronize(g->stream);
+    for (auto& d : g->acc) d.release();
+    for (auto& d : g->stage) d.release();
+    if (g->stream) (void)hipStreamDestroy(g->stream);
+    delete g;
+    return CHR_SUCCESS;
+}
+
+int chr_local_group_stream(const chr_local_group* g, hipStream_t* s) {
+    if (!g || !s) return CHR_ERR_INVALID_ARG;
+    *s = g->stream;
+    return CHR_SUCCESS;
+}
+
+int chr_local_allreduce_radix_batch(chr_local_group* g, const void* const* sends, void* const* recvs, size_t count,
+                                    chr_dtype dtype, chr_op op, int k, int b) {
+    return local_collective(g, chr::MODE_ALLREDUCE, sends, recvs, count, dtype, op, k, b);
+}
+
+int chr_local_reduce_scatter_radix_batch(chr_local_group* g, const void* const* sends, void* const* recvs,
+                                         size_t recvcount, chr_dtype dtype, chr_op op, int k, int b) {
+    return local_collective(g, chr::MODE_REDUCE_SCATTER, sends, recvs, recvcount, dtype, op, k, b);
+}
+
+}  // extern "C"

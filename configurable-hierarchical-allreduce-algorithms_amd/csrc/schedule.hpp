@@ -1,0 +1,92 @@
+// schedule.hpp -- host-side radix/batch schedule compiler (no device code).
+//
+// Re-states CHiArA's hierarchical reduce-scatter / allreduce schedule
+// (Fugaku_experiments/Allreduce/all_reduce_radix_batch.cpp:202-788,
+//  Fugaku_experiments/Reduce-scatter/reduce_scatter_radix_batch.cpp:200-653)
+// as a per-rank PLAN: a list of steps, each one RCCL group of sends/receives followed by
+// local device ops (fused bucket reductions, copies).  Steps are numbered globally, so
+// every message is posted by both of its endpoints in the same step and a rank can
+// enqueue its whole plan without ever blocking the host (deadlock-free by construction).
+//
+// HBM layout of the accumulator (ACC): block-major.  The reference keeps
+// tmp_results stage-major ([stage][lane block][IRC], :339-400), so each recexch phase
+// touches `nstages` (+1 truncated) separate slices.  Here chunk N = stage*b + lane sits
+// at position P[lane] + stage, i.e. [lane block][stage][IRC]: the region a phase
+// exchanges is ONE contiguous range covering every stage (and exactly the reference's
+// truncated leftover-stage region, :422-446), so each neighbour gets one message and
+// each phase is one fused kernel.  Element-wise reduction order is unchanged.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace chr {
+
+enum Buf : uint8_t { BUF_SEND = 0, BUF_RECV = 1, BUF_ACC = 2, BUF_STAGE = 3 };
+
+struct Ref {
+    uint8_t buf;
+    uint64_t off;  // elements
+};
+
+struct Xfer {
+    int peer;
+    Ref ref;
+    uint64_t count;  // elements
+};
+
+enum LocalKind : uint8_t { L_COPY = 0, L_REDUCE = 1 };
+
+// L_REDUCE: dst = (...((acc op ins[0]) op ins[1])...) op ins[m-1]   (dst may equal acc)
+// L_COPY:   dst = acc
+struct LocalOp {
+    LocalKind kind;
+    Ref dst;
+    Ref acc;
+    std::vector<Ref> ins;
+    uint64_t count;
+    int site;  // reference call site this op restates (line in all_reduce_radix_batch.cpp)
+};
+
+struct Step {
+    std::vector<Xfer> sends, recvs;
+    std::vector<LocalOp> post;
+    std::string label;
+};
+
+enum Mode : int { MODE_ALLREDUCE = 0, MODE_REDUCE_SCATTER = 1 };
+
+struct Geometry {
+    int nranks = 0, b = 0, k = 0, nnodes = 0, nstages = 0, nu = 0, nph = 0;
+    uint64_t recvcount = 0, irc = 0, total = 0;
+    std::vector<int> S, P;  // chunks per lane block, prefix (P.size() == b+1)
+};
+
+struct Plan {
+    int error = 0;  // chr_result
+    Mode mode = MODE_ALLREDUCE;
+    int rank = 0;
+    Geometry g;
+    uint64_t send_elems = 0, recv_elems = 0, acc_elems = 0, stage_elems = 0;
+    std::vector<LocalOp> pre;
+    std::vector<Step> steps;
+};
+
+// Recexch tables of one group of `nranks` (= b) ranks: all_reduce_radix_batch.cpp:11-198.
+struct Recexch {
+    int k = 0, p_of_k = 0, rem = 0, T = 0;
+    int step1_sendto = -1, step1_nrecvs = 0;
+    std::vector<int> step1_recvfrom;
+    int step2_nphases = 0;
+    std::vector<std::vector<int>> step2_nbrs;
+};
+int recexch_neighbors(int rank, int nranks, int k, Recexch* out);
+void recexch_count_offset(int nranks, int max_phases, int k, std::vector<int>* count,
+                          std::vector<int>* offset);
+
+// count = allreduce element count, or reduce-scatter recvcount.
+Plan build_plan(Mode mode, int nranks, int rank, int k, int b, uint64_t count);
+std::string describe(const Plan& p);
+
+}  // namespace chr

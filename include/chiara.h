@@ -1,0 +1,138 @@
+/*
+ * chiara.h -- C ABI of the MI355X-native CHiArA hot path (libchiara.so).
+ *
+ * Drop-in boundary for the per-step local bucket reduction of CHiArA's hierarchical
+ * radix/batch collectives (reference snapshot 2025-11-21, paths relative to the
+ * reference root).  Every entry point cites the reference interface it replaces.
+ * Plain pointers and sizes only; streams are HIP streams (hipStream_t).
+ *
+ * Status codes: 0 = CHR_SUCCESS (== MPI_SUCCESS), nonzero = chr_result below.  Unlike
+ * the reference (which returns MPI_SUCCESS unconditionally, all_reduce_radix_batch.cpp:206,
+ * :784), every precondition the reference leaves unchecked is rejected with a code.
+ */
+#ifndef CHIARA_H
+#define CHIARA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CHR_ABI_VERSION 1
+
+typedef enum {
+    CHR_FLOAT32 = 0,   /* MPI_FLOAT */
+    CHR_FLOAT64 = 1,   /* MPI_DOUBLE (testing/main.cpp harness) */
+    CHR_INT32 = 2,     /* MPI_INT (Fugaku_experiments harnesses); wraps on overflow */
+    CHR_BFLOAT16 = 3   /* no MPI equivalent: f32 arithmetic, RNE-rounded after every step */
+} chr_dtype;
+
+typedef enum { CHR_SUM = 0, CHR_PROD = 1, CHR_MAX = 2, CHR_MIN = 3 } chr_op;
+
+typedef enum {
+    CHR_SUCCESS = 0,
+    CHR_ERR_INVALID_ARG = 1,
+    CHR_ERR_COUNT_NOT_DIVISIBLE = 2, /* count % nranks != 0: reference silently leaves a
+                                        wrong tail (all_reduce_radix_batch.cpp:239) */
+    CHR_ERR_BATCH_NOT_DIVISOR = 3,   /* nranks % b != 0: reference aborts in MPI_Irecv */
+    CHR_ERR_HIP = 4,
+    CHR_ERR_RCCL = 5,
+    CHR_ERR_NO_DEVICE = 6,
+    CHR_ERR_OUT_OF_MEMORY = 7,
+    CHR_ERR_UNSUPPORTED = 8
+} chr_result;
+
+/* MPI_IN_PLACE analogue (all_reduce_radix_batch.cpp:234, :306-321): pass as `send`. */
+#define CHR_IN_PLACE ((const void*)(uintptr_t)1)
+
+/* ---- kernel boundary: replaces MPI_Reduce_local --------------------------------------
+ * Reference call sites (MPI_Reduce_local(in, inout, count, datatype, op)):
+ *   Fugaku_experiments/Allreduce/all_reduce_radix_batch.cpp:332, :364, :446, :529
+ *   Fugaku_experiments/Reduce-scatter/reduce_scatter_radix_batch.cpp:332, :366, :447, :552
+ * Semantics (MPICH 3.3.2 predefined ops): inout[i] = in[i] (op) inout[i].
+ * Device pointers; the kernel is enqueued on `stream` and the call returns at once. */
+int chr_reduce_local(const void* in, void* inout, size_t n, chr_dtype dtype, chr_op op,
+                     hipStream_t stream);
+
+/* Fused form of the k-1 (phase 1) or nnodes-1 (phase 2) consecutive Reduce_local calls
+ * that target one region: out = (...((acc (op) ins[0]) (op) ins[1]) ...) (op) ins[m-1],
+ * left to right, rounding after every step exactly as the sequential calls do
+ * (all_reduce_radix_batch.cpp:343-364, :523-530).  `out` may alias `acc`. m >= 0. */
+int chr_reduce_multi(void* out, const void* acc, const void* const* ins, int m, size_t n,
+                     chr_dtype dtype, chr_op op, hipStream_t stream);
+
+/* ---- communicator (replaces MPI_Comm + MPI p2p: RCCL over xGMI) -------------------- */
+typedef struct chr_comm chr_comm;
+typedef struct { char internal[128]; } chr_unique_id; /* == ncclUniqueId */
+
+int chr_get_unique_id(chr_unique_id* id);
+/* One rank per process (or thread), one MI355X per rank.  Collective across `nranks`. */
+int chr_comm_init_rank(chr_comm** comm, int nranks, const chr_unique_id* id, int rank, int device);
+int chr_comm_destroy(chr_comm* comm);
+int chr_comm_rank(const chr_comm* comm, int* rank);
+int chr_comm_size(const chr_comm* comm, int* nranks);
+/* The stream all of this communicator's collective work is enqueued on. */
+int chr_comm_stream(const chr_comm* comm, hipStream_t* stream);
+
+/* ---- schedule boundary ----------------------------------------------------------------
+ * Replaces  int all_reduce_radix_batch(char* sendbuf, char* recvbuf, int count,
+ *             MPI_Datatype, MPI_Op, MPI_Comm, int k, int b)
+ *           (Fugaku_experiments/Allreduce/all_reduce_radix_batch.cpp:202-204)
+ * and       int reduce_scatter_radix_batch(const void* sendbuf, void* recvbuf,
+ *             MPI_Aint recvcount, MPI_Datatype, MPI_Op, MPI_Comm, int k, int b)
+ *           (Fugaku_experiments/Reduce-scatter/reduce_scatter_radix_batch.cpp:200-202).
+ * Same arguments and results (bit-identical for the same (nranks, k, b)).
+ * send/recv may be device pointers (device-resident path) or host pointers (staged
+ * through HBM: the reference's host-memory-in / host-memory-out contract).  The call
+ * returns once the result is in `recv` (stream synchronised).  Scratch is owned by the
+ * communicator and reused across calls (the reference mallocs 2x the buffer per call). */
+int chr_allreduce_radix_batch(const void* send, void* recv, size_t count, chr_dtype dtype,
+                              chr_op op, chr_comm* comm, int k, int b);
+int chr_reduce_scatter_radix_batch(const void* send, void* recv, size_t recvcount,
+                                   chr_dtype dtype, chr_op op, chr_comm* comm, int k, int b);
+/* Asynchronous device-resident variants: enqueue on the comm stream and return. */
+int chr_allreduce_radix_batch_async(const void* send, void* recv, size_t count, chr_dtype dtype,
+                                    chr_op op, chr_comm* comm, int k, int b);
+int chr_reduce_scatter_radix_batch_async(const void* send, void* recv, size_t recvcount,
+                                         chr_dtype dtype, chr_op op, chr_comm* comm, int k, int b);
+
+/* ---- virtual ranks on one device (loopback transport) ---------------------------------
+ * `nranks` logical ranks sharing ONE device, messages become device-to-device copies;
+ * every reduction runs the same HIP kernels as the RCCL path.  One call performs the
+ * collective for all ranks: sends[r] / recvs[r] are rank r's device buffers. */
+typedef struct chr_local_group chr_local_group;
+int chr_local_group_create(chr_local_group** group, int nranks, int device);
+int chr_local_group_destroy(chr_local_group* group);
+int chr_local_group_stream(const chr_local_group* group, hipStream_t* stream);
+int chr_local_allreduce_radix_batch(chr_local_group* group, const void* const* sends,
+                                    void* const* recvs, size_t count, chr_dtype dtype, chr_op op,
+                                    int k, int b);
+int chr_local_reduce_scatter_radix_batch(chr_local_group* group, const void* const* sends,
+                                         void* const* recvs, size_t recvcount, chr_dtype dtype,
+                                         chr_op op, int k, int b);
+
+/* ---- schedule introspection (host only, no device needed) -----------------------------
+ * The radix/batch schedule is compiled once per (mode, nranks, rank, k, b, count) into a
+ * plan of steps; each step is one RCCL group of sends/receives followed by local ops.
+ * chr_plan_describe writes rank `rank`'s plan as text (one op per line) into buf
+ * (truncated to len, NUL-terminated); returns the length needed (excluding NUL) or < 0. */
+typedef enum { CHR_MODE_ALLREDUCE = 0, CHR_MODE_REDUCE_SCATTER = 1 } chr_mode;
+long chr_plan_describe(chr_mode mode, int nranks, int rank, int k, int b, size_t count,
+                       char* buf, size_t len);
+
+/* ---- utilities -------------------------------------------------------------------------- */
+/* Synthetic inputs on the device with the shared generator (oracle/chiara_oracle.h):
+ * pattern 0 = U[-1,1) (random 32-bit ints for INT32), 1 = rank*count_for_seq + i. */
+int chr_fill(void* buf, size_t n, chr_dtype dtype, int pattern, uint64_t seed, int rank,
+             uint64_t count_for_seq, hipStream_t stream);
+const char* chr_error_string(int code);
+int chr_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CHIARA_H */

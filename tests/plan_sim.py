@@ -1,0 +1,89 @@
+"""Test-side interpreter of libchiara plans (host only, no GPU).
+
+Executes every rank's compiled plan (chr_plan_describe) with numpy buffers: messages
+are matched exactly as the loopback/RCCL transports match them (same step, per-pair
+order), local reductions go through the oracle's MPI_Reduce_local restatement.  This
+checks the schedule compiler's data movement and reduction order on CPU.
+"""
+import numpy as np
+
+import chiara_amd as ca
+import pyoracle as po
+
+
+def load_plans(mode, n, k, b, count):
+    return [ca.parse_plan(ca.describe_plan(mode, n, r, k, b, count)) for r in range(n)]
+
+
+class RankState:
+    def __init__(self, plan, send, recv_init, dtype):
+        h = plan["header"]
+        npdt = po.NP_DTYPES[dtype]
+        self.buf = {
+            "SEND": send,
+            "RECV": recv_init if recv_init is not None else np.zeros(h["recv"], dtype=npdt),
+            "ACC": np.zeros(h["acc"], dtype=npdt),
+            "STAGE": np.zeros(max(h["stage"], 1), dtype=npdt),
+        }
+
+    def view(self, ref, n):
+        name, off = ref
+        return self.buf[name][off:off + n]
+
+
+def run_local(st, op, dtype, rop):
+    kind, dst, acc, n, ins = op
+    if n == 0:
+        return
+    if kind == "copy":
+        st.view(dst, n)[:] = st.view(acc, n).copy()
+        return
+    a = st.view(acc, n).copy()
+    po.reduce_multi(a, [st.view(r, n).copy() for r in ins], dtype, rop)
+    st.view(dst, n)[:] = a
+
+
+def execute(plans, sends, dtype, rop, inplace=False):
+    n = len(plans)
+    states = []
+    for r in range(n):
+        if inplace:
+            buf = sends[r].copy()
+            st = RankState(plans[r], buf, buf, dtype)
+        else:
+            st = RankState(plans[r], sends[r], None, dtype)
+        states.append(st)
+    for r in range(n):
+        for op in plans[r]["pre"]:
+            run_local(states[r], op, dtype, rop)
+    nsteps = len(plans[0]["steps"])
+    assert all(len(p["steps"]) == nsteps for p in plans)
+    for si in range(nsteps):
+        used = [[False] * len(plans[r]["steps"][si]["sends"]) for r in range(n)]
+        payload = []
+        for r in range(n):
+            for peer, ref, cnt in plans[r]["steps"][si]["recvs"]:
+                qs = plans[peer]["steps"][si]["sends"]
+                j = next(j for j, s in enumerate(qs) if not used[peer][j] and s[0] == r)
+                assert qs[j][2] == cnt, "send/recv size mismatch"
+                used[peer][j] = True
+                payload.append((r, ref, states[peer].view(qs[j][1], cnt).copy()))
+        assert all(all(u) for u in used), f"unmatched send in step {si}"
+        for r, ref, data in payload:
+            states[r].view(ref, data.size)[:] = data
+        for r in range(n):
+            for op in plans[r]["steps"][si]["post"]:
+                run_local(states[r], op, dtype, rop)
+    return [st.buf["RECV"] for st in states]
+
+
+def simulate(mode, sends, k, b, dtype, op, inplace=False):
+    n = len(sends)
+    count = sends[0].size if mode == ca.MODE_ALLREDUCE else sends[0].size // n
+    plans = load_plans(mode, n, k, b, count)
+    if plans[0]["header"]["error"]:
+        raise ValueError(f"plan error {plans[0]['header']['error']}")
+    outs = execute(plans, sends, dtype, op, inplace)
+    if mode == ca.MODE_REDUCE_SCATTER:
+        outs = [o[:count] for o in outs]
+    return outs

@@ -1,0 +1,50 @@
+"""The C-ABI library loads on a CPU-only host and exports every symbol include/chiara.h
+declares (no compute calls without a GPU)."""
+import os
+import re
+import subprocess
+
+import chiara_amd as ca
+from chiara_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    hdr = open(os.path.join(REPO, "include", "chiara.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    return sorted(set(re.findall(r"\b(chr_[a-z_]+)\s*\(", hdr)))
+
+
+def test_header_symbols_exported():
+    decl = _declared()
+    assert len(decl) >= 20
+    out = subprocess.check_output(["nm", "-D", "--defined-only", _lib.LIB_PATH]).decode()
+    exported = set(re.findall(r"\bT (chr_\w+)", out))
+    missing = [s for s in decl if s not in exported]
+    assert not missing, f"declared but not exported: {missing}"
+    assert sorted(_lib.EXPORTED) == decl
+
+
+def test_library_is_gfx950_code_object():
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob  # the embedded HIP fat binary targets gfx950
+
+
+def test_abi_basics():
+    assert ca.lib().chr_abi_version() == 1
+    assert ca.lib().chr_error_string(2).decode().startswith("count")
+    assert ca.lib().chr_error_string(0) == b"success"
+
+
+def test_no_cpu_fallback_for_compute():
+    """Without a device the compute entry points fail with an error code (no CPU path)."""
+    import torch
+
+    if torch.cuda.is_available():
+        return
+    g = ca.lib().chr_local_group_create
+    import ctypes
+
+    h = ctypes.c_void_p()
+    assert g(ctypes.byref(h), 2, 0) == 6  # CHR_ERR_NO_DEVICE

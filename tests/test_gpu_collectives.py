@@ -1,0 +1,163 @@
+"""Whole radix/batch collectives on the GPU vs the reference's golden vectors and the oracle.
+
+Multi-rank schedules run on ONE MI355X through the loopback transport (LocalGroup):
+the same compiled plans and the same HIP reduction kernels as the RCCL path, with
+messages as device copies.  The RCCL path itself is exercised at nranks=1 here (the
+box has one GPU) and at 2/4/8 GPUs by bench.py on the driver's 8-GPU node."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import chiara_amd as ca
+import pyoracle as po
+
+pytestmark = pytest.mark.gpu
+
+DT = {"f32": ca.FLOAT32, "f64": ca.FLOAT64, "i32": ca.INT32, "bf16": ca.BFLOAT16}
+OP = {"sum": ca.SUM, "prod": ca.PROD, "max": ca.MAX, "min": ca.MIN}
+
+
+@pytest.fixture(scope="module")
+def gu():
+    import gpu_util
+
+    return gpu_util
+
+
+@pytest.fixture(scope="module")
+def groups():
+    cache = {}
+
+    def get(n):
+        if n not in cache:
+            cache[n] = ca.LocalGroup(n, 0)
+        return cache[n]
+
+    yield get
+    for g in cache.values():
+        g.destroy()
+
+
+def run_local(gu, group, mode, sends, k, b, dtype, op, inplace=False):
+    n = len(sends)
+    npdt = po.NP_DTYPES[dtype]
+    es = np.dtype(npdt).itemsize
+    count = sends[0].size if mode == "ar" else sends[0].size // n
+    d_send = [gu.to_dev(s) for s in sends]
+    if inplace:
+        d_recv, d_sendp = d_send, [ca.IN_PLACE] * n
+    else:
+        d_recv = [gu.empty_dev((count if mode == "ar" else count) * es) for _ in range(n)]
+        d_sendp = d_send
+    fn = group.all_reduce_radix_batch if mode == "ar" else group.reduce_scatter_radix_batch
+    rc = fn(d_sendp, d_recv, count, DT[dtype], OP[op], k, b)
+    assert rc == 0, f"rc={rc}"
+    outc = count
+    return [gu.from_dev(d, npdt, outc) for d in d_recv]
+
+
+def test_local_group_matches_reference_golden(gu, groups, golden):
+    """Every golden case (1000+ geometries/dtypes/ops/in-place) bit-exact on the device."""
+    cases, _ = golden
+    bad = []
+    for c in cases:
+        n = c["n"]
+        in_n = c["count"] if c["mode"] == "ar" else c["count"] * n
+        sends = [po.fill(in_n, c["dtype"], c["pattern"], c["seed"], r) for r in range(n)]
+        outs = run_local(gu, groups(n), c["mode"], sends, c["k"], c["b"], c["dtype"], c["op"], bool(c["inplace"]))
+        h = hashlib.sha256(b"".join(o.tobytes() for o in outs)).hexdigest()
+        if h != c["sha256"]:
+            bad.append(c["id"])
+    assert not bad, f"{len(bad)} device/reference mismatches, e.g. {bad[:5]}"
+
+
+@pytest.mark.parametrize("mode,n,k,b,dtype", [
+    ("ar", 8, 4, 4, "f32"), ("ar", 8, 4, 4, "bf16"), ("ar", 8, 2, 2, "f32"), ("ar", 8, 3, 4, "bf16"),
+    ("ar", 8, 2, 4, "bf16"), ("ar", 8, 4, 8, "f32"), ("rs", 2, 2, 1, "f32"), ("rs", 2, 2, 2, "f32"),
+    ("ar", 2, 2, 1, "f32"), ("ar", 2, 2, 2, "f32"), ("ar", 16, 4, 4, "f32"), ("rs", 8, 4, 4, "bf16"),
+])
+def test_baseline_geometries_vs_oracle(gu, groups, mode, n, k, b, dtype):
+    """BASELINE configs' (n, k, b) at 4-16 MiB per rank: bit-exact vs the oracle."""
+    per_rank = (1 << 22) if dtype == "f32" else (1 << 23)
+    in_n = per_rank if mode == "ar" else per_rank // n * n
+    sends = [po.fill(in_n, dtype, 0, 0xC41A5EED, r) for r in range(n)]
+    got = run_local(gu, groups(n), mode, sends, k, b, dtype, "sum")
+    f = po.allreduce_radix_batch if mode == "ar" else po.reduce_scatter_radix_batch
+    ref = f(sends, k, b, dtype, "sum")
+    for r in range(n):
+        np.testing.assert_array_equal(got[r], ref[r])
+
+
+def test_c4_full_size_exact_int(gu, groups):
+    """C4 at full size (1 GiB per rank, 8 ranks, k=4, b=4) with the reference harness's
+    int32 pattern rank*count+i: every rank must hold sum_r (r*count + i) exactly."""
+    import torch
+
+    n, k, b, count = 8, 4, 4, 1 << 28
+    g = groups(n)
+    sends = [torch.empty(count, dtype=torch.int32, device=gu.DEV) for _ in range(n)]
+    for r, s in enumerate(sends):
+        assert ca.fill(s, count, ca.INT32, 1, 0, r, count, gu.stream()) == 0
+    recvs = [torch.empty(count, dtype=torch.int32, device=gu.DEV) for _ in range(n)]
+    gu.sync()
+    assert g.all_reduce_radix_batch(sends, recvs, count, ca.INT32, ca.SUM, k, b) == 0
+    i = torch.arange(count, dtype=torch.int64, device=gu.DEV)
+    expect = ((count * (n * (n - 1) // 2) + n * i) & 0xFFFFFFFF).to(torch.int64)
+    expect = torch.where(expect >= 2**31, expect - 2**32, expect).to(torch.int32)
+    for r in range(n):
+        assert torch.equal(recvs[r], expect), f"rank {r}"
+    del sends, recvs, i, expect
+    torch.cuda.empty_cache()
+
+
+def test_c5_full_size_bf16_properties(gu, groups):
+    """C5 geometry at full size (1 GiB bf16 per rank, 8 ranks, b=4, k=4): all ranks
+    bit-identical, and within (n-1) bf16 ulps of the fp32 sum of the inputs."""
+    import torch
+
+    n, k, b, count = 8, 4, 4, 1 << 29
+    g = groups(n)
+    sends = [torch.empty(count, dtype=torch.bfloat16, device=gu.DEV) for _ in range(n)]
+    for r, s in enumerate(sends):
+        assert ca.fill(s, count, ca.BFLOAT16, 0, 0xC41A5EED, r, count, gu.stream()) == 0
+    recvs = [torch.empty(count, dtype=torch.bfloat16, device=gu.DEV) for _ in range(n)]
+    gu.sync()
+    assert g.all_reduce_radix_batch(sends, recvs, count, ca.BFLOAT16, ca.SUM, k, b) == 0
+    for r in range(1, n):
+        assert torch.equal(recvs[r].view(torch.int16), recvs[0].view(torch.int16))
+    step = 1 << 24
+    for s0 in range(0, count, step):
+        exact = sum(x[s0:s0 + step].float() for x in sends)
+        bound = (n - 1) * 2.0 ** -8 * sum(x[s0:s0 + step].float().abs() for x in sends) + 1e-30
+        assert bool(((recvs[0][s0:s0 + step].float() - exact).abs() <= bound).all())
+    del sends, recvs
+    torch.cuda.empty_cache()
+
+
+def test_preconditions_rejected(gu, groups):
+    g = groups(8)
+    d = [gu.empty_dev(131 * 4) for _ in range(8)]
+    assert g.all_reduce_radix_batch(d, d, 131, ca.FLOAT32, ca.SUM, 2, 2) == 2
+    g6 = groups(6)
+    d6 = [gu.empty_dev(24 * 4) for _ in range(6)]
+    assert g6.all_reduce_radix_batch(d6, d6, 24, ca.FLOAT32, ca.SUM, 2, 4) == 3
+
+
+def test_rccl_comm_single_rank(gu):
+    """The RCCL transport end to end at nranks=1 (device and host buffers)."""
+    import torch
+
+    uid = ca.get_unique_id()
+    comm = ca.Comm(1, uid, 0, 0)
+    x = po.fill(4096, "f32", 0, 3, 0)
+    ds, dr = gu.to_dev(x), gu.empty_dev(x.nbytes)
+    assert ca.all_reduce_radix_batch(ds, dr, x.size, ca.FLOAT32, ca.SUM, comm, 2, 1) == 0
+    np.testing.assert_array_equal(gu.from_dev(dr, np.float32), x)
+    host_out = np.zeros_like(x)
+    assert ca.all_reduce_radix_batch(x, host_out, x.size, ca.FLOAT32, ca.SUM, comm, 2, 1) == 0
+    np.testing.assert_array_equal(host_out, x)
+    assert ca.reduce_scatter_radix_batch(ds, dr, x.size, ca.FLOAT32, ca.SUM, comm, 2, 1) == 0
+    np.testing.assert_array_equal(gu.from_dev(dr, np.float32), x)
+    comm.destroy()
+    torch.cuda.synchronize()

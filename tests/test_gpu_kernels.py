@@ -1,0 +1,130 @@
+"""HIP bucket-reduction kernels vs the oracle's MPI_Reduce_local restatement.
+
+Bar: bit-exact for every dtype (f32/f64 IEEE with the reference's association, int32
+wrapping, bf16 per-step RNE) -- the kernels restate the same per-element operations."""
+import numpy as np
+import pytest
+
+import chiara_amd as ca
+import pyoracle as po
+
+pytestmark = pytest.mark.gpu
+
+DT = {"f32": ca.FLOAT32, "f64": ca.FLOAT64, "i32": ca.INT32, "bf16": ca.BFLOAT16}
+OP = {"sum": ca.SUM, "prod": ca.PROD, "max": ca.MAX, "min": ca.MIN}
+
+
+@pytest.fixture(scope="module")
+def gu():
+    import gpu_util
+
+    return gpu_util
+
+
+def _bits(a):
+    return a.view({2: np.uint16, 4: np.uint32, 8: np.uint64}[a.itemsize])
+
+
+def _check_multi(gu, dtype, op, m, n, off=0, in_off=None, seed=5):
+    """out = acc op ins[0] ... op ins[m-1] on device, element offsets to test alignment."""
+    npdt = po.NP_DTYPES[dtype]
+    es = np.dtype(npdt).itemsize
+    in_off = off if in_off is None else in_off
+    acc = po.fill(n, dtype, 0, seed, 0)
+    ins = [po.fill(n, dtype, 0, seed, r + 1) for r in range(m)]
+    if op == "prod" and dtype == "i32":
+        ins = [(x % 7).astype(np.int32) for x in ins]
+    d_acc = gu.empty_dev((n + off) * es)
+    d_acc[off * es:(off + n) * es] = gu.to_dev(acc)
+    d_ins = []
+    for x in ins:
+        t = gu.empty_dev((n + in_off) * es)
+        t[in_off * es:(in_off + n) * es] = gu.to_dev(x)
+        d_ins.append(t)
+    rc = ca.reduce_multi(d_acc.data_ptr() + off * es, d_acc.data_ptr() + off * es,
+                         [t.data_ptr() + in_off * es for t in d_ins], n, DT[dtype], OP[op], gu.stream())
+    assert rc == 0
+    gu.sync()
+    got = gu.from_dev(d_acc, npdt)[off:off + n]
+    ref = po.reduce_multi(acc.copy(), ins, dtype, op)
+    np.testing.assert_array_equal(_bits(got), _bits(ref))
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64", "i32", "bf16"])
+@pytest.mark.parametrize("op", ["sum", "prod", "max", "min"])
+@pytest.mark.parametrize("m", [1, 3, 7])
+def test_reduce_multi_all_dtypes_ops(gu, dtype, op, m):
+    _check_multi(gu, dtype, op, m, 100003)
+
+
+@pytest.mark.parametrize("m", [1, 2, 4, 5, 6, 8, 9, 16, 17])
+def test_fan_in_and_chaining(gu, m):
+    _check_multi(gu, "f32", "sum", m, 65536 + 13)
+    _check_multi(gu, "bf16", "sum", m, 4099)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 7, 8, 9, 255, 256, 1023, 1024, 1025, 4096 * 4 + 3])
+def test_edge_sizes(gu, n):
+    for dt in ("f32", "bf16", "f64"):
+        _check_multi(gu, dt, "sum", 3, n)
+
+
+@pytest.mark.parametrize("off,in_off", [(1, 1), (3, 3), (2, 2), (1, 2), (0, 3), (5, 0)])
+def test_misaligned_buffers(gu, off, in_off):
+    for dt in ("f32", "bf16", "i32"):
+        _check_multi(gu, dt, "sum", 2, 10007, off, in_off)
+
+
+def test_reduce_local_mpi_semantics(gu):
+    """MPI_Reduce_local: inout = in op inout; MAX keeps inout unless in > inout (NaN, -0)."""
+    a = np.array([1.0, -0.0, np.nan, 3.0, 0.0, -np.inf], dtype=np.float32)
+    b = np.array([2.0, 0.0, 1.0, np.nan, -0.0, np.inf], dtype=np.float32)
+    for op in ("max", "min", "sum", "prod"):
+        da, db = gu.to_dev(a), gu.to_dev(b)
+        assert ca.reduce_local(da, db, a.size, ca.FLOAT32, OP[op], gu.stream()) == 0
+        gu.sync()
+        ref = po.reduce_local(a, b.copy(), "f32", op)
+        np.testing.assert_array_equal(_bits(gu.from_dev(db, np.float32)), _bits(ref))
+    # bf16 NaN payloads and RNE ties
+    x = np.array([0x7FC1, 0x3F80, 0x3F81, 0xFF80, 0x0001], dtype=np.uint16)
+    y = np.array([0x3F80, 0x3B80, 0x3B80, 0x7F80, 0x8001], dtype=np.uint16)
+    dx, dy = gu.to_dev(x), gu.to_dev(y)
+    assert ca.reduce_local(dx, dy, x.size, ca.BFLOAT16, ca.SUM, gu.stream()) == 0
+    gu.sync()
+    np.testing.assert_array_equal(gu.from_dev(dy, np.uint16), po.reduce_local(x, y.copy(), "bf16", "sum"))
+
+
+def test_int32_wraps(gu):
+    a = np.array([2**31 - 1, -(2**31), 123], dtype=np.int32)
+    b = np.array([1, -1, -123], dtype=np.int32)
+    da, db = gu.to_dev(a), gu.to_dev(b)
+    assert ca.reduce_local(da, db, 3, ca.INT32, ca.SUM, gu.stream()) == 0
+    gu.sync()
+    assert list(gu.from_dev(db, np.int32)) == [-(2**31), 2**31 - 1, 0]
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64", "i32", "bf16"])
+@pytest.mark.parametrize("pattern", [0, 1])
+def test_device_fill_matches_oracle_generator(gu, dtype, pattern):
+    n = 300001
+    npdt = po.NP_DTYPES[dtype]
+    d = gu.empty_dev(n * np.dtype(npdt).itemsize)
+    assert ca.fill(d, n, DT[dtype], pattern, 0xC41A5EED, 5, stream=gu.stream()) == 0
+    gu.sync()
+    np.testing.assert_array_equal(_bits(gu.from_dev(d, npdt)), _bits(po.fill(n, dtype, pattern, 0xC41A5EED, 5)))
+
+
+@pytest.mark.parametrize("nbytes", [1 << 10, 1 << 20, 64 << 20, 1 << 30])
+def test_bucket_sizes_1k_to_1g(gu, nbytes):
+    """BASELINE sweep range (1 KiB .. 1 GiB per bucket), k=2 (m=1) and k=4 (m=3): bit-exact."""
+    n = nbytes // 4
+    _check_multi(gu, "f32", "sum", 1, n, seed=11)
+    if nbytes <= 64 << 20:
+        _check_multi(gu, "f32", "sum", 3, n, seed=12)
+
+
+def test_invalid_args(gu):
+    assert ca.reduce_local(0, 0, 0, ca.FLOAT32, ca.SUM) == 0  # n == 0 is a no-op
+    assert ca.reduce_local(0, 0, 5, ca.FLOAT32, ca.SUM) == 1
+    assert ca.reduce_local(1, 1, 5, 9, ca.SUM) == 1
+    assert ca.reduce_local(1, 1, 5, ca.FLOAT32, 9) == 1
