@@ -23,6 +23,13 @@ class UniqueId(ctypes.Structure):
 
 
 def _load():
+    # One HIP runtime per process: torch bundles its own libamdhip64.so.7 / librccl.so.1.
+    # Loading torch first makes libchiara's NEEDED entries resolve (by SONAME) to those
+    # copies instead of a second runtime from /opt/rocm competing for the device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"libchiara.so not found at {LIB_PATH}; build it with "

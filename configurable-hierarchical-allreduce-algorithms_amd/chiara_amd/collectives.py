@@ -89,15 +89,16 @@ def fill(buf, count, datatype, pattern, seed, rank, count_for_seq=None, stream=N
 def get_unique_id():
     uid = UniqueId()
     check(lib().chr_get_unique_id(ctypes.byref(uid)), "chr_get_unique_id")
-    return bytes(uid.internal)
+    return ctypes.string_at(ctypes.addressof(uid), ctypes.sizeof(uid))  # all 128 bytes (NULs included)
 
 
 class Comm:
     """RCCL-backed communicator (one rank per process, one MI355X per rank)."""
 
     def __init__(self, nranks, unique_id, rank, device):
-        uid = UniqueId()
-        ctypes.memmove(ctypes.byref(uid), unique_id, 128)
+        if len(unique_id) != ctypes.sizeof(UniqueId):
+            raise ValueError("unique_id must be the 128 bytes returned by get_unique_id()")
+        uid = UniqueId.from_buffer_copy(unique_id)
         h = ctypes.c_void_p()
         check(lib().chr_comm_init_rank(ctypes.byref(h), nranks, ctypes.byref(uid), rank, device),
               "chr_comm_init_rank")

@@ -22,11 +22,13 @@ hipError_t launch_fill(void* buf, size_t n, int dtype, int pattern, uint64_t see
                        uint64_t count_for_seq, hipStream_t stream);
 
 // Tunables (read once from the environment):
-//   CHR_REDUCE_MAX_BLOCKS  cap on the grid (default 2048 = 8 per CU)
-//   CHR_REDUCE_NT          1: non-temporal stores of the result
+//   CHR_REDUCE_MAX_BLOCKS    cap on the grid (default 0 = one trip per workgroup)
+//   CHR_REDUCE_NT            0 / 1 forces plain / non-temporal loads+stores; unset = by size
+//   CHR_REDUCE_NT_MIN_BYTES  bytes streamed by one call from which NT is used (128 MiB)
 struct ReduceTuning {
     int max_blocks;
-    int nt_store;
+    int nt_mode;
+    size_t nt_min_bytes;
 };
 ReduceTuning& reduce_tuning();
 

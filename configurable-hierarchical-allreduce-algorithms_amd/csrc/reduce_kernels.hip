@@ -12,8 +12,10 @@
 // and the accumulator, write the result), ~0.1-0.5 FLOP/byte: no MFMA.  Design:
 //  * one 16-byte global_load_dwordx4 per lane per operand (1 KiB per wave-instruction),
 //    U independent vectors per lane in flight (ILP) with every operand's loads issued
-//    before the first add, grid-stride over the buffer, 256-thread workgroups,
-//    grid capped at 8 workgroups per CU (2048) so every CU keeps ~32-64 KiB in flight;
+//    before the first add, 256-thread workgroups, one trip per workgroup (the full grid
+//    measured faster than a capped grid-stride grid on large buckets);
+//  * non-temporal loads and stores for calls that stream >= 128 MiB (HBM-cold buckets
+//    +15-40 % over plain accesses; plain stays faster on small, cache-warm calls);
 //  * no LDS: a pure stream has no reuse, and staging through LDS (global_load_lds) was
 //    measured null-to-negative for this regime (profiles/);
 //  * no XCD remap: no inter-workgroup reuse, so L2 placement cannot matter;
@@ -48,10 +50,11 @@ ReduceTuning& reduce_tuning() {
     static ReduceTuning t = [] {
         ReduceTuning r;
         const char* s = std::getenv("CHR_REDUCE_MAX_BLOCKS");
-        r.max_blocks = s ? std::atoi(s) : 2048;
-        if (r.max_blocks < 1) r.max_blocks = 2048;
-        s = std::getenv("CHR_REDUCE_NT");
-        r.nt_store = s ? std::atoi(s) : 0;
+        r.max_blocks = s ? std::atoi(s) : 0;  // 0: one trip per workgroup (full grid)
+        s = std::getenv("CHR_REDUCE_NT");     // 0 / 1 / unset = by size
+        r.nt_mode = s ? std::atoi(s) : -1;
+        s = std::getenv("CHR_REDUCE_NT_MIN_BYTES");
+        r.nt_min_bytes = s ? (size_t)std::atoll(s) : (size_t)128 << 20;
         return r;
     }();
     return t;
@@ -114,23 +117,35 @@ struct VecArgs {
     const u32x4* acc;
     const u32x4* ins[kMaxFanIn];
     size_t nvec;
-    int nt_store;
 };
 
+template <bool NT>
+__device__ __forceinline__ u32x4 ld(const u32x4* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st(u32x4* p, u32x4 v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 // U vectors (16 B each) per lane per trip; all M+1 operands of the trip are loaded
-// before the first add so (M+1)*U*16 bytes per lane are in flight.
-template <int DT, int OP, int M, int U>
+// before the first add so (M+1)*U*16 bytes per lane are in flight.  NT: non-temporal
+// loads and stores (global_load/store_dwordx4 ... nt) for calls that stream far more
+// than the caches hold: measured +15-40 % on HBM-cold buckets.
+template <int DT, int OP, int M, int U, bool NT>
 __global__ __launch_bounds__(kBlock) void k_reduce_vec(VecArgs a) {
     const size_t stride = (size_t)gridDim.x * kBlock * U;
     for (size_t base = (size_t)blockIdx.x * kBlock * U + threadIdx.x; base < a.nvec; base += stride) {
         if (base + (size_t)(U - 1) * kBlock < a.nvec) {
             u32x4 acc[U], x[M][U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) acc[u] = a.acc[base + (size_t)u * kBlock];
+            for (int u = 0; u < U; ++u) acc[u] = ld<NT>(&a.acc[base + (size_t)u * kBlock]);
 #pragma unroll
             for (int j = 0; j < M; ++j)
 #pragma unroll
-                for (int u = 0; u < U; ++u) x[j][u] = a.ins[j][base + (size_t)u * kBlock];
+                for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&a.ins[j][base + (size_t)u * kBlock]);
             // Keep every load of the trip ahead of the first add: without this the
             // scheduler interleaves the first add (and its vmcnt(0)) between the loads.
             __builtin_amdgcn_sched_barrier(0);
@@ -138,13 +153,8 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(VecArgs a) {
             for (int j = 0; j < M; ++j)
 #pragma unroll
                 for (int u = 0; u < U; ++u) acc[u] = apply_vec<DT, OP>(x[j][u], acc[u]);
-            if (a.nt_store) {
 #pragma unroll
-                for (int u = 0; u < U; ++u) __builtin_nontemporal_store(acc[u], &a.out[base + (size_t)u * kBlock]);
-            } else {
-#pragma unroll
-                for (int u = 0; u < U; ++u) a.out[base + (size_t)u * kBlock] = acc[u];
-            }
+            for (int u = 0; u < U; ++u) st<NT>(&a.out[base + (size_t)u * kBlock], acc[u]);
         } else {
             for (int u = 0; u < U; ++u) {
                 const size_t i = base + (size_t)u * kBlock;
@@ -184,9 +194,16 @@ __global__ __launch_bounds__(kBlock) void k_reduce_scalar(ScalarArgs a) {
 template <int DT, int OP, int M>
 static hipError_t launch_vec_m(const VecArgs& a, hipStream_t s) {
     constexpr int U = M <= 2 ? 4 : 2;
+    const ReduceTuning& t = reduce_tuning();
     const size_t trips = (a.nvec + (size_t)kBlock * U - 1) / ((size_t)kBlock * U);
-    const int grid = (int)(trips < (size_t)reduce_tuning().max_blocks ? trips : (size_t)reduce_tuning().max_blocks);
-    hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U>), dim3(grid), dim3(kBlock), 0, s, a);
+    const size_t cap = t.max_blocks > 0 ? (size_t)t.max_blocks : trips;
+    const int grid = (int)(trips < cap ? trips : cap);
+    const size_t call_bytes = (size_t)(M + 2) * a.nvec * 16;
+    const bool nt = t.nt_mode == 1 || (t.nt_mode < 0 && call_bytes >= t.nt_min_bytes);
+    if (nt)
+        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true>), dim3(grid), dim3(kBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, false>), dim3(grid), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
 
@@ -269,7 +286,6 @@ static hipError_t launch_group(void* out, const void* acc, const void* const* in
         a.acc = (const u32x4*)((const char*)acc + head * es);
         for (int j = 0; j < m; ++j) a.ins[j] = (const u32x4*)((const char*)ins[j] + head * es);
         a.nvec = nvec;
-        a.nt_store = reduce_tuning().nt_store;
         switch (dtype) {
         case CHR_FLOAT32: err = launch_vec_dt<CHR_FLOAT32>(a, m, op, s); break;
         case CHR_FLOAT64: err = launch_vec_dt<CHR_FLOAT64>(a, m, op, s); break;

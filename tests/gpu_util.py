@@ -15,7 +15,9 @@ def empty_dev(nbytes):
 
 
 def from_dev(t, npdt, n=None):
-    a = t.cpu().numpy().view(npdt)
+    raw = t.cpu().numpy()
+    isz = np.dtype(npdt).itemsize
+    a = raw[: raw.size - raw.size % isz].view(npdt)
     return a if n is None else a[:n]
 
 

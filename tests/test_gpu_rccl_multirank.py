@@ -1,0 +1,96 @@
+"""The RCCL transport with several ranks on the single-GPU test box.
+
+RCCL refuses two ranks on one device on the same host ("Duplicate GPU detected"), so
+each rank process gets its own NCCL_HOSTID: RCCL then treats the ranks as separate hosts
+and moves messages over its socket transport (loopback).  Same executor, same plans,
+same kernels as the xGMI path on the 8-GPU node; only the wire differs.  Results must
+be bit-exact vs the oracle."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, cases, q):
+    os.environ["NCCL_HOSTID"] = f"chiara-test-host-{rank}"
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    os.environ.setdefault("NCCL_IB_DISABLE", "1")
+    sys.path[:0] = [HERE, os.path.join(REPO, "oracle"),
+                    os.path.join(REPO, "configurable-hierarchical-allreduce-algorithms_amd")]
+    import torch
+    import torch.distributed as dist
+
+    import chiara_amd as ca
+    import pyoracle as po
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    comm = ca.Comm.from_torch_distributed(device=0)
+    dev = torch.device("cuda:0")
+    try:
+        for (mode, k, b, count, dtype, host) in cases:
+            npdt = po.NP_DTYPES[dtype]
+            cdt = {"f32": ca.FLOAT32, "bf16": ca.BFLOAT16, "i32": ca.INT32}[dtype]
+            in_n = count if mode == "ar" else count * world
+            x = po.fill(in_n, dtype, 0, 4242, rank)
+            if host:
+                send, out = x, np.zeros(count, dtype=npdt)
+            else:
+                send = torch.from_numpy(x.view(np.uint8).copy()).to(dev)
+                out_t = torch.zeros(count * x.itemsize, dtype=torch.uint8, device=dev)
+            fn = ca.all_reduce_radix_batch if mode == "ar" else ca.reduce_scatter_radix_batch
+            rc = fn(send, out if host else out_t, count, cdt, ca.SUM, comm, k, b)
+            if not host:
+                out = out_t.cpu().numpy().view(npdt)
+            allx = [po.fill(in_n, dtype, 0, 4242, r) for r in range(world)]
+            f = po.allreduce_radix_batch if mode == "ar" else po.reduce_scatter_radix_batch
+            ref = f(allx, k, b, dtype, "sum")[rank]
+            q.put((rank, mode, k, b, rc, bool(np.array_equal(out.view(np.uint8), ref.view(np.uint8)))))
+    finally:
+        comm.destroy()
+        dist.destroy_process_group()
+
+
+def _run(world, cases, timeout=300):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout)
+    alive = [p for p in procs if p.is_alive()]
+    for p in alive:
+        p.kill()
+    assert not alive, "RCCL multi-rank test hung"
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = [q.get() for _ in range(world * len(cases))]
+    bad = [r for r in res if r[4] != 0 or not r[5]]
+    assert not bad, bad
+
+
+def test_rccl_world2_reduce_scatter_and_allreduce():
+    _run(2, [("rs", 2, 1, 1 << 16, "f32", False), ("rs", 2, 2, 1 << 16, "f32", False),
+             ("ar", 2, 2, 1 << 16, "f32", False), ("ar", 2, 1, 2 * 1001, "bf16", False),
+             ("ar", 2, 2, 1 << 14, "f32", True)])
+
+
+def test_rccl_world8_c4_c5_geometries():
+    _run(8, [("ar", 4, 4, 8 * 4096, "f32", False), ("ar", 4, 4, 8 * 4096, "bf16", False),
+             ("ar", 2, 2, 8 * 4096, "f32", False), ("ar", 3, 4, 8 * 2048, "bf16", False),
+             ("ar", 4, 8, 8 * 1024, "f32", False), ("rs", 4, 4, 1000, "f32", False)], timeout=600)

@@ -1,0 +1,397 @@
+// reduce_microbench.hip -- design-space sweep for the fused bucket reduction on gfx950.
+// Not part of the product: each variant here is a candidate for csrc/reduce_kernels.hip.
+//   hipcc -O3 --offload-arch=gfx950 -o reduce_microbench reduce_microbench.hip
+//   ./reduce_microbench [bucket_MiB ...]
+// Output: one line per (variant, m, bucket): us per launch and algorithmic GB/s
+// ((m+2) x bucket bytes per launch), buffers rotated so the working set exceeds the
+// 256 MiB Infinity Cache.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#define CK(x)                                                                          \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) {                                                        \
+            std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            std::exit(1);                                                              \
+        }                                                                              \
+    } while (0)
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct Args {
+    f32x4* out;
+    const f32x4* acc;
+    const f32x4* ins[8];
+    size_t nvec;
+};
+
+template <int M, int U, int BLOCK, bool NTL, bool NTS, bool NTA = NTL>
+__global__ __launch_bounds__(BLOCK) void k_reg(Args a) {
+    const size_t stride = (size_t)gridDim.x * BLOCK * U;
+    for (size_t base = (size_t)blockIdx.x * BLOCK * U + threadIdx.x; base < a.nvec; base += stride) {
+        if (base + (size_t)(U - 1) * BLOCK < a.nvec) {
+            f32x4 acc[U], x[M][U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                acc[u] = NTA ? __builtin_nontemporal_load(&a.acc[base + (size_t)u * BLOCK]) : a.acc[base + (size_t)u * BLOCK];
+#pragma unroll
+            for (int j = 0; j < M; ++j)
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    x[j][u] = NTL ? __builtin_nontemporal_load(&a.ins[j][base + (size_t)u * BLOCK])
+                                  : a.ins[j][base + (size_t)u * BLOCK];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < M; ++j)
+#pragma unroll
+                for (int u = 0; u < U; ++u) acc[u] = x[j][u] + acc[u];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (NTS)
+                    __builtin_nontemporal_store(acc[u], &a.out[base + (size_t)u * BLOCK]);
+                else
+                    a.out[base + (size_t)u * BLOCK] = acc[u];
+            }
+        } else {
+            for (int u = 0; u < U; ++u) {
+                const size_t i = base + (size_t)u * BLOCK;
+                if (i >= a.nvec) break;
+                f32x4 v = a.acc[i];
+                for (int j = 0; j < M; ++j) v = a.ins[j][i] + v;
+                a.out[i] = v;
+            }
+        }
+    }
+}
+
+// Contiguous-chunk-per-block form: block b owns [b*CH, (b+1)*CH) vectors.
+template <int M, int U, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_chunk(Args a, size_t chunk) {
+    const size_t lo = (size_t)blockIdx.x * chunk;
+    size_t hi = lo + chunk;
+    if (hi > a.nvec) hi = a.nvec;
+    for (size_t base = lo + threadIdx.x; base < hi; base += (size_t)BLOCK * U) {
+        if (base + (size_t)(U - 1) * BLOCK < hi) {
+            f32x4 acc[U], x[M][U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc[u] = a.acc[base + (size_t)u * BLOCK];
+#pragma unroll
+            for (int j = 0; j < M; ++j)
+#pragma unroll
+                for (int u = 0; u < U; ++u) x[j][u] = a.ins[j][base + (size_t)u * BLOCK];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < M; ++j)
+#pragma unroll
+                for (int u = 0; u < U; ++u) acc[u] = x[j][u] + acc[u];
+#pragma unroll
+            for (int u = 0; u < U; ++u) a.out[base + (size_t)u * BLOCK] = acc[u];
+        } else {
+            for (int u = 0; u < U; ++u) {
+                const size_t i = base + (size_t)u * BLOCK;
+                if (i >= hi) break;
+                f32x4 v = a.acc[i];
+                for (int j = 0; j < M; ++j) v = a.ins[j][i] + v;
+                a.out[i] = v;
+            }
+        }
+    }
+}
+
+// LDS-DMA staging: every operand tile goes global -> LDS by global_load_lds_dwordx4
+// (1 KiB per wave-instruction), double-buffered, then ds_read_b128 -> add -> store.
+// Each lane reads back exactly the 16 B its own DMA wrote, so only the wave's own
+// vmcnt orders the read (no workgroup barrier).
+template <int M, int U>
+__global__ __launch_bounds__(256) void k_lds(Args a) {
+    constexpr int OPS = M + 1;
+    constexpr int TILE = U * 64;                       // vectors per wave per operand
+    __shared__ __attribute__((aligned(16))) f32x4 lds[2][4][OPS][TILE];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const size_t per_block = (size_t)256 * U;
+    const size_t ntiles = a.nvec / per_block;           // full tiles only (tail below)
+    auto issue = [&](size_t t, int buf) {
+        const size_t base = t * per_block + (size_t)wave * TILE;
+#pragma unroll
+        for (int o = 0; o < OPS; ++o) {
+            const f32x4* src = o == 0 ? a.acc : a.ins[o - 1];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(src + base + u * 64 + lane),
+                    (__attribute__((address_space(3))) void*)&lds[buf][wave][o][u * 64], 16, 0, 0);
+            }
+        }
+    };
+    size_t t = blockIdx.x;
+    int buf = 0;
+    if (t < ntiles) issue(t, 0);
+    for (; t < ntiles; t += gridDim.x) {
+        const size_t tn = t + gridDim.x;
+        if (tn < ntiles) {
+            issue(tn, buf ^ 1);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS * U) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const size_t base = t * per_block + (size_t)wave * TILE;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            f32x4 v = lds[buf][wave][0][u * 64 + lane];
+#pragma unroll
+            for (int j = 1; j < OPS; ++j) v = lds[buf][wave][j][u * 64 + lane] + v;
+            a.out[base + u * 64 + lane] = v;
+        }
+        buf ^= 1;
+    }
+    if (blockIdx.x == 0) {  // tail vectors
+        for (size_t i = ntiles * per_block + threadIdx.x; i < a.nvec; i += 256) {
+            f32x4 v = a.acc[i];
+            for (int j = 0; j < M; ++j) v = a.ins[j][i] + v;
+            a.out[i] = v;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_copy(f32x4* out, const f32x4* in, size_t nvec) {
+    for (size_t i = (size_t)blockIdx.x * 1024 + threadIdx.x; i < nvec; i += (size_t)gridDim.x * 1024) {
+        f32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (i + u * 256 < nvec) v[u] = in[i + u * 256];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (i + u * 256 < nvec) out[i + u * 256] = v[u];
+    }
+}
+
+struct Sets {
+    std::vector<std::vector<f32x4*>> bufs;  // [set][operand]
+};
+
+static Sets make_sets(int m, size_t nvec, int sets) {
+    Sets s;
+    s.bufs.resize(sets);
+    for (int i = 0; i < sets; ++i)
+        for (int j = 0; j < m + 1; ++j) {
+            f32x4* p;
+            CK(hipMalloc(&p, nvec * 16));
+            CK(hipMemset(p, 0, nvec * 16));
+            s.bufs[i].push_back(p);
+        }
+    return s;
+}
+static void free_sets(Sets& s) {
+    for (auto& v : s.bufs)
+        for (auto* p : v) CK(hipFree(p));
+}
+
+template <typename L>
+static double time_launches(L launch, int reps) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int i = 0; i < 5; ++i) launch(i);
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < reps; ++i) launch(i);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+    return ms * 1e3 / reps;  // us
+}
+
+static void report(const char* name, int m, size_t bytes, double us) {
+    const double gbps = (m + 2) * (double)bytes / (us * 1e-6) / 1e9;
+    std::printf("%-34s m=%d bucket=%6zu MiB  %9.2f us  %8.1f GB/s  %.3f of 8 TB/s\n", name, m, bytes >> 20, us, gbps,
+                gbps / 8000.0);
+    std::fflush(stdout);
+}
+
+template <int M>
+static void run_m(size_t bytes) {
+    const size_t nvec = bytes / 16;
+    const int sets = std::max(1, std::min(8, (int)((1024ull << 20) / ((M + 2) * bytes))));
+    Sets S = make_sets(M, nvec, sets);
+    const int reps = std::max(10, std::min(300, (int)((8ull << 30) / ((M + 2) * bytes))));
+    auto args_for = [&](int i) {
+        Args a{};
+        auto& b = S.bufs[i % sets];
+        a.out = b[0];
+        a.acc = b[0];
+        for (int j = 0; j < M; ++j) a.ins[j] = b[j + 1];
+        a.nvec = nvec;
+        return a;
+    };
+#define REG(U, BL, GRIDCAP, NTL, NTS, NAME)                                                              \
+    {                                                                                                  \
+        const size_t trips = (nvec + (size_t)BL * U - 1) / ((size_t)BL * U);                          \
+        const int grid = (int)std::min<size_t>(trips, GRIDCAP);                                        \
+        double us = time_launches([&](int i) { hipLaunchKernelGGL((k_reg<M, U, BL, NTL, NTS>), dim3(grid), dim3(BL), 0, 0, args_for(i)); }, reps); \
+        report(NAME, M, bytes, us);                                                                    \
+    }
+    REG(4, 256, 2048, false, false, "reg U4 B256 cap2048 (product)");
+    REG(4, 256, 1 << 30, false, false, "reg U4 B256 full-grid");
+    REG(4, 256, 1024, false, false, "reg U4 B256 cap1024");
+    REG(4, 256, 4096, false, false, "reg U4 B256 cap4096");
+    REG(2, 256, 1 << 30, false, false, "reg U2 B256 full-grid");
+    REG(8, 256, 1 << 30, false, false, "reg U8 B256 full-grid");
+    REG(8, 256, 2048, false, false, "reg U8 B256 cap2048");
+    REG(1, 256, 1 << 30, false, false, "reg U1 B256 full-grid");
+    REG(4, 512, 1 << 30, false, false, "reg U4 B512 full-grid");
+    REG(2, 1024, 1 << 30, false, false, "reg U2 B1024 full-grid");
+    REG(4, 256, 1 << 30, true, false, "reg U4 full-grid NT-load");
+    REG(4, 256, 1 << 30, false, true, "reg U4 full-grid NT-store");
+    REG(4, 256, 1 << 30, true, true, "reg U4 full-grid NT-load+store");
+    REG(4, 256, 2048, true, true, "reg U4 cap2048 NT-load+store");
+#undef REG
+    for (size_t blocks : {256ul, 512ul, 1024ul, 2048ul}) {
+        const size_t chunk = (nvec + blocks - 1) / blocks;
+        double us = time_launches([&](int i) { hipLaunchKernelGGL((k_chunk<M, 4, 256>), dim3(blocks), dim3(256), 0, 0, args_for(i), chunk); }, reps);
+        char name[64];
+        std::snprintf(name, sizeof name, "chunk U4 B256 blocks=%zu", blocks);
+        report(name, M, bytes, us);
+    }
+    if (M <= 3) {
+        for (int cap : {512, 1024, 2048}) {
+            const size_t trips = nvec / (256 * 2);
+            const int grid = (int)std::min<size_t>(std::max<size_t>(trips, 1), cap);
+            double us = time_launches([&](int i) { hipLaunchKernelGGL((k_lds<M, 2>), dim3(grid), dim3(256), 0, 0, args_for(i)); }, reps);
+            char name[64];
+            std::snprintf(name, sizeof name, "LDS-DMA U2 dbuf cap%d", cap);
+            report(name, M, bytes, us);
+        }
+    }
+    if (M == 1) {
+        double us = time_launches([&](int i) {
+            auto& b = S.bufs[i % sets];
+            hipLaunchKernelGGL(k_copy, dim3(2048), dim3(256), 0, 0, b[0], b[1], nvec);
+        }, reps);
+        const double gbps = 2.0 * bytes / (us * 1e-6) / 1e9;
+        std::printf("%-34s      bucket=%6zu MiB  %9.2f us  %8.1f GB/s  (copy: 2 x bytes)\n", "float4 copy (ceiling ref)",
+                    bytes >> 20, us, gbps);
+    }
+    free_sets(S);
+}
+
+
+template <int M>
+static void focus_m(size_t bytes, int sets_override, int rounds) {
+    const size_t nvec = bytes / 16;
+    const int sets = sets_override > 0 ? sets_override : std::max(1, std::min(8, (int)((1024ull << 20) / ((M + 2) * bytes))));
+    Sets S = make_sets(M, nvec, sets);
+    const int reps = std::max(10, std::min(300, (int)((8ull << 30) / ((M + 2) * bytes))));
+    auto args_for = [&](int i) {
+        Args a{};
+        auto& b = S.bufs[i % sets];
+        a.out = b[0];
+        a.acc = b[0];
+        for (int j = 0; j < M; ++j) a.ins[j] = b[j + 1];
+        a.nvec = nvec;
+        return a;
+    };
+    char tag[64];
+    std::snprintf(tag, sizeof tag, " sets=%d", sets);
+    for (int r = 0; r < rounds; ++r) {
+#define F(U, CAP, NTL, NTS, NTA, NAME)                                                              \
+    {                                                                                                  \
+        const size_t trips = (nvec + (size_t)256 * U - 1) / ((size_t)256 * U);                          \
+        const int grid = (int)std::min<size_t>(trips, CAP);                                            \
+        double us = time_launches([&](int i) { hipLaunchKernelGGL((k_reg<M, U, 256, NTL, NTS, NTA>), dim3(grid), dim3(256), 0, 0, args_for(i)); }, reps); \
+        report((std::string(NAME) + tag).c_str(), M, bytes, us);                                                                    \
+    }
+        F(4, 2048, false, false, false, "plain U4 cap2048 (product)");
+        F(1, 1 << 30, false, false, false, "plain U1 full");
+        F(4, 1 << 30, true, false, false, "ntIN U4 full");
+        F(4, 1 << 30, true, false, true, "ntIN+ACC U4 full");
+        F(4, 1 << 30, true, true, false, "ntIN+ST U4 full");
+        F(4, 1 << 30, true, true, true, "ntIN+ACC+ST U4 full");
+        F(2, 1 << 30, true, false, true, "ntIN+ACC U2 full");
+        F(2, 1 << 30, true, true, true, "ntIN+ACC+ST U2 full");
+        F(1, 1 << 30, true, false, true, "ntIN+ACC U1 full");
+        F(1, 1 << 30, true, true, true, "ntIN+ACC+ST U1 full");
+        F(8, 1 << 30, true, false, true, "ntIN+ACC U8 full");
+        F(4, 2048, true, false, true, "ntIN+ACC U4 cap2048");
+        F(4, 2048, true, true, true, "ntIN+ACC+ST U4 cap2048");
+        F(4, 4096, true, false, true, "ntIN+ACC U4 cap4096");
+#undef F
+        std::printf("--\n");
+    }
+    free_sets(S);
+}
+
+// correctness spot check of every variant family against a host sum
+static void check() {
+    const size_t nvec = (1 << 20) + 37;
+    std::vector<f32x4> h0(nvec), h1(nvec);
+    for (size_t i = 0; i < nvec; ++i) {
+        h0[i] = f32x4{(float)(i % 7), 1.f, 2.f, (float)(i % 3)};
+        h1[i] = f32x4{0.5f, (float)(i % 5), 0.25f, 1.f};
+    }
+    f32x4 *d0, *d1;
+    CK(hipMalloc(&d0, nvec * 16));
+    CK(hipMalloc(&d1, nvec * 16));
+    auto reset = [&] {
+        CK(hipMemcpy(d0, h0.data(), nvec * 16, hipMemcpyHostToDevice));
+        CK(hipMemcpy(d1, h1.data(), nvec * 16, hipMemcpyHostToDevice));
+    };
+    auto verify = [&](const char* name) {
+        std::vector<f32x4> r(nvec);
+        CK(hipMemcpy(r.data(), d0, nvec * 16, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < nvec; ++i)
+            for (int c = 0; c < 4; ++c)
+                if (r[i][c] != h0[i][c] + h1[i][c]) {
+                    std::printf("CHECK FAIL %s at %zu\n", name, i);
+                    std::exit(2);
+                }
+    };
+    Args a{};
+    a.out = d0;
+    a.acc = d0;
+    a.ins[0] = d1;
+    a.nvec = nvec;
+    reset();
+    hipLaunchKernelGGL((k_reg<1, 4, 256, true, true>), dim3(777), dim3(256), 0, 0, a);
+    verify("reg");
+    reset();
+    hipLaunchKernelGGL((k_chunk<1, 4, 256>), dim3(300), dim3(256), 0, 0, a, (nvec + 299) / 300);
+    verify("chunk");
+    reset();
+    hipLaunchKernelGGL((k_lds<1, 2>), dim3(555), dim3(256), 0, 0, a);
+    verify("lds");
+    CK(hipFree(d0));
+    CK(hipFree(d1));
+    std::printf("variant correctness: ok\n");
+}
+
+int main(int argc, char** argv) {
+    check();
+    if (argc > 1 && std::string(argv[1]) == "focus") {
+        focus_m<1>(64 << 20, 4, 3);
+        focus_m<1>(64 << 20, 16, 1);
+        focus_m<3>(64 << 20, 4, 2);
+        focus_m<1>(1024ull << 20, 1, 2);
+        focus_m<3>(512ull << 20, 1, 1);
+        focus_m<7>(64 << 20, 4, 1);
+        focus_m<1>(1 << 20, 0, 1);
+        focus_m<1>(16 << 20, 0, 1);
+        return 0;
+    }
+    std::vector<size_t> mib;
+    for (int i = 1; i < argc; ++i) mib.push_back(std::strtoul(argv[i], nullptr, 10));
+    if (mib.empty()) mib = {64, 1024};
+    for (size_t mb : mib) {
+        run_m<1>(mb << 20);
+        run_m<3>(mb << 20);
+        if (mb <= 256) run_m<7>(mb << 20);
+    }
+    return 0;
+}
