@@ -205,7 +205,12 @@ def bench_allreduce(args):
     import chiara_amd as ca
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    local = int(os.environ.get("LOCAL_RANK", rank))
+    local = int(os.environ.get("LOCAL_RANK", rank)) % max(1, torch.cuda.device_count())
+    if os.environ.get("CHR_BENCH_VIRTUAL_HOSTS") == "1":
+        # rehearsal of the N>1 path on fewer GPUs than ranks: distinct host ids make RCCL
+        # use its socket transport between ranks that share a device (numbers meaningless)
+        os.environ["NCCL_HOSTID"] = f"chiara-bench-vhost-{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)

@@ -125,6 +125,10 @@ class Comm:
     def handle(self):
         return self._h
 
+    def set_slices(self, slices):
+        """Pipeline depth (0 = automatic); results are bit-identical for every depth."""
+        check(lib().chr_comm_set_slices(self._h, slices))
+
     @property
     def stream(self):
         s = ctypes.c_void_p()
@@ -157,6 +161,9 @@ class LocalGroup:
         s = ctypes.c_void_p()
         check(lib().chr_local_group_stream(self._h, ctypes.byref(s)))
         return s.value
+
+    def set_slices(self, slices):
+        check(lib().chr_local_group_set_slices(self._h, slices))
 
     def all_reduce_radix_batch(self, sendbufs, recvbufs, count, datatype, op, k, b):
         S = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in sendbufs])
@@ -194,12 +201,12 @@ def reduce_scatter_radix_batch(sendbuf, recvbuf, recvcount, datatype, op, comm, 
 
 # ---- plan introspection (host only) --------------------------------------------------------------
 
-def describe_plan(mode, nranks, rank, k, b, count):
-    n = lib().chr_plan_describe(mode, nranks, rank, k, b, count, None, 0)
+def describe_plan(mode, nranks, rank, k, b, count, slices=1):
+    n = lib().chr_plan_describe(mode, nranks, rank, k, b, count, slices, None, 0)
     if n < 0:
         raise ValueError("bad plan request")
     buf = ctypes.create_string_buffer(n + 1)
-    lib().chr_plan_describe(mode, nranks, rank, k, b, count, buf, n + 1)
+    lib().chr_plan_describe(mode, nranks, rank, k, b, count, slices, buf, n + 1)
     return buf.value.decode()
 
 
@@ -214,6 +221,9 @@ def parse_plan(text):
     def local(tok):
         if tok[0] == "copy":
             return ("copy", (tok[1], int(tok[2])), (tok[3], int(tok[4])), int(tok[5]), [])
+        if tok[0] == "copy2d":  # (width, rows, dpitch, spitch) in the last field
+            return ("copy2d", (tok[1], int(tok[2])), (tok[3], int(tok[4])), int(tok[5]),
+                    [int(tok[6]), int(tok[7]), int(tok[8])])
         m = int(tok[6])
         ins = [(tok[7 + 2 * j], int(tok[8 + 2 * j])) for j in range(m)]
         return ("reduce", (tok[1], int(tok[2])), (tok[3], int(tok[4])), int(tok[5]), ins)

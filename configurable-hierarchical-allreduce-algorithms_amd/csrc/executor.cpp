@@ -87,6 +87,9 @@ int run_local(const chr::LocalOp& op, const Bufs& B, int dtype, int rop, hipStre
         if (d == src) return CHR_SUCCESS;
         return hip_code(hipMemcpyAsync(d, src, op.count * B.es, hipMemcpyDeviceToDevice, s));
     }
+    if (op.kind == chr::L_COPY2D)
+        return hip_code(hipMemcpy2DAsync(B.ptr(op.dst), op.dpitch * B.es, B.ptr(op.acc), op.spitch * B.es,
+                                         op.count * B.es, op.rows, hipMemcpyDeviceToDevice, s));
     std::vector<const void*> ins(op.ins.size());
     for (size_t j = 0; j < op.ins.size(); ++j) ins[j] = B.ptr(op.ins[j]);
     return hip_code(chr::launch_reduce(B.ptr(op.dst), B.ptr(op.acc), ins.data(), (int)ins.size(), op.count, dtype,
@@ -104,22 +107,36 @@ bool is_device_ptr(const void* p) {
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
 }
 
-using PlanKey = std::tuple<int, int, int, int, uint64_t>;  // mode, rank, k, b, count
+using PlanKey = std::tuple<int, int, int, int, uint64_t, int, int>;  // mode, rank, k, b, count, dtype size, slices
+
+// Pipeline depth: explicit setting, else CHR_SLICES, else by chunk size (schedule.cpp).
+int pick_slices(int setting, uint64_t count, int mode, int nranks, int b, size_t es) {
+    if (setting > 0) return setting;
+    static const int env = [] {
+        const char* v = std::getenv("CHR_SLICES");
+        return v ? std::atoi(v) : 0;
+    }();
+    if (env > 0) return env;
+    const uint64_t recvcount = mode == chr::MODE_ALLREDUCE ? count / (uint64_t)(nranks > 0 ? nranks : 1) : count;
+    return chr::auto_slices(recvcount * (uint64_t)(b > 0 ? b : 1) * es);
+}
 
 }  // namespace
 
 struct chr_comm {
     int rank = 0, nranks = 0, device = 0;
+    int slices = 0;  // 0 = auto
     ncclComm_t nccl = nullptr;
     hipStream_t stream = nullptr;
     DevBuf acc, stage, hsend, hrecv;
     std::map<PlanKey, std::unique_ptr<Plan>> plans;
 
-    const Plan& plan(int mode, int k, int b, uint64_t count) {
-        PlanKey key{mode, rank, k, b, count};
+    const Plan& plan(int mode, int k, int b, uint64_t count, size_t es) {
+        const int P = pick_slices(slices, count, mode, nranks, b, es);
+        PlanKey key{mode, rank, k, b, count, (int)es, P};
         auto it = plans.find(key);
         if (it == plans.end())
-            it = plans.emplace(key, std::make_unique<Plan>(chr::build_plan((chr::Mode)mode, nranks, rank, k, b, count)))
+            it = plans.emplace(key, std::make_unique<Plan>(chr::build_plan((chr::Mode)mode, nranks, rank, k, b, count, P)))
                      .first;
         return *it->second;
     }
@@ -127,9 +144,10 @@ struct chr_comm {
 
 struct chr_local_group {
     int nranks = 0, device = 0;
+    int slices = 0;  // 0 = auto
     hipStream_t stream = nullptr;
     std::vector<DevBuf> acc, stage;
-    std::map<std::tuple<int, int, int, uint64_t>, std::vector<Plan>> plans;
+    std::map<std::tuple<int, int, int, uint64_t, int, int>, std::vector<Plan>> plans;
 };
 
 namespace {
@@ -167,7 +185,7 @@ int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int d
 int collective(chr_comm* c, int mode, const void* send, void* recv, size_t count, int dtype, int op, int k, int b,
                bool sync) {
     if (!c || !chr::valid_dtype_op(dtype, op)) return CHR_ERR_INVALID_ARG;
-    const Plan& p = c->plan(mode, k, b, count);
+    const Plan& p = c->plan(mode, k, b, count, chr::dtype_size(dtype));
     if (p.error) return p.error;
     if (p.g.total == 0) return CHR_SUCCESS;
     if (!recv) return CHR_ERR_INVALID_ARG;
@@ -209,11 +227,12 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
                      int dtype, int op, int k, int b) {
     if (!g || !sends || !recvs || !chr::valid_dtype_op(dtype, op)) return CHR_ERR_INVALID_ARG;
     const int n = g->nranks;
-    auto key = std::make_tuple(mode, k, b, (uint64_t)count);
+    const int depth = pick_slices(g->slices, count, mode, n, b, chr::dtype_size(dtype));
+    auto key = std::make_tuple(mode, k, b, (uint64_t)count, (int)chr::dtype_size(dtype), depth);
     auto it = g->plans.find(key);
     if (it == g->plans.end()) {
         std::vector<Plan> v;
-        for (int r = 0; r < n; ++r) v.push_back(chr::build_plan((chr::Mode)mode, n, r, k, b, count));
+        for (int r = 0; r < n; ++r) v.push_back(chr::build_plan((chr::Mode)mode, n, r, k, b, count, depth));
         it = g->plans.emplace(key, std::move(v)).first;
     }
     const std::vector<Plan>& P = it->second;
@@ -329,6 +348,18 @@ int chr_comm_rank(const chr_comm* c, int* rank) {
 int chr_comm_size(const chr_comm* c, int* n) {
     if (!c || !n) return CHR_ERR_INVALID_ARG;
     *n = c->nranks;
+    return CHR_SUCCESS;
+}
+
+int chr_comm_set_slices(chr_comm* c, int slices) {
+    if (!c || slices < 0) return CHR_ERR_INVALID_ARG;
+    c->slices = slices;
+    return CHR_SUCCESS;
+}
+
+int chr_local_group_set_slices(chr_local_group* g, int slices) {
+    if (!g || slices < 0) return CHR_ERR_INVALID_ARG;
+    g->slices = slices;
     return CHR_SUCCESS;
 }
 

@@ -8,7 +8,7 @@
 // every message is posted by both of its endpoints in the same step and a rank can
 // enqueue its whole plan without ever blocking the host (deadlock-free by construction).
 //
-// HBM layout of the accumulator (ACC): block-major.  The reference keeps
+// HBM layout of the accumulator (ACC): slice-major, then block-major.  The reference keeps
 // tmp_results stage-major ([stage][lane block][IRC], :339-400), so each recexch phase
 // touches `nstages` (+1 truncated) separate slices.  Here chunk N = stage*b + lane sits
 // at position P[lane] + stage, i.e. [lane block][stage][IRC]: the region a phase
@@ -36,10 +36,11 @@ struct Xfer {
     uint64_t count;  // elements
 };
 
-enum LocalKind : uint8_t { L_COPY = 0, L_REDUCE = 1 };
+enum LocalKind : uint8_t { L_COPY = 0, L_REDUCE = 1, L_COPY2D = 2 };
 
 // L_REDUCE: dst = (...((acc op ins[0]) op ins[1])...) op ins[m-1]   (dst may equal acc)
-// L_COPY:   dst = acc
+// L_COPY:   dst = acc                                    (count elements)
+// L_COPY2D: rows x count elements, row r: dst + r*dpitch <- acc + r*spitch
 struct LocalOp {
     LocalKind kind;
     Ref dst;
@@ -47,6 +48,7 @@ struct LocalOp {
     std::vector<Ref> ins;
     uint64_t count;
     int site;  // reference call site this op restates (line in all_reduce_radix_batch.cpp)
+    uint64_t rows = 1, dpitch = 0, spitch = 0;
 };
 
 struct Step {
@@ -65,6 +67,7 @@ struct Geometry {
 
 struct Plan {
     int error = 0;  // chr_result
+    int slices = 1;  // pipeline depth actually used
     Mode mode = MODE_ALLREDUCE;
     int rank = 0;
     Geometry g;
@@ -85,8 +88,12 @@ int recexch_neighbors(int rank, int nranks, int k, Recexch* out);
 void recexch_count_offset(int nranks, int max_phases, int k, std::vector<int>* count,
                           std::vector<int>* offset);
 
-// count = allreduce element count, or reduce-scatter recvcount.
-Plan build_plan(Mode mode, int nranks, int rank, int k, int b, uint64_t count);
+// count = allreduce element count, or reduce-scatter recvcount.  `slices` = pipeline
+// depth: every chunk is cut into that many element slices; slice s runs logical step
+// t-s in super-step t, so consecutive phases of different slices share an RCCL group.
+// The per-element reduction order is unchanged (results are bit-identical for any depth).
+Plan build_plan(Mode mode, int nranks, int rank, int k, int b, uint64_t count, int slices = 1);
+int auto_slices(uint64_t irc_bytes);
 std::string describe(const Plan& p);
 
 }  // namespace chr

@@ -77,6 +77,11 @@ int chr_comm_rank(const chr_comm* comm, int* rank);
 int chr_comm_size(const chr_comm* comm, int* nranks);
 /* The stream all of this communicator's collective work is enqueued on. */
 int chr_comm_stream(const chr_comm* comm, hipStream_t* stream);
+/* Pipeline depth of the schedules: every chunk is cut into `slices` element slices and
+ * consecutive phases of different slices share one RCCL group (different xGMI links
+ * busy at once).  0 = automatic (~64 MiB per slice message, up to 8; env CHR_SLICES).
+ * Results are bit-identical for every depth. */
+int chr_comm_set_slices(chr_comm* comm, int slices);
 
 /* ---- schedule boundary ----------------------------------------------------------------
  * Replaces  int all_reduce_radix_batch(char* sendbuf, char* recvbuf, int count,
@@ -108,6 +113,7 @@ typedef struct chr_local_group chr_local_group;
 int chr_local_group_create(chr_local_group** group, int nranks, int device);
 int chr_local_group_destroy(chr_local_group* group);
 int chr_local_group_stream(const chr_local_group* group, hipStream_t* stream);
+int chr_local_group_set_slices(chr_local_group* group, int slices);
 int chr_local_allreduce_radix_batch(chr_local_group* group, const void* const* sends,
                                     void* const* recvs, size_t count, chr_dtype dtype, chr_op op,
                                     int k, int b);
@@ -122,7 +128,7 @@ int chr_local_reduce_scatter_radix_batch(chr_local_group* group, const void* con
  * (truncated to len, NUL-terminated); returns the length needed (excluding NUL) or < 0. */
 typedef enum { CHR_MODE_ALLREDUCE = 0, CHR_MODE_REDUCE_SCATTER = 1 } chr_mode;
 long chr_plan_describe(chr_mode mode, int nranks, int rank, int k, int b, size_t count,
-                       char* buf, size_t len);
+                       int slices, char* buf, size_t len);
 
 /* ---- utilities -------------------------------------------------------------------------- */
 /* Synthetic inputs on the device with the shared generator (oracle/chiara_oracle.h):

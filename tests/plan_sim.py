@@ -11,8 +11,8 @@ import chiara_amd as ca
 import pyoracle as po
 
 
-def load_plans(mode, n, k, b, count):
-    return [ca.parse_plan(ca.describe_plan(mode, n, r, k, b, count)) for r in range(n)]
+def load_plans(mode, n, k, b, count, slices=1):
+    return [ca.parse_plan(ca.describe_plan(mode, n, r, k, b, count, slices)) for r in range(n)]
 
 
 class RankState:
@@ -34,6 +34,11 @@ class RankState:
 def run_local(st, op, dtype, rop):
     kind, dst, acc, n, ins = op
     if n == 0:
+        return
+    if kind == "copy2d":
+        rows, dp, sp = ins
+        for r in range(rows):
+            st.view((dst[0], dst[1] + r * dp), n)[:] = st.view((acc[0], acc[1] + r * sp), n).copy()
         return
     if kind == "copy":
         st.view(dst, n)[:] = st.view(acc, n).copy()
@@ -77,10 +82,10 @@ def execute(plans, sends, dtype, rop, inplace=False):
     return [st.buf["RECV"] for st in states]
 
 
-def simulate(mode, sends, k, b, dtype, op, inplace=False):
+def simulate(mode, sends, k, b, dtype, op, inplace=False, slices=1):
     n = len(sends)
     count = sends[0].size if mode == ca.MODE_ALLREDUCE else sends[0].size // n
-    plans = load_plans(mode, n, k, b, count)
+    plans = load_plans(mode, n, k, b, count, slices)
     if plans[0]["header"]["error"]:
         raise ValueError(f"plan error {plans[0]['header']['error']}")
     outs = execute(plans, sends, dtype, op, inplace)

@@ -77,12 +77,18 @@ def test_local_group_matches_reference_golden(gu, groups, golden):
     ("ar", 8, 2, 4, "bf16"), ("ar", 8, 4, 8, "f32"), ("rs", 2, 2, 1, "f32"), ("rs", 2, 2, 2, "f32"),
     ("ar", 2, 2, 1, "f32"), ("ar", 2, 2, 2, "f32"), ("ar", 16, 4, 4, "f32"), ("rs", 8, 4, 4, "bf16"),
 ])
-def test_baseline_geometries_vs_oracle(gu, groups, mode, n, k, b, dtype):
-    """BASELINE configs' (n, k, b) at 4-16 MiB per rank: bit-exact vs the oracle."""
+@pytest.mark.parametrize("slices", [1, 3, 8])
+def test_baseline_geometries_vs_oracle(gu, groups, mode, n, k, b, dtype, slices):
+    """BASELINE configs' (n, k, b) at 4-16 MiB per rank, unsliced and pipelined: bit-exact vs the oracle."""
     per_rank = (1 << 22) if dtype == "f32" else (1 << 23)
     in_n = per_rank if mode == "ar" else per_rank // n * n
     sends = [po.fill(in_n, dtype, 0, 0xC41A5EED, r) for r in range(n)]
-    got = run_local(gu, groups(n), mode, sends, k, b, dtype, "sum")
+    g = groups(n)
+    g.set_slices(slices)
+    try:
+        got = run_local(gu, g, mode, sends, k, b, dtype, "sum")
+    finally:
+        g.set_slices(0)
     f = po.allreduce_radix_batch if mode == "ar" else po.reduce_scatter_radix_batch
     ref = f(sends, k, b, dtype, "sum")
     for r in range(n):

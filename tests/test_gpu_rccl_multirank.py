@@ -42,7 +42,8 @@ def _worker(rank, world, port, cases, q):
     comm = ca.Comm.from_torch_distributed(device=0)
     dev = torch.device("cuda:0")
     try:
-        for (mode, k, b, count, dtype, host) in cases:
+        for (mode, k, b, count, dtype, host, slices) in cases:
+            comm.set_slices(slices)
             npdt = po.NP_DTYPES[dtype]
             cdt = {"f32": ca.FLOAT32, "bf16": ca.BFLOAT16, "i32": ca.INT32}[dtype]
             in_n = count if mode == "ar" else count * world
@@ -85,12 +86,12 @@ def _run(world, cases, timeout=300):
 
 
 def test_rccl_world2_reduce_scatter_and_allreduce():
-    _run(2, [("rs", 2, 1, 1 << 16, "f32", False), ("rs", 2, 2, 1 << 16, "f32", False),
-             ("ar", 2, 2, 1 << 16, "f32", False), ("ar", 2, 1, 2 * 1001, "bf16", False),
-             ("ar", 2, 2, 1 << 14, "f32", True)])
+    _run(2, [("rs", 2, 1, 1 << 16, "f32", False, 0), ("rs", 2, 2, 1 << 16, "f32", False, 3),
+             ("ar", 2, 2, 1 << 16, "f32", False, 4), ("ar", 2, 1, 2 * 1001, "bf16", False, 0),
+             ("ar", 2, 2, 1 << 14, "f32", True, 2)])
 
 
 def test_rccl_world8_c4_c5_geometries():
-    _run(8, [("ar", 4, 4, 8 * 4096, "f32", False), ("ar", 4, 4, 8 * 4096, "bf16", False),
-             ("ar", 2, 2, 8 * 4096, "f32", False), ("ar", 3, 4, 8 * 2048, "bf16", False),
-             ("ar", 4, 8, 8 * 1024, "f32", False), ("rs", 4, 4, 1000, "f32", False)], timeout=600)
+    _run(8, [("ar", 4, 4, 8 * 4096, "f32", False, 0), ("ar", 4, 4, 8 * 4096, "bf16", False, 4),
+             ("ar", 2, 2, 8 * 4096, "f32", False, 3), ("ar", 3, 4, 8 * 2048, "bf16", False, 2),
+             ("ar", 4, 8, 8 * 1024, "f32", False, 0), ("rs", 4, 4, 4000, "f32", False, 3)], timeout=600)

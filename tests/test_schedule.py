@@ -57,12 +57,42 @@ def test_plan_errors_match_reference_preconditions():
 
 def test_plan_shape_c4():
     """C4 geometry (n=8, k=4, b=4): one recexch phase with k-1=3 concurrent neighbours,
-    one fused 3-input reduction per active lane, 1-input lane reduction at the roots."""
+    one fused 3-input reduction per active lane, 1-input lane reduction at the roots,
+    then the link-balanced distribute (scatter 1/7 pieces, forward)."""
     p = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 1 << 20))
-    assert p["header"]["k"] == 4 and p["header"]["steps"] == 5
-    ph = [s for s in p["steps"] if s["label"].startswith("recexch")]
-    assert len(ph) == 1 and len(ph[0]["recvs"]) == 3 and len(ph[0]["sends"]) == 1
-    red = [op for op in ph[0]["post"] if op[0] == "reduce"]
+    assert p["header"]["k"] == 4 and p["header"]["steps"] == 4 and p["header"]["slices"] == 1
+    ph = p["steps"][0]
+    assert len(ph["recvs"]) == 3 and len(ph["sends"]) == 1
+    red = [op for op in ph["post"] if op[0] == "reduce"]
     assert len(red) == 1 and len(red[0][4]) == 3
-    lane = [s for s in p["steps"] if s["label"] == "inter-lane-reduce"][0]
+    lane = p["steps"][1]
     assert len(lane["recvs"]) == 1 and lane["post"][0][0] == "reduce"
+    d1, d2 = p["steps"][2], p["steps"][3]
+    assert len(d1["sends"]) == 7 and len(d1["recvs"]) == 1   # rank 0 owns chunk 0, gets a piece of chunk 1
+    assert len(d2["sends"]) == 6 and len(d2["recvs"]) == 6  # forwards its piece of chunk 1, gets the rest
+
+
+@pytest.mark.parametrize("slices", [2, 3, 5, 8])
+@pytest.mark.parametrize("mode,n,k,b", [("ar", 8, 4, 4), ("ar", 8, 2, 2), ("ar", 8, 3, 4), ("ar", 12, 3, 6),
+                                         ("ar", 2, 2, 1), ("rs", 8, 4, 4), ("rs", 2, 2, 2), ("rs", 12, 5, 6),
+                                         ("ar", 16, 4, 8), ("ar", 9, 2, 3)])
+def test_pipelined_plans_bit_exact(mode, n, k, b, slices):
+    """Wavefront super-steps over element slices: same bits as the unsliced reference."""
+    per = 256 * 5 + 64  # several 256-element slice granules per chunk, ragged last slice
+    count = per * n
+    m = ca.MODE_ALLREDUCE if mode == "ar" else ca.MODE_REDUCE_SCATTER
+    in_n = count if mode == "ar" else count * n
+    for dt in ("f32", "bf16"):
+        sends = [po.fill(in_n, dt, 0, 314, r) for r in range(n)]
+        f = po.allreduce_radix_batch if mode == "ar" else po.reduce_scatter_radix_batch
+        ref = f(sends, k, b, dt, "sum")
+        got = plan_sim.simulate(m, sends, k, b, dt, "sum", slices=slices)
+        for r in range(n):
+            np.testing.assert_array_equal(got[r], ref[r])
+
+
+def test_pipelined_plan_structure():
+    p = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 8 * 4 * 4096, 4))
+    assert p["header"]["slices"] == 4 and p["header"]["steps"] == 4 + 4 - 1
+    # super-step 1 holds slice 0's lane reduce and slice 1's recexch phase in ONE group
+    assert "lane/s0" in p["steps"][1]["label"] and "phase0/s1" in p["steps"][1]["label"]
