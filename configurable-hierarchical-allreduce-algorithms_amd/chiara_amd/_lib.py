@@ -60,6 +60,9 @@ def _load():
         "chr_local_reduce_scatter_radix_batch": ([vp, pp, pp, sz, i, i, i, i], i),
         "chr_plan_describe": ([i, i, i, i, i, sz, i, ctypes.c_char_p, sz], ctypes.c_long),
         "chr_comm_set_slices": ([vp, i], i),
+        "chr_comm_profile": ([vp, i], i),
+        "chr_comm_profile_read": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ctypes.c_long), i], i),
         "chr_local_group_set_slices": ([vp, i], i),
     }
     for name, (args, res) in sig.items():
@@ -80,7 +83,8 @@ def lib():
 # Every symbol include/chiara.h declares (checked by tests/test_abi.py).
 EXPORTED = [
     "chr_reduce_local", "chr_reduce_multi", "chr_get_unique_id", "chr_comm_init_rank", "chr_comm_destroy",
-    "chr_comm_rank", "chr_comm_size", "chr_comm_stream", "chr_comm_set_slices", "chr_local_group_set_slices", "chr_allreduce_radix_batch",
+    "chr_comm_rank", "chr_comm_size", "chr_comm_stream", "chr_comm_set_slices", "chr_local_group_set_slices",
+    "chr_comm_profile", "chr_comm_profile_read", "chr_allreduce_radix_batch",
     "chr_reduce_scatter_radix_batch", "chr_allreduce_radix_batch_async", "chr_reduce_scatter_radix_batch_async",
     "chr_local_group_create", "chr_local_group_destroy", "chr_local_group_stream",
     "chr_local_allreduce_radix_batch", "chr_local_reduce_scatter_radix_batch", "chr_plan_describe", "chr_fill",

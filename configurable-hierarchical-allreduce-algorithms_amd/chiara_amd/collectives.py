@@ -129,6 +129,17 @@ class Comm:
         """Pipeline depth (0 = automatic); results are bit-identical for every depth."""
         check(lib().chr_comm_set_slices(self._h, slices))
 
+    def profile(self, enable=True):
+        """Time every fused reduction launch of this communicator (HIP events)."""
+        check(lib().chr_comm_profile(self._h, 1 if enable else 0))
+
+    def profile_read(self, reset=True):
+        """(kernel_ms, algorithmic_bytes, launches) of the reductions since the last reset."""
+        ms, by, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_long()
+        check(lib().chr_comm_profile_read(self._h, ctypes.byref(ms), ctypes.byref(by), ctypes.byref(n),
+                                          1 if reset else 0))
+        return ms.value, by.value, n.value
+
     @property
     def stream(self):
         s = ctypes.c_void_p()

@@ -79,7 +79,45 @@ int nccl_code(ncclResult_t r) {
     return CHR_ERR_RCCL;
 }
 
-int run_local(const chr::LocalOp& op, const Bufs& B, int dtype, int rop, hipStream_t s) {
+// Opt-in timing of the fused reduction launches (chr_comm_profile): HIP events on the
+// launch stream around each reduction, summed when read.
+struct ReduceProfile {
+    bool on = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, spare;
+    double ms = 0, bytes = 0;
+    long launches = 0;
+    std::pair<hipEvent_t, hipEvent_t> take() {
+        if (!spare.empty()) {
+            auto e = spare.back();
+            spare.pop_back();
+            return e;
+        }
+        std::pair<hipEvent_t, hipEvent_t> e{nullptr, nullptr};
+        (void)hipEventCreate(&e.first);
+        (void)hipEventCreate(&e.second);
+        return e;
+    }
+    void drain() {
+        for (auto& e : pending) {
+            float t = 0;
+            if (hipEventSynchronize(e.second) == hipSuccess && hipEventElapsedTime(&t, e.first, e.second) == hipSuccess)
+                ms += t;
+            spare.push_back(e);
+        }
+        pending.clear();
+    }
+    void release() {
+        drain();
+        for (auto& e : spare) {
+            (void)hipEventDestroy(e.first);
+            (void)hipEventDestroy(e.second);
+        }
+        spare.clear();
+    }
+};
+
+int run_local(const chr::LocalOp& op, const Bufs& B, int dtype, int rop, hipStream_t s,
+              ReduceProfile* prof = nullptr) {
     if (op.count == 0) return CHR_SUCCESS;
     if (op.kind == chr::L_COPY) {
         char* d = B.ptr(op.dst);
@@ -92,8 +130,21 @@ int run_local(const chr::LocalOp& op, const Bufs& B, int dtype, int rop, hipStre
                                          op.count * B.es, op.rows, hipMemcpyDeviceToDevice, s));
     std::vector<const void*> ins(op.ins.size());
     for (size_t j = 0; j < op.ins.size(); ++j) ins[j] = B.ptr(op.ins[j]);
-    return hip_code(chr::launch_reduce(B.ptr(op.dst), B.ptr(op.acc), ins.data(), (int)ins.size(), op.count, dtype,
-                                       rop, s));
+    const bool timed = prof && prof->on && !ins.empty();
+    std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+    if (timed) {
+        ev = prof->take();
+        (void)hipEventRecord(ev.first, s);
+    }
+    const int rc = hip_code(chr::launch_reduce(B.ptr(op.dst), B.ptr(op.acc), ins.data(), (int)ins.size(), op.count,
+                                               dtype, rop, s));
+    if (timed) {
+        (void)hipEventRecord(ev.second, s);
+        prof->pending.push_back(ev);
+        prof->bytes += (double)(ins.size() + 2) * op.count * B.es;
+        prof->launches += 1;
+    }
+    return rc;
 }
 
 bool is_device_ptr(const void* p) {
@@ -129,6 +180,7 @@ struct chr_comm {
     ncclComm_t nccl = nullptr;
     hipStream_t stream = nullptr;
     DevBuf acc, stage, hsend, hrecv;
+    ReduceProfile prof;
     std::map<PlanKey, std::unique_ptr<Plan>> plans;
 
     const Plan& plan(int mode, int k, int b, uint64_t count, size_t es) {
@@ -160,7 +212,7 @@ int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int d
     Bufs B{(const char*)send, (char*)recv, (char*)c->acc.p, (char*)c->stage.p, es};
     int rc;
     for (const auto& op_ : p.pre)
-        if ((rc = run_local(op_, B, dtype, op, c->stream))) return rc;
+        if ((rc = run_local(op_, B, dtype, op, c->stream, &c->prof))) return rc;
     for (const chr::Step& s : p.steps) {
         if (!s.sends.empty() || !s.recvs.empty()) {
             if ((rc = nccl_code(ncclGroupStart()))) return rc;
@@ -177,7 +229,7 @@ int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int d
             if ((rc = nccl_code(ncclGroupEnd()))) return rc;
         }
         for (const auto& op_ : s.post)
-            if ((rc = run_local(op_, B, dtype, op, c->stream))) return rc;
+            if ((rc = run_local(op_, B, dtype, op, c->stream, &c->prof))) return rc;
     }
     return CHR_SUCCESS;
 }
@@ -329,6 +381,7 @@ int chr_comm_destroy(chr_comm* c) {
     if (!c) return CHR_SUCCESS;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    c->prof.release();
     if (c->nccl) (void)ncclCommDestroy(c->nccl);
     c->acc.release();
     c->stage.release();
@@ -354,6 +407,27 @@ int chr_comm_size(const chr_comm* c, int* n) {
 int chr_comm_set_slices(chr_comm* c, int slices) {
     if (!c || slices < 0) return CHR_ERR_INVALID_ARG;
     c->slices = slices;
+    return CHR_SUCCESS;
+}
+
+int chr_comm_profile(chr_comm* c, int enable) {
+    if (!c) return CHR_ERR_INVALID_ARG;
+    c->prof.on = enable != 0;
+    return CHR_SUCCESS;
+}
+
+int chr_comm_profile_read(chr_comm* c, double* reduce_ms, double* reduce_bytes, long* launches, int reset) {
+    if (!c) return CHR_ERR_INVALID_ARG;
+    (void)hipSetDevice(c->device);
+    c->prof.drain();
+    if (reduce_ms) *reduce_ms = c->prof.ms;
+    if (reduce_bytes) *reduce_bytes = c->prof.bytes;
+    if (launches) *launches = c->prof.launches;
+    if (reset) {
+        c->prof.ms = 0;
+        c->prof.bytes = 0;
+        c->prof.launches = 0;
+    }
     return CHR_SUCCESS;
 }
 

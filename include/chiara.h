@@ -82,6 +82,13 @@ int chr_comm_stream(const chr_comm* comm, hipStream_t* stream);
  * busy at once).  0 = automatic (~64 MiB per slice message, up to 8; env CHR_SLICES).
  * Results are bit-identical for every depth. */
 int chr_comm_set_slices(chr_comm* comm, int slices);
+/* Opt-in timing of the fused bucket-reduction launches of this communicator (HIP events
+ * on its stream).  _read synchronises on the recorded launches and returns the summed
+ * kernel milliseconds, the algorithmic bytes ((m+2)*n*sizeof(T) per launch) and the
+ * launch count since the last reset. */
+int chr_comm_profile(chr_comm* comm, int enable);
+int chr_comm_profile_read(chr_comm* comm, double* reduce_ms, double* reduce_bytes, long* launches,
+                          int reset);
 
 /* ---- schedule boundary ----------------------------------------------------------------
  * Replaces  int all_reduce_radix_batch(char* sendbuf, char* recvbuf, int count,
