@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--sweep", action="store_true", help="N=1: bucket sizes 1 KiB..1 GiB, m=1/3/7 (table to stderr)")
     p.add_argument("--count", type=int, default=None, help="N>1: elements per rank (default 2^28)")
     p.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
+    p.add_argument("--e2e", action="store_true",
+                   help="N=1: host-memory (PCIe-inclusive) staging cost of the reference's host-buffer contract")
     return p.parse_args()
 
 
@@ -159,22 +161,23 @@ def bench_bucket(args, cpu):
 
 
 def sweep(ca, torch, dev, stream):
-    """Bucket sizes 1 KiB .. 1 GiB, m = 1, 3, 7: kernel-time GB/s (HIP events)."""
+    """Bucket sizes 1 KiB .. 1 GiB, m = 1, 3, 7 (fp32) and m = 3 (bf16): GB/s over HIP events."""
     rows = []
-    for m in (1, 3, 7):
+    for m, dname in ((1, "f32"), (3, "f32"), (7, "f32"), (1, "bf16"), (3, "bf16")):
+        cdt, es, tdt = (ca.FLOAT32, 4, torch.float32) if dname == "f32" else (ca.BFLOAT16, 2, torch.bfloat16)
         for lg in range(10, 31, 2):
             nbytes = 1 << lg
-            n = nbytes // 4
-            sets = max(1, min(8, (768 << 20) // ((m + 2) * nbytes)))
-            bufs = [[torch.empty(n, dtype=torch.float32, device=dev) for _ in range(m + 1)] for _ in range(sets)]
+            n = nbytes // es
+            sets = max(1, min(16, (2048 << 20) // ((m + 1) * nbytes)))
+            bufs = [[torch.empty(n, dtype=tdt, device=dev) for _ in range(m + 1)] for _ in range(sets)]
             for s in bufs:
                 for j, t in enumerate(s):
-                    ca.fill(t, n, ca.FLOAT32, 0, SEED, j, stream=stream)
+                    ca.fill(t, n, cdt, 0, SEED, j, stream=stream)
             reps = max(5, min(200, (4 << 30) // ((m + 2) * nbytes)))
 
             def go(i):
                 s = bufs[i % sets]
-                return ca.reduce_multi(s[0], s[0], s[1:], n, ca.FLOAT32, ca.SUM, stream)
+                return ca.reduce_multi(s[0], s[0], s[1:], n, cdt, ca.SUM, stream)
 
             for i in range(3):
                 go(i)
@@ -187,13 +190,50 @@ def sweep(ca, torch, dev, stream):
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / reps
             gbps = (m + 2) * nbytes / (ms * 1e-3) / 1e9
-            rows.append({"m": m, "bucket_bytes": nbytes, "us": round(ms * 1e3, 2), "GBps": round(gbps, 1),
-                         "frac": round(gbps / HBM_PEAK_GBPS, 4)})
-            print(f"sweep m={m} bucket={nbytes:>11d} B  {ms * 1e3:9.2f} us  {gbps:8.1f} GB/s", file=sys.stderr,
-                  flush=True)
+            rows.append({"dtype": dname, "m": m, "bucket_bytes": nbytes, "us": round(ms * 1e3, 2),
+                         "GBps": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBPS, 4)})
+            print(f"sweep {dname} m={m} bucket={nbytes:>11d} B  {ms * 1e3:9.2f} us  {gbps:8.1f} GB/s",
+                  file=sys.stderr, flush=True)
             del bufs
     torch.cuda.empty_cache()
     return rows
+
+
+def bench_e2e(args):
+    """PCIe-inclusive cost of the reference's host-memory contract on one rank: the
+    collective stages send H2D and recv D2H around the device-resident schedule."""
+    import numpy as np
+    import torch
+
+    import chiara_amd as ca
+
+    torch.cuda.set_device(0)
+    comm = ca.Comm(1, ca.get_unique_id(), 0, 0)
+    n = 1 << 28  # 1 GiB fp32 per rank, the C4 buffer
+    out = {"workload": "host-buffer staging, 1 GiB fp32, nranks=1 (H2D + schedule + D2H)"}
+    for kind in ("pageable", "pinned"):
+        if kind == "pageable":
+            h_send, h_recv = np.ones(n, dtype=np.float32), np.zeros(n, dtype=np.float32)
+        else:
+            h_send = torch.ones(n, dtype=torch.float32).pin_memory()
+            h_recv = torch.zeros(n, dtype=torch.float32).pin_memory()
+        ca.check(ca.all_reduce_radix_batch(h_send, h_recv, n, ca.FLOAT32, ca.SUM, comm, 2, 1))
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ca.check(ca.all_reduce_radix_batch(h_send, h_recv, n, ca.FLOAT32, ca.SUM, comm, 2, 1))
+        dt = (time.perf_counter() - t0) / reps
+        out[kind] = {"ms": round(dt * 1e3, 2), "GBps_per_direction": round(4 * n / (dt / 2) / 1e9, 2)}
+        assert float(h_recv[12345]) == 1.0
+    d_send = torch.ones(n, dtype=torch.float32, device="cuda:0")
+    d_recv = torch.zeros(n, dtype=torch.float32, device="cuda:0")
+    ca.check(ca.all_reduce_radix_batch(d_send, d_recv, n, ca.FLOAT32, ca.SUM, comm, 2, 1))
+    t0 = time.perf_counter()
+    for _ in range(3):
+        ca.check(ca.all_reduce_radix_batch(d_send, d_recv, n, ca.FLOAT32, ca.SUM, comm, 2, 1))
+    out["device_resident_ms"] = round((time.perf_counter() - t0) / 3 * 1e3, 3)
+    comm.destroy()
+    print(json.dumps({"e2e": out}), flush=True)
 
 
 # ---- N > 1: hierarchical allreduce over RCCL ---------------------------------------------------
@@ -287,6 +327,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
         bench_allreduce(args)
+        return
+    if args.e2e:
+        bench_e2e(args)
         return
     cpu = None if args.no_cpu_baseline else cpu_baseline(args.cpu_seconds)
     bench_bucket(args, cpu)

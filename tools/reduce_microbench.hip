@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+
+#include "chiara.h"
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -70,7 +72,7 @@ __global__ __launch_bounds__(BLOCK) void k_reg(Args a) {
 }
 
 // Contiguous-chunk-per-block form: block b owns [b*CH, (b+1)*CH) vectors.
-template <int M, int U, int BLOCK>
+template <int M, int U, int BLOCK, bool NT = false>
 __global__ __launch_bounds__(BLOCK) void k_chunk(Args a, size_t chunk) {
     const size_t lo = (size_t)blockIdx.x * chunk;
     size_t hi = lo + chunk;
@@ -79,18 +81,23 @@ __global__ __launch_bounds__(BLOCK) void k_chunk(Args a, size_t chunk) {
         if (base + (size_t)(U - 1) * BLOCK < hi) {
             f32x4 acc[U], x[M][U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) acc[u] = a.acc[base + (size_t)u * BLOCK];
+            for (int u = 0; u < U; ++u)
+                acc[u] = NT ? __builtin_nontemporal_load(&a.acc[base + (size_t)u * BLOCK]) : a.acc[base + (size_t)u * BLOCK];
 #pragma unroll
             for (int j = 0; j < M; ++j)
 #pragma unroll
-                for (int u = 0; u < U; ++u) x[j][u] = a.ins[j][base + (size_t)u * BLOCK];
+                for (int u = 0; u < U; ++u)
+                    x[j][u] = NT ? __builtin_nontemporal_load(&a.ins[j][base + (size_t)u * BLOCK]) : a.ins[j][base + (size_t)u * BLOCK];
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int j = 0; j < M; ++j)
 #pragma unroll
                 for (int u = 0; u < U; ++u) acc[u] = x[j][u] + acc[u];
 #pragma unroll
-            for (int u = 0; u < U; ++u) a.out[base + (size_t)u * BLOCK] = acc[u];
+            for (int u = 0; u < U; ++u) {
+                if (NT) __builtin_nontemporal_store(acc[u], &a.out[base + (size_t)u * BLOCK]);
+                else a.out[base + (size_t)u * BLOCK] = acc[u];
+            }
         } else {
             for (int u = 0; u < U; ++u) {
                 const size_t i = base + (size_t)u * BLOCK;
@@ -343,6 +350,61 @@ static void focus_m(size_t bytes, int sets_override, int rounds) {
     free_sets(S);
 }
 
+
+template <int M>
+static void focus2_m(size_t bytes, int sets, int rounds) {
+    const size_t nvec = bytes / 16;
+    Sets S = make_sets(M, nvec, sets);
+    const int reps = std::max(10, std::min(300, (int)((8ull << 30) / ((M + 2) * bytes))));
+    auto args_for = [&](int i) {
+        Args a{};
+        auto& b = S.bufs[i % sets];
+        a.out = b[0];
+        a.acc = b[0];
+        for (int j = 0; j < M; ++j) a.ins[j] = b[j + 1];
+        a.nvec = nvec;
+        return a;
+    };
+    char tag[64];
+    std::snprintf(tag, sizeof tag, " sets=%d", sets);
+    for (int r = 0; r < rounds; ++r) {
+#define F(U, BL, CAP, NAME)                                                                             \
+    {                                                                                                  \
+        const size_t trips = (nvec + (size_t)BL * U - 1) / ((size_t)BL * U);                          \
+        const int grid = (int)std::min<size_t>(trips, CAP);                                            \
+        double us = time_launches([&](int i) { hipLaunchKernelGGL((k_reg<M, U, BL, true, true, true>), dim3(grid), dim3(BL), 0, 0, args_for(i)); }, reps); \
+        report((std::string(NAME) + tag).c_str(), M, bytes, us);                                      \
+    }
+        F(4, 256, 1 << 30, "NT U4 B256 full (shipped)");
+        {
+            double us = time_launches([&](int i) {
+                Args a = args_for(i);
+                const void* ins[8];
+                for (int j = 0; j < M; ++j) ins[j] = a.ins[j];
+                chr_reduce_multi(a.out, a.acc, ins, M, a.nvec * 4, CHR_FLOAT32, CHR_SUM, 0);
+            }, reps);
+            report((std::string("libchiara chr_reduce_multi") + tag).c_str(), M, bytes, us);
+        }
+        F(8, 256, 1 << 30, "NT U8 B256 full");
+        F(16, 256, 1 << 30, "NT U16 B256 full");
+        F(4, 512, 1 << 30, "NT U4 B512 full");
+        F(2, 1024, 1 << 30, "NT U2 B1024 full");
+        F(4, 1024, 1 << 30, "NT U4 B1024 full");
+        F(8, 256, 2048, "NT U8 B256 cap2048");
+        F(4, 256, 8192, "NT U4 B256 cap8192");
+#undef F
+        for (size_t blocks : {1024ul, 2048ul, 4096ul}) {
+            const size_t chunk = (nvec + blocks - 1) / blocks;
+            double us = time_launches([&](int i) { hipLaunchKernelGGL((k_chunk<M, 4, 256, true>), dim3(blocks), dim3(256), 0, 0, args_for(i), chunk); }, reps);
+            char name[64];
+            std::snprintf(name, sizeof name, "NT chunk U4 blocks=%zu%s", blocks, tag);
+            report(name, M, bytes, us);
+        }
+        std::printf("--\n");
+    }
+    free_sets(S);
+}
+
 // correctness spot check of every variant family against a host sum
 static void check() {
     const size_t nvec = (1 << 20) + 37;
@@ -389,6 +451,12 @@ static void check() {
 
 int main(int argc, char** argv) {
     check();
+    if (argc > 1 && std::string(argv[1]) == "focus2") {
+        focus2_m<1>(64 << 20, 16, 2);
+        focus2_m<1>(1024ull << 20, 1, 1);
+        focus2_m<3>(64 << 20, 8, 1);
+        return 0;
+    }
     if (argc > 1 && std::string(argv[1]) == "focus") {
         focus_m<1>(64 << 20, 16, 2);
         focus_m<1>(1024ull << 20, 1, 2);
