@@ -30,6 +30,9 @@ _IN_PLACE_PTR = 1     # CHR_IN_PLACE
 
 DTYPE_SIZE = {FLOAT32: 4, FLOAT64: 8, INT32: 4, BFLOAT16: 2}
 MODE_ALLREDUCE, MODE_REDUCE_SCATTER = 0, 1
+# MPICH baselines (testing/mpich_implementations/all_reduce/), chr_mode numbering
+MODE_MPICH_RING, MODE_MPICH_RD, MODE_MPICH_RSAG, MODE_MPICH_RECEXCH = 2, 3, 4, 5
+REDUCE_RUNNING_FIRST = 1  # chr_reduce_multi_ex flag (MPICH_do_reduce operand order)
 
 
 def _addr(buf):
@@ -186,6 +189,12 @@ class LocalGroup:
         R = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in recvbufs])
         return lib().chr_local_reduce_scatter_radix_batch(self._h, S, R, recvcount, datatype, op, k, b)
 
+    def allreduce_mpich(self, algo, sendbufs, recvbufs, count, datatype, op, k=2, single_phase_recv=0):
+        """algo: MODE_MPICH_RING / _RD / _RSAG / _RECEXCH."""
+        S = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in sendbufs])
+        R = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in recvbufs])
+        return lib().chr_local_allreduce_mpich(self._h, S, R, count, datatype, op, algo, k, single_phase_recv)
+
     def destroy(self):
         if self._h:
             lib().chr_local_group_destroy(self._h)
@@ -208,6 +217,41 @@ def all_reduce_radix_batch(sendbuf, recvbuf, count, datatype, op, comm, k, b, as
 def reduce_scatter_radix_batch(sendbuf, recvbuf, recvcount, datatype, op, comm, k, b, async_op=False):
     fn = lib().chr_reduce_scatter_radix_batch_async if async_op else lib().chr_reduce_scatter_radix_batch
     return fn(_addr(sendbuf), _addr(recvbuf), recvcount, datatype, op, comm.handle, k, b)
+
+
+# ---- MPICH baselines driven by testing/main.cpp (same names and argument order) -----------------
+
+def _mpich(algo, sendbuf, recvbuf, count, datatype, op, comm, k=0, single_phase_recv=0, async_op=False):
+    fn = lib().chr_allreduce_mpich_async if async_op else lib().chr_allreduce_mpich
+    return fn(_addr(sendbuf), _addr(recvbuf), count, datatype, op, comm.handle, algo, k, single_phase_recv)
+
+
+def MPICH_Allreduce_ring(sendbuf, recvbuf, count, datatype, op, comm, async_op=False):
+    """allreduce_ring.cpp:3 -- ring reduce-scatter (reduction :80) + allgatherv."""
+    return _mpich(MODE_MPICH_RING, sendbuf, recvbuf, count, datatype, op, comm, async_op=async_op)
+
+
+def MPICH_Allreduce_recursive_doubling(sendbuf, recvbuf, count, datatype, op, comm, async_op=False):
+    """allreduce_recursive_doubling.cpp:4."""
+    return _mpich(MODE_MPICH_RD, sendbuf, recvbuf, count, datatype, op, comm, async_op=async_op)
+
+
+def MPICH_Allreduce_reduce_scatter_allgather(sendbuf, recvbuf, count, datatype, op, comm, async_op=False):
+    """allreduce_reduce_scatter_allgather.cpp:3 (Rabenseifner)."""
+    return _mpich(MODE_MPICH_RSAG, sendbuf, recvbuf, count, datatype, op, comm, async_op=async_op)
+
+
+def MPICH_Allreduce_recursive_exchange(sendbuf, recvbuf, count, datatype, op, comm, k, single_phase_recv,
+                                       async_op=False):
+    """allreduce_recexch.cpp:188 -- k-way MPICH_do_reduce (:147-186) on the fused kernel."""
+    return _mpich(MODE_MPICH_RECEXCH, sendbuf, recvbuf, count, datatype, op, comm, k, single_phase_recv,
+                  async_op=async_op)
+
+
+def reduce_multi_ex(out, acc, ins, count, datatype, op, flags, stream=None):
+    arr = (ctypes.c_void_p * max(1, len(ins)))(*[_addr(x) for x in ins])
+    return lib().chr_reduce_multi_ex(_addr(out), _addr(acc), arr, len(ins), count, datatype, op, flags,
+                                     _stream(stream))
 
 
 # ---- plan introspection (host only) --------------------------------------------------------------
@@ -237,7 +281,8 @@ def parse_plan(text):
                     [int(tok[6]), int(tok[7]), int(tok[8])])
         m = int(tok[6])
         ins = [(tok[7 + 2 * j], int(tok[8 + 2 * j])) for j in range(m)]
-        return ("reduce", (tok[1], int(tok[2])), (tok[3], int(tok[4])), int(tok[5]), ins)
+        # "reduce_sw": running value first in every step (MPICH_do_reduce order)
+        return (tok[0], (tok[1], int(tok[2])), (tok[3], int(tok[4])), int(tok[5]), ins)
 
     for ln in lines[1:]:
         tok = ln.split()

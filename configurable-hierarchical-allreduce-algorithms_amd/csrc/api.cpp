@@ -49,9 +49,19 @@ int chr_reduce_multi(void* out, const void* acc, const void* const* ins, int m, 
     return status(chr::launch_reduce(out, acc, ins, m, n, dtype, op, stream));
 }
 
+int chr_reduce_multi_ex(void* out, const void* acc, const void* const* ins, int m, size_t n, chr_dtype dtype,
+                        chr_op op, int flags, hipStream_t stream) {
+    if (!chr::valid_dtype_op(dtype, op) || m < 0 || (flags & ~CHR_REDUCE_RUNNING_FIRST)) return CHR_ERR_INVALID_ARG;
+    if (n == 0) return CHR_SUCCESS;
+    if (!out || !acc || (m > 0 && !ins)) return CHR_ERR_INVALID_ARG;
+    for (int j = 0; j < m; ++j)
+        if (!ins[j]) return CHR_ERR_INVALID_ARG;
+    return status(chr::launch_reduce(out, acc, ins, m, n, dtype, op, stream, (flags & CHR_REDUCE_RUNNING_FIRST) != 0));
+}
+
 int chr_fill(void* buf, size_t n, chr_dtype dtype, int pattern, uint64_t seed, int rank, uint64_t count_for_seq,
              hipStream_t stream) {
-    if (!chr::dtype_size(dtype) || (pattern != 0 && pattern != 1)) return CHR_ERR_INVALID_ARG;
+    if (!chr::dtype_size(dtype) || (pattern < 0 || pattern > 2)) return CHR_ERR_INVALID_ARG;
     if (n == 0) return CHR_SUCCESS;
     if (!buf) return CHR_ERR_INVALID_ARG;
     return status(chr::launch_fill(buf, n, dtype, pattern, seed, rank, count_for_seq, stream));
@@ -59,7 +69,7 @@ int chr_fill(void* buf, size_t n, chr_dtype dtype, int pattern, uint64_t seed, i
 
 long chr_plan_describe(chr_mode mode, int nranks, int rank, int k, int b, size_t count, int slices, char* buf,
                        size_t len) {
-    if (mode != CHR_MODE_ALLREDUCE && mode != CHR_MODE_REDUCE_SCATTER) return -1;
+    if (mode < CHR_MODE_ALLREDUCE || mode > CHR_MODE_MPICH_RECEXCH) return -1;
     const std::string s = chr::describe(chr::build_plan((chr::Mode)mode, nranks, rank, k, b, count, slices));
     if (buf && len) {
         const size_t c = s.size() < len - 1 ? s.size() : len - 1;

@@ -13,10 +13,12 @@ namespace chr {
 size_t dtype_size(int dtype);
 bool valid_dtype_op(int dtype, int op);
 
-// Fused bucket reduction: out = (...((acc op ins[0]) op ins[1])...) op ins[m-1].
-// Device pointers.  m may exceed the kernel's fan-in: chained left to right.
+// Fused bucket reduction: out = (...((acc op ins[0]) op ins[1])...) op ins[m-1], each step
+// MPI_Reduce_local(ins[j], acc) = OP(ins[j], acc); with running_first each step is
+// OP(acc, ins[j]) instead (MPICH_do_reduce's order).  Device pointers.  m may exceed the
+// kernel's fan-in: chained left to right.
 hipError_t launch_reduce(void* out, const void* acc, const void* const* ins, int m, size_t n,
-                         int dtype, int op, hipStream_t stream);
+                         int dtype, int op, hipStream_t stream, bool running_first = false);
 
 hipError_t launch_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int rank,
                        uint64_t count_for_seq, hipStream_t stream);

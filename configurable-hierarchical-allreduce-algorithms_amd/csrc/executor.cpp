@@ -137,7 +137,7 @@ int run_local(const chr::LocalOp& op, const Bufs& B, int dtype, int rop, hipStre
         (void)hipEventRecord(ev.first, s);
     }
     const int rc = hip_code(chr::launch_reduce(B.ptr(op.dst), B.ptr(op.acc), ins.data(), (int)ins.size(), op.count,
-                                               dtype, rop, s));
+                                               dtype, rop, s, op.swap));
     if (timed) {
         (void)hipEventRecord(ev.second, s);
         prof->pending.push_back(ev);
@@ -162,6 +162,7 @@ using PlanKey = std::tuple<int, int, int, int, uint64_t, int, int>;  // mode, ra
 
 // Pipeline depth: explicit setting, else CHR_SLICES, else by chunk size (schedule.cpp).
 int pick_slices(int setting, uint64_t count, int mode, int nranks, int b, size_t es) {
+    if (chr::is_mpich(mode)) return 1;  // the MPICH baselines run unpipelined, as written
     if (setting > 0) return setting;
     static const int env = [] {
         const char* v = std::getenv("CHR_SLICES");
@@ -505,6 +506,29 @@ int chr_local_allreduce_radix_batch(chr_local_group* g, const void* const* sends
 int chr_local_reduce_scatter_radix_batch(chr_local_group* g, const void* const* sends, void* const* recvs,
                                          size_t recvcount, chr_dtype dtype, chr_op op, int k, int b) {
     return local_collective(g, chr::MODE_REDUCE_SCATTER, sends, recvs, recvcount, dtype, op, k, b);
+}
+
+static bool valid_mpich_mode(chr_mode m) {
+    return m == CHR_MODE_MPICH_RING || m == CHR_MODE_MPICH_RD || m == CHR_MODE_MPICH_RSAG ||
+           m == CHR_MODE_MPICH_RECEXCH;
+}
+
+int chr_allreduce_mpich(const void* send, void* recv, size_t count, chr_dtype dtype, chr_op op, chr_comm* comm,
+                        chr_mode algo, int k, int single_phase_recv) {
+    if (!valid_mpich_mode(algo)) return CHR_ERR_INVALID_ARG;
+    return collective(comm, algo, send, recv, count, dtype, op, k, single_phase_recv, true);
+}
+
+int chr_allreduce_mpich_async(const void* send, void* recv, size_t count, chr_dtype dtype, chr_op op, chr_comm* comm,
+                              chr_mode algo, int k, int single_phase_recv) {
+    if (!valid_mpich_mode(algo)) return CHR_ERR_INVALID_ARG;
+    return collective(comm, algo, send, recv, count, dtype, op, k, single_phase_recv, false);
+}
+
+int chr_local_allreduce_mpich(chr_local_group* g, const void* const* sends, void* const* recvs, size_t count,
+                              chr_dtype dtype, chr_op op, chr_mode algo, int k, int single_phase_recv) {
+    if (!valid_mpich_mode(algo)) return CHR_ERR_INVALID_ARG;
+    return local_collective(g, algo, sends, recvs, count, dtype, op, k, single_phase_recv);
 }
 
 }  // extern "C"

@@ -76,24 +76,38 @@ template <> struct DTy<CHR_FLOAT64> { using T = double; };
 template <> struct DTy<CHR_INT32> { using T = int32_t; };
 template <> struct DTy<CHR_BFLOAT16> { using T = uint16_t; };
 
-// acc_new = OP(in, acc): MPICH argument order (a = inbuf, b = inoutbuf).
+// Internal op codes for the running-value-first order of MPICH_do_reduce
+// (allreduce_recexch.cpp:147-186): each step is MPI_Reduce_local(running, next).  SUM and
+// PROD are bitwise commutative (IEEE add/mul, wrapping int, bf16 RNE of a commutative f32
+// op), so only MAX/MIN need their own instantiations (they differ on ties such as -0/+0
+// and on NaN compares).
+constexpr int kMaxSw = 6, kMinSw = 7;
+
+// MPI_Reduce_local(in = x, inout = y): MPICH 3.3.2's loop is inout = OP(inout, in) with
+// MAX(p, q) = p > q ? p : q (MPIR_OP_TYPE_REDUCE_CASE, a = inoutvec, b = invec), so MAX/MIN
+// keep the accumulator on ties and NaN compares.  kMaxSw/kMinSw: the running value is the
+// `in` operand and the result takes the place of the incoming buffer: OP(x, y).
 template <int DT, int OP>
 __device__ __forceinline__ typename DTy<DT>::T apply(typename DTy<DT>::T x, typename DTy<DT>::T y) {
     if constexpr (DT == CHR_BFLOAT16) {
         const float fx = bf2f(x), fy = bf2f(y);
-        if constexpr (OP == CHR_SUM) return f2bf(fx + fy);
-        else if constexpr (OP == CHR_PROD) return f2bf(fx * fy);
-        else if constexpr (OP == CHR_MAX) return fx > fy ? x : y;
+        if constexpr (OP == CHR_SUM) return f2bf(fy + fx);
+        else if constexpr (OP == CHR_PROD) return f2bf(fy * fx);
+        else if constexpr (OP == CHR_MAX) return fy > fx ? y : x;
+        else if constexpr (OP == CHR_MIN) return fy < fx ? y : x;
+        else if constexpr (OP == kMaxSw) return fx > fy ? x : y;
         else return fx < fy ? x : y;
     } else if constexpr (DT == CHR_INT32) {
-        if constexpr (OP == CHR_SUM) return (int32_t)((uint32_t)x + (uint32_t)y);
-        else if constexpr (OP == CHR_PROD) return (int32_t)((uint32_t)x * (uint32_t)y);
-        else if constexpr (OP == CHR_MAX) return x > y ? x : y;
-        else return x < y ? x : y;
+        if constexpr (OP == CHR_SUM) return (int32_t)((uint32_t)y + (uint32_t)x);
+        else if constexpr (OP == CHR_PROD) return (int32_t)((uint32_t)y * (uint32_t)x);
+        else if constexpr (OP == CHR_MAX || OP == kMaxSw) return y > x ? y : x;
+        else return y < x ? y : x;
     } else {
-        if constexpr (OP == CHR_SUM) return x + y;
-        else if constexpr (OP == CHR_PROD) return x * y;
-        else if constexpr (OP == CHR_MAX) return x > y ? x : y;
+        if constexpr (OP == CHR_SUM) return y + x;
+        else if constexpr (OP == CHR_PROD) return y * x;
+        else if constexpr (OP == CHR_MAX) return y > x ? y : x;
+        else if constexpr (OP == CHR_MIN) return y < x ? y : x;
+        else if constexpr (OP == kMaxSw) return x > y ? x : y;
         else return x < y ? x : y;
     }
 }
@@ -132,8 +146,11 @@ __device__ __forceinline__ void st(u32x4* p, u32x4 v) {
 
 // U vectors (16 B each) per lane per trip; all M+1 operands of the trip are loaded
 // before the first add so (M+1)*U*16 bytes per lane are in flight.  NT: non-temporal
-// loads and stores (global_load/store_dwordx4 ... nt) for calls that stream far more
-// than the caches hold: measured +15-40 % on HBM-cold buckets.
+// loads of the incoming buckets and non-temporal stores (global_load/store_dwordx4 ...
+// nt) for calls that stream far more than the caches hold: measured +15-40 % on HBM-cold
+// buckets.  The accumulator stream keeps the default policy even then: per-slot policy
+// sweep (profiles/r01/microbench_focus4.txt) +15 % at 1 GiB m=1, +9 % at 512 MiB m=3,
+// never slower.
 template <int DT, int OP, int M, int U, bool NT>
 __global__ __launch_bounds__(kBlock) void k_reduce_vec(VecArgs a) {
     const size_t stride = (size_t)gridDim.x * kBlock * U;
@@ -141,7 +158,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(VecArgs a) {
         if (base + (size_t)(U - 1) * kBlock < a.nvec) {
             u32x4 acc[U], x[M][U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) acc[u] = ld<NT>(&a.acc[base + (size_t)u * kBlock]);
+            for (int u = 0; u < U; ++u) acc[u] = ld<false>(&a.acc[base + (size_t)u * kBlock]);
 #pragma unroll
             for (int j = 0; j < M; ++j)
 #pragma unroll
@@ -229,6 +246,12 @@ static hipError_t launch_vec_dt(const VecArgs& a, int m, int op, hipStream_t s) 
     case CHR_PROD: return launch_vec_op<DT, CHR_PROD>(a, m, s);
     case CHR_MAX: return launch_vec_op<DT, CHR_MAX>(a, m, s);
     case CHR_MIN: return launch_vec_op<DT, CHR_MIN>(a, m, s);
+    case kMaxSw:
+        if constexpr (DT == CHR_INT32) return launch_vec_op<DT, CHR_MAX>(a, m, s);
+        else return launch_vec_op<DT, kMaxSw>(a, m, s);
+    case kMinSw:
+        if constexpr (DT == CHR_INT32) return launch_vec_op<DT, CHR_MIN>(a, m, s);
+        else return launch_vec_op<DT, kMinSw>(a, m, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -242,6 +265,8 @@ static hipError_t launch_scalar_dt(const ScalarArgs& a, int op, hipStream_t s) {
     case CHR_PROD: hipLaunchKernelGGL((k_reduce_scalar<DT, CHR_PROD>), dim3(grid), dim3(kBlock), 0, s, a); break;
     case CHR_MAX: hipLaunchKernelGGL((k_reduce_scalar<DT, CHR_MAX>), dim3(grid), dim3(kBlock), 0, s, a); break;
     case CHR_MIN: hipLaunchKernelGGL((k_reduce_scalar<DT, CHR_MIN>), dim3(grid), dim3(kBlock), 0, s, a); break;
+    case kMaxSw: hipLaunchKernelGGL((k_reduce_scalar<DT, kMaxSw>), dim3(grid), dim3(kBlock), 0, s, a); break;
+    case kMinSw: hipLaunchKernelGGL((k_reduce_scalar<DT, kMinSw>), dim3(grid), dim3(kBlock), 0, s, a); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -305,8 +330,10 @@ static hipError_t launch_group(void* out, const void* acc, const void* const* in
 }
 
 hipError_t launch_reduce(void* out, const void* acc, const void* const* ins, int m, size_t n, int dtype, int op,
-                         hipStream_t stream) {
+                         hipStream_t stream, bool running_first) {
     if (n == 0) return hipSuccess;
+    if (op < CHR_SUM || op > CHR_MIN) return hipErrorInvalidValue;
+    if (running_first && (op == CHR_MAX || op == CHR_MIN)) op = op == CHR_MAX ? kMaxSw : kMinSw;
     const size_t es = dtype_size(dtype);
     if (m == 0) {
         if (out == acc) return hipSuccess;
@@ -340,6 +367,21 @@ __global__ __launch_bounds__(kBlock) void k_fill(void* buf, size_t n, int dtype,
             case CHR_FLOAT64: ((double*)buf)[i] = (double)v; break;
             case CHR_INT32: ((int32_t*)buf)[i] = v; break;
             default: ((uint16_t*)buf)[i] = f2bf((float)v); break;
+            }
+        } else if (pattern == 2) {  // ties / signed zeros / per-rank NaN payloads
+            const unsigned sel = (unsigned)(splitmix64(seed ^ (rank << 40) ^ (uint64_t)i) >> 61);
+            const uint32_t pay = (uint32_t)(rank + 1) & 0x3Fu;
+            const float fv = sel == 2 ? 1.0f : sel == 3 ? -1.0f : sel == 6 ? 0.5f : (sel & 1) ? -0.0f : 0.0f;
+            switch (dtype) {
+            case CHR_FLOAT32:
+                ((uint32_t*)buf)[i] = sel == 7 ? (0x7FC00000u | (pay << 16) | pay) : __float_as_uint(fv);
+                break;
+            case CHR_FLOAT64:
+                ((uint64_t*)buf)[i] = sel == 7 ? (0x7FF8000000000000ull | ((uint64_t)pay << 40) | pay)
+                                               : (uint64_t)__double_as_longlong((double)fv);
+                break;
+            case CHR_INT32: ((int32_t*)buf)[i] = sel == 6 ? 2 : sel == 7 ? 7 : sel == 2 ? 1 : sel == 3 ? -1 : 0; break;
+            default: ((uint16_t*)buf)[i] = sel == 7 ? (uint16_t)(0x7FC0u | pay) : f2bf(fv); break;
             }
         } else {
             const uint64_t u = splitmix64(seed ^ (rank << 40) ^ (uint64_t)i);

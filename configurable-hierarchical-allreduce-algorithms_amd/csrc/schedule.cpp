@@ -298,6 +298,7 @@ int auto_slices(uint64_t irc_bytes) {
 }
 
 Plan build_plan(Mode mode, int n, int me, int k_in, int b, uint64_t count, int slices) {
+    if (is_mpich(mode)) return build_plan_mpich(mode, n, me, k_in, b, count);
     Plan p;
     p.mode = mode;
     p.rank = me;
@@ -442,7 +443,7 @@ std::string describe(const Plan& p) {
             o << "copy2d " << buf_name(op.dst.buf) << " " << op.dst.off << " " << buf_name(op.acc.buf) << " "
               << op.acc.off << " " << op.count << " " << op.rows << " " << op.dpitch << " " << op.spitch << "\n";
         } else {
-            o << "reduce " << buf_name(op.dst.buf) << " " << op.dst.off << " " << buf_name(op.acc.buf) << " "
+            o << (op.swap ? "reduce_sw " : "reduce ") << buf_name(op.dst.buf) << " " << op.dst.off << " " << buf_name(op.acc.buf) << " "
               << op.acc.off << " " << op.count << " " << op.ins.size();
             for (const Ref& r : op.ins) o << " " << buf_name(r.buf) << " " << r.off;
             o << "\n";
@@ -462,6 +463,249 @@ std::string describe(const Plan& p) {
         for (const LocalOp& op : s.post) local(op);
     }
     return o.str();
+}
+
+}  // namespace chr
+
+// ==== MPICH baseline allreduces driven by the reference's testing/main.cpp ==================
+// (testing/mpich_implementations/all_reduce/*.cpp).  They work in
+// recvbuf; STAGE holds incoming blocks; every reduction goes through the same fused kernel.
+namespace chr {
+namespace {
+
+struct MB {
+    Plan& p;
+    int n, me;
+    uint64_t count;
+    Step& add(const char* label) {
+        p.steps.emplace_back();
+        p.steps.back().label = label;
+        return p.steps.back();
+    }
+    void need(uint64_t e) { p.stage_elems = std::max(p.stage_elems, e); }
+    // recvbuf[off, +len) = OP(STAGE[soff], recvbuf)  (MPI_Reduce_local(tmp, recvbuf + off))
+    void reduce_in(Step& s, uint64_t off, uint64_t soff, uint64_t len, int site) {
+        if (len) s.post.push_back(make_reduce({BUF_RECV, off}, {BUF_RECV, off}, {{BUF_STAGE, soff}}, len, site));
+    }
+};
+
+// Fold of the non-power-of-two ranks (recursive doubling :35-55, reduce_scatter_allgather :28-52):
+// even r < 2*rem sends its whole buffer to r+1, which reduces it.
+void mb_fold(MB& b, int rem, int site) {
+    Step& s = b.add("fold");
+    if (b.me < 2 * rem) {
+        if (b.me % 2 == 0) {
+            s.sends.push_back({b.me + 1, {BUF_RECV, 0}, b.count});
+        } else {
+            s.recvs.push_back({b.me - 1, {BUF_STAGE, 0}, b.count});
+            b.need(b.count);
+            b.reduce_in(s, 0, 0, b.count, site);
+        }
+    }
+}
+void mb_unfold(MB& b, int rem) {  // :88-97 / :161-171
+    Step& s = b.add("unfold");
+    if (b.me < 2 * rem) {
+        if (b.me % 2) s.sends.push_back({b.me - 1, {BUF_RECV, 0}, b.count});
+        else s.recvs.push_back({b.me + 1, {BUF_RECV, 0}, b.count});
+    }
+}
+
+void build_ring(MB& b) {  // allreduce_ring.cpp:3-104
+    const int n = b.n, me = b.me;
+    std::vector<uint64_t> cnts(n, 0), displs(n, 0);
+    uint64_t total = 0;
+    for (int i = 0; i < n; ++i) {  // :31-38
+        cnts[i] = (b.count + n - 1) / n;
+        if (total + cnts[i] > b.count) {
+            cnts[i] = b.count - total;
+            break;
+        }
+        total += cnts[i];
+    }
+    for (int i = 1; i < n; ++i) displs[i] = displs[i - 1] + cnts[i - 1];
+    const int src = (n + me - 1) % n, dst = (me + 1) % n;
+    for (int i = 0; i < n - 1; ++i) {  // :56-84
+        Step& s = b.add("ring-rs");
+        const int recv_rank = (2 * n + me - 2 - i) % n, send_rank = (2 * n + me - 1 - i) % n;
+        if (cnts[send_rank]) s.sends.push_back({dst, {BUF_RECV, displs[send_rank]}, cnts[send_rank]});
+        if (cnts[recv_rank]) {
+            s.recvs.push_back({src, {BUF_STAGE, 0}, cnts[recv_rank]});
+            b.need(cnts[recv_rank]);
+            b.reduce_in(s, displs[recv_rank], 0, cnts[recv_rank], 80);
+        }
+    }
+    Step& s = b.add("allgatherv");  // MPI_Allgatherv (:86): block j is final on rank j
+    for (int j = 0; j < n; ++j) {
+        if (j == me) continue;
+        if (cnts[me]) s.sends.push_back({j, {BUF_RECV, displs[me]}, cnts[me]});
+        if (cnts[j]) s.recvs.push_back({j, {BUF_RECV, displs[j]}, cnts[j]});
+    }
+}
+
+void build_rd(MB& b) {  // allreduce_recursive_doubling.cpp:4-101 (commutative path)
+    int pof2 = 1;
+    while (pof2 <= b.n) pof2 <<= 1;
+    pof2 >>= 1;
+    const int rem = b.n - pof2;
+    mb_fold(b, rem, 48);
+    const int newrank = b.me < 2 * rem ? (b.me % 2 ? b.me / 2 : -1) : b.me - rem;
+    for (int mask = 1; mask < pof2; mask <<= 1) {
+        Step& s = b.add("rd");
+        if (newrank < 0) continue;
+        const int newdst = newrank ^ mask, dst = newdst < rem ? newdst * 2 + 1 : newdst + rem;
+        s.sends.push_back({dst, {BUF_RECV, 0}, b.count});
+        s.recvs.push_back({dst, {BUF_STAGE, 0}, b.count});
+        b.need(b.count);
+        b.reduce_in(s, 0, 0, b.count, 70);
+    }
+    mb_unfold(b, rem);
+}
+
+void build_rsag(MB& b) {  // allreduce_reduce_scatter_allgather.cpp:3-173
+    int pof2 = 1;
+    while (pof2 <= b.n) pof2 *= 2;
+    pof2 /= 2;
+    const int rem = b.n - pof2;
+    mb_fold(b, rem, 43);
+    const int newrank = b.me < 2 * rem ? (b.me % 2 ? b.me / 2 : -1) : b.me - rem;
+    std::vector<uint64_t> cnts(pof2), disps(pof2, 0);
+    for (int i = 0; i < pof2; ++i) cnts[i] = b.count / pof2 + ((uint64_t)i < b.count % pof2 ? 1 : 0);
+    for (int i = 1; i < pof2; ++i) disps[i] = disps[i - 1] + cnts[i - 1];
+    auto sum = [&](int a, int e) {
+        uint64_t t = 0;
+        for (int i = a; i < e; ++i) t += cnts[i];
+        return t;
+    };
+    int send_idx = 0, recv_idx = 0, last_idx = pof2;
+    int mask = 1;
+    for (; mask < pof2; mask <<= 1) {  // reduce-scatter (:76-117)
+        Step& s = b.add("rsag-rs");
+        if (newrank < 0) continue;
+        const int newdst = newrank ^ mask, dst = newdst < rem ? newdst * 2 + 1 : newdst + rem;
+        uint64_t send_cnt, recv_cnt;
+        if (newrank < newdst) {
+            send_idx = recv_idx + pof2 / (mask * 2);
+            send_cnt = sum(send_idx, last_idx);
+            recv_cnt = sum(recv_idx, send_idx);
+        } else {
+            recv_idx = send_idx + pof2 / (mask * 2);
+            send_cnt = sum(send_idx, recv_idx);
+            recv_cnt = sum(recv_idx, last_idx);
+        }
+        if (send_cnt) s.sends.push_back({dst, {BUF_RECV, disps[send_idx]}, send_cnt});
+        if (recv_cnt) {
+            s.recvs.push_back({dst, {BUF_STAGE, disps[recv_idx]}, recv_cnt});
+            b.need(b.count);
+            b.reduce_in(s, disps[recv_idx], disps[recv_idx], recv_cnt, 104);
+        }
+        send_idx = recv_idx;
+        if ((mask << 1) < pof2) last_idx = recv_idx + pof2 / (mask << 1);
+    }
+    for (mask >>= 1; mask > 0; mask >>= 1) {  // allgather (:119-160)
+        Step& s = b.add("rsag-ag");
+        if (newrank < 0) continue;
+        const int newdst = newrank ^ mask, dst = newdst < rem ? newdst * 2 + 1 : newdst + rem;
+        uint64_t send_cnt, recv_cnt;
+        if (newrank < newdst) {
+            if (mask != pof2 / 2) last_idx = last_idx + pof2 / (mask * 2);
+            recv_idx = send_idx + pof2 / (mask * 2);
+            send_cnt = sum(send_idx, recv_idx);
+            recv_cnt = sum(recv_idx, last_idx);
+        } else {
+            recv_idx = send_idx - pof2 / (mask * 2);
+            send_cnt = sum(send_idx, last_idx);
+            recv_cnt = sum(recv_idx, send_idx);
+        }
+        if (send_cnt) s.sends.push_back({dst, {BUF_RECV, disps[send_idx]}, send_cnt});
+        if (recv_cnt) s.recvs.push_back({dst, {BUF_RECV, disps[recv_idx]}, recv_cnt});
+        if (newrank > newdst) send_idx = recv_idx;
+    }
+    mb_unfold(b, rem);
+}
+
+void build_recexch(MB& b, int k_in) {  // allreduce_recexch.cpp:188-440 (float path)
+    if (b.n == 1) return;
+    Recexch x;
+    if (recexch_neighbors(b.me, b.n, k_in, &x)) {
+        b.p.error = 1;
+        return;
+    }
+    const int k = x.k;
+    const uint64_t cnt = b.count;
+    {  // step 1 (:267-296): non-participants send, participants reduce in recvfrom order
+        Step& s = b.add("rx-step1");
+        if (x.step1_sendto != -1) {
+            s.sends.push_back({x.step1_sendto, {BUF_RECV, 0}, cnt});
+        } else if (x.step1_nrecvs) {
+            std::vector<Ref> ins;
+            for (int i = 0; i < x.step1_nrecvs; ++i) {
+                s.recvs.push_back({x.step1_recvfrom[i], {BUF_STAGE, (uint64_t)i * cnt}, cnt});
+                ins.push_back({BUF_STAGE, (uint64_t)i * cnt});
+            }
+            b.need((uint64_t)x.step1_nrecvs * cnt);
+            s.post.push_back(make_reduce({BUF_RECV, 0}, {BUF_RECV, 0}, ins, cnt, 298));
+        }
+    }
+    for (int ph = 0; ph < x.step2_nphases; ++ph) {  // step 2 (:298-365)
+        Step& s = b.add("rx-phase");
+        if (x.step1_sendto != -1) continue;
+        for (int i = 0; i < k - 1; ++i) {
+            s.sends.push_back({x.step2_nbrs[ph][i], {BUF_RECV, 0}, cnt});
+            s.recvs.push_back({x.step2_nbrs[ph][i], {BUF_STAGE, (uint64_t)i * cnt}, cnt});
+        }
+        b.need((uint64_t)(k - 1) * cnt);
+        // MPICH_do_reduce (:147-186): fold [b_0..b_{idx-1}, recv, b_idx..b_{k-2}] left to right
+        // with the running value as the FIRST operand; MPICH_find_myidx (:137-145) picks idx.
+        int idx = k - 1;
+        for (int i = 0; i < k - 1; ++i)
+            if (x.step2_nbrs[ph][i] > b.me) {
+                idx = i;
+                break;
+            }
+        std::vector<Ref> seq;
+        for (int i = 0; i < idx; ++i) seq.push_back({BUF_STAGE, (uint64_t)i * cnt});
+        seq.push_back({BUF_RECV, 0});
+        for (int i = idx; i < k - 1; ++i) seq.push_back({BUF_STAGE, (uint64_t)i * cnt});
+        LocalOp op = make_reduce({BUF_RECV, 0}, seq[0], std::vector<Ref>(seq.begin() + 1, seq.end()), cnt, 153);
+        op.swap = true;
+        s.post.push_back(op);
+    }
+    {  // step 3 (:367-386)
+        Step& s = b.add("rx-step3");
+        if (x.step1_sendto != -1) s.recvs.push_back({x.step1_sendto, {BUF_RECV, 0}, cnt});
+        else
+            for (int i = 0; i < x.step1_nrecvs; ++i) s.sends.push_back({x.step1_recvfrom[i], {BUF_RECV, 0}, cnt});
+    }
+}
+
+}  // namespace
+
+Plan build_plan_mpich(Mode mode, int n, int me, int k, int aux, uint64_t count) {
+    (void)aux;  // recexch single_phase_recv: buffering only, same data flow
+    Plan p;
+    p.mode = mode;
+    p.rank = me;
+    if (n < 1 || me < 0 || me >= n || (mode == MODE_MPICH_RECEXCH && k < 2)) {
+        p.error = 1;
+        return p;
+    }
+    p.g.nranks = n;
+    p.g.k = k;
+    p.g.total = count;
+    p.send_elems = p.recv_elems = count;
+    if (count == 0) return p;
+    // pre: recvbuf <- sendbuf (every algorithm starts with this memcpy; no-op in place)
+    p.pre.push_back(make_copy({BUF_RECV, 0}, {BUF_SEND, 0}, count, 0));
+    MB b{p, n, me, count};
+    switch (mode) {
+    case MODE_MPICH_RING: build_ring(b); break;
+    case MODE_MPICH_RD: build_rd(b); break;
+    case MODE_MPICH_RSAG: build_rsag(b); break;
+    case MODE_MPICH_RECEXCH: build_recexch(b, k); break;
+    default: p.error = 1;
+    }
+    return p;
 }
 
 }  // namespace chr

@@ -49,6 +49,7 @@ struct LocalOp {
     uint64_t count;
     int site;  // reference call site this op restates (line in all_reduce_radix_batch.cpp)
     uint64_t rows = 1, dpitch = 0, spitch = 0;
+    bool swap = false;  // L_REDUCE: running value is the FIRST operand, OP(acc, in) (MPICH_do_reduce)
 };
 
 struct Step {
@@ -57,7 +58,15 @@ struct Step {
     std::string label;
 };
 
-enum Mode : int { MODE_ALLREDUCE = 0, MODE_REDUCE_SCATTER = 1 };
+enum Mode : int {
+    MODE_ALLREDUCE = 0,        // all_reduce_radix_batch
+    MODE_REDUCE_SCATTER = 1,   // reduce_scatter_radix_batch
+    MODE_MPICH_RING = 2,       // testing/mpich_implementations/all_reduce/allreduce_ring.cpp
+    MODE_MPICH_RD = 3,         // .../allreduce_recursive_doubling.cpp
+    MODE_MPICH_RSAG = 4,       // .../allreduce_reduce_scatter_allgather.cpp
+    MODE_MPICH_RECEXCH = 5     // .../allreduce_recexch.cpp (k, single_phase_recv)
+};
+inline bool is_mpich(int mode) { return mode >= MODE_MPICH_RING && mode <= MODE_MPICH_RECEXCH; }
 
 struct Geometry {
     int nranks = 0, b = 0, k = 0, nnodes = 0, nstages = 0, nu = 0, nph = 0;
@@ -94,6 +103,8 @@ void recexch_count_offset(int nranks, int max_phases, int k, std::vector<int>* c
 // The per-element reduction order is unchanged (results are bit-identical for any depth).
 Plan build_plan(Mode mode, int nranks, int rank, int k, int b, uint64_t count, int slices = 1);
 int auto_slices(uint64_t irc_bytes);
+// MPICH baseline allreduces (count = elements per rank; aux = recexch single_phase_recv).
+Plan build_plan_mpich(Mode mode, int nranks, int rank, int k, int aux, uint64_t count);
 std::string describe(const Plan& p);
 
 }  // namespace chr

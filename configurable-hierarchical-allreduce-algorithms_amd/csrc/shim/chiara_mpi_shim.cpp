@@ -8,6 +8,10 @@
 //       replaces Fugaku_experiments/Allreduce/all_reduce_radix_batch.cpp:202-204
 //   int reduce_scatter_radix_batch(const void*, void*, MPI_Aint, MPI_Datatype, MPI_Op, MPI_Comm, int, int)
 //       replaces Fugaku_experiments/Reduce-scatter/reduce_scatter_radix_batch.cpp:200-202
+//   MPICH_Allreduce_{ring, recursive_doubling, reduce_scatter_allgather, recursive_exchange}
+//       replace testing/mpich_implementations/all_reduce/allreduce_{ring.cpp:3,
+//       recursive_doubling.cpp:4, reduce_scatter_allgather.cpp:3, recexch.cpp:188}
+//       (the baselines testing/main.cpp times CHiArA against)
 //
 // One chr_comm per MPI communicator, created on first use (RCCL unique id broadcast with
 // MPI_Bcast, device = node-local rank mod visible GPUs) and cached as an MPI attribute.
@@ -99,4 +103,41 @@ int reduce_scatter_radix_batch(const void* sendbuf, void* recvbuf, MPI_Aint recv
     if (!c) return MPI_ERR_OTHER;
     const void* send = sendbuf == MPI_IN_PLACE ? CHR_IN_PLACE : sendbuf;
     return to_mpi(chr_reduce_scatter_radix_batch(send, recvbuf, (size_t)recvcount, dt, o, c, k, b));
+}
+
+namespace {
+
+int mpich_call(chr_mode algo, const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+               MPI_Comm comm, int k, int single_phase_recv) {
+    chr_dtype dt;
+    chr_op o;
+    if (!map_type(datatype, &dt)) return MPI_ERR_TYPE;
+    if (!map_op(op, &o)) return MPI_ERR_OP;
+    if (count < 0) return MPI_ERR_COUNT;
+    chr_comm* c = comm_for(comm);
+    if (!c) return MPI_ERR_OTHER;
+    const void* send = sendbuf == (const char*)MPI_IN_PLACE ? CHR_IN_PLACE : (const void*)sendbuf;
+    return to_mpi(chr_allreduce_mpich(send, recvbuf, (size_t)count, dt, o, c, algo, k, single_phase_recv));
+}
+
+}  // namespace
+
+int MPICH_Allreduce_ring(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+                         MPI_Comm comm) {
+    return mpich_call(CHR_MODE_MPICH_RING, sendbuf, recvbuf, count, datatype, op, comm, 0, 0);
+}
+
+int MPICH_Allreduce_recursive_doubling(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype,
+                                       MPI_Op op, MPI_Comm comm) {
+    return mpich_call(CHR_MODE_MPICH_RD, sendbuf, recvbuf, count, datatype, op, comm, 0, 0);
+}
+
+int MPICH_Allreduce_reduce_scatter_allgather(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype,
+                                             MPI_Op op, MPI_Comm comm) {
+    return mpich_call(CHR_MODE_MPICH_RSAG, sendbuf, recvbuf, count, datatype, op, comm, 0, 0);
+}
+
+int MPICH_Allreduce_recursive_exchange(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype,
+                                       MPI_Op op, MPI_Comm comm, int k, int single_phase_recv) {
+    return mpich_call(CHR_MODE_MPICH_RECEXCH, sendbuf, recvbuf, count, datatype, op, comm, k, single_phase_recv);
 }

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define CHR_ABI_VERSION 1
+#define CHR_ABI_VERSION 2
 
 typedef enum {
     CHR_FLOAT32 = 0,   /* MPI_FLOAT */
@@ -64,6 +64,14 @@ int chr_reduce_local(const void* in, void* inout, size_t n, chr_dtype dtype, chr
  * (all_reduce_radix_batch.cpp:343-364, :523-530).  `out` may alias `acc`. m >= 0. */
 int chr_reduce_multi(void* out, const void* acc, const void* const* ins, int m, size_t n,
                      chr_dtype dtype, chr_op op, hipStream_t stream);
+/* chr_reduce_multi with flags.  CHR_REDUCE_RUNNING_FIRST: the running value is the FIRST
+ * operand of every step, acc = acc (op) ins[j], i.e. MPI_Reduce_local(acc, ins[j]) chained
+ * the way MPICH_do_reduce does it
+ * (testing/mpich_implementations/all_reduce/allreduce_recexch.cpp:147-186).  Only MAX/MIN
+ * on floating types can differ bitwise from the default order (ties of -0/+0, NaN). */
+#define CHR_REDUCE_RUNNING_FIRST 1
+int chr_reduce_multi_ex(void* out, const void* acc, const void* const* ins, int m, size_t n,
+                        chr_dtype dtype, chr_op op, int flags, hipStream_t stream);
 
 /* ---- communicator (replaces MPI_Comm + MPI p2p: RCCL over xGMI) -------------------- */
 typedef struct chr_comm chr_comm;
@@ -133,13 +141,41 @@ int chr_local_reduce_scatter_radix_batch(chr_local_group* group, const void* con
  * plan of steps; each step is one RCCL group of sends/receives followed by local ops.
  * chr_plan_describe writes rank `rank`'s plan as text (one op per line) into buf
  * (truncated to len, NUL-terminated); returns the length needed (excluding NUL) or < 0. */
-typedef enum { CHR_MODE_ALLREDUCE = 0, CHR_MODE_REDUCE_SCATTER = 1 } chr_mode;
+typedef enum {
+    CHR_MODE_ALLREDUCE = 0,        /* all_reduce_radix_batch */
+    CHR_MODE_REDUCE_SCATTER = 1,   /* reduce_scatter_radix_batch */
+    CHR_MODE_MPICH_RING = 2,       /* testing/mpich_implementations/all_reduce/allreduce_ring.cpp:3 */
+    CHR_MODE_MPICH_RD = 3,         /* .../allreduce_recursive_doubling.cpp:4 */
+    CHR_MODE_MPICH_RSAG = 4,       /* .../allreduce_reduce_scatter_allgather.cpp:3 */
+    CHR_MODE_MPICH_RECEXCH = 5     /* .../allreduce_recexch.cpp:188 (k, b = single_phase_recv) */
+} chr_mode;
 long chr_plan_describe(chr_mode mode, int nranks, int rank, int k, int b, size_t count,
                        int slices, char* buf, size_t len);
 
+/* ---- MPICH baseline allreduces (the ones testing/main.cpp benchmarks CHiArA against) --
+ * Replace  int MPICH_Allreduce_ring(const char* sendbuf, char* recvbuf, int count,
+ *            MPI_Datatype, MPI_Op, MPI_Comm)                       (allreduce_ring.cpp:3)
+ *          MPICH_Allreduce_recursive_doubling(...)        (allreduce_recursive_doubling.cpp:4)
+ *          MPICH_Allreduce_reduce_scatter_allgather(...)  (allreduce_reduce_scatter_allgather.cpp:3)
+ *          MPICH_Allreduce_recursive_exchange(..., int k, int single_phase_recv)
+ *                                                             (allreduce_recexch.cpp:188)
+ * algo is one of CHR_MODE_MPICH_*; k / single_phase_recv are used by RECEXCH only
+ * (single_phase_recv changes MPICH's buffering, not the data flow or the result).  Same
+ * buffer contract as chr_allreduce_radix_batch; results bit-identical to the reference's
+ * code on the same inputs, every reduction on the fused HIP kernel. */
+int chr_allreduce_mpich(const void* send, void* recv, size_t count, chr_dtype dtype, chr_op op,
+                        chr_comm* comm, chr_mode algo, int k, int single_phase_recv);
+int chr_allreduce_mpich_async(const void* send, void* recv, size_t count, chr_dtype dtype,
+                              chr_op op, chr_comm* comm, chr_mode algo, int k,
+                              int single_phase_recv);
+int chr_local_allreduce_mpich(chr_local_group* group, const void* const* sends,
+                              void* const* recvs, size_t count, chr_dtype dtype, chr_op op,
+                              chr_mode algo, int k, int single_phase_recv);
+
 /* ---- utilities -------------------------------------------------------------------------- */
 /* Synthetic inputs on the device with the shared generator (oracle/chiara_oracle.h):
- * pattern 0 = U[-1,1) (random 32-bit ints for INT32), 1 = rank*count_for_seq + i. */
+ * pattern 0 = U[-1,1) (random 32-bit ints for INT32), 1 = rank*count_for_seq + i,
+ * 2 = ties probe for MAX/MIN ({+0,-0,1,-1,0.5, NaN with per-rank payload}). */
 int chr_fill(void* buf, size_t n, chr_dtype dtype, int pattern, uint64_t seed, int rank,
              uint64_t count_for_seq, hipStream_t stream);
 const char* chr_error_string(int code);

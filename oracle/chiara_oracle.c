@@ -43,6 +43,35 @@ void orc_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int ra
             case ORC_I32: ((int32_t*)buf)[i] = (int32_t)v; break;
             case ORC_BF16: ((uint16_t*)buf)[i] = orc_f32_to_bf16((float)(int32_t)v); break;
             }
+        } else if (pattern == ORC_PAT_TIES) {
+            const unsigned sel = (unsigned)(orc_key(seed, (uint64_t)rank, i) >> 61);
+            const uint32_t pay = (uint32_t)(rank + 1) & 0x3Fu;
+            static const float ft[7] = {0.0f, -0.0f, 1.0f, -1.0f, 0.0f, -0.0f, 0.5f};
+            static const int32_t it[8] = {0, 0, 1, -1, 0, 0, 2, 7};
+            switch (dtype) {
+            case ORC_F32: {
+                uint32_t u;
+                if (sel == 7) u = 0x7FC00000u | (pay << 16) | pay;
+                else memcpy(&u, &ft[sel], 4);
+                memcpy((char*)buf + 4 * i, &u, 4);
+                break;
+            }
+            case ORC_F64: {
+                double d;
+                if (sel == 7) {
+                    uint64_t u = 0x7FF8000000000000ull | ((uint64_t)pay << 40) | pay;
+                    memcpy(&d, &u, 8);
+                } else {
+                    d = (double)ft[sel];
+                }
+                ((double*)buf)[i] = d;
+                break;
+            }
+            case ORC_I32: ((int32_t*)buf)[i] = it[sel]; break;
+            case ORC_BF16:
+                ((uint16_t*)buf)[i] = sel == 7 ? (uint16_t)(0x7FC0u | pay) : orc_f32_to_bf16(ft[sel]);
+                break;
+            }
         } else {
             switch (dtype) {
             case ORC_F32: ((float*)buf)[i] = orc_gen_f32(seed, (uint64_t)rank, i); break;
@@ -56,8 +85,11 @@ void orc_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int ra
     }
 }
 
-/* MPICH 3.3.2 predefined ops (src/mpi/coll/op/opsum.c, opmax.c, ...): the loop is
- * `b[i] = MPIR_OP(a[i], b[i])` with a = inbuf, b = inoutbuf; MAX(a,b) = a > b ? a : b. */
+/* MPICH 3.3.2 predefined ops (src/mpi/coll/op/opsum.c, opmax.c, ... via
+ * MPIR_OP_TYPE_REDUCE_CASE): with a = inoutvec and b = invec the loop is
+ * `a[i] = OP(a[i], b[i])`, OP(p, q) = p + q, p * q, (p > q ? p : q), (p < q ? p : q).  So
+ * MAX/MIN keep the inout value on ties (-0/+0) and whenever a NaN makes the compare false.
+ * Below: x = in[i], y = inout[i], result = OP(y, x). */
 #define ORC_LOOP(T, EXPR)                                     \
     do {                                                      \
         const T* a = (const T*)in;                            \
@@ -69,34 +101,35 @@ void orc_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int ra
 void orc_reduce_local(const void* in, void* inout, size_t n, int dtype, int op) {
     switch (dtype) {
     case ORC_F32:
-        if (op == ORC_SUM) ORC_LOOP(float, x + y);
-        else if (op == ORC_PROD) ORC_LOOP(float, x * y);
-        else if (op == ORC_MAX) ORC_LOOP(float, x > y ? x : y);
-        else ORC_LOOP(float, x < y ? x : y);
+        if (op == ORC_SUM) ORC_LOOP(float, y + x);
+        else if (op == ORC_PROD) ORC_LOOP(float, y * x);
+        else if (op == ORC_MAX) ORC_LOOP(float, y > x ? y : x);
+        else ORC_LOOP(float, y < x ? y : x);
         break;
     case ORC_F64:
-        if (op == ORC_SUM) ORC_LOOP(double, x + y);
-        else if (op == ORC_PROD) ORC_LOOP(double, x * y);
-        else if (op == ORC_MAX) ORC_LOOP(double, x > y ? x : y);
-        else ORC_LOOP(double, x < y ? x : y);
+        if (op == ORC_SUM) ORC_LOOP(double, y + x);
+        else if (op == ORC_PROD) ORC_LOOP(double, y * x);
+        else if (op == ORC_MAX) ORC_LOOP(double, y > x ? y : x);
+        else ORC_LOOP(double, y < x ? y : x);
         break;
     case ORC_I32:
-        if (op == ORC_SUM) ORC_LOOP(int32_t, (int32_t)((uint32_t)x + (uint32_t)y));
-        else if (op == ORC_PROD) ORC_LOOP(int32_t, (int32_t)((uint32_t)x * (uint32_t)y));
-        else if (op == ORC_MAX) ORC_LOOP(int32_t, x > y ? x : y);
-        else ORC_LOOP(int32_t, x < y ? x : y);
+        if (op == ORC_SUM) ORC_LOOP(int32_t, (int32_t)((uint32_t)y + (uint32_t)x));
+        else if (op == ORC_PROD) ORC_LOOP(int32_t, (int32_t)((uint32_t)y * (uint32_t)x));
+        else if (op == ORC_MAX) ORC_LOOP(int32_t, y > x ? y : x);
+        else ORC_LOOP(int32_t, y < x ? y : x);
         break;
     case ORC_BF16:
         /* The reference has no bf16; the golden driver runs it as a user-defined op on
-         * MPI_Type_contiguous(2, MPI_BYTE) computing bf16_rne(f32(a) op f32(b)). */
+         * MPI_Type_contiguous(2, MPI_BYTE) computing bf16_rne(f32(inout) op f32(in)) with the
+         * same operand order as the predefined float ops. */
         if (op == ORC_SUM)
-            ORC_LOOP(uint16_t, orc_f32_to_bf16(orc_bf16_to_f32(x) + orc_bf16_to_f32(y)));
+            ORC_LOOP(uint16_t, orc_f32_to_bf16(orc_bf16_to_f32(y) + orc_bf16_to_f32(x)));
         else if (op == ORC_PROD)
-            ORC_LOOP(uint16_t, orc_f32_to_bf16(orc_bf16_to_f32(x) * orc_bf16_to_f32(y)));
+            ORC_LOOP(uint16_t, orc_f32_to_bf16(orc_bf16_to_f32(y) * orc_bf16_to_f32(x)));
         else if (op == ORC_MAX)
-            ORC_LOOP(uint16_t, orc_bf16_to_f32(x) > orc_bf16_to_f32(y) ? x : y);
+            ORC_LOOP(uint16_t, orc_bf16_to_f32(y) > orc_bf16_to_f32(x) ? y : x);
         else
-            ORC_LOOP(uint16_t, orc_bf16_to_f32(x) < orc_bf16_to_f32(y) ? x : y);
+            ORC_LOOP(uint16_t, orc_bf16_to_f32(y) < orc_bf16_to_f32(x) ? y : x);
         break;
     }
 }
@@ -365,5 +398,227 @@ int orc_reduce_scatter_radix_batch(int nranks, int k, int b, size_t recvcount, i
         for (j = 0; j < b; j++)
             memcpy(recv[N * b + j], orc_chunk(&st, N) + (size_t)j * recvcount * st.es, recvcount * st.es);
     orc_free_state(&st);
+    return 0;
+}
+
+/* ==== MPICH baseline allreduces driven by testing/main.cpp ============
+ * Paths relative to /root/reference/testing/mpich_implementations/all_reduce/.  Every rank's
+ * buffers live in one process; each step reads the sending rank's buffer region that the
+ * sender does not modify in that step (disjoint regions), or a snapshot where both ends
+ * update the whole buffer (recursive doubling / exchange). */
+
+static void orc_copy_in(int n, size_t count, size_t es, const void* const* send, void* const* recv) {
+    int r;
+    for (r = 0; r < n; r++)
+        if (send[r]) memcpy(recv[r], send[r], count * es);
+}
+
+/* MPICH_Allreduce_ring (allreduce_ring.cpp:3-104) */
+int orc_allreduce_ring(int n, size_t count, int dtype, int op, const void* const* send, void* const* recv) {
+    size_t es = orc_dtype_size(dtype), total = 0, *cnts, *displs;
+    int i, r;
+    char** R = (char**)recv;
+    if (n < 1 || !es) return 1;
+    cnts = (size_t*)calloc((size_t)n, sizeof(size_t));
+    displs = (size_t*)calloc((size_t)n, sizeof(size_t));
+    for (i = 0; i < n; i++) { /* :31-38 */
+        cnts[i] = (count + (size_t)n - 1) / (size_t)n;
+        if (total + cnts[i] > count) {
+            cnts[i] = count - total;
+            break;
+        }
+        total += cnts[i];
+    }
+    for (i = 1; i < n; i++) displs[i] = displs[i - 1] + cnts[i - 1];
+    orc_copy_in(n, count, es, send, recv); /* :44-47 */
+    for (i = 0; i < n - 1; i++) {          /* :56-84 */
+        for (r = 0; r < n; r++) {
+            int src = (n + r - 1) % n, recv_rank = (2 * n + r - 2 - i) % n;
+            /* src sends its block recv_rank (its send_rank), reduced into mine (:80) */
+            orc_reduce_local(R[src] + displs[recv_rank] * es, R[r] + displs[recv_rank] * es, cnts[recv_rank],
+                             dtype, op);
+        }
+    }
+    for (r = 0; r < n; r++) /* MPI_Allgatherv (:86): block j comes from rank j */
+        for (i = 0; i < n; i++)
+            if (i != r) memcpy(R[r] + displs[i] * es, R[i] + displs[i] * es, cnts[i] * es);
+    free(cnts);
+    free(displs);
+    return 0;
+}
+
+/* MPICH_Allreduce_recursive_doubling (allreduce_recursive_doubling.cpp:4-101), commutative path */
+int orc_allreduce_recursive_doubling(int n, size_t count, int dtype, int op, const void* const* send,
+                                     void* const* recv) {
+    size_t es = orc_dtype_size(dtype);
+    int pof2 = 1, rem, r, mask;
+    char** R = (char**)recv;
+    char* snap;
+    if (n < 1 || !es) return 1;
+    orc_copy_in(n, count, es, send, recv);
+    while (pof2 <= n) pof2 <<= 1;
+    pof2 >>= 1;
+    rem = n - pof2;
+    for (r = 1; r < 2 * rem; r += 2) orc_reduce_local(R[r - 1], R[r], count, dtype, op); /* :35-50 */
+    snap = (char*)malloc(count * es * (size_t)n + 1);
+    for (mask = 1; mask < pof2; mask <<= 1) { /* :59-85 */
+        for (r = 0; r < n; r++) memcpy(snap + (size_t)r * count * es, R[r], count * es);
+        for (r = 0; r < n; r++) {
+            int newrank = r < 2 * rem ? (r % 2 ? r / 2 : -1) : r - rem, newdst, dst;
+            if (newrank < 0) continue;
+            newdst = newrank ^ mask;
+            dst = newdst < rem ? newdst * 2 + 1 : newdst + rem;
+            orc_reduce_local(snap + (size_t)dst * count * es, R[r], count, dtype, op); /* :70 */
+        }
+    }
+    free(snap);
+    for (r = 0; r < 2 * rem; r += 2) memcpy(R[r], R[r + 1], count * es); /* :88-97 */
+    return 0;
+}
+
+/* MPICH_Allreduce_reduce_scatter_allgather (allreduce_reduce_scatter_allgather.cpp:3-173) */
+int orc_allreduce_reduce_scatter_allgather(int n, size_t count, int dtype, int op, const void* const* send,
+                                           void* const* recv) {
+    size_t es = orc_dtype_size(dtype);
+    int pof2 = 1, rem, r, i, mask;
+    char** R = (char**)recv;
+    size_t *cnts, *disps;
+    int *send_idx, *recv_idx, *last_idx;
+    if (n < 1 || !es) return 1;
+    orc_copy_in(n, count, es, send, recv);
+    while (pof2 <= n) pof2 *= 2;
+    pof2 /= 2;
+    rem = n - pof2;
+    for (r = 1; r < 2 * rem; r += 2) orc_reduce_local(R[r - 1], R[r], count, dtype, op); /* :28-51 */
+    cnts = (size_t*)calloc((size_t)pof2, sizeof(size_t));
+    disps = (size_t*)calloc((size_t)pof2, sizeof(size_t));
+    for (i = 0; i < pof2; i++) cnts[i] = count / (size_t)pof2 + ((size_t)i < count % (size_t)pof2 ? 1 : 0);
+    for (i = 1; i < pof2; i++) disps[i] = disps[i - 1] + cnts[i - 1];
+    send_idx = (int*)calloc((size_t)n, sizeof(int));
+    recv_idx = (int*)calloc((size_t)n, sizeof(int));
+    last_idx = (int*)calloc((size_t)n, sizeof(int));
+    for (r = 0; r < n; r++) last_idx[r] = pof2;
+#define NEWRANK(rr) ((rr) < 2 * rem ? ((rr) % 2 ? (rr) / 2 : -1) : (rr) - rem)
+#define REALRANK(nr) ((nr) < rem ? (nr) * 2 + 1 : (nr) + rem)
+    for (mask = 1; mask < pof2; mask <<= 1) { /* reduce-scatter :76-117 */
+        /* indices first (every rank), then data: rank r reduces [recv_idx, ...) from dst's buffer */
+        int *rs = (int*)calloc((size_t)n, sizeof(int)), *re = (int*)calloc((size_t)n, sizeof(int));
+        for (r = 0; r < n; r++) {
+            int nr = NEWRANK(r), nd;
+            if (nr < 0) continue;
+            nd = nr ^ mask;
+            if (nr < nd) {
+                send_idx[r] = recv_idx[r] + pof2 / (mask * 2);
+                rs[r] = recv_idx[r];
+                re[r] = send_idx[r];
+            } else {
+                recv_idx[r] = send_idx[r] + pof2 / (mask * 2);
+                rs[r] = recv_idx[r];
+                re[r] = last_idx[r];
+            }
+        }
+        for (r = 0; r < n; r++) {
+            int nr = NEWRANK(r), dst;
+            size_t cnt = 0;
+            if (nr < 0) continue;
+            dst = REALRANK(nr ^ mask);
+            for (i = rs[r]; i < re[r]; i++) cnt += cnts[i];
+            orc_reduce_local(R[dst] + disps[rs[r]] * es, R[r] + disps[rs[r]] * es, cnt, dtype, op); /* :104 */
+        }
+        for (r = 0; r < n; r++) {
+            if (NEWRANK(r) < 0) continue;
+            send_idx[r] = recv_idx[r];
+            if ((mask << 1) < pof2) last_idx[r] = recv_idx[r] + pof2 / (mask << 1);
+        }
+        free(rs);
+        free(re);
+    }
+    /* allgather (:119-160): pure data movement; after it every participant holds all blocks */
+    {
+        int nr;
+        char* full = (char*)malloc(count * es + 1);
+        for (nr = 0; nr < pof2; nr++) {
+            /* newrank nr ends the reduce-scatter owning block index (bit-reversal is not used here:
+             * the owner of block b is the participant whose final recv_idx == b) */
+            (void)nr;
+        }
+        for (r = 0; r < n; r++) {
+            if (NEWRANK(r) < 0) continue;
+            memcpy(full + disps[recv_idx[r]] * es, R[r] + disps[recv_idx[r]] * es, cnts[recv_idx[r]] * es);
+        }
+        for (r = 0; r < n; r++)
+            if (NEWRANK(r) >= 0) memcpy(R[r], full, count * es);
+        free(full);
+    }
+#undef NEWRANK
+#undef REALRANK
+    for (r = 0; r < 2 * rem; r += 2) memcpy(R[r], R[r + 1], count * es); /* :161-171 */
+    free(cnts);
+    free(disps);
+    free(send_idx);
+    free(recv_idx);
+    free(last_idx);
+    return 0;
+}
+
+/* MPICH_do_reduce (allreduce_recexch.cpp:147-186): acc_{i+1} = OP(acc_i, next): the running
+ * value is the `in` operand. */
+static void orc_do_reduce(char** bufs, char* recvbuf, int k, int idx, size_t count, int dtype, int op) {
+    int i;
+    size_t es = orc_dtype_size(dtype);
+    for (i = 0; i < idx - 1; i++) orc_reduce_local(bufs[i], bufs[i + 1], count, dtype, op);
+    if (idx > 0) orc_reduce_local(bufs[idx - 1], recvbuf, count, dtype, op);
+    if (idx < k - 1) {
+        orc_reduce_local(recvbuf, bufs[idx], count, dtype, op);
+        for (i = idx; i < k - 2; i++) orc_reduce_local(bufs[i], bufs[i + 1], count, dtype, op);
+        memcpy(recvbuf, bufs[k - 2], count * es);
+    }
+}
+
+/* MPICH_Allreduce_recursive_exchange (allreduce_recexch.cpp:188-440), float path (myidx from
+ * MPICH_find_myidx, :137-145); single_phase_recv changes buffering only, not the data flow. */
+int orc_allreduce_recexch(int n, int k_in, size_t count, int dtype, int op, const void* const* send,
+                          void* const* recv) {
+    size_t es = orc_dtype_size(dtype);
+    int r, i, ph, k;
+    char** R = (char**)recv;
+    orc_recexch_t* x;
+    char *snap, **bufs;
+    if (n < 1 || !es || k_in < 2) return 1;
+    orc_copy_in(n, count, es, send, recv);
+    if (n == 1) return 0;
+    x = (orc_recexch_t*)calloc((size_t)n, sizeof(orc_recexch_t));
+    for (r = 0; r < n; r++)
+        if (orc_recexch_neighbors(r, n, k_in, &x[r])) {
+            free(x);
+            return 1;
+        }
+    k = x[0].k;
+    for (r = 0; r < n; r++) /* step 1 (:267-296) */
+        if (x[r].step1_sendto == -1)
+            for (i = 0; i < x[r].step1_nrecvs; i++) orc_reduce_local(R[x[r].step1_recvfrom[i]], R[r], count, dtype, op);
+    snap = (char*)malloc(count * es * (size_t)n + 1);
+    bufs = (char**)calloc((size_t)k, sizeof(char*));
+    for (i = 0; i < k; i++) bufs[i] = (char*)malloc(count * es + 1);
+    for (ph = 0; ph < x[0].step2_nphases; ph++) { /* step 2 (:298-365) */
+        for (r = 0; r < n; r++) memcpy(snap + (size_t)r * count * es, R[r], count * es);
+        for (r = 0; r < n; r++) {
+            int idx = k - 1;
+            if (x[r].step1_sendto != -1) continue;
+            for (i = 0; i < k - 1; i++) memcpy(bufs[i], snap + (size_t)x[r].step2_nbrs[ph][i] * count * es, count * es);
+            for (i = 0; i < k - 1; i++) /* MPICH_find_myidx */
+                if (x[r].step2_nbrs[ph][i] > r) {
+                    idx = i;
+                    break;
+                }
+            orc_do_reduce(bufs, R[r], k, idx, count, dtype, op);
+        }
+    }
+    for (r = 0; r < n; r++) /* step 3 (:367-386) */
+        if (x[r].step1_sendto != -1) memcpy(R[r], R[x[r].step1_sendto], count * es);
+    for (i = 0; i < k; i++) free(bufs[i]);
+    free(bufs);
+    free(snap);
+    free(x);
     return 0;
 }

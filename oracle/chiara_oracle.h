@@ -34,8 +34,13 @@ enum { ORC_SUM = 0, ORC_PROD = 1, ORC_MAX = 2, ORC_MIN = 3 };
 /* Input patterns for the generator. */
 enum {
     ORC_PAT_UNIFORM = 0,  /* f32/f64/bf16: U[-1,1); i32: full-range random 32-bit ints */
-    ORC_PAT_SEQ = 1       /* the reference harness pattern: rank*count + i
+    ORC_PAT_SEQ = 1,      /* the reference harness pattern: rank*count + i
                              (Fugaku_experiments/Allreduce/main.cpp:48-49) */
+    ORC_PAT_TIES = 2      /* MAX/MIN operand-order probe: each element one of {+0, -0, 1, -1,
+                             0.5, NaN with a per-rank payload} (ints: {0, 1, -1, 2, 7}), so
+                             ties and unordered compares are frequent and OP(a,b) vs OP(b,a)
+                             differ bitwise.  Used with MAX/MIN only (NaN payloads through
+                             arithmetic are not specified identically on CPU and GPU). */
 };
 
 static inline uint64_t orc_splitmix64(uint64_t x) {
@@ -81,7 +86,8 @@ size_t orc_dtype_size(int dtype);
 void orc_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int rank,
               uint64_t count_for_seq);
 
-/* MPI_Reduce_local restated (MPICH 3.3.2 predefined ops): inout[i] = in[i] (op) inout[i].
+/* MPI_Reduce_local restated (MPICH 3.3.2 predefined ops): inout[i] = inout[i] (op) in[i]
+ * (MPICH's loop order: MAX/MIN keep inout on ties and NaN compares).
  * int32 arithmetic wraps; bf16 is computed in f32 and rounded to bf16 RNE per call. */
 void orc_reduce_local(const void* in, void* inout, size_t n, int dtype, int op);
 
@@ -110,6 +116,16 @@ int orc_allreduce_radix_batch(int nranks, int k, int b, size_t count, int dtype,
                               const void* const* send, void* const* recv);
 int orc_reduce_scatter_radix_batch(int nranks, int k, int b, size_t recvcount, int dtype,
                                    int op, const void* const* send, void* const* recv);
+
+/* MPICH baseline allreduces driven by the reference's testing/main.cpp.
+ * send[r] may be NULL (in place: recv[r] holds the input). */
+int orc_allreduce_ring(int nranks, size_t count, int dtype, int op, const void* const* send, void* const* recv);
+int orc_allreduce_recursive_doubling(int nranks, size_t count, int dtype, int op, const void* const* send,
+                                     void* const* recv);
+int orc_allreduce_reduce_scatter_allgather(int nranks, size_t count, int dtype, int op, const void* const* send,
+                                           void* const* recv);
+int orc_allreduce_recexch(int nranks, int k, size_t count, int dtype, int op, const void* const* send,
+                          void* const* recv);
 
 #ifdef __cplusplus
 }

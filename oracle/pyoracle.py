@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(HERE, "liboracle.so")
 DTYPES = {"f32": 0, "f64": 1, "i32": 2, "bf16": 3}
 OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3}
 NP_DTYPES = {"f32": np.float32, "f64": np.float64, "i32": np.int32, "bf16": np.uint16}
-PAT_UNIFORM, PAT_SEQ = 0, 1
+PAT_UNIFORM, PAT_SEQ, PAT_TIES = 0, 1, 2
 
 _lib = None
 
@@ -100,3 +100,42 @@ def reduce_scatter_radix_batch(sends, k, b, dtype, op, inplace=False):
     if rc:
         raise ValueError(f"oracle reduce_scatter rejected geometry (rc={rc})")
     return [r[:recvcount] for r in recvs]
+
+
+def _setup_mpich(L):
+    vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    for name in ("orc_allreduce_ring", "orc_allreduce_recursive_doubling", "orc_allreduce_reduce_scatter_allgather"):
+        fn = getattr(L, name)
+        fn.argtypes = [i, sz, i, i, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+        fn.restype = i
+    L.orc_allreduce_recexch.argtypes = [i, i, sz, i, i, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+    L.orc_allreduce_recexch.restype = i
+
+
+MPICH_ALGOS = ("ring", "rd", "rsag", "rx")
+
+
+def mpich_allreduce(algo, sends, dtype, op, k=2, inplace=False):
+    """All ranks' outputs of the MPICH baseline `algo` (testing/mpich_implementations/all_reduce/)."""
+    L = lib()
+    if not getattr(L, "_mpich_ready", False):
+        _setup_mpich(L)
+        L._mpich_ready = True
+    n = len(sends)
+    count = sends[0].size
+    recvs = [s.copy() for s in sends] if inplace else [np.zeros_like(s) for s in sends]
+    sp = _ptr_array([None] * n) if inplace else _ptr_array(sends)
+    rp = _ptr_array(recvs)
+    if algo == "ring":
+        rc = L.orc_allreduce_ring(n, count, DTYPES[dtype], OPS[op], sp, rp)
+    elif algo == "rd":
+        rc = L.orc_allreduce_recursive_doubling(n, count, DTYPES[dtype], OPS[op], sp, rp)
+    elif algo == "rsag":
+        rc = L.orc_allreduce_reduce_scatter_allgather(n, count, DTYPES[dtype], OPS[op], sp, rp)
+    elif algo == "rx":
+        rc = L.orc_allreduce_recexch(n, k, count, DTYPES[dtype], OPS[op], sp, rp)
+    else:
+        raise ValueError(algo)
+    if rc:
+        raise ValueError(f"oracle {algo} rejected (rc={rc})")
+    return recvs

@@ -10,8 +10,9 @@
 // reduce_scatter_radix_batch.cpp:200-202.
 //
 // Usage: mpiexec -n N ref_driver <cases.txt> <outdir>
-//   one case per line: id mode(ar|rs|rl) k b count dtype op pattern seed inplace
-//   mode rl = a single MPI_Reduce_local timing/semantics probe on rank 0.
+//   one case per line: id mode k b count dtype op pattern seed inplace
+//   mode: ar | rs (radix_batch), ring | rd | rsag | rx (MPICH baselines; rx uses b as
+//   single_phase_recv)
 // For each case rank 0 writes <outdir>/<id>.out (all ranks' outputs, rank-major) and
 // <outdir>/<id>.lib (the MPI library collective's result on the same inputs).
 #include <mpi.h>
@@ -31,6 +32,15 @@ int all_reduce_radix_batch(char* sendbuf, char* recvbuf, int aCount, MPI_Datatyp
                            MPI_Op op, MPI_Comm comm, int k, int b);
 int reduce_scatter_radix_batch(const void* sendbuf, void* recvbuf, MPI_Aint recvcount,
                                MPI_Datatype datatype, MPI_Op op, MPI_Comm comm, int k, int b);
+// testing/mpich_implementations/all_reduce/ (the baselines testing/main.cpp drives)
+int MPICH_Allreduce_ring(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+                         MPI_Comm comm);
+int MPICH_Allreduce_recursive_doubling(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype,
+                                       MPI_Op op, MPI_Comm comm);
+int MPICH_Allreduce_reduce_scatter_allgather(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype,
+                                             MPI_Op op, MPI_Comm comm);
+int MPICH_Allreduce_recursive_exchange(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype,
+                                       MPI_Op op, MPI_Comm comm, int k, int single_phase_recv);
 
 // orc_reduce_local is the single definition of the bf16 op semantics.
 static void bf16_user_op(void* in, void* inout, int* len, MPI_Datatype*) {
@@ -103,7 +113,7 @@ int main(int argc, char** argv) {
                                               : bf16_t;
         MPI_Op mop = dtype == ORC_BF16 ? bf16_ops[op] : std_ops[op];
 
-        size_t in_n = (mode == "ar") ? (size_t)count : (size_t)count * nprocs;
+        size_t in_n = (mode == "rs") ? (size_t)count * nprocs : (size_t)count;
         size_t out_n = (size_t)count;
         std::vector<char> send(in_n * es), recv(in_n * es, 0), lib(out_n * es, 0);
         orc_fill(send.data(), in_n, dtype, pattern, seed, rank, in_n);
@@ -114,6 +124,16 @@ int main(int argc, char** argv) {
             MPI_Barrier(MPI_COMM_WORLD);
             all_reduce_radix_batch(inplace ? (char*)MPI_IN_PLACE : send.data(), recv.data(), (int)count,
                                    mdt, mop, MPI_COMM_WORLD, k, b);
+        } else if (mode == "ring" || mode == "rd" || mode == "rsag" || mode == "rx") {
+            MPI_Allreduce(send.data(), lib.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
+            if (inplace) memcpy(recv.data(), send.data(), in_n * es);
+            MPI_Barrier(MPI_COMM_WORLD);
+            const char* sb = inplace ? (const char*)MPI_IN_PLACE : send.data();
+            if (mode == "ring") MPICH_Allreduce_ring(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
+            else if (mode == "rd") MPICH_Allreduce_recursive_doubling(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
+            else if (mode == "rsag")
+                MPICH_Allreduce_reduce_scatter_allgather(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
+            else MPICH_Allreduce_recursive_exchange(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD, k, b);
         } else {
             MPI_Reduce_scatter_block(send.data(), lib.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
             if (inplace) memcpy(recv.data(), send.data(), in_n * es);

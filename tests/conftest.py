@@ -26,3 +26,17 @@ def golden():
         manifest = json.load(f)
     arrays = np.load(os.path.join(here, "outputs.npz"), allow_pickle=False)
     return manifest["cases"], arrays
+
+
+@pytest.fixture(scope="session")
+def golden_mpich():
+    """Golden vectors of the MPICH baselines testing/main.cpp drives (gen_golden.py mpich)."""
+    import json
+
+    import numpy as np
+
+    here = os.path.join(REPO, "tests", "golden")
+    with open(os.path.join(here, "mpich_manifest.json")) as f:
+        manifest = json.load(f)
+    arrays = np.load(os.path.join(here, "mpich_outputs.npz"), allow_pickle=False)
+    return manifest["cases"], arrays

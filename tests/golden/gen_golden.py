@@ -68,6 +68,10 @@ def cases_for(n):
             add("rs", k, b, 16, "bf16", "sum", pyoracle.PAT_UNIFORM, 0)
             add("rs", k, b, 16, "f32", "sum", pyoracle.PAT_UNIFORM, 1)
             add("rs", k, b, 16, "i32", "max", pyoracle.PAT_UNIFORM, 0)
+            # MAX/MIN operand order: ties, signed zeros, NaN payloads (PAT_TIES)
+            add("ar", k, b, n * 16, "f32", "max", pyoracle.PAT_TIES, 0)
+            add("ar", k, b, n * 16, "bf16", "min", pyoracle.PAT_TIES, 0)
+            add("rs", k, b, 16, "f64", "max", pyoracle.PAT_TIES, 1)
     return out
 
 
@@ -88,6 +92,41 @@ LARGE = [
 ]
 
 
+def mpich_cases_for(n):
+    """testing/main.cpp baselines: ring, recursive doubling,
+    reduce-scatter+allgather (Rabenseifner), recursive exchange (k, single_phase_recv)."""
+    out = []
+
+    def add(mode, k, b, count, dt, op, pat, inplace):
+        cid = f"{mode}_n{n}_k{k}_b{b}_c{count}_{dt}_{op}_p{pat}_ip{inplace}"
+        out.append(dict(id=cid, mode=mode, n=n, k=k, b=b, count=count, dtype=dt, op=op,
+                        pattern=pat, seed=SEED, inplace=inplace))
+
+    for mode in ("ring", "rd", "rsag"):
+        for count in (1, 7, 3 * n + 1, 256, 1000):
+            add(mode, 0, 0, count, "f32", "sum", pyoracle.PAT_UNIFORM, 0)
+        add(mode, 0, 0, 96, "f64", "sum", pyoracle.PAT_UNIFORM, 0)   # testing/main.cpp uses double
+        add(mode, 0, 0, 64, "i32", "sum", pyoracle.PAT_SEQ, 0)
+        add(mode, 0, 0, 64, "bf16", "sum", pyoracle.PAT_UNIFORM, 0)
+        add(mode, 0, 0, 64, "f32", "max", pyoracle.PAT_UNIFORM, 0)
+        add(mode, 0, 0, 64, "f32", "sum", pyoracle.PAT_UNIFORM, 1)
+        add(mode, 0, 0, 64, "f32", "max", pyoracle.PAT_TIES, 0)
+        add(mode, 0, 0, 64, "f64", "min", pyoracle.PAT_TIES, 1)
+        add(mode, 0, 0, 64, "bf16", "max", pyoracle.PAT_TIES, 0)
+    for k in (2, 3, 4, 5):
+        for spr in (0, 1):
+            for count in (1, 33, 500):
+                add("rx", k, spr, count, "f32", "sum", pyoracle.PAT_UNIFORM, 0)
+            add("rx", k, spr, 64, "f64", "sum", pyoracle.PAT_UNIFORM, 0)
+            add("rx", k, spr, 64, "i32", "sum", pyoracle.PAT_SEQ, 0)
+            add("rx", k, spr, 64, "f32", "prod", pyoracle.PAT_UNIFORM, 1)
+            # MPICH_do_reduce runs the running value as the FIRST operand: order-sensitive
+            add("rx", k, spr, 64, "f32", "max", pyoracle.PAT_TIES, 0)
+            add("rx", k, spr, 64, "f32", "min", pyoracle.PAT_TIES, 1)
+            add("rx", k, spr, 64, "bf16", "max", pyoracle.PAT_TIES, 0)
+    return out
+
+
 def run_n(n, cases, tmp):
     cf = os.path.join(tmp, f"cases_{n}.txt")
     with open(cf, "w") as f:
@@ -103,14 +142,21 @@ def run_n(n, cases, tmp):
 
 def main():
     subprocess.check_call(["make", "-s", "-C", ORACLE, "ref", "liboracle.so"])
+    which = sys.argv[1] if len(sys.argv) > 1 else "radix_batch"
     all_cases = []
-    for n in (1, 2, 3, 4, 5, 6, 8, 9, 12, 16):
-        all_cases += cases_for(n)
-    for c in LARGE:
-        c = dict(c, pattern=pyoracle.PAT_UNIFORM, seed=SEED, inplace=0)
-        c["id"] = (f"{c['mode']}_n{c['n']}_k{c['k']}_b{c['b']}_c{c['count']}_{c['dtype']}_{c['op']}"
-                   f"_p{c['pattern']}_ip0_large")
-        all_cases.append(c)
+    if which == "mpich":
+        for n in (1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 16):
+            all_cases += mpich_cases_for(n)
+        prefix = "mpich_"
+    else:
+        prefix = ""
+        for n in (1, 2, 3, 4, 5, 6, 8, 9, 12, 16):
+            all_cases += cases_for(n)
+        for c in LARGE:
+            c = dict(c, pattern=pyoracle.PAT_UNIFORM, seed=SEED, inplace=0)
+            c["id"] = (f"{c['mode']}_n{c['n']}_k{c['k']}_b{c['b']}_c{c['count']}_{c['dtype']}_{c['op']}"
+                       f"_p{c['pattern']}_ip0_large")
+            all_cases.append(c)
     manifest, arrays = [], {}
     with tempfile.TemporaryDirectory() as tmp:
         by_n = {}
@@ -134,18 +180,21 @@ def main():
             else:
                 af, lf = a.astype(np.float64), lb.astype(np.float64)
             rec["n_diff_vs_lib"] = int(np.count_nonzero(a != lb))
-            rec["max_abs_diff_vs_lib"] = float(np.max(np.abs(af - lf))) if a.size else 0.0
+            ok = np.isfinite(af) & np.isfinite(lf)
+            rec["max_abs_diff_vs_lib"] = float(np.max(np.abs(af[ok] - lf[ok]))) if ok.any() else 0.0
             rec["stored"] = len(out) <= STORE_LIMIT
             if rec["stored"]:
                 arrays[c["id"]] = a.copy()
                 arrays[c["id"] + "__lib"] = lb.copy()
             manifest.append(rec)
-    with open(os.path.join(HERE, "manifest.json"), "w") as f:
-        json.dump({"generator": "tests/golden/gen_golden.py",
-                   "reference": "Fugaku_experiments/{Allreduce/all_reduce_radix_batch.cpp,"
-                                "Reduce-scatter/reduce_scatter_radix_batch.cpp} @ 2025-11-21, MPICH 3.3.2",
-                   "seed": SEED, "cases": manifest}, f, indent=0)
-    np.savez_compressed(os.path.join(HERE, "outputs.npz"), **arrays)
+    ref_desc = ("testing/mpich_implementations/all_reduce/{allreduce_ring,allreduce_recursive_doubling,"
+                "allreduce_reduce_scatter_allgather,allreduce_recexch}.cpp" if which == "mpich" else
+                "Fugaku_experiments/{Allreduce/all_reduce_radix_batch.cpp,Reduce-scatter/reduce_scatter_radix_batch.cpp}")
+    with open(os.path.join(HERE, prefix + "manifest.json"), "w") as f:
+        json.dump({"generator": f"tests/golden/gen_golden.py {which}",
+                   "reference": ref_desc + " @ 2025-11-21, MPICH 3.3.2", "seed": SEED, "cases": manifest},
+                  f, indent=0)
+    np.savez_compressed(os.path.join(HERE, prefix + "outputs.npz"), **arrays)
     print(f"{len(manifest)} cases, {len(arrays) // 2} stored in full")
 
 

@@ -44,7 +44,13 @@ def run_local(st, op, dtype, rop):
         st.view(dst, n)[:] = st.view(acc, n).copy()
         return
     a = st.view(acc, n).copy()
-    po.reduce_multi(a, [st.view(r, n).copy() for r in ins], dtype, rop)
+    if kind == "reduce_sw":  # running value first: a = MPI_Reduce_local(a -> in, x -> inout)
+        for r in ins:
+            x = st.view(r, n).copy()
+            po.reduce_local(a, x, dtype, rop)
+            a = x
+    else:
+        po.reduce_multi(a, [st.view(r, n).copy() for r in ins], dtype, rop)
     st.view(dst, n)[:] = a
 
 
@@ -84,7 +90,7 @@ def execute(plans, sends, dtype, rop, inplace=False):
 
 def simulate(mode, sends, k, b, dtype, op, inplace=False, slices=1):
     n = len(sends)
-    count = sends[0].size if mode == ca.MODE_ALLREDUCE else sends[0].size // n
+    count = sends[0].size // n if mode == ca.MODE_REDUCE_SCATTER else sends[0].size
     plans = load_plans(mode, n, k, b, count, slices)
     if plans[0]["header"]["error"]:
         raise ValueError(f"plan error {plans[0]['header']['error']}")

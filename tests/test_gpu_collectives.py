@@ -167,3 +167,44 @@ def test_rccl_comm_single_rank(gu):
     np.testing.assert_array_equal(gu.from_dev(dr, np.float32), x)
     comm.destroy()
     torch.cuda.synchronize()
+
+
+# ---- MPICH baselines (testing/main.cpp) on the same kernels --------------------------------
+
+MPICH_MODE = {"ring": ca.MODE_MPICH_RING, "rd": ca.MODE_MPICH_RD, "rsag": ca.MODE_MPICH_RSAG,
+              "rx": ca.MODE_MPICH_RECEXCH}
+
+
+def test_mpich_baselines_match_reference_golden(gu, groups, golden_mpich):
+    """ring / recursive doubling / Rabenseifner / recexch: every golden case bit-exact."""
+    cases, _ = golden_mpich
+    bad = []
+    for c in cases:
+        n = c["n"]
+        npdt = po.NP_DTYPES[c["dtype"]]
+        sends = [po.fill(c["count"], c["dtype"], c["pattern"], c["seed"], r) for r in range(n)]
+        d_send = [gu.to_dev(s) for s in sends]
+        if c["inplace"]:
+            d_recv, d_sendp = d_send, [ca.IN_PLACE] * n
+        else:
+            d_recv, d_sendp = [gu.empty_dev(s.nbytes) for s in sends], d_send
+        rc = groups(n).allreduce_mpich(MPICH_MODE[c["mode"]], d_sendp, d_recv, c["count"], DT[c["dtype"]],
+                                       OP[c["op"]], c["k"], c["b"])
+        assert rc == 0, (c["id"], rc)
+        outs = [gu.from_dev(d, npdt, c["count"]) for d in d_recv]
+        if hashlib.sha256(b"".join(o.tobytes() for o in outs)).hexdigest() != c["sha256"]:
+            bad.append(c["id"])
+    assert not bad, f"{len(bad)} device/reference mismatches, e.g. {bad[:5]}"
+
+
+@pytest.mark.parametrize("algo", ["ring", "rd", "rsag", "rx"])
+def test_mpich_baselines_large_int_exact(gu, groups, algo):
+    """8 ranks, 4M int32 (the size class testing/main.cpp reaches): exact vs the oracle."""
+    n, count = 8, (1 << 22) + 5
+    sends = [po.fill(count, "i32", po.PAT_UNIFORM, 99, r) for r in range(n)]
+    want = po.mpich_allreduce(algo, sends, "i32", "sum", k=3)
+    d_send = [gu.to_dev(s) for s in sends]
+    d_recv = [gu.empty_dev(s.nbytes) for s in sends]
+    assert groups(n).allreduce_mpich(MPICH_MODE[algo], d_send, d_recv, count, ca.INT32, ca.SUM, 3, 0) == 0
+    for r in range(n):
+        np.testing.assert_array_equal(gu.from_dev(d_recv[r], np.int32, count), want[r])

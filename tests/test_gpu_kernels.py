@@ -76,7 +76,8 @@ def test_misaligned_buffers(gu, off, in_off):
 
 
 def test_reduce_local_mpi_semantics(gu):
-    """MPI_Reduce_local: inout = in op inout; MAX keeps inout unless in > inout (NaN, -0)."""
+    """MPI_Reduce_local (MPICH loop): inout = OP(inout, in); MAX keeps inout only when
+    inout > in, so ties (-0/+0) and NaN compares take `in`."""
     a = np.array([1.0, -0.0, np.nan, 3.0, 0.0, -np.inf], dtype=np.float32)
     b = np.array([2.0, 0.0, 1.0, np.nan, -0.0, np.inf], dtype=np.float32)
     for op in ("max", "min", "sum", "prod"):
@@ -104,7 +105,7 @@ def test_int32_wraps(gu):
 
 
 @pytest.mark.parametrize("dtype", ["f32", "f64", "i32", "bf16"])
-@pytest.mark.parametrize("pattern", [0, 1])
+@pytest.mark.parametrize("pattern", [0, 1, 2])
 def test_device_fill_matches_oracle_generator(gu, dtype, pattern):
     n = 300001
     npdt = po.NP_DTYPES[dtype]
@@ -128,3 +129,33 @@ def test_invalid_args(gu):
     assert ca.reduce_local(0, 0, 5, ca.FLOAT32, ca.SUM) == 1
     assert ca.reduce_local(1, 1, 5, 9, ca.SUM) == 1
     assert ca.reduce_local(1, 1, 5, ca.FLOAT32, 9) == 1
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64", "bf16", "i32"])
+@pytest.mark.parametrize("op", ["max", "min", "sum"])
+@pytest.mark.parametrize("m", [1, 3, 8, 11])
+def test_reduce_multi_running_first(gu, dtype, op, m):
+    """CHR_REDUCE_RUNNING_FIRST = MPICH_do_reduce's chain (allreduce_recexch.cpp:147-186):
+    every step is MPI_Reduce_local(running, next).  Ties/NaN data make the order visible."""
+    n = 4099
+    npdt = po.NP_DTYPES[dtype]
+    pat = po.PAT_TIES if op != "sum" else po.PAT_UNIFORM
+    acc = po.fill(n, dtype, pat, 77, 0)
+    ins = [po.fill(n, dtype, pat, 77, j + 1) for j in range(m)]
+    run = acc.copy()
+    for x in ins:
+        nxt = x.copy()
+        po.reduce_local(run, nxt, dtype, op)
+        run = nxt
+    d_acc, d_ins, d_out = gu.to_dev(acc), [gu.to_dev(x) for x in ins], gu.empty_dev(acc.nbytes)
+    assert ca.reduce_multi_ex(d_out, d_acc, d_ins, n, DT[dtype], OP[op], ca.REDUCE_RUNNING_FIRST, gu.stream()) == 0
+    gu.sync()
+    np.testing.assert_array_equal(_bits(gu.from_dev(d_out, npdt)), _bits(run))
+    if op != "sum" and dtype != "i32":  # and the default order really differs on this data
+        dflt = po.reduce_multi(acc.copy(), ins, dtype, op)
+        assert not np.array_equal(_bits(dflt), _bits(run))
+
+
+def test_reduce_multi_ex_rejects_bad_flags(gu):
+    d = gu.empty_dev(64)
+    assert ca.reduce_multi_ex(d, d, [d], 4, ca.FLOAT32, ca.MAX, 2, gu.stream()) == 1

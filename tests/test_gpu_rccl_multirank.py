@@ -46,20 +46,31 @@ def _worker(rank, world, port, cases, q):
             comm.set_slices(slices)
             npdt = po.NP_DTYPES[dtype]
             cdt = {"f32": ca.FLOAT32, "bf16": ca.BFLOAT16, "i32": ca.INT32}[dtype]
-            in_n = count if mode == "ar" else count * world
-            x = po.fill(in_n, dtype, 0, 4242, rank)
+            in_n = count * world if mode == "rs" else count
+            pat = po.PAT_TIES if mode == "rx" else 0  # recexch: operand-order sensitive data, MAX
+            x = po.fill(in_n, dtype, pat, 4242, rank)
             if host:
                 send, out = x, np.zeros(count, dtype=npdt)
             else:
                 send = torch.from_numpy(x.view(np.uint8).copy()).to(dev)
                 out_t = torch.zeros(count * x.itemsize, dtype=torch.uint8, device=dev)
-            fn = ca.all_reduce_radix_batch if mode == "ar" else ca.reduce_scatter_radix_batch
-            rc = fn(send, out if host else out_t, count, cdt, ca.SUM, comm, k, b)
+            dst = out if host else out_t
+            allx = [po.fill(in_n, dtype, pat, 4242, r) for r in range(world)]
+            if mode in ("ar", "rs"):
+                fn = ca.all_reduce_radix_batch if mode == "ar" else ca.reduce_scatter_radix_batch
+                rc = fn(send, dst, count, cdt, ca.SUM, comm, k, b)
+                f = po.allreduce_radix_batch if mode == "ar" else po.reduce_scatter_radix_batch
+                ref = f(allx, k, b, dtype, "sum")[rank]
+            elif mode == "rx":
+                rc = ca.MPICH_Allreduce_recursive_exchange(send, dst, count, cdt, ca.MAX, comm, k, b)
+                ref = po.mpich_allreduce("rx", allx, dtype, "max", k=k)[rank]
+            else:
+                fn = {"ring": ca.MPICH_Allreduce_ring, "rd": ca.MPICH_Allreduce_recursive_doubling,
+                      "rsag": ca.MPICH_Allreduce_reduce_scatter_allgather}[mode]
+                rc = fn(send, dst, count, cdt, ca.SUM, comm)
+                ref = po.mpich_allreduce(mode, allx, dtype, "sum")[rank]
             if not host:
                 out = out_t.cpu().numpy().view(npdt)
-            allx = [po.fill(in_n, dtype, 0, 4242, r) for r in range(world)]
-            f = po.allreduce_radix_batch if mode == "ar" else po.reduce_scatter_radix_batch
-            ref = f(allx, k, b, dtype, "sum")[rank]
             q.put((rank, mode, k, b, rc, bool(np.array_equal(out.view(np.uint8), ref.view(np.uint8)))))
     finally:
         comm.destroy()
@@ -95,3 +106,13 @@ def test_rccl_world8_c4_c5_geometries():
     _run(8, [("ar", 4, 4, 8 * 4096, "f32", False, 0), ("ar", 4, 4, 8 * 4096, "bf16", False, 4),
              ("ar", 2, 2, 8 * 4096, "f32", False, 3), ("ar", 3, 4, 8 * 2048, "bf16", False, 2),
              ("ar", 4, 8, 8 * 1024, "f32", False, 0), ("rs", 4, 4, 4000, "f32", False, 3)], timeout=600)
+
+
+def test_rccl_mpich_baselines_world5_and_8():
+    """testing/main.cpp's baselines over RCCL, non-power-of-two (fold/unfold) and 8 ranks."""
+    cases = [("ring", 0, 0, 100003, "f32", False, 0), ("rd", 0, 0, 4099, "f32", False, 0),
+             ("rsag", 0, 0, 65537, "f32", True, 0), ("rx", 3, 0, 20000, "f32", False, 0),
+             ("rx", 2, 1, 777, "bf16", False, 0)]
+    _run(5, cases)
+    _run(8, cases[:1] + [("rx", 4, 0, 1 << 16, "f32", False, 0), ("rsag", 0, 0, 1 << 16, "bf16", False, 0)],
+         timeout=600)

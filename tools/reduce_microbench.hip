@@ -405,6 +405,202 @@ static void focus2_m(size_t bytes, int sets, int rounds) {
     free_sets(S);
 }
 
+
+// Per-slot cache policy: bit u of PA / PI / PS set = the acc load / every input load /
+// the store of unroll slot u is PLAIN (temporal); clear = non-temporal.
+template <int M, int U, int PA, int PI, int PS>
+__global__ __launch_bounds__(256) void k_mask(Args a) {
+    const size_t stride = (size_t)gridDim.x * 256 * U;
+    for (size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x; base < a.nvec; base += stride) {
+        if (base + (size_t)(U - 1) * 256 < a.nvec) {
+            f32x4 acc[U], x[M][U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                acc[u] = ((PA >> u) & 1) ? a.acc[base + (size_t)u * 256] : __builtin_nontemporal_load(&a.acc[base + (size_t)u * 256]);
+#pragma unroll
+            for (int j = 0; j < M; ++j)
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    x[j][u] = ((PI >> u) & 1) ? a.ins[j][base + (size_t)u * 256] : __builtin_nontemporal_load(&a.ins[j][base + (size_t)u * 256]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < M; ++j)
+#pragma unroll
+                for (int u = 0; u < U; ++u) acc[u] = x[j][u] + acc[u];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if ((PS >> u) & 1) a.out[base + (size_t)u * 256] = acc[u];
+                else __builtin_nontemporal_store(acc[u], &a.out[base + (size_t)u * 256]);
+            }
+        } else {
+            for (int u = 0; u < U; ++u) {
+                const size_t i = base + (size_t)u * 256;
+                if (i >= a.nvec) break;
+                f32x4 v = __builtin_nontemporal_load(&a.acc[i]);
+                for (int j = 0; j < M; ++j) v = __builtin_nontemporal_load(&a.ins[j][i]) + v;
+                __builtin_nontemporal_store(v, &a.out[i]);
+            }
+        }
+    }
+}
+
+template <int M>
+static void focus3_m(size_t bytes, int sets, int rounds) {
+    const size_t nvec = bytes / 16;
+    Sets S = make_sets(M, nvec, sets);
+    const int reps = std::max(10, std::min(300, (int)((8ull << 30) / ((M + 2) * bytes))));
+    auto args_for = [&](int i) {
+        Args a{};
+        auto& b = S.bufs[i % sets];
+        a.out = b[0];
+        a.acc = b[0];
+        for (int j = 0; j < M; ++j) a.ins[j] = b[j + 1];
+        a.nvec = nvec;
+        return a;
+    };
+    char tag[64];
+    std::snprintf(tag, sizeof tag, " sets=%d", sets);
+    for (int r = 0; r < rounds; ++r) {
+#define F(U, PA, PI, PS, NAME)                                                                          \
+    {                                                                                                  \
+        const int grid = (int)((nvec + (size_t)256 * U - 1) / ((size_t)256 * U));                      \
+        double us = time_launches([&](int i) { hipLaunchKernelGGL((k_mask<M, U, PA, PI, PS>), dim3(grid), dim3(256), 0, 0, args_for(i)); }, reps); \
+        report((std::string(NAME) + tag).c_str(), M, bytes, us);                                      \
+    }
+        F(4, 0, 0, 0, "mask all-NT (product)");
+        F(4, 1, 0, 0, "mask acc0 plain");
+        F(4, 3, 0, 0, "mask acc0,1 plain");
+        F(4, 5, 0, 0, "mask acc0,2 plain");
+        F(4, 15, 0, 0, "mask acc all plain");
+        F(4, 0, 1, 0, "mask in0 plain");
+        F(4, 1, 1, 0, "mask acc0+in0 plain");
+        F(4, 0, 0, 1, "mask st0 plain");
+        F(4, 1, 0, 1, "mask acc0+st0 plain");
+        F(2, 1, 0, 0, "U2 mask acc0 plain");
+        F(8, 1, 0, 0, "U8 mask acc0 plain");
+        F(8, 17, 0, 0, "U8 mask acc0,4 plain");
+#undef F
+        {
+            double us = time_launches([&](int i) { hipLaunchKernelGGL((k_reg<M, 4, 256, true, true, true>), dim3((nvec + 1023) / 1024), dim3(256), 0, 0, args_for(i)); }, reps);
+            report((std::string("k_reg NT (hoisted acc0)") + tag).c_str(), M, bytes, us);
+        }
+        std::printf("--\n");
+    }
+    free_sets(S);
+}
+
+
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+template <int AUX>
+__device__ __forceinline__ u32x4v bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
+}
+template <int AUX>
+__device__ __forceinline__ void bstore(u32x4v v, __amdgpu_buffer_rsrc_t r, unsigned off) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, AUX);
+}
+// Buffer-load form with an explicit cache policy per slot: aux 2 = nt, 0 = default.
+// Bit u of PA / PI / PS = slot u's acc load / input loads / store use the DEFAULT policy.
+template <int M, int U, int PA, int PI, int PS>
+__global__ __launch_bounds__(256) void k_buf(Args a) {
+    const __amdgpu_buffer_rsrc_t racc = __builtin_amdgcn_make_buffer_rsrc((void*)a.acc, 0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc((void*)a.out, 0, 0x7FFFFFFF, 0x00020000);
+    __amdgpu_buffer_rsrc_t rin[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) rin[j] = __builtin_amdgcn_make_buffer_rsrc((void*)a.ins[j], 0, 0x7FFFFFFF, 0x00020000);
+    const size_t stride = (size_t)gridDim.x * 256 * U;
+    for (size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x; base < a.nvec; base += stride) {
+        if (base + (size_t)(U - 1) * 256 < a.nvec) {
+            u32x4v acc[U], x[M][U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                acc[u] = ((PA >> u) & 1) ? bload<0>(racc, (unsigned)((base + u * 256) * 16)) : bload<2>(racc, (unsigned)((base + u * 256) * 16));
+#pragma unroll
+            for (int j = 0; j < M; ++j)
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    x[j][u] = ((PI >> u) & 1) ? bload<0>(rin[j], (unsigned)((base + u * 256) * 16)) : bload<2>(rin[j], (unsigned)((base + u * 256) * 16));
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < M; ++j)
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    f32x4 p, q;
+                    __builtin_memcpy(&p, &x[j][u], 16);
+                    __builtin_memcpy(&q, &acc[u], 16);
+                    q = p + q;
+                    __builtin_memcpy(&acc[u], &q, 16);
+                }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if ((PS >> u) & 1) bstore<0>(acc[u], rout, (unsigned)((base + u * 256) * 16));
+                else bstore<2>(acc[u], rout, (unsigned)((base + u * 256) * 16));
+        } else {
+            for (int u = 0; u < U; ++u) {
+                const size_t i = base + (size_t)u * 256;
+                if (i >= a.nvec) break;
+                f32x4 v = a.acc[i];
+                for (int j = 0; j < M; ++j) v = a.ins[j][i] + v;
+                a.out[i] = v;
+            }
+        }
+    }
+}
+
+template <int M>
+static void focus4_m(size_t bytes, int sets, int rounds) {
+    const size_t nvec = bytes / 16;
+    Sets S = make_sets(M, nvec, sets);
+    const int reps = std::max(10, std::min(300, (int)((8ull << 30) / ((M + 2) * bytes))));
+    auto args_for = [&](int i) {
+        Args a{};
+        auto& b = S.bufs[i % sets];
+        a.out = b[0];
+        a.acc = b[0];
+        for (int j = 0; j < M; ++j) a.ins[j] = b[j + 1];
+        a.nvec = nvec;
+        return a;
+    };
+    char tag[64];
+    std::snprintf(tag, sizeof tag, " sets=%d", sets);
+    for (int r = 0; r < rounds; ++r) {
+#define F(U, PA, PI, PS, NAME)                                                                          \
+    {                                                                                                  \
+        const int grid = (int)((nvec + (size_t)256 * U - 1) / ((size_t)256 * U));                      \
+        double us = time_launches([&](int i) { hipLaunchKernelGGL((k_buf<M, U, PA, PI, PS>), dim3(grid), dim3(256), 0, 0, args_for(i)); }, reps); \
+        report((std::string(NAME) + tag).c_str(), M, bytes, us);                                      \
+    }
+        F(4, 0, 0, 0, "buf all-nt U4");
+        F(4, 1, 0, 0, "buf acc0 dflt U4");
+        F(4, 3, 0, 0, "buf acc0,1 dflt U4");
+        F(4, 15, 0, 0, "buf acc* dflt U4");
+        F(4, 0, 1, 0, "buf in0 dflt U4");
+        F(4, 0, 0, 1, "buf st0 dflt U4");
+        F(4, 1, 1, 0, "buf acc0+in0 dflt U4");
+        F(4, 15, 15, 15, "buf all dflt U4");
+        F(2, 0, 0, 0, "buf all-nt U2");
+        F(2, 1, 0, 0, "buf acc0 dflt U2");
+        F(8, 1, 0, 0, "buf acc0 dflt U8");
+        F(8, 0, 0, 0, "buf all-nt U8");
+#undef F
+        {
+            double us = time_launches([&](int i) { hipLaunchKernelGGL((k_reg<M, 4, 256, true, true, true>), dim3((nvec + 1023) / 1024), dim3(256), 0, 0, args_for(i)); }, reps);
+            report((std::string("k_reg NT (hoisted acc0 plain)") + tag).c_str(), M, bytes, us);
+        }
+        {
+            double us = time_launches([&](int i) {
+                Args a = args_for(i);
+                const void* ins[8];
+                for (int j = 0; j < M; ++j) ins[j] = a.ins[j];
+                chr_reduce_multi(a.out, a.acc, ins, M, a.nvec * 4, CHR_FLOAT32, CHR_SUM, 0);
+            }, reps);
+            report((std::string("libchiara chr_reduce_multi") + tag).c_str(), M, bytes, us);
+        }
+        std::printf("--\n");
+    }
+    free_sets(S);
+}
+
 // correctness spot check of every variant family against a host sum
 static void check() {
     const size_t nvec = (1 << 20) + 37;
@@ -444,6 +640,9 @@ static void check() {
     reset();
     hipLaunchKernelGGL((k_lds<1, 2>), dim3(555), dim3(256), 0, 0, a);
     verify("lds");
+    reset();
+    hipLaunchKernelGGL((k_buf<1, 4, 1, 0, 0>), dim3(777), dim3(256), 0, 0, a);
+    verify("buf");
     CK(hipFree(d0));
     CK(hipFree(d1));
     std::printf("variant correctness: ok\n");
@@ -451,6 +650,21 @@ static void check() {
 
 int main(int argc, char** argv) {
     check();
+    if (argc > 1 && std::string(argv[1]) == "focus4") {
+        focus4_m<1>(1024ull << 20, 1, 2);
+        focus4_m<1>(64 << 20, 16, 2);
+        focus4_m<3>(512ull << 20, 1, 1);
+        focus4_m<3>(64 << 20, 8, 1);
+        focus4_m<7>(64 << 20, 4, 1);
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus3") {
+        focus3_m<1>(1024ull << 20, 1, 2);
+        focus3_m<1>(64 << 20, 16, 2);
+        focus3_m<3>(512ull << 20, 1, 1);
+        focus3_m<3>(64 << 20, 8, 1);
+        return 0;
+    }
     if (argc > 1 && std::string(argv[1]) == "focus2") {
         focus2_m<1>(64 << 20, 16, 2);
         focus2_m<1>(1024ull << 20, 1, 1);
