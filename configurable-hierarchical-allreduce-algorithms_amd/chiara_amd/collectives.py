@@ -32,6 +32,7 @@ DTYPE_SIZE = {FLOAT32: 4, FLOAT64: 8, INT32: 4, BFLOAT16: 2}
 MODE_ALLREDUCE, MODE_REDUCE_SCATTER = 0, 1
 # MPICH baselines (testing/mpich_implementations/all_reduce/), chr_mode numbering
 MODE_MPICH_RING, MODE_MPICH_RD, MODE_MPICH_RSAG, MODE_MPICH_RECEXCH = 2, 3, 4, 5
+MODE_MPICH_KRSAG, MODE_MPICH_RMULT = 6, 7
 REDUCE_RUNNING_FIRST = 1  # chr_reduce_multi_ex flag (MPICH_do_reduce operand order)
 
 
@@ -246,6 +247,18 @@ def MPICH_Allreduce_recursive_exchange(sendbuf, recvbuf, count, datatype, op, co
     """allreduce_recexch.cpp:188 -- k-way MPICH_do_reduce (:147-186) on the fused kernel."""
     return _mpich(MODE_MPICH_RECEXCH, sendbuf, recvbuf, count, datatype, op, comm, k, single_phase_recv,
                   async_op=async_op)
+
+
+def MPICH_Allreduce_k_reduce_scatter_allgather(sendbuf, recvbuf, count, datatype, op, comm, k, single_phase_recv,
+                                               async_op=False):
+    """allreduce_k_reduce_scatter_allgather.cpp:257 -- k-ary digit-reversed reduce-scatter + allgather."""
+    return _mpich(MODE_MPICH_KRSAG, sendbuf, recvbuf, count, datatype, op, comm, k, single_phase_recv,
+                  async_op=async_op)
+
+
+def MPICH_Allreduce_recursive_multiplying(sendbuf, recvbuf, count, datatype, op, comm, k, async_op=False):
+    """allreduce_recursive_multiplying.cpp:3 -- k-ary recursive doubling."""
+    return _mpich(MODE_MPICH_RMULT, sendbuf, recvbuf, count, datatype, op, comm, k, async_op=async_op)
 
 
 def reduce_multi_ex(out, acc, ins, count, datatype, op, flags, stream=None):

@@ -509,8 +509,7 @@ int chr_local_reduce_scatter_radix_batch(chr_local_group* g, const void* const* 
 }
 
 static bool valid_mpich_mode(chr_mode m) {
-    return m == CHR_MODE_MPICH_RING || m == CHR_MODE_MPICH_RD || m == CHR_MODE_MPICH_RSAG ||
-           m == CHR_MODE_MPICH_RECEXCH;
+    return m >= CHR_MODE_MPICH_RING && m <= CHR_MODE_MPICH_RMULT;
 }
 
 int chr_allreduce_mpich(const void* send, void* recv, size_t count, chr_dtype dtype, chr_op op, chr_comm* comm,

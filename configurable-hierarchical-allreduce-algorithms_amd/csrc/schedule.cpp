@@ -679,6 +679,174 @@ void build_recexch(MB& b, int k_in) {  // allreduce_recexch.cpp:188-440 (float p
     }
 }
 
+// allreduce_recursive_multiplying.cpp:3-176.  Every k-way combine (the pre-fold :58-84 and
+// each level :110-145) folds the members' buffers left to right with the running value as
+// the first operand -- the same chain as MPICH_do_reduce.
+void build_rmult(MB& b, int k) {
+    const int n = b.n, me = b.me;
+    const uint64_t cnt = b.count;
+    int pofk = 1;
+    while (pofk * k <= n) pofk *= k;
+    auto chain = [&](Step& s, const std::vector<Ref>& seq) {
+        LocalOp op = make_reduce({BUF_RECV, 0}, seq[0], std::vector<Ref>(seq.begin() + 1, seq.end()), cnt, 123);
+        op.swap = true;
+        s.post.push_back(op);
+    };
+    if (pofk < n) {
+        Step& s = b.add("rm-pre");
+        if (me >= pofk) {
+            s.sends.push_back({me % pofk, {BUF_RECV, 0}, cnt});
+        } else {
+            std::vector<Ref> seq;
+            for (int src = me + pofk; src < n; src += pofk) {
+                const uint64_t slot = (uint64_t)seq.size() * cnt;
+                s.recvs.push_back({src, {BUF_STAGE, slot}, cnt});
+                seq.push_back({BUF_STAGE, slot});
+            }
+            if (!seq.empty()) {
+                b.need((uint64_t)seq.size() * cnt);
+                seq.push_back({BUF_RECV, 0});
+                chain(s, seq);
+            }
+        }
+    }
+    for (int distance = 1, next = k; distance < pofk; distance = next, next *= k) {
+        Step& s = b.add("rm-level");
+        if (me >= pofk) continue;
+        const int start = me / next * next;
+        std::vector<Ref> seq;
+        uint64_t e = 0;
+        for (int dst = start + me % distance; dst < start + next; dst += distance) {
+            if (dst == me) {
+                seq.push_back({BUF_RECV, 0});
+                continue;
+            }
+            s.sends.push_back({dst, {BUF_RECV, 0}, cnt});
+            s.recvs.push_back({dst, {BUF_STAGE, e * cnt}, cnt});
+            seq.push_back({BUF_STAGE, e * cnt});
+            ++e;
+        }
+        b.need(e * cnt);
+        chain(s, seq);
+    }
+    if (pofk < n) {
+        Step& s = b.add("rm-post");
+        if (me >= pofk) s.recvs.push_back({me % pofk, {BUF_RECV, 0}, cnt});
+        else
+            for (int dst = me + pofk; dst < n; dst += pofk) s.sends.push_back({dst, {BUF_RECV, 0}, cnt});
+    }
+}
+
+// allreduce_k_reduce_scatter_allgather.cpp:257-533: recexch step 1, a k-ary reduce-scatter
+// over the base-k digit-reversed blocks, the mirror allgather, step 3.  The reference runs
+// each neighbour of a phase as its own blocking exchange; the blocks involved are disjoint,
+// so one group per phase with a fused (k-1)-way reduce in neighbour order is the same data
+// flow and the same per-element reduction order.
+struct KrsagGeom {
+    int n, k, pofk, rem, T, log_pofk;
+    std::vector<uint64_t> cnts, displs;
+    int reverse_digits(int rank) const {  // :66-120
+        int s2 = rank < T ? rank / k : rank - rem;
+        std::vector<int> digit(std::max(log_pofk, 1), 0);
+        for (int i = 0; s2 != 0; ++i) {
+            digit[i] = s2 % k;
+            s2 /= k;
+        }
+        int rev = 0, power = 1;
+        for (int i = 0; i < log_pofk; ++i) {
+            rev += digit[log_pofk - 1 - i] * power;
+            power *= k;
+        }
+        return step2_to_orig(rev, rem, k);
+    }
+    void block(int rank, int level, uint64_t* off, uint64_t* cnt) const {  // :25-63
+        const int rr = reverse_digits(rank);
+        int kpp = 1;
+        while (level-- > 0) kpp *= k;
+        const int s2 = rr < T ? rr / k : rr - rem;
+        const int mn = (s2 / kpp) * kpp - 1, mx = mn + kpp;
+        const int omn = mn >= 0 ? step2_to_orig(mn, rem, k) : mn, omx = step2_to_orig(mx, rem, k);
+        *off = displs[omn + 1];
+        *cnt = 0;
+        for (int x = omn + 1; x <= omx; ++x) *cnt += cnts[x];
+    }
+};
+
+void build_krsag(MB& b, int k_in) {
+    const int n = b.n, me = b.me;
+    const uint64_t cnt = b.count;
+    if (k_in <= 1) k_in = 2;  // :273-275
+    Recexch x;
+    if (recexch_neighbors(me, n, k_in, &x)) {
+        b.p.error = 1;
+        return;
+    }
+    const int k = x.k, nph = x.step2_nphases;
+    const bool part = x.step1_sendto == -1;
+    {  // step 1 (:313-333): sequential receive + reduce, recvfrom order
+        Step& s = b.add("krsag-step1");
+        if (!part) {
+            s.sends.push_back({x.step1_sendto, {BUF_RECV, 0}, cnt});
+        } else if (x.step1_nrecvs) {
+            std::vector<Ref> ins;
+            for (int i = 0; i < x.step1_nrecvs; ++i) {
+                s.recvs.push_back({x.step1_recvfrom[i], {BUF_STAGE, (uint64_t)i * cnt}, cnt});
+                ins.push_back({BUF_STAGE, (uint64_t)i * cnt});
+            }
+            b.need((uint64_t)x.step1_nrecvs * cnt);
+            s.post.push_back(make_reduce({BUF_RECV, 0}, {BUF_RECV, 0}, ins, cnt, 327));
+        }
+    }
+    KrsagGeom g{n, k, x.p_of_k, n - x.p_of_k, x.T, nph, {}, {}};
+    g.cnts.assign(n + 1, 0);
+    g.displs.assign(n + 1, 0);
+    for (int i = 0; i < g.pofk - 1; ++i) g.cnts[step2_to_orig(i, g.rem, k)] = cnt / (uint64_t)g.pofk;  // :341-345
+    g.cnts[n - 1] = cnt - (cnt / (uint64_t)g.pofk) * (uint64_t)(g.pofk - 1);  // :346-347 (always rank n-1)
+    for (int i = 1; i < n; ++i) g.displs[i] = g.displs[i - 1] + g.cnts[i - 1];
+    for (int p = 0; p < nph; ++p) {  // reduce-scatter (:353-401)
+        Step& s = b.add("krsag-rs");
+        if (!part) continue;
+        const int j = nph - 1 - p;
+        uint64_t off, len;
+        g.block(me, j, &off, &len);
+        std::vector<Ref> ins;
+        for (int i = 0; i < k - 1; ++i) {
+            const int dst = x.step2_nbrs[p][i];
+            uint64_t soff, slen;
+            g.block(dst, j, &soff, &slen);
+            if (slen) s.sends.push_back({dst, {BUF_RECV, soff}, slen});
+            if (len) {
+                s.recvs.push_back({dst, {BUF_STAGE, (uint64_t)i * cnt + off}, len});
+                ins.push_back({BUF_STAGE, (uint64_t)i * cnt + off});
+            }
+        }
+        if (len) {
+            b.need((uint64_t)(k - 1) * cnt);
+            s.post.push_back(make_reduce({BUF_RECV, off}, {BUF_RECV, off}, ins, len, 395));
+        }
+    }
+    for (int p = 0; p < nph; ++p) {  // allgather (:403-493): level p, phase nph-1-p neighbours
+        Step& s = b.add("krsag-ag");
+        if (!part) continue;
+        const int ph = nph - 1 - p;
+        uint64_t off, len;
+        g.block(me, p, &off, &len);
+        for (int i = 0; i < k - 1; ++i) {
+            const int nbr = x.step2_nbrs[ph][i];
+            uint64_t roff, rlen;
+            g.block(nbr, p, &roff, &rlen);
+            if (len) s.sends.push_back({nbr, {BUF_RECV, off}, len});
+            if (rlen) s.recvs.push_back({nbr, {BUF_RECV, roff}, rlen});
+        }
+    }
+    {  // step 3 (:496-520)
+        Step& s = b.add("krsag-step3");
+        if (!part) s.recvs.push_back({x.step1_sendto, {BUF_RECV, 0}, cnt});
+        else
+            for (int i = 0; i < x.step1_nrecvs; ++i) s.sends.push_back({x.step1_recvfrom[i], {BUF_RECV, 0}, cnt});
+    }
+}
+
 }  // namespace
 
 Plan build_plan_mpich(Mode mode, int n, int me, int k, int aux, uint64_t count) {
@@ -686,7 +854,7 @@ Plan build_plan_mpich(Mode mode, int n, int me, int k, int aux, uint64_t count) 
     Plan p;
     p.mode = mode;
     p.rank = me;
-    if (n < 1 || me < 0 || me >= n || (mode == MODE_MPICH_RECEXCH && k < 2)) {
+    if (n < 1 || me < 0 || me >= n || ((mode == MODE_MPICH_RECEXCH || mode == MODE_MPICH_RMULT) && k < 2)) {
         p.error = 1;
         return p;
     }
@@ -703,6 +871,8 @@ Plan build_plan_mpich(Mode mode, int n, int me, int k, int aux, uint64_t count) 
     case MODE_MPICH_RD: build_rd(b); break;
     case MODE_MPICH_RSAG: build_rsag(b); break;
     case MODE_MPICH_RECEXCH: build_recexch(b, k); break;
+    case MODE_MPICH_KRSAG: build_krsag(b, k); break;
+    case MODE_MPICH_RMULT: build_rmult(b, k); break;
     default: p.error = 1;
     }
     return p;

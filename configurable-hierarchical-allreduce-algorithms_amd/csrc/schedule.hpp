@@ -64,9 +64,11 @@ enum Mode : int {
     MODE_MPICH_RING = 2,       // testing/mpich_implementations/all_reduce/allreduce_ring.cpp
     MODE_MPICH_RD = 3,         // .../allreduce_recursive_doubling.cpp
     MODE_MPICH_RSAG = 4,       // .../allreduce_reduce_scatter_allgather.cpp
-    MODE_MPICH_RECEXCH = 5     // .../allreduce_recexch.cpp (k, single_phase_recv)
+    MODE_MPICH_RECEXCH = 5,    // .../allreduce_recexch.cpp (k, single_phase_recv)
+    MODE_MPICH_KRSAG = 6,      // .../allreduce_k_reduce_scatter_allgather.cpp (k, single_phase_recv)
+    MODE_MPICH_RMULT = 7       // .../allreduce_recursive_multiplying.cpp (k)
 };
-inline bool is_mpich(int mode) { return mode >= MODE_MPICH_RING && mode <= MODE_MPICH_RECEXCH; }
+inline bool is_mpich(int mode) { return mode >= MODE_MPICH_RING && mode <= MODE_MPICH_RMULT; }
 
 struct Geometry {
     int nranks = 0, b = 0, k = 0, nnodes = 0, nstages = 0, nu = 0, nph = 0;

@@ -8,10 +8,12 @@
 //       replaces Fugaku_experiments/Allreduce/all_reduce_radix_batch.cpp:202-204
 //   int reduce_scatter_radix_batch(const void*, void*, MPI_Aint, MPI_Datatype, MPI_Op, MPI_Comm, int, int)
 //       replaces Fugaku_experiments/Reduce-scatter/reduce_scatter_radix_batch.cpp:200-202
-//   MPICH_Allreduce_{ring, recursive_doubling, reduce_scatter_allgather, recursive_exchange}
+//   MPICH_Allreduce_{ring, recursive_doubling, reduce_scatter_allgather, recursive_exchange,
+//                    k_reduce_scatter_allgather, recursive_multiplying}
 //       replace testing/mpich_implementations/all_reduce/allreduce_{ring.cpp:3,
-//       recursive_doubling.cpp:4, reduce_scatter_allgather.cpp:3, recexch.cpp:188}
-//       (the baselines testing/main.cpp times CHiArA against)
+//       recursive_doubling.cpp:4, reduce_scatter_allgather.cpp:3, recexch.cpp:188,
+//       k_reduce_scatter_allgather.cpp:257, recursive_multiplying.cpp:3}: all six baselines
+//       testing/main.cpp times, so that harness links against libchiara unchanged
 //
 // One chr_comm per MPI communicator, created on first use (RCCL unique id broadcast with
 // MPI_Bcast, device = node-local rank mod visible GPUs) and cached as an MPI attribute.
@@ -140,4 +142,14 @@ int MPICH_Allreduce_reduce_scatter_allgather(const char* sendbuf, char* recvbuf,
 int MPICH_Allreduce_recursive_exchange(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype,
                                        MPI_Op op, MPI_Comm comm, int k, int single_phase_recv) {
     return mpich_call(CHR_MODE_MPICH_RECEXCH, sendbuf, recvbuf, count, datatype, op, comm, k, single_phase_recv);
+}
+
+int MPICH_Allreduce_k_reduce_scatter_allgather(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype,
+                                               MPI_Op op, MPI_Comm comm, int k, int single_phase_recv) {
+    return mpich_call(CHR_MODE_MPICH_KRSAG, sendbuf, recvbuf, count, datatype, op, comm, k, single_phase_recv);
+}
+
+int MPICH_Allreduce_recursive_multiplying(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype,
+                                          MPI_Op op, MPI_Comm comm, int k) {
+    return mpich_call(CHR_MODE_MPICH_RMULT, sendbuf, recvbuf, count, datatype, op, comm, k, 0);
 }

@@ -147,7 +147,9 @@ typedef enum {
     CHR_MODE_MPICH_RING = 2,       /* testing/mpich_implementations/all_reduce/allreduce_ring.cpp:3 */
     CHR_MODE_MPICH_RD = 3,         /* .../allreduce_recursive_doubling.cpp:4 */
     CHR_MODE_MPICH_RSAG = 4,       /* .../allreduce_reduce_scatter_allgather.cpp:3 */
-    CHR_MODE_MPICH_RECEXCH = 5     /* .../allreduce_recexch.cpp:188 (k, b = single_phase_recv) */
+    CHR_MODE_MPICH_RECEXCH = 5,    /* .../allreduce_recexch.cpp:188 (k, b = single_phase_recv) */
+    CHR_MODE_MPICH_KRSAG = 6,      /* .../allreduce_k_reduce_scatter_allgather.cpp:257 (k, b = spr) */
+    CHR_MODE_MPICH_RMULT = 7       /* .../allreduce_recursive_multiplying.cpp:3 (k) */
 } chr_mode;
 long chr_plan_describe(chr_mode mode, int nranks, int rank, int k, int b, size_t count,
                        int slices, char* buf, size_t len);
@@ -159,8 +161,12 @@ long chr_plan_describe(chr_mode mode, int nranks, int rank, int k, int b, size_t
  *          MPICH_Allreduce_reduce_scatter_allgather(...)  (allreduce_reduce_scatter_allgather.cpp:3)
  *          MPICH_Allreduce_recursive_exchange(..., int k, int single_phase_recv)
  *                                                             (allreduce_recexch.cpp:188)
- * algo is one of CHR_MODE_MPICH_*; k / single_phase_recv are used by RECEXCH only
- * (single_phase_recv changes MPICH's buffering, not the data flow or the result).  Same
+ *          MPICH_Allreduce_k_reduce_scatter_allgather(..., int k, int single_phase_recv)
+ *                                          (allreduce_k_reduce_scatter_allgather.cpp:257)
+ *          MPICH_Allreduce_recursive_multiplying(..., int k)
+ *                                              (allreduce_recursive_multiplying.cpp:3)
+ * algo is one of CHR_MODE_MPICH_*; k is used by RECEXCH / KRSAG / RMULT, single_phase_recv
+ * by RECEXCH / KRSAG (it changes MPICH's receive posting, not the data flow or result).  Same
  * buffer contract as chr_allreduce_radix_batch; results bit-identical to the reference's
  * code on the same inputs, every reduction on the fused HIP kernel. */
 int chr_allreduce_mpich(const void* send, void* recv, size_t count, chr_dtype dtype, chr_op op,

@@ -622,3 +622,163 @@ int orc_allreduce_recexch(int n, int k_in, size_t count, int dtype, int op, cons
     free(x);
     return 0;
 }
+
+/* ---- testing/mpich_implementations/all_reduce/allreduce_recursive_multiplying.cpp ---- */
+
+/* running-value-first chain over seq[0..m-1] (MPI_Reduce_local(running, next) per step),
+ * result into out. */
+static void orc_chain_running_first(char* const* seq, int m, char* out, size_t count, int dtype, int op) {
+    size_t nb = count * orc_dtype_size(dtype);
+    char* run = (char*)malloc(nb + 1);
+    char* nxt = (char*)malloc(nb + 1);
+    int j;
+    memcpy(run, seq[0], nb);
+    for (j = 1; j < m; j++) {
+        char* t;
+        memcpy(nxt, seq[j], nb);
+        orc_reduce_local(run, nxt, count, dtype, op);
+        t = run;
+        run = nxt;
+        nxt = t;
+    }
+    memcpy(out, run, nb);
+    free(run);
+    free(nxt);
+}
+
+int orc_allreduce_recursive_multiplying(int n, int k, size_t count, int dtype, int op, const void* const* send,
+                                        void* const* recv) {
+    size_t es = orc_dtype_size(dtype), nb;
+    int r, pofk = 1, distance, next_distance;
+    char** R = (char**)recv;
+    char *snap, **seq;
+    if (n < 1 || !es || k < 2) return 1;
+    nb = count * es;
+    orc_copy_in(n, count, es, send, recv);
+    while (pofk * k <= n) pofk *= k; /* :13-17 */
+    seq = (char**)calloc((size_t)(n > k ? n : k) + 1, sizeof(char*));
+    if (pofk < n) /* :43-86: rank r < pofk folds r+pofk, r+2pofk, ... then its own buffer */
+        for (r = 0; r < pofk; r++) {
+            int m = 0, src;
+            for (src = r + pofk; src < n; src += pofk) seq[m++] = R[src];
+            if (!m) continue;
+            seq[m++] = R[r];
+            orc_chain_running_first(seq, m, R[r], count, dtype, op);
+        }
+    snap = (char*)malloc(nb * (size_t)n + 1);
+    for (distance = 1, next_distance = k; distance < pofk; distance = next_distance, next_distance *= k) {
+        for (r = 0; r < pofk; r++) memcpy(snap + (size_t)r * nb, R[r], nb);
+        for (r = 0; r < pofk; r++) { /* :88-152: group members ascending, folded left */
+            int start = r / next_distance * next_distance, m = 0, dst;
+            for (dst = start + r % distance; dst < start + next_distance; dst += distance)
+                seq[m++] = snap + (size_t)dst * nb;
+            orc_chain_running_first(seq, m, R[r], count, dtype, op);
+        }
+    }
+    for (r = pofk; r < n; r++) memcpy(R[r], R[r % pofk], nb); /* :154-172 */
+    free(snap);
+    free(seq);
+    return 0;
+}
+
+/* ---- testing/mpich_implementations/all_reduce/allreduce_k_reduce_scatter_allgather.cpp ---- */
+
+static int orc_reverse_digits_step2(int rank, int n, int k) { /* :66-120 */
+    int pofk = 1, log_pofk = 0, rem, T, s2, i, rev = 0, power = 1;
+    int digit[32];
+    while (pofk <= n) { pofk *= k; log_pofk++; }
+    pofk /= k;
+    log_pofk--;
+    rem = n - pofk;
+    T = (rem * k) / (k - 1);
+    s2 = (rank < T) ? rank / k : rank - rem;
+    for (i = 0; i < log_pofk; i++) digit[i] = 0;
+    for (i = 0; s2 != 0; i++) { digit[i] = s2 % k; s2 /= k; }
+    for (i = 0; i < log_pofk; i++) { rev += digit[log_pofk - 1 - i] * power; power *= k; }
+    return orc_step2_to_orig(rev, rem, k);
+}
+
+static void orc_krsag_block(int rank, int level, int n, int k, const size_t* cnts, const size_t* displs,
+                            size_t* off, size_t* cnt) { /* :25-63 on the reversed rank */
+    int pofk = 1, rem, T, s2, kpp = 1, mn, mx, omn, omx, x;
+    int rr = orc_reverse_digits_step2(rank, n, k);
+    while (pofk <= n) pofk *= k;
+    pofk /= k;
+    rem = n - pofk;
+    T = (rem * k) / (k - 1);
+    while (level-- > 0) kpp *= k;
+    s2 = (rr < T) ? rr / k : rr - rem;
+    mn = ((s2 / kpp) * kpp) - 1;
+    mx = mn + kpp;
+    omn = (mn >= 0) ? orc_step2_to_orig(mn, rem, k) : mn;
+    omx = orc_step2_to_orig(mx, rem, k);
+    *off = displs[omn + 1];
+    *cnt = 0;
+    for (x = 0; x < omx - omn; x++) *cnt += cnts[omn + 1 + x];
+}
+
+int orc_allreduce_k_reduce_scatter_allgather(int n, int k_in, size_t count, int dtype, int op,
+                                             const void* const* send, void* const* recv) {
+    size_t es = orc_dtype_size(dtype), nb;
+    int r, i, p, k, nph, pofk, rem;
+    char** R = (char**)recv;
+    orc_recexch_t* x;
+    size_t *cnts, *displs;
+    char* snap;
+    if (n < 1 || !es) return 1;
+    if (k_in <= 1) k_in = 2; /* :273-275 */
+    nb = count * es;
+    orc_copy_in(n, count, es, send, recv);
+    x = (orc_recexch_t*)calloc((size_t)n, sizeof(orc_recexch_t));
+    for (r = 0; r < n; r++)
+        if (orc_recexch_neighbors(r, n, k_in, &x[r])) {
+            free(x);
+            return 1;
+        }
+    k = x[0].k;
+    nph = x[0].step2_nphases;
+    pofk = x[0].p_of_k;
+    rem = n - pofk;
+    for (r = 0; r < n; r++) /* step 1 (:313-333) */
+        if (x[r].step1_sendto == -1)
+            for (i = 0; i < x[r].step1_nrecvs; i++) orc_reduce_local(R[x[r].step1_recvfrom[i]], R[r], count, dtype, op);
+    /* block sizes (:335-351); the last participant (always rank n-1: rem/(k-1) < p_of_k)
+     * takes the remainder */
+    cnts = (size_t*)calloc((size_t)n + 1, sizeof(size_t));
+    displs = (size_t*)calloc((size_t)n + 1, sizeof(size_t));
+    for (i = 0; i < pofk - 1; i++) cnts[orc_step2_to_orig(i, rem, k)] = count / (size_t)pofk;
+    cnts[n - 1] = count - (count / (size_t)pofk) * (size_t)(pofk - 1);
+    for (i = 1; i < n; i++) displs[i] = displs[i - 1] + cnts[i - 1];
+    snap = (char*)malloc(nb * (size_t)n + 1);
+    for (p = 0; p < nph; p++) { /* reduce-scatter (:353-401): level j = nph-1-p */
+        const int j = nph - 1 - p;
+        for (r = 0; r < n; r++) memcpy(snap + (size_t)r * nb, R[r], nb);
+        for (r = 0; r < n; r++) {
+            size_t off, cnt;
+            if (x[r].step1_sendto != -1) continue;
+            orc_krsag_block(r, j, n, k, cnts, displs, &off, &cnt);
+            for (i = 0; i < k - 1; i++)
+                orc_reduce_local(snap + (size_t)x[r].step2_nbrs[p][i] * nb + off * es, R[r] + off * es, cnt, dtype, op);
+        }
+    }
+    for (p = 0; p < nph; p++) { /* allgather (:403-493): level p with phase nph-1-p nbrs */
+        const int ph = nph - 1 - p;
+        for (r = 0; r < n; r++) memcpy(snap + (size_t)r * nb, R[r], nb);
+        for (r = 0; r < n; r++) {
+            if (x[r].step1_sendto != -1) continue;
+            for (i = 0; i < k - 1; i++) {
+                size_t off, cnt;
+                const int nbr = x[r].step2_nbrs[ph][i];
+                orc_krsag_block(nbr, p, n, k, cnts, displs, &off, &cnt);
+                memcpy(R[r] + off * es, snap + (size_t)nbr * nb + off * es, cnt * es);
+            }
+        }
+    }
+    for (r = 0; r < n; r++) /* step 3 (:496-520) */
+        if (x[r].step1_sendto != -1) memcpy(R[r], R[x[r].step1_sendto], nb);
+    free(snap);
+    free(cnts);
+    free(displs);
+    free(x);
+    return 0;
+}

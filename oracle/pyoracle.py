@@ -108,11 +108,14 @@ def _setup_mpich(L):
         fn = getattr(L, name)
         fn.argtypes = [i, sz, i, i, ctypes.POINTER(vp), ctypes.POINTER(vp)]
         fn.restype = i
-    L.orc_allreduce_recexch.argtypes = [i, i, sz, i, i, ctypes.POINTER(vp), ctypes.POINTER(vp)]
-    L.orc_allreduce_recexch.restype = i
+    for name in ("orc_allreduce_recexch", "orc_allreduce_recursive_multiplying",
+                 "orc_allreduce_k_reduce_scatter_allgather"):
+        fn = getattr(L, name)
+        fn.argtypes = [i, i, sz, i, i, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+        fn.restype = i
 
 
-MPICH_ALGOS = ("ring", "rd", "rsag", "rx")
+MPICH_ALGOS = ("ring", "rd", "rsag", "rx", "krsag", "rm")
 
 
 def mpich_allreduce(algo, sends, dtype, op, k=2, inplace=False):
@@ -134,6 +137,10 @@ def mpich_allreduce(algo, sends, dtype, op, k=2, inplace=False):
         rc = L.orc_allreduce_reduce_scatter_allgather(n, count, DTYPES[dtype], OPS[op], sp, rp)
     elif algo == "rx":
         rc = L.orc_allreduce_recexch(n, k, count, DTYPES[dtype], OPS[op], sp, rp)
+    elif algo == "rm":
+        rc = L.orc_allreduce_recursive_multiplying(n, k, count, DTYPES[dtype], OPS[op], sp, rp)
+    elif algo == "krsag":
+        rc = L.orc_allreduce_k_reduce_scatter_allgather(n, k, count, DTYPES[dtype], OPS[op], sp, rp)
     else:
         raise ValueError(algo)
     if rc:

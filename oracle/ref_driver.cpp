@@ -11,8 +11,8 @@
 //
 // Usage: mpiexec -n N ref_driver <cases.txt> <outdir>
 //   one case per line: id mode k b count dtype op pattern seed inplace
-//   mode: ar | rs (radix_batch), ring | rd | rsag | rx (MPICH baselines; rx uses b as
-//   single_phase_recv)
+//   mode: ar | rs (radix_batch), ring | rd | rsag | rx | krsag | rm (MPICH baselines; rx and
+//   krsag use b as single_phase_recv)
 // For each case rank 0 writes <outdir>/<id>.out (all ranks' outputs, rank-major) and
 // <outdir>/<id>.lib (the MPI library collective's result on the same inputs).
 #include <mpi.h>
@@ -41,6 +41,10 @@ int MPICH_Allreduce_reduce_scatter_allgather(const char* sendbuf, char* recvbuf,
                                              MPI_Op op, MPI_Comm comm);
 int MPICH_Allreduce_recursive_exchange(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype,
                                        MPI_Op op, MPI_Comm comm, int k, int single_phase_recv);
+int MPICH_Allreduce_k_reduce_scatter_allgather(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype,
+                                               MPI_Op op, MPI_Comm comm, int k, int single_phase_recv);
+int MPICH_Allreduce_recursive_multiplying(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype,
+                                          MPI_Op op, MPI_Comm comm, int k);
 
 // orc_reduce_local is the single definition of the bf16 op semantics.
 static void bf16_user_op(void* in, void* inout, int* len, MPI_Datatype*) {
@@ -124,7 +128,8 @@ int main(int argc, char** argv) {
             MPI_Barrier(MPI_COMM_WORLD);
             all_reduce_radix_batch(inplace ? (char*)MPI_IN_PLACE : send.data(), recv.data(), (int)count,
                                    mdt, mop, MPI_COMM_WORLD, k, b);
-        } else if (mode == "ring" || mode == "rd" || mode == "rsag" || mode == "rx") {
+        } else if (mode == "ring" || mode == "rd" || mode == "rsag" || mode == "rx" || mode == "krsag" ||
+                   mode == "rm") {
             MPI_Allreduce(send.data(), lib.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
             if (inplace) memcpy(recv.data(), send.data(), in_n * es);
             MPI_Barrier(MPI_COMM_WORLD);
@@ -133,7 +138,11 @@ int main(int argc, char** argv) {
             else if (mode == "rd") MPICH_Allreduce_recursive_doubling(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
             else if (mode == "rsag")
                 MPICH_Allreduce_reduce_scatter_allgather(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
-            else MPICH_Allreduce_recursive_exchange(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD, k, b);
+            else if (mode == "rx")
+                MPICH_Allreduce_recursive_exchange(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD, k, b);
+            else if (mode == "krsag")
+                MPICH_Allreduce_k_reduce_scatter_allgather(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD, k, b);
+            else MPICH_Allreduce_recursive_multiplying(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD, k);
         } else {
             MPI_Reduce_scatter_block(send.data(), lib.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
             if (inplace) memcpy(recv.data(), send.data(), in_n * es);

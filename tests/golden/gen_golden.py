@@ -94,7 +94,8 @@ LARGE = [
 
 def mpich_cases_for(n):
     """testing/main.cpp baselines: ring, recursive doubling,
-    reduce-scatter+allgather (Rabenseifner), recursive exchange (k, single_phase_recv)."""
+    reduce-scatter+allgather (Rabenseifner), recursive exchange and k-reduce-scatter-allgather
+    (k, single_phase_recv), recursive multiplying (k)."""
     out = []
 
     def add(mode, k, b, count, dt, op, pat, inplace):
@@ -124,6 +125,22 @@ def mpich_cases_for(n):
             add("rx", k, spr, 64, "f32", "max", pyoracle.PAT_TIES, 0)
             add("rx", k, spr, 64, "f32", "min", pyoracle.PAT_TIES, 1)
             add("rx", k, spr, 64, "bf16", "max", pyoracle.PAT_TIES, 0)
+            # k-reduce-scatter-allgather (k, single_phase_recv)
+            for count in (1, 33, 500):
+                add("krsag", k, spr, count, "f32", "sum", pyoracle.PAT_UNIFORM, 0)
+            add("krsag", k, spr, 64, "f64", "sum", pyoracle.PAT_UNIFORM, 1)
+            add("krsag", k, spr, 64, "i32", "sum", pyoracle.PAT_SEQ, 0)
+            add("krsag", k, spr, 64, "f32", "max", pyoracle.PAT_TIES, 0)
+            add("krsag", k, spr, 64, "bf16", "sum", pyoracle.PAT_UNIFORM, 0)
+        # recursive multiplying (k)
+        for count in (1, 33, 500):
+            add("rm", k, 0, count, "f32", "sum", pyoracle.PAT_UNIFORM, 0)
+        add("rm", k, 0, 64, "f64", "sum", pyoracle.PAT_UNIFORM, 1)
+        add("rm", k, 0, 64, "i32", "sum", pyoracle.PAT_SEQ, 0)
+        add("rm", k, 0, 64, "f32", "max", pyoracle.PAT_TIES, 0)
+        add("rm", k, 0, 64, "f32", "min", pyoracle.PAT_TIES, 1)
+        add("rm", k, 0, 64, "bf16", "max", pyoracle.PAT_TIES, 0)
+        add("rm", k, 0, 64, "bf16", "sum", pyoracle.PAT_UNIFORM, 0)
     return out
 
 
@@ -188,7 +205,8 @@ def main():
                 arrays[c["id"] + "__lib"] = lb.copy()
             manifest.append(rec)
     ref_desc = ("testing/mpich_implementations/all_reduce/{allreduce_ring,allreduce_recursive_doubling,"
-                "allreduce_reduce_scatter_allgather,allreduce_recexch}.cpp" if which == "mpich" else
+                "allreduce_reduce_scatter_allgather,allreduce_recexch,allreduce_k_reduce_scatter_allgather,"
+                "allreduce_recursive_multiplying}.cpp" if which == "mpich" else
                 "Fugaku_experiments/{Allreduce/all_reduce_radix_batch.cpp,Reduce-scatter/reduce_scatter_radix_batch.cpp}")
     with open(os.path.join(HERE, prefix + "manifest.json"), "w") as f:
         json.dump({"generator": f"tests/golden/gen_golden.py {which}",

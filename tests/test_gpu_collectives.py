@@ -172,11 +172,11 @@ def test_rccl_comm_single_rank(gu):
 # ---- MPICH baselines (testing/main.cpp) on the same kernels --------------------------------
 
 MPICH_MODE = {"ring": ca.MODE_MPICH_RING, "rd": ca.MODE_MPICH_RD, "rsag": ca.MODE_MPICH_RSAG,
-              "rx": ca.MODE_MPICH_RECEXCH}
+              "rx": ca.MODE_MPICH_RECEXCH, "krsag": ca.MODE_MPICH_KRSAG, "rm": ca.MODE_MPICH_RMULT}
 
 
 def test_mpich_baselines_match_reference_golden(gu, groups, golden_mpich):
-    """ring / recursive doubling / Rabenseifner / recexch: every golden case bit-exact."""
+    """All six testing/main.cpp baselines: every golden case bit-exact on the device."""
     cases, _ = golden_mpich
     bad = []
     for c in cases:
@@ -197,7 +197,7 @@ def test_mpich_baselines_match_reference_golden(gu, groups, golden_mpich):
     assert not bad, f"{len(bad)} device/reference mismatches, e.g. {bad[:5]}"
 
 
-@pytest.mark.parametrize("algo", ["ring", "rd", "rsag", "rx"])
+@pytest.mark.parametrize("algo", sorted(MPICH_MODE))
 def test_mpich_baselines_large_int_exact(gu, groups, algo):
     """8 ranks, 4M int32 (the size class testing/main.cpp reaches): exact vs the oracle."""
     n, count = 8, (1 << 22) + 5

@@ -64,6 +64,12 @@ def _worker(rank, world, port, cases, q):
             elif mode == "rx":
                 rc = ca.MPICH_Allreduce_recursive_exchange(send, dst, count, cdt, ca.MAX, comm, k, b)
                 ref = po.mpich_allreduce("rx", allx, dtype, "max", k=k)[rank]
+            elif mode == "krsag":
+                rc = ca.MPICH_Allreduce_k_reduce_scatter_allgather(send, dst, count, cdt, ca.SUM, comm, k, b)
+                ref = po.mpich_allreduce("krsag", allx, dtype, "sum", k=k)[rank]
+            elif mode == "rm":
+                rc = ca.MPICH_Allreduce_recursive_multiplying(send, dst, count, cdt, ca.SUM, comm, k)
+                ref = po.mpich_allreduce("rm", allx, dtype, "sum", k=k)[rank]
             else:
                 fn = {"ring": ca.MPICH_Allreduce_ring, "rd": ca.MPICH_Allreduce_recursive_doubling,
                       "rsag": ca.MPICH_Allreduce_reduce_scatter_allgather}[mode]
@@ -112,7 +118,9 @@ def test_rccl_mpich_baselines_world5_and_8():
     """testing/main.cpp's baselines over RCCL, non-power-of-two (fold/unfold) and 8 ranks."""
     cases = [("ring", 0, 0, 100003, "f32", False, 0), ("rd", 0, 0, 4099, "f32", False, 0),
              ("rsag", 0, 0, 65537, "f32", True, 0), ("rx", 3, 0, 20000, "f32", False, 0),
-             ("rx", 2, 1, 777, "bf16", False, 0)]
+             ("rx", 2, 1, 777, "bf16", False, 0), ("krsag", 2, 0, 30011, "f32", False, 0),
+             ("rm", 2, 0, 4097, "f32", False, 0)]
     _run(5, cases)
-    _run(8, cases[:1] + [("rx", 4, 0, 1 << 16, "f32", False, 0), ("rsag", 0, 0, 1 << 16, "bf16", False, 0)],
+    _run(8, cases[:1] + [("rx", 4, 0, 1 << 16, "f32", False, 0), ("rsag", 0, 0, 1 << 16, "bf16", False, 0),
+                         ("krsag", 2, 1, 1 << 16, "f32", False, 0), ("rm", 3, 0, 12345, "bf16", False, 0)],
          timeout=600)

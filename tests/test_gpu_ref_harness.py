@@ -2,7 +2,8 @@
 and Reduce-scatter/main.cpp, compiled unchanged in the container into oracle/_ref/) linked
 against libchiara through the reference-signature shim (csrc/shim/chiara_mpi_shim.cpp).
 Their built-in is_correct (equality with MPI_Allreduce / MPI_Reduce_scatter_block on int32)
-must be 1 on every row.  4 MPI ranks share the test box's one GPU: each gets its own
+must be 1 on every row.  Likewise testing/main.cpp, the sweep of the six MPICH baselines
+(check_correctness vs MPI_Allreduce on doubles, eps 1e-6).  4-5 MPI ranks share the test box's one GPU: each gets its own
 NCCL_HOSTID so RCCL treats them as separate hosts."""
 import csv
 import os
@@ -46,4 +47,15 @@ def test_reference_reduce_scatter_harness_on_mi355x(tmp_path):
     rows = _run("ref_harness_reduce_scatter", ["2", "--overwrite", "b=4", "base=1000"], 4, tmp_path)
     ours = [r for r in rows if r["algorithm_name"] == "reduce_scatter_radix_batch"]
     assert len(ours) == 2 * 2 * 20
+    assert all(r["is_correct"] == "1" for r in rows)
+
+
+def test_reference_mpich_baseline_harness_on_mi355x(tmp_path):
+    """testing/main.cpp unchanged: every baseline, k = 2..nprocs-1, 50 reps per size."""
+    rows = _run("ref_harness_testing", ["3", "--overwrite"], 5, tmp_path)
+    names = {r["algorithm_name"] for r in rows}
+    assert names == {"reduce_scatter_allgather_k", "recursive_exchange", "recursive_multiplying",
+                     "reduce_scatter_allgather", "ring", "recursive_doubling"}
+    assert len(rows) == 3 * (3 * 3 + 3) * 50  # sizes x (k in 2..4 x 3 + 3 without k) x reps
+    assert {r["send_count"] for r in rows} == {"8", "16", "32"}
     assert all(r["is_correct"] == "1" for r in rows)

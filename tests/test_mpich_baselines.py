@@ -16,7 +16,7 @@ import plan_sim
 import pyoracle as po
 
 MODE = {"ring": ca.MODE_MPICH_RING, "rd": ca.MODE_MPICH_RD, "rsag": ca.MODE_MPICH_RSAG,
-        "rx": ca.MODE_MPICH_RECEXCH}
+        "rx": ca.MODE_MPICH_RECEXCH, "krsag": ca.MODE_MPICH_KRSAG, "rm": ca.MODE_MPICH_RMULT}
 
 
 def _sends(c):
@@ -31,7 +31,7 @@ def test_manifest_covers_main_cpp_baselines(golden_mpich):
     cases, _ = golden_mpich
     assert len(cases) > 1000
     have = {(c["mode"], c["dtype"], c["op"], c["pattern"]) for c in cases}
-    for m in ("ring", "rd", "rsag", "rx"):
+    for m in MODE:
         assert (m, "f64", "sum", po.PAT_UNIFORM) in have  # testing/main.cpp's datatype
         assert (m, "f32", "max", po.PAT_TIES) in have
     assert {c["n"] for c in cases} >= {1, 2, 3, 5, 8, 12, 16}
@@ -63,13 +63,14 @@ def test_compiled_plans_match_reference(golden_mpich):
 
 def test_ties_pattern_detects_operand_order(golden_mpich):
     """The PAT_TIES cases really pin MPICH_do_reduce's running-value-first order: replaying
-    recexch with the default order (running value second) must disagree somewhere."""
+    recexch / recursive multiplying with the default order (running value second) must
+    disagree somewhere."""
     cases, _ = golden_mpich
-    rx = [c for c in cases if c["mode"] == "rx" and c["pattern"] == po.PAT_TIES and c["n"] >= 4]
+    rx = [c for c in cases if c["mode"] in ("rx", "rm") and c["pattern"] == po.PAT_TIES and c["n"] >= 4]
     assert rx
     flipped = 0
     for c in rx:
-        plans = plan_sim.load_plans(MODE["rx"], c["n"], c["k"], c["b"], c["count"])
+        plans = plan_sim.load_plans(MODE[c["mode"]], c["n"], c["k"], c["b"], c["count"])
         for p in plans:
             for st in p["steps"]:
                 st["post"] = [("reduce",) + op[1:] if op[0] == "reduce_sw" else op for op in st["post"]]
@@ -78,7 +79,7 @@ def test_ties_pattern_detects_operand_order(golden_mpich):
     assert flipped > 0
 
 
-@pytest.mark.parametrize("mode", ["ring", "rd", "rsag", "rx"])
+@pytest.mark.parametrize("mode", sorted(MODE))
 def test_plan_step_counts(mode):
     """Step structure follows the reference loops (all ranks agree on the step count)."""
     for n in (1, 2, 3, 6, 8, 13):
