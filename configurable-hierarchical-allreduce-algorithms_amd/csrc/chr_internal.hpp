@@ -27,10 +27,15 @@ hipError_t launch_fill(void* buf, size_t n, int dtype, int pattern, uint64_t see
 //   CHR_REDUCE_MAX_BLOCKS    cap on the grid (default 0 = one trip per workgroup)
 //   CHR_REDUCE_NT            0 / 1 forces plain / non-temporal loads+stores; unset = by size
 //   CHR_REDUCE_NT_MIN_BYTES  bytes streamed by one call from which NT is used (128 MiB)
+//   CHR_REDUCE_ACC0          0 / 1 forces the first accumulator slot nt / default policy
+//                            under NT; unset = default policy for m >= 2 or large buckets
+//   CHR_REDUCE_ACC0_MIN_BYTES  bucket size from which m = 1 uses it too (512 MiB)
 struct ReduceTuning {
     int max_blocks;
     int nt_mode;
     size_t nt_min_bytes;
+    int acc0_mode;
+    size_t acc0_min_bytes;
 };
 ReduceTuning& reduce_tuning();
 

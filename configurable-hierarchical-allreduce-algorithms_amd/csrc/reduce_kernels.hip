@@ -55,6 +55,10 @@ ReduceTuning& reduce_tuning() {
         r.nt_mode = s ? std::atoi(s) : -1;
         s = std::getenv("CHR_REDUCE_NT_MIN_BYTES");
         r.nt_min_bytes = s ? (size_t)std::atoll(s) : (size_t)128 << 20;
+        s = std::getenv("CHR_REDUCE_ACC0");   // 0 / 1 / unset = by fan-in and size
+        r.acc0_mode = s ? std::atoi(s) : -1;
+        s = std::getenv("CHR_REDUCE_ACC0_MIN_BYTES");
+        r.acc0_min_bytes = s ? (size_t)std::atoll(s) : (size_t)512 << 20;
         return r;
     }();
     return t;
@@ -146,19 +150,24 @@ __device__ __forceinline__ void st(u32x4* p, u32x4 v) {
 
 // U vectors (16 B each) per lane per trip; all M+1 operands of the trip are loaded
 // before the first add so (M+1)*U*16 bytes per lane are in flight.  NT: non-temporal
-// loads of the incoming buckets and non-temporal stores (global_load/store_dwordx4 ...
-// nt) for calls that stream far more than the caches hold: measured +15-40 % on HBM-cold
-// buckets.  The accumulator stream keeps the default policy even then: per-slot policy
-// sweep (profiles/r01/microbench_focus4.txt) +15 % at 1 GiB m=1, +9 % at 512 MiB m=3,
-// never slower.
-template <int DT, int OP, int M, int U, bool NT>
+// loads and stores (global_load/store_dwordx4 ... nt) for calls that stream far more than
+// the caches hold: +15-40 % on HBM-cold buckets.  ACC0: under NT, the FIRST of the U
+// accumulator vectors keeps the default policy (in place, a quarter of the write-backs then
+// go through the Infinity Cache): per-slot policy sweep
+// (profiles/r01/microbench_focus4_slot_policy.txt) +15 % at 1 GiB m=1, +3-5 % for m>=2,
+// -2 % for 64 MiB m=1, where launch_vec_m keeps every slot nt; making ALL accumulator
+// slots temporal thrashes the cache (-7 %).  Slot 0 is peeled so that the two policies
+// are separate instructions (a select between a plain and an nt load of one address is
+// merged by LLVM, dropping the nt bit).
+template <int DT, int OP, int M, int U, bool NT, bool ACC0>
 __global__ __launch_bounds__(kBlock) void k_reduce_vec(VecArgs a) {
     const size_t stride = (size_t)gridDim.x * kBlock * U;
     for (size_t base = (size_t)blockIdx.x * kBlock * U + threadIdx.x; base < a.nvec; base += stride) {
         if (base + (size_t)(U - 1) * kBlock < a.nvec) {
             u32x4 acc[U], x[M][U];
+            acc[0] = ld<NT && !ACC0>(&a.acc[base]);
 #pragma unroll
-            for (int u = 0; u < U; ++u) acc[u] = ld<false>(&a.acc[base + (size_t)u * kBlock]);
+            for (int u = 1; u < U; ++u) acc[u] = ld<NT>(&a.acc[base + (size_t)u * kBlock]);
 #pragma unroll
             for (int j = 0; j < M; ++j)
 #pragma unroll
@@ -217,10 +226,13 @@ static hipError_t launch_vec_m(const VecArgs& a, hipStream_t s) {
     const int grid = (int)(trips < cap ? trips : cap);
     const size_t call_bytes = (size_t)(M + 2) * a.nvec * 16;
     const bool nt = t.nt_mode == 1 || (t.nt_mode < 0 && call_bytes >= t.nt_min_bytes);
-    if (nt)
-        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true>), dim3(grid), dim3(kBlock), 0, s, a);
+    const bool acc0 = t.acc0_mode == 1 || (t.acc0_mode < 0 && (M >= 2 || a.nvec * 16 >= t.acc0_min_bytes));
+    if (!nt)
+        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, false, false>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (acc0)
+        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, true>), dim3(grid), dim3(kBlock), 0, s, a);
     else
-        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, false>), dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, false>), dim3(grid), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
 

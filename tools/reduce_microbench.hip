@@ -648,8 +648,58 @@ static void check() {
     std::printf("variant correctness: ok\n");
 }
 
+// Layout sensitivity of the product kernel (m = 1, 64 MiB buckets, 16 sets):
+//   paired   acc_s, in_s allocated back to back (per set)
+//   split    all acc buffers, then all in buffers (bench.py's order)
+//   split+off  split, every buffer inside a larger allocation at +odd*4 KiB
+//   slab     one slab, acc_s / in_s at s*2*B and s*2*B+B (exact power-of-two distances)
+//   slab+off the slab with in_s shifted by 4 KiB * (2s+1)
+static void layout_mode() {
+    const size_t B = 64ull << 20, nvec = B / 16;
+    const int sets = 16, reps = 200;
+    auto run = [&](const char* name, std::vector<f32x4*> acc, std::vector<f32x4*> in) {
+        for (int i = 0; i < sets; ++i) {
+            hipLaunchKernelGGL(k_rand, dim3(4096), dim3(256), 0, 0, acc[i], nvec, 0x9E37ull * (2 * i + 1));
+            hipLaunchKernelGGL(k_rand, dim3(4096), dim3(256), 0, 0, in[i], nvec, 0x9E37ull * (2 * i + 2));
+        }
+        CK(hipDeviceSynchronize());
+        for (int round = 0; round < 2; ++round) {
+            double us = time_launches([&](int i) {
+                const void* ins[1] = {in[i % sets]};
+                chr_reduce_multi(acc[i % sets], acc[i % sets], ins, 1, nvec * 4, CHR_FLOAT32, CHR_SUM, 0);
+            }, reps);
+            report(name, 1, B, us);
+        }
+    };
+    std::vector<void*> owned;
+    auto alloc = [&](size_t bytes) { void* p; CK(hipMalloc(&p, bytes)); owned.push_back(p); return (char*)p; };
+    auto release = [&]() { for (void* p : owned) CK(hipFree(p)); owned.clear(); };
+    std::vector<f32x4*> a(sets), b(sets);
+    for (int i = 0; i < sets; ++i) { a[i] = (f32x4*)alloc(B); b[i] = (f32x4*)alloc(B); }
+    run("layout paired", a, b);
+    release();
+    for (int i = 0; i < sets; ++i) a[i] = (f32x4*)alloc(B);
+    for (int i = 0; i < sets; ++i) b[i] = (f32x4*)alloc(B);
+    run("layout split", a, b);
+    release();
+    for (int i = 0; i < sets; ++i) a[i] = (f32x4*)(alloc(B + (1 << 20)) + 4096 * (2 * i + 1));
+    for (int i = 0; i < sets; ++i) b[i] = (f32x4*)(alloc(B + (1 << 20)) + 4096 * (2 * i + 1) + 65536);
+    run("layout split+off", a, b);
+    release();
+    char* slab = alloc(2 * B * sets + (4 << 20));
+    for (int i = 0; i < sets; ++i) { a[i] = (f32x4*)(slab + 2 * B * i); b[i] = (f32x4*)(slab + 2 * B * i + B); }
+    run("layout slab", a, b);
+    for (int i = 0; i < sets; ++i) b[i] = (f32x4*)(slab + 2 * B * i + B + 4096 * (2 * i + 1));
+    run("layout slab+off", a, b);
+    release();
+}
+
 int main(int argc, char** argv) {
     check();
+    if (argc > 1 && std::string(argv[1]) == "layout") {
+        layout_mode();
+        return 0;
+    }
     if (argc > 1 && std::string(argv[1]) == "focus4") {
         focus4_m<1>(1024ull << 20, 1, 2);
         focus4_m<1>(64 << 20, 16, 2);
