@@ -7,12 +7,13 @@ package is the Python mirror of the reference's operator interface over its C AB
 from ._lib import EXPORTED, ChiaraError, lib  # noqa: F401  (fails loudly without libchiara.so)
 from .collectives import (  # noqa: F401
     BFLOAT16, DOUBLE, DTYPE_SIZE, FLOAT, FLOAT32, FLOAT64, IN_PLACE, INT, INT32, MAX, MIN,
-    MODE_ALLREDUCE, MODE_MPICH_KRSAG, MODE_MPICH_RD, MODE_MPICH_RECEXCH, MODE_MPICH_RING,
+    MODE_ALLGATHER, MODE_ALLREDUCE, MODE_MPICH_KRSAG, MODE_MPICH_RD, MODE_MPICH_RECEXCH, MODE_MPICH_RING,
     MODE_MPICH_RMULT, MODE_MPICH_RSAG, MPICH_Allreduce_k_reduce_scatter_allgather,
     MPICH_Allreduce_recursive_multiplying,
     MODE_REDUCE_SCATTER, PROD, REDUCE_RUNNING_FIRST, SUCCESS, SUM, Comm, LocalGroup,
     MPICH_Allreduce_recursive_doubling, MPICH_Allreduce_recursive_exchange,
-    MPICH_Allreduce_reduce_scatter_allgather, MPICH_Allreduce_ring, all_reduce_radix_batch, check,
+    MPICH_Allreduce_reduce_scatter_allgather, MPICH_Allreduce_ring, all_reduce_radix_batch,
+    allgather_radix_batch, check,
     describe_plan, fill, get_unique_id, parse_plan, reduce_local, reduce_multi, reduce_multi_ex,
     reduce_scatter_radix_batch,
 )

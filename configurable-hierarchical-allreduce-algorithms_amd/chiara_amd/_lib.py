@@ -68,6 +68,9 @@ def _load():
         "chr_allreduce_mpich": ([vp, vp, sz, i, i, vp, i, i, i], i),
         "chr_allreduce_mpich_async": ([vp, vp, sz, i, i, vp, i, i, i], i),
         "chr_local_allreduce_mpich": ([vp, pp, pp, sz, i, i, i, i, i], i),
+        "chr_allgather_radix_batch": ([vp, sz, i, vp, vp, i, i], i),
+        "chr_allgather_radix_batch_async": ([vp, sz, i, vp, vp, i, i], i),
+        "chr_local_allgather_radix_batch": ([vp, pp, pp, sz, i, i, i], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -93,5 +96,6 @@ EXPORTED = [
     "chr_local_group_create", "chr_local_group_destroy", "chr_local_group_stream",
     "chr_local_allreduce_radix_batch", "chr_local_reduce_scatter_radix_batch", "chr_plan_describe", "chr_fill",
     "chr_error_string", "chr_abi_version", "chr_reduce_multi_ex", "chr_allreduce_mpich",
-    "chr_allreduce_mpich_async", "chr_local_allreduce_mpich",
+    "chr_allreduce_mpich_async", "chr_local_allreduce_mpich", "chr_allgather_radix_batch",
+    "chr_allgather_radix_batch_async", "chr_local_allgather_radix_batch",
 ]

@@ -33,6 +33,7 @@ MODE_ALLREDUCE, MODE_REDUCE_SCATTER = 0, 1
 # MPICH baselines (testing/mpich_implementations/all_reduce/), chr_mode numbering
 MODE_MPICH_RING, MODE_MPICH_RD, MODE_MPICH_RSAG, MODE_MPICH_RECEXCH = 2, 3, 4, 5
 MODE_MPICH_KRSAG, MODE_MPICH_RMULT = 6, 7
+MODE_ALLGATHER = 8
 REDUCE_RUNNING_FIRST = 1  # chr_reduce_multi_ex flag (MPICH_do_reduce operand order)
 
 
@@ -190,6 +191,11 @@ class LocalGroup:
         R = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in recvbufs])
         return lib().chr_local_reduce_scatter_radix_batch(self._h, S, R, recvcount, datatype, op, k, b)
 
+    def allgather_radix_batch(self, sendbufs, sendcount, datatype, recvbufs, k, b):
+        S = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in sendbufs])
+        R = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in recvbufs])
+        return lib().chr_local_allgather_radix_batch(self._h, S, R, sendcount, datatype, k, b)
+
     def allreduce_mpich(self, algo, sendbufs, recvbufs, count, datatype, op, k=2, single_phase_recv=0):
         """algo: MODE_MPICH_RING / _RD / _RSAG / _RECEXCH."""
         S = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in sendbufs])
@@ -218,6 +224,12 @@ def all_reduce_radix_batch(sendbuf, recvbuf, count, datatype, op, comm, k, b, as
 def reduce_scatter_radix_batch(sendbuf, recvbuf, recvcount, datatype, op, comm, k, b, async_op=False):
     fn = lib().chr_reduce_scatter_radix_batch_async if async_op else lib().chr_reduce_scatter_radix_batch
     return fn(_addr(sendbuf), _addr(recvbuf), recvcount, datatype, op, comm.handle, k, b)
+
+
+def allgather_radix_batch(sendbuf, sendcount, datatype, recvbuf, comm, k, b, async_op=False):
+    """all_gather_radix_batch_1_0.cpp:37 -- same argument order (sendbuf, sendcount, datatype, recvbuf, comm, k, b)."""
+    fn = lib().chr_allgather_radix_batch_async if async_op else lib().chr_allgather_radix_batch
+    return fn(_addr(sendbuf), sendcount, datatype, _addr(recvbuf), comm.handle, k, b)
 
 
 # ---- MPICH baselines driven by testing/main.cpp (same names and argument order) -----------------

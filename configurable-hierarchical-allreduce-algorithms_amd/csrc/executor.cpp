@@ -162,7 +162,7 @@ using PlanKey = std::tuple<int, int, int, int, uint64_t, int, int>;  // mode, ra
 
 // Pipeline depth: explicit setting, else CHR_SLICES, else by chunk size (schedule.cpp).
 int pick_slices(int setting, uint64_t count, int mode, int nranks, int b, size_t es) {
-    if (chr::is_mpich(mode)) return 1;  // the MPICH baselines run unpipelined, as written
+    if (chr::is_mpich(mode) || mode == chr::MODE_ALLGATHER) return 1;  // unpipelined schedules
     if (setting > 0) return setting;
     static const int env = [] {
         const char* v = std::getenv("CHR_SLICES");
@@ -244,7 +244,9 @@ int collective(chr_comm* c, int mode, const void* send, void* recv, size_t count
     if (!recv) return CHR_ERR_INVALID_ARG;
     const size_t es = chr::dtype_size(dtype);
     const bool inplace = send == CHR_IN_PLACE;
-    const void* input = inplace ? (const void*)recv : send;
+    const void* input = !inplace ? send
+                        : mode == chr::MODE_ALLGATHER ? (const void*)((char*)recv + (size_t)c->rank * count * es)
+                                                      : (const void*)recv;
     if (!input) return CHR_ERR_INVALID_ARG;
     hipError_t e = hipSetDevice(c->device);
     if (e != hipSuccess) return hip_code(e);
@@ -299,7 +301,9 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
         if (!recvs[r]) return CHR_ERR_INVALID_ARG;
         if ((e = g->acc[r].reserve(P[r].acc_elems * es, g->stream)) != hipSuccess) return hip_code(e);
         if ((e = g->stage[r].reserve(P[r].stage_elems * es, g->stream)) != hipSuccess) return hip_code(e);
-        const void* in = sends[r] == CHR_IN_PLACE ? recvs[r] : sends[r];
+        const void* in = sends[r] != CHR_IN_PLACE ? sends[r]
+                         : mode == chr::MODE_ALLGATHER ? (const void*)((char*)recvs[r] + (size_t)r * count * es)
+                                                       : (const void*)recvs[r];
         if (!in || !is_device_ptr(in) || !is_device_ptr(recvs[r])) return CHR_ERR_INVALID_ARG;
         B[r] = Bufs{(const char*)in, (char*)recvs[r], (char*)g->acc[r].p, (char*)g->stage[r].p, es};
     }
@@ -528,6 +532,21 @@ int chr_local_allreduce_mpich(chr_local_group* g, const void* const* sends, void
                               chr_dtype dtype, chr_op op, chr_mode algo, int k, int single_phase_recv) {
     if (!valid_mpich_mode(algo)) return CHR_ERR_INVALID_ARG;
     return local_collective(g, algo, sends, recvs, count, dtype, op, k, single_phase_recv);
+}
+
+int chr_allgather_radix_batch(const void* send, size_t sendcount, chr_dtype dtype, void* recv, chr_comm* comm, int k,
+                              int b) {
+    return collective(comm, chr::MODE_ALLGATHER, send, recv, sendcount, dtype, CHR_SUM, k, b, true);
+}
+
+int chr_allgather_radix_batch_async(const void* send, size_t sendcount, chr_dtype dtype, void* recv, chr_comm* comm,
+                                    int k, int b) {
+    return collective(comm, chr::MODE_ALLGATHER, send, recv, sendcount, dtype, CHR_SUM, k, b, false);
+}
+
+int chr_local_allgather_radix_batch(chr_local_group* g, const void* const* sends, void* const* recvs, size_t sendcount,
+                                    chr_dtype dtype, int k, int b) {
+    return local_collective(g, chr::MODE_ALLGATHER, sends, recvs, sendcount, dtype, CHR_SUM, k, b);
 }
 
 }  // extern "C"

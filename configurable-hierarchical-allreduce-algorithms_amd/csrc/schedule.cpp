@@ -299,6 +299,7 @@ int auto_slices(uint64_t irc_bytes) {
 
 Plan build_plan(Mode mode, int n, int me, int k_in, int b, uint64_t count, int slices) {
     if (is_mpich(mode)) return build_plan_mpich(mode, n, me, k_in, b, count);
+    if (mode == MODE_ALLGATHER) return build_plan_allgather(n, me, k_in, b, count);
     Plan p;
     p.mode = mode;
     p.rank = me;
@@ -874,6 +875,61 @@ Plan build_plan_mpich(Mode mode, int n, int me, int k, int aux, uint64_t count) 
     case MODE_MPICH_KRSAG: build_krsag(b, k); break;
     case MODE_MPICH_RMULT: build_rmult(b, k); break;
     default: p.error = 1;
+    }
+    return p;
+}
+
+}  // namespace chr
+
+// ==== allgather_radix_batch (Fugaku_experiments/Allgather/all_gather_radix_batch_1_0.cpp) ====
+// The reference gathers each group of b ranks to a root with a k-nomial tree (:55-133),
+// exchanges the group blocks between roots linearly (:137-163) and spreads them inside every
+// group with a k-port Bruck allgather (:168-360).  Its output is the rank-major concatenation
+// (checked against MPI_Allgather for every geometry of tests/golden).  On one node every pair
+// of GPUs has its own xGMI link, so relaying blocks through roots only adds hops: here each
+// rank sends its block straight to every peer, k-1 peers per step (k ports, as the Bruck
+// phase), peers of its own group of b first and then the other groups.  Every link carries
+// each block exactly once; no local copies besides placing the own block.
+namespace chr {
+
+Plan build_plan_allgather(int n, int me, int k, int b, uint64_t count) {
+    Plan p;
+    p.mode = MODE_ALLGATHER;
+    p.rank = me;
+    if (n < 1 || me < 0 || me >= n || k < 2 || b < 1) {
+        p.error = 1;
+        return p;
+    }
+    if (n % b) {
+        p.error = 3;  // CHR_ERR_BATCH_NOT_DIVISOR
+        return p;
+    }
+    p.g.nranks = n;
+    p.g.k = k;
+    p.g.b = b;
+    p.g.nnodes = n / b;
+    p.g.total = count;
+    p.send_elems = count;
+    p.recv_elems = count * (uint64_t)n;
+    if (count == 0) return p;
+    const Ref mine{BUF_RECV, (uint64_t)me * count};
+    p.pre.push_back(make_copy(mine, {BUF_SEND, 0}, count, 0));
+    // (to, from) pairs: offset d inside the group, then group offset D with in-group rotation e.
+    // For every pair, `to` receives from this rank in the same step (same offset list).
+    const int g = me / b, lr = me % b, nn = n / b;
+    std::vector<std::pair<int, int>> peers;
+    for (int d = 1; d < b; ++d) peers.push_back({g * b + (lr + d) % b, g * b + (lr - d + b) % b});
+    for (int D = 1; D < nn; ++D)
+        for (int e = 0; e < b; ++e)
+            peers.push_back({((g + D) % nn) * b + (lr + e) % b, ((g - D + nn) % nn) * b + (lr - e + b) % b});
+    for (size_t i = 0; i < peers.size(); i += (size_t)(k - 1)) {
+        p.steps.emplace_back();
+        Step& s = p.steps.back();
+        s.label = i < (size_t)(b - 1) ? "ag-intra" : "ag-inter";
+        for (size_t j = i; j < peers.size() && j < i + (size_t)(k - 1); ++j) {
+            s.sends.push_back({peers[j].first, mine, count});
+            s.recvs.push_back({peers[j].second, {BUF_RECV, (uint64_t)peers[j].second * count}, count});
+        }
     }
     return p;
 }

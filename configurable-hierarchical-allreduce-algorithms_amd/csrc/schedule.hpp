@@ -66,7 +66,8 @@ enum Mode : int {
     MODE_MPICH_RSAG = 4,       // .../allreduce_reduce_scatter_allgather.cpp
     MODE_MPICH_RECEXCH = 5,    // .../allreduce_recexch.cpp (k, single_phase_recv)
     MODE_MPICH_KRSAG = 6,      // .../allreduce_k_reduce_scatter_allgather.cpp (k, single_phase_recv)
-    MODE_MPICH_RMULT = 7       // .../allreduce_recursive_multiplying.cpp (k)
+    MODE_MPICH_RMULT = 7,      // .../allreduce_recursive_multiplying.cpp (k)
+    MODE_ALLGATHER = 8         // allgather_radix_batch (count = sendcount)
 };
 inline bool is_mpich(int mode) { return mode >= MODE_MPICH_RING && mode <= MODE_MPICH_RMULT; }
 
@@ -107,6 +108,7 @@ Plan build_plan(Mode mode, int nranks, int rank, int k, int b, uint64_t count, i
 int auto_slices(uint64_t irc_bytes);
 // MPICH baseline allreduces (count = elements per rank; aux = recexch single_phase_recv).
 Plan build_plan_mpich(Mode mode, int nranks, int rank, int k, int aux, uint64_t count);
+Plan build_plan_allgather(int nranks, int rank, int k, int b, uint64_t sendcount);
 std::string describe(const Plan& p);
 
 }  // namespace chr

@@ -8,6 +8,8 @@
 //       replaces Fugaku_experiments/Allreduce/all_reduce_radix_batch.cpp:202-204
 //   int reduce_scatter_radix_batch(const void*, void*, MPI_Aint, MPI_Datatype, MPI_Op, MPI_Comm, int, int)
 //       replaces Fugaku_experiments/Reduce-scatter/reduce_scatter_radix_batch.cpp:200-202
+//   int allgather_radix_batch(char*, int, MPI_Datatype, char*, MPI_Comm, int k, int b)
+//       replaces Fugaku_experiments/Allgather/all_gather_radix_batch_1_0.cpp:37
 //   MPICH_Allreduce_{ring, recursive_doubling, reduce_scatter_allgather, recursive_exchange,
 //                    k_reduce_scatter_allgather, recursive_multiplying}
 //       replace testing/mpich_implementations/all_reduce/allreduce_{ring.cpp:3,
@@ -152,4 +154,15 @@ int MPICH_Allreduce_k_reduce_scatter_allgather(const char* sendbuf, char* recvbu
 int MPICH_Allreduce_recursive_multiplying(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype,
                                           MPI_Op op, MPI_Comm comm, int k) {
     return mpich_call(CHR_MODE_MPICH_RMULT, sendbuf, recvbuf, count, datatype, op, comm, k, 0);
+}
+
+int allgather_radix_batch(char* sendbuf, int sendcount, MPI_Datatype datatype, char* recvbuf, MPI_Comm comm, int k,
+                          int b) {
+    chr_dtype dt;
+    if (!map_type(datatype, &dt)) return MPI_ERR_TYPE;
+    if (sendcount < 0) return MPI_ERR_COUNT;
+    chr_comm* c = comm_for(comm);
+    if (!c) return MPI_ERR_OTHER;
+    const void* send = sendbuf == (char*)MPI_IN_PLACE ? CHR_IN_PLACE : (const void*)sendbuf;
+    return to_mpi(chr_allgather_radix_batch(send, (size_t)sendcount, dt, recvbuf, c, k, b));
 }

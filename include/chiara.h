@@ -114,11 +114,22 @@ int chr_allreduce_radix_batch(const void* send, void* recv, size_t count, chr_dt
                               chr_op op, chr_comm* comm, int k, int b);
 int chr_reduce_scatter_radix_batch(const void* send, void* recv, size_t recvcount,
                                    chr_dtype dtype, chr_op op, chr_comm* comm, int k, int b);
+/* Replaces  int allgather_radix_batch(char* sendbuf, int sendcount, MPI_Datatype,
+ *             char* recvbuf, MPI_Comm, int k, int b)
+ *           (Fugaku_experiments/Allgather/all_gather_radix_batch_1_0.cpp:37).
+ * recv holds nranks*sendcount elements, rank-major (the reference's output on every
+ * geometry).  k = peers per step (k-port), b = group size (nranks % b == 0; group peers
+ * first).  send may be CHR_IN_PLACE: the own block is then already at recv + rank*sendcount.
+ * Pure data movement: any dtype, bit-exact. */
+int chr_allgather_radix_batch(const void* send, size_t sendcount, chr_dtype dtype, void* recv,
+                              chr_comm* comm, int k, int b);
 /* Asynchronous device-resident variants: enqueue on the comm stream and return. */
 int chr_allreduce_radix_batch_async(const void* send, void* recv, size_t count, chr_dtype dtype,
                                     chr_op op, chr_comm* comm, int k, int b);
 int chr_reduce_scatter_radix_batch_async(const void* send, void* recv, size_t recvcount,
                                          chr_dtype dtype, chr_op op, chr_comm* comm, int k, int b);
+int chr_allgather_radix_batch_async(const void* send, size_t sendcount, chr_dtype dtype,
+                                    void* recv, chr_comm* comm, int k, int b);
 
 /* ---- virtual ranks on one device (loopback transport) ---------------------------------
  * `nranks` logical ranks sharing ONE device, messages become device-to-device copies;
@@ -135,6 +146,9 @@ int chr_local_allreduce_radix_batch(chr_local_group* group, const void* const* s
 int chr_local_reduce_scatter_radix_batch(chr_local_group* group, const void* const* sends,
                                          void* const* recvs, size_t recvcount, chr_dtype dtype,
                                          chr_op op, int k, int b);
+int chr_local_allgather_radix_batch(chr_local_group* group, const void* const* sends,
+                                    void* const* recvs, size_t sendcount, chr_dtype dtype, int k,
+                                    int b);
 
 /* ---- schedule introspection (host only, no device needed) -----------------------------
  * The radix/batch schedule is compiled once per (mode, nranks, rank, k, b, count) into a
@@ -149,7 +163,8 @@ typedef enum {
     CHR_MODE_MPICH_RSAG = 4,       /* .../allreduce_reduce_scatter_allgather.cpp:3 */
     CHR_MODE_MPICH_RECEXCH = 5,    /* .../allreduce_recexch.cpp:188 (k, b = single_phase_recv) */
     CHR_MODE_MPICH_KRSAG = 6,      /* .../allreduce_k_reduce_scatter_allgather.cpp:257 (k, b = spr) */
-    CHR_MODE_MPICH_RMULT = 7       /* .../allreduce_recursive_multiplying.cpp:3 (k) */
+    CHR_MODE_MPICH_RMULT = 7,      /* .../allreduce_recursive_multiplying.cpp:3 (k) */
+    CHR_MODE_ALLGATHER = 8         /* allgather_radix_batch (count = sendcount) */
 } chr_mode;
 long chr_plan_describe(chr_mode mode, int nranks, int rank, int k, int b, size_t count,
                        int slices, char* buf, size_t len);

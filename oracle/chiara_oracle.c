@@ -782,3 +782,25 @@ int orc_allreduce_k_reduce_scatter_allgather(int n, int k_in, size_t count, int 
     free(x);
     return 0;
 }
+
+/* ---- Fugaku_experiments/Allgather/all_gather_radix_batch_1_0.cpp:37 ---------------------
+ * Pure data movement; the reference's output is the rank-major concatenation of the send
+ * blocks on every geometry of tests/golden (its k-nomial gather :55-133, linear inter-root
+ * exchange :137-163 and k-Bruck :168-360 only decide the route).  Preconditions as the
+ * product: k >= 2, b >= 1, nranks % b == 0.  send[r] NULL = in place (block already at
+ * recv[r] + r*count). */
+int orc_allgather_radix_batch(int n, int k, int b, size_t count, int dtype, const void* const* send,
+                              void* const* recv) {
+    size_t es = orc_dtype_size(dtype), nb;
+    int r, j;
+    char** R = (char**)recv;
+    if (n < 1 || !es || k < 2 || b < 1) return 1;
+    if (n % b) return 3;
+    nb = count * es;
+    for (r = 0; r < n; r++) {
+        const char* src = send[r] ? (const char*)send[r] : R[r] + (size_t)r * nb;
+        for (j = 0; j < n; j++)
+            if (j != r || send[j]) memmove(R[j] + (size_t)r * nb, src, nb);
+    }
+    return 0;
+}

@@ -126,6 +126,8 @@ int orc_allreduce_reduce_scatter_allgather(int nranks, size_t count, int dtype, 
                                            void* const* recv);
 int orc_allreduce_recexch(int nranks, int k, size_t count, int dtype, int op, const void* const* send,
                           void* const* recv);
+int orc_allgather_radix_batch(int nranks, int k, int b, size_t sendcount, int dtype, const void* const* send,
+                              void* const* recv);
 int orc_allreduce_recursive_multiplying(int nranks, int k, size_t count, int dtype, int op,
                                         const void* const* send, void* const* recv);
 int orc_allreduce_k_reduce_scatter_allgather(int nranks, int k, size_t count, int dtype, int op,

@@ -102,6 +102,28 @@ def reduce_scatter_radix_batch(sends, k, b, dtype, op, inplace=False):
     return [r[:recvcount] for r in recvs]
 
 
+def allgather_radix_batch(sends, k, b, dtype, inplace=False):
+    """All ranks' outputs of allgather_radix_batch (n*sendcount each, rank-major)."""
+    L = lib()
+    if not getattr(L, "_ag_ready", False):
+        L.orc_allgather_radix_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
+                                                ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                                ctypes.POINTER(ctypes.c_void_p)]
+        L.orc_allgather_radix_batch.restype = ctypes.c_int
+        L._ag_ready = True
+    n = len(sends)
+    count = sends[0].size
+    recvs = [np.zeros(count * n, dtype=sends[0].dtype) for _ in range(n)]
+    if inplace:
+        for r in range(n):
+            recvs[r][r * count:(r + 1) * count] = sends[r]
+    sp = _ptr_array([None] * n) if inplace else _ptr_array(sends)
+    rc = L.orc_allgather_radix_batch(n, k, b, count, DTYPES[dtype], sp, _ptr_array(recvs))
+    if rc:
+        raise ValueError(f"oracle allgather rejected geometry (rc={rc})")
+    return recvs
+
+
 def _setup_mpich(L):
     vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
     for name in ("orc_allreduce_ring", "orc_allreduce_recursive_doubling", "orc_allreduce_reduce_scatter_allgather"):

@@ -11,7 +11,7 @@
 //
 // Usage: mpiexec -n N ref_driver <cases.txt> <outdir>
 //   one case per line: id mode k b count dtype op pattern seed inplace
-//   mode: ar | rs (radix_batch), ring | rd | rsag | rx | krsag | rm (MPICH baselines; rx and
+//   mode: ar | rs | ag (radix_batch), ring | rd | rsag | rx | krsag | rm (MPICH baselines; rx and
 //   krsag use b as single_phase_recv)
 // For each case rank 0 writes <outdir>/<id>.out (all ranks' outputs, rank-major) and
 // <outdir>/<id>.lib (the MPI library collective's result on the same inputs).
@@ -43,6 +43,9 @@ int MPICH_Allreduce_recursive_exchange(const char* sendbuf, char* recvbuf, int c
                                        MPI_Op op, MPI_Comm comm, int k, int single_phase_recv);
 int MPICH_Allreduce_k_reduce_scatter_allgather(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype,
                                                MPI_Op op, MPI_Comm comm, int k, int single_phase_recv);
+// Fugaku_experiments/Allgather/all_gather_radix_batch_1_0.cpp:37
+int allgather_radix_batch(char* sendbuf, int sendcount, MPI_Datatype datatype, char* recvbuf, MPI_Comm comm, int k,
+                          int b);
 int MPICH_Allreduce_recursive_multiplying(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype,
                                           MPI_Op op, MPI_Comm comm, int k);
 
@@ -118,11 +121,16 @@ int main(int argc, char** argv) {
         MPI_Op mop = dtype == ORC_BF16 ? bf16_ops[op] : std_ops[op];
 
         size_t in_n = (mode == "rs") ? (size_t)count * nprocs : (size_t)count;
-        size_t out_n = (size_t)count;
+        size_t out_n = (mode == "ag") ? (size_t)count * nprocs : (size_t)count;
         std::vector<char> send(in_n * es), recv(in_n * es, 0), lib(out_n * es, 0);
         orc_fill(send.data(), in_n, dtype, pattern, seed, rank, in_n);
 
-        if (mode == "ar") {
+        if (mode == "ag") {
+            MPI_Allgather(send.data(), (int)count, mdt, lib.data(), (int)count, mdt, MPI_COMM_WORLD);
+            recv.assign(out_n * es, 0);
+            MPI_Barrier(MPI_COMM_WORLD);
+            allgather_radix_batch(send.data(), (int)count, mdt, recv.data(), MPI_COMM_WORLD, k, b);
+        } else if (mode == "ar") {
             MPI_Allreduce(send.data(), lib.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
             if (inplace) memcpy(recv.data(), send.data(), in_n * es);
             MPI_Barrier(MPI_COMM_WORLD);

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Generate golden vectors from the REAL reference (container-only).
 
-Builds oracle/_ref/ref_driver (the reference's two algorithm files, compiled unchanged
+Builds oracle/_ref/ref_driver (the reference's algorithm files, compiled unchanged
 from /root/reference against the container's MPICH 3.3.2) and runs it under
 `mpiexec -n N` for a grid of (mode, n, k, b, count, dtype, op, pattern, inplace) cases.
 Writes:
@@ -57,6 +57,8 @@ def cases_for(n):
             # reduce-scatter (block): recvcount odd and even
             add("rs", k, b, 7, "i32", "sum", pyoracle.PAT_SEQ, 0)
             add("rs", k, b, 33, "f32", "sum", pyoracle.PAT_UNIFORM, 0)
+            # allgather_radix_batch (Allgather/main.cpp's int32 pattern; op unused)
+            add("ag", k, b, 6, "i32", "sum", pyoracle.PAT_SEQ, 0)
         # a few extra dtypes / ops / in-place per geometry at k = 2 and 3
         for k in (2, 3):
             add("ar", k, b, n * 16, "f64", "sum", pyoracle.PAT_UNIFORM, 0)
@@ -72,6 +74,9 @@ def cases_for(n):
             add("ar", k, b, n * 16, "f32", "max", pyoracle.PAT_TIES, 0)
             add("ar", k, b, n * 16, "bf16", "min", pyoracle.PAT_TIES, 0)
             add("rs", k, b, 16, "f64", "max", pyoracle.PAT_TIES, 1)
+            add("ag", k, b, 33, "f32", "sum", pyoracle.PAT_UNIFORM, 0)
+            add("ag", k, b, 7, "bf16", "sum", pyoracle.PAT_UNIFORM, 0)
+            add("ag", k, b, 5, "f64", "sum", pyoracle.PAT_TIES, 0)
     return out
 
 
@@ -89,6 +94,8 @@ LARGE = [
     dict(mode="rs", n=2, k=2, b=2, count=1 << 18, dtype="f32", op="sum"),
     dict(mode="ar", n=4, k=2, b=2, count=1 << 18, dtype="f32", op="sum"),
     dict(mode="ar", n=4, k=4, b=4, count=1 << 18, dtype="f32", op="sum"),
+    dict(mode="ag", n=8, k=4, b=4, count=1 << 16, dtype="f32", op="sum"),
+    dict(mode="ag", n=16, k=3, b=4, count=1 << 14, dtype="bf16", op="sum"),
 ]
 
 
@@ -207,7 +214,8 @@ def main():
     ref_desc = ("testing/mpich_implementations/all_reduce/{allreduce_ring,allreduce_recursive_doubling,"
                 "allreduce_reduce_scatter_allgather,allreduce_recexch,allreduce_k_reduce_scatter_allgather,"
                 "allreduce_recursive_multiplying}.cpp" if which == "mpich" else
-                "Fugaku_experiments/{Allreduce/all_reduce_radix_batch.cpp,Reduce-scatter/reduce_scatter_radix_batch.cpp}")
+                "Fugaku_experiments/{Allreduce/all_reduce_radix_batch.cpp,Reduce-scatter/reduce_scatter_radix_batch.cpp,"
+                "Allgather/all_gather_radix_batch_1_0.cpp}")
     with open(os.path.join(HERE, prefix + "manifest.json"), "w") as f:
         json.dump({"generator": f"tests/golden/gen_golden.py {which}",
                    "reference": ref_desc + " @ 2025-11-21, MPICH 3.3.2", "seed": SEED, "cases": manifest},

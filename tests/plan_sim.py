@@ -58,7 +58,13 @@ def execute(plans, sends, dtype, rop, inplace=False):
     n = len(plans)
     states = []
     for r in range(n):
-        if inplace:
+        if inplace and plans[r]["header"]["mode"] == ca.MODE_ALLGATHER:
+            # MPI_IN_PLACE allgather: the own block already sits at recv + r*sendcount
+            c = sends[r].size
+            buf = np.zeros(plans[r]["header"]["recv"], dtype=sends[r].dtype)
+            buf[r * c:(r + 1) * c] = sends[r]
+            st = RankState(plans[r], buf[r * c:(r + 1) * c], buf, dtype)
+        elif inplace:
             buf = sends[r].copy()
             st = RankState(plans[r], buf, buf, dtype)
         else:

@@ -43,17 +43,28 @@ def run_local(gu, group, mode, sends, k, b, dtype, op, inplace=False):
     n = len(sends)
     npdt = po.NP_DTYPES[dtype]
     es = np.dtype(npdt).itemsize
-    count = sends[0].size if mode == "ar" else sends[0].size // n
+    count = sends[0].size // n if mode == "rs" else sends[0].size
+    outc = count * n if mode == "ag" else count
+    if mode == "ag":
+        d_recv = [gu.empty_dev(outc * es) for _ in range(n)]
+        if inplace:
+            for r in range(n):
+                d_recv[r][r * count * es:(r + 1) * count * es].copy_(gu.to_dev(sends[r]))
+            d_sendp = [ca.IN_PLACE] * n
+        else:
+            d_sendp = [gu.to_dev(s) for s in sends]
+        rc = group.allgather_radix_batch(d_sendp, count, DT[dtype], d_recv, k, b)
+        assert rc == 0, f"rc={rc}"
+        return [gu.from_dev(d, npdt, outc) for d in d_recv]
     d_send = [gu.to_dev(s) for s in sends]
     if inplace:
         d_recv, d_sendp = d_send, [ca.IN_PLACE] * n
     else:
-        d_recv = [gu.empty_dev((count if mode == "ar" else count) * es) for _ in range(n)]
+        d_recv = [gu.empty_dev(count * es) for _ in range(n)]
         d_sendp = d_send
     fn = group.all_reduce_radix_batch if mode == "ar" else group.reduce_scatter_radix_batch
     rc = fn(d_sendp, d_recv, count, DT[dtype], OP[op], k, b)
     assert rc == 0, f"rc={rc}"
-    outc = count
     return [gu.from_dev(d, npdt, outc) for d in d_recv]
 
 
@@ -63,7 +74,7 @@ def test_local_group_matches_reference_golden(gu, groups, golden):
     bad = []
     for c in cases:
         n = c["n"]
-        in_n = c["count"] if c["mode"] == "ar" else c["count"] * n
+        in_n = c["count"] * n if c["mode"] == "rs" else c["count"]
         sends = [po.fill(in_n, c["dtype"], c["pattern"], c["seed"], r) for r in range(n)]
         outs = run_local(gu, groups(n), c["mode"], sends, c["k"], c["b"], c["dtype"], c["op"], bool(c["inplace"]))
         h = hashlib.sha256(b"".join(o.tobytes() for o in outs)).hexdigest()
@@ -208,3 +219,14 @@ def test_mpich_baselines_large_int_exact(gu, groups, algo):
     assert groups(n).allreduce_mpich(MPICH_MODE[algo], d_send, d_recv, count, ca.INT32, ca.SUM, 3, 0) == 0
     for r in range(n):
         np.testing.assert_array_equal(gu.from_dev(d_recv[r], np.int32, count), want[r])
+
+
+@pytest.mark.parametrize("n,k,b,inplace", [(8, 4, 4, False), (8, 8, 8, True), (16, 3, 4, False), (6, 2, 3, True)])
+def test_allgather_large_bit_exact(gu, groups, n, k, b, inplace):
+    """allgather_radix_batch at 8 MiB per rank block: every byte in place."""
+    count = (1 << 21) + 3
+    sends = [po.fill(count, "f32", po.PAT_UNIFORM, 21, r) for r in range(n)]
+    outs = run_local(gu, groups(n), "ag", sends, k, b, "f32", "sum", inplace)
+    want = np.concatenate(sends)
+    for r in range(n):
+        np.testing.assert_array_equal(outs[r].view(np.uint32), want.view(np.uint32))

@@ -47,16 +47,20 @@ def _worker(rank, world, port, cases, q):
             npdt = po.NP_DTYPES[dtype]
             cdt = {"f32": ca.FLOAT32, "bf16": ca.BFLOAT16, "i32": ca.INT32}[dtype]
             in_n = count * world if mode == "rs" else count
+            out_n = count * world if mode == "ag" else count
             pat = po.PAT_TIES if mode == "rx" else 0  # recexch: operand-order sensitive data, MAX
             x = po.fill(in_n, dtype, pat, 4242, rank)
             if host:
-                send, out = x, np.zeros(count, dtype=npdt)
+                send, out = x, np.zeros(out_n, dtype=npdt)
             else:
                 send = torch.from_numpy(x.view(np.uint8).copy()).to(dev)
-                out_t = torch.zeros(count * x.itemsize, dtype=torch.uint8, device=dev)
+                out_t = torch.zeros(out_n * x.itemsize, dtype=torch.uint8, device=dev)
             dst = out if host else out_t
             allx = [po.fill(in_n, dtype, pat, 4242, r) for r in range(world)]
-            if mode in ("ar", "rs"):
+            if mode == "ag":
+                rc = ca.allgather_radix_batch(send, count, cdt, dst, comm, k, b)
+                ref = np.concatenate(allx)
+            elif mode in ("ar", "rs"):
                 fn = ca.all_reduce_radix_batch if mode == "ar" else ca.reduce_scatter_radix_batch
                 rc = fn(send, dst, count, cdt, ca.SUM, comm, k, b)
                 f = po.allreduce_radix_batch if mode == "ar" else po.reduce_scatter_radix_batch
@@ -124,3 +128,8 @@ def test_rccl_mpich_baselines_world5_and_8():
     _run(8, cases[:1] + [("rx", 4, 0, 1 << 16, "f32", False, 0), ("rsag", 0, 0, 1 << 16, "bf16", False, 0),
                          ("krsag", 2, 1, 1 << 16, "f32", False, 0), ("rm", 3, 0, 12345, "bf16", False, 0)],
          timeout=600)
+
+
+def test_rccl_allgather_world4_and_8():
+    _run(4, [("ag", 2, 2, 1 << 16, "f32", False, 0), ("ag", 3, 4, 1001, "bf16", True, 0)])
+    _run(8, [("ag", 4, 4, 1 << 18, "f32", False, 0), ("ag", 8, 2, 4097, "i32", False, 0)], timeout=600)

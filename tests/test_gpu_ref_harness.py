@@ -17,8 +17,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MPIEXEC = "/opt/conda/bin/mpiexec"
 
 
-def _run(binary, args, n, tmp_path):
-    exe = os.path.join(REPO, "oracle", "_ref", binary)
+def _run(binary, args, n, tmp_path, where=("oracle", "_ref")):
+    exe = os.path.join(REPO, *where, binary)
     if not os.path.exists(exe) or not os.path.exists(MPIEXEC):
         pytest.skip("reference harness binary or MPICH not present")
     cmd = [MPIEXEC]
@@ -59,3 +59,29 @@ def test_reference_mpich_baseline_harness_on_mi355x(tmp_path):
     assert len(rows) == 3 * (3 * 3 + 3) * 50  # sizes x (k in 2..4 x 3 + 3 without k) x reps
     assert {r["send_count"] for r in rows} == {"8", "16", "32"}
     assert all(r["is_correct"] == "1" for r in rows)
+
+
+def test_reference_allgather_harness_on_mi355x(tmp_path):
+    """Fugaku_experiments/Allgather/main.cpp unchanged: k = 2..b-1, check_correctness vs MPI_Allgather."""
+    rows = _run("ref_harness_allgather", ["3", "--overwrite", "b=4", "base=16"], 8, tmp_path)
+    ours = [r for r in rows if r["algorithm_name"] == "allgather_radix_batch"]
+    assert ours and {r["k"] for r in ours} == {"2", "3"}
+    assert all(r["is_correct"] == "1" for r in rows)
+
+
+BIN = ("configurable-hierarchical-allreduce-algorithms_amd", "bin")
+
+
+@pytest.mark.parametrize("binary,args,n,name", [
+    ("chiara_allreduce", ["2", "--overwrite", "b=4", "base=4096", "mem=device", "dtype=f32", "reps=5"], 8,
+     "all_reduce_radix_batch"),
+    ("chiara_reduce_scatter", ["2", "--overwrite", "b=4", "base=1000", "mem=device", "reps=5"], 4,
+     "reduce_scatter_radix_batch"),
+    ("chiara_allgather", ["3", "--overwrite", "b=4", "base=100", "mem=device", "dtype=bf16", "reps=5"], 8,
+     "allgather_radix_batch"),
+])
+def test_own_harnesses_device_resident(tmp_path, binary, args, n, name):
+    """csrc/harness: the reference CLI/CSV with the HBM-resident extension (mem=device)."""
+    rows = _run(binary, args, n, tmp_path, where=BIN)
+    ours = [r for r in rows if r["algorithm_name"] == name]
+    assert ours and all(r["is_correct"] == "1" for r in rows)

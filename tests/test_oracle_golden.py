@@ -14,8 +14,10 @@ import pyoracle as po
 
 def _run_oracle(c):
     n = c["n"]
-    in_n = c["count"] if c["mode"] == "ar" else c["count"] * n
+    in_n = c["count"] * n if c["mode"] == "rs" else c["count"]
     sends = [po.fill(in_n, c["dtype"], c["pattern"], c["seed"], r) for r in range(n)]
+    if c["mode"] == "ag":
+        return po.allgather_radix_batch(sends, c["k"], c["b"], c["dtype"], inplace=bool(c["inplace"]))
     f = po.allreduce_radix_batch if c["mode"] == "ar" else po.reduce_scatter_radix_batch
     return f(sends, c["k"], c["b"], c["dtype"], c["op"], inplace=bool(c["inplace"]))
 
@@ -26,6 +28,7 @@ def test_golden_manifest_is_complete(golden):
     assert len({c["id"] for c in cases}) == len(cases)
     modes = {(c["mode"], c["dtype"], c["op"]) for c in cases}
     for need in [("ar", "i32", "sum"), ("ar", "f32", "sum"), ("ar", "bf16", "sum"), ("rs", "f32", "sum"),
+                 ("ag", "i32", "sum"), ("ag", "f64", "sum"),
                  ("ar", "f32", "max"), ("ar", "f64", "sum"), ("rs", "bf16", "sum")]:
         assert need in modes
 
@@ -48,6 +51,14 @@ def test_reference_exact_on_integers(golden):
     cases, _ = golden
     ints = [c for c in cases if c["dtype"] == "i32"]
     assert ints and all(c["n_diff_vs_lib"] == 0 for c in ints)
+
+
+def test_reference_allgather_equals_mpi_allgather(golden):
+    """allgather_radix_batch is pure data movement: on every golden geometry its bytes equal
+    MPI_Allgather's (which is why the product may route blocks differently)."""
+    cases, _ = golden
+    ag = [c for c in cases if c["mode"] == "ag"]
+    assert len(ag) > 150 and all(c["sha256"] == c["sha256_lib"] for c in ag)
 
 
 def test_float_tolerance_vs_library(golden):

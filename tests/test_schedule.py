@@ -12,7 +12,7 @@ import pyoracle as po
 
 def _inputs(c):
     n = c["n"]
-    in_n = c["count"] if c["mode"] == "ar" else c["count"] * n
+    in_n = c["count"] * n if c["mode"] == "rs" else c["count"]
     return [po.fill(in_n, c["dtype"], c["pattern"], c["seed"], r) for r in range(n)]
 
 
@@ -22,7 +22,7 @@ def test_plans_match_reference_golden(golden):
     for c in cases:
         if c["count"] * c["n"] > (1 << 16):
             continue  # the large hash-only cases are covered on the GPU
-        mode = ca.MODE_ALLREDUCE if c["mode"] == "ar" else ca.MODE_REDUCE_SCATTER
+        mode = {"ar": ca.MODE_ALLREDUCE, "rs": ca.MODE_REDUCE_SCATTER, "ag": ca.MODE_ALLGATHER}[c["mode"]]
         outs = plan_sim.simulate(mode, _inputs(c), c["k"], c["b"], c["dtype"], c["op"], bool(c["inplace"]))
         h = hashlib.sha256(b"".join(o.tobytes() for o in outs)).hexdigest()
         if h != c["sha256"]:
@@ -96,3 +96,26 @@ def test_pipelined_plan_structure():
     assert p["header"]["slices"] == 4 and p["header"]["steps"] == 4 + 4 - 1
     # super-step 1 holds slice 0's lane reduce and slice 1's recexch phase in ONE group
     assert "lane/s0" in p["steps"][1]["label"] and "phase0/s1" in p["steps"][1]["label"]
+
+
+@pytest.mark.parametrize("n,k,b", [(8, 4, 4), (8, 2, 8), (16, 3, 4), (6, 5, 3), (12, 8, 2), (1, 2, 1)])
+def test_allgather_plans(n, k, b):
+    """k-port direct allgather: in place and not, every rank gets the rank-major concatenation,
+    k-1 peers per step, group peers first, each peer exactly once."""
+    sends = [po.fill(11, "f32", po.PAT_UNIFORM, 3, r) for r in range(n)]
+    want = po.allgather_radix_batch(sends, k, b, "f32")
+    for inplace in (False, True):
+        got = plan_sim.simulate(ca.MODE_ALLGATHER, sends, k, b, "f32", "sum", inplace=inplace)
+        for r in range(n):
+            np.testing.assert_array_equal(got[r], want[r])
+    plans = plan_sim.load_plans(ca.MODE_ALLGATHER, n, k, b, 11)
+    for r, p in enumerate(plans):
+        peers = [x[0] for st in p["steps"] for x in st["sends"]]
+        assert sorted(peers) == [q for q in range(n) if q != r]
+        assert all(len(st["sends"]) <= k - 1 for st in p["steps"])
+        assert set(peers[:b - 1]) == {q for q in range(r // b * b, r // b * b + b) if q != r}
+
+
+def test_allgather_plan_errors():
+    assert plan_sim.load_plans(ca.MODE_ALLGATHER, 6, 2, 4, 8)[0]["header"]["error"] == 3
+    assert plan_sim.load_plans(ca.MODE_ALLGATHER, 6, 1, 3, 8)[0]["header"]["error"] == 1
