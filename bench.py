@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--sweep", action="store_true", help="N=1: bucket sizes 1 KiB..1 GiB, m=1/3/7 (table to stderr)")
     p.add_argument("--count", type=int, default=None, help="N>1: elements per rank (default 2^28)")
     p.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
+    p.add_argument("--no-compare", action="store_true",
+                   help="N>1: skip the same-run context lines (RCCL allreduce, MPICH ring on libchiara)")
     p.add_argument("--e2e", action="store_true",
                    help="N=1: host-memory (PCIe-inclusive) staging cost of the reference's host-buffer contract")
     return p.parse_args()
@@ -307,6 +309,8 @@ def bench_allreduce(args):
                     "kernel": "chr::k_reduce_vec (fused bucket reductions inside the collective, busiest rank)",
                     "algorithmic_bytes_per_call": float(busiest[1]), "launches_per_call": int(busiest[2]),
                     "kernel_ms_per_call": round(float(busiest[0]), 4)}
+    compare = None if args.no_compare else compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b,
+                                                         world, dev)
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(world * S * args.steps / el / 1e9, 2), "unit": "GB/s",
@@ -322,9 +326,56 @@ def bench_allreduce(args):
                               "busbw_frac_aggregate": round(busbw / (7 * XGMI_LINK_GBPS), 4)},
             "roofline": roofline, "cpu_baseline": None,
         }
+        if compare:
+            line["compare"] = compare
         print(json.dumps(line), flush=True)
     comm.destroy()
     dist.destroy_process_group()
+
+
+def _timed_max(torch, dist, fn, steps, warmup):
+    """Seconds for `steps` calls of fn after `warmup`, barrier + sync on both sides, max over ranks."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, world, dev):
+    """Context, not the metric: on the same buffers and ranks, (1) RCCL's own ncclAllReduce
+    (torch.distributed nccl group) and (2) the reference's MPICH ring baseline
+    (testing/mpich_implementations/all_reduce/allreduce_ring.cpp) run on libchiara's executor."""
+    steps, warm = max(1, min(args.steps, 20)), 2
+    S = count * (4 if dt == ca.FLOAT32 else 2)
+    out = {"steps": steps}
+
+    def entry(el):
+        algbw = S * steps / el / 1e9
+        return {"algbw_GBps": round(algbw, 2), "busbw_GBps": round(algbw * 2 * (world - 1) / world, 2),
+                "ms_per_call": round(el / steps * 1e3, 4)}
+
+    try:
+        g = dist.new_group(backend="nccl")
+        x = torch.empty(count, dtype=torch.float32 if dt == ca.FLOAT32 else torch.bfloat16, device=dev)
+        x.view(torch.uint8).copy_(send)
+        out["rccl_allreduce"] = entry(_timed_max(torch, dist, lambda: dist.all_reduce(x, group=g), steps, warm))
+        dist.destroy_process_group(g)
+    except Exception as e:  # context only: never fail the metric line for it
+        out["rccl_allreduce"] = {"error": str(e)[:200]}
+
+    def ring():
+        ca.check(ca.MPICH_Allreduce_ring(send, recv, count, dt, ca.SUM, comm, async_op=True))
+    out["mpich_ring_on_libchiara"] = entry(_timed_max(torch, dist, ring, steps, warm))
+    return out
 
 
 def main():
