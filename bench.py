@@ -31,6 +31,7 @@ XGMI_LINK_GBPS = 153.0       # per link, per the task statement; 7 links per GPU
 C2_ELEMS = 16 << 20          # 64 MiB fp32 per bucket
 NSETS = 16                   # 16 x 128 MiB distinct = 2 GiB working set: 8x the 256 MiB Infinity Cache
 SEED = 0xC41A5EED
+CPU_THREADS = 16             # the GPU box's CPU share per GPU (nproc shows the whole machine)
 
 
 def parse():
@@ -60,10 +61,21 @@ def cpu_baseline(seconds):
                                  timeout=seconds + 60)
             if out.returncode == 0:
                 r = json.loads(out.stdout.strip().splitlines()[-1])
-                return {"value": round(r["gbps"], 3), "unit": "GB/s", "cores": 1, "kind": "reference",
+                line = {"value": round(r["gbps"], 3), "unit": "GB/s", "cores": 1, "kind": "reference",
                         "sample": f"MPICH 3.3.2 MPI_Reduce_local(MPI_FLOAT, MPI_SUM) on a 64 MiB bucket, m=1, "
                                   f"{r['calls']} calls in {r['seconds']:.1f} s, 1 thread "
                                   f"(oracle/_ref/ref_reduce_local; nproc={os.cpu_count()})"}
+                # all-cores variant: the bucket cut into CPU_THREADS slices, one
+                # MPI_Reduce_local stream per thread; the box's CPU share per GPU is 16 cores
+                out = subprocess.run([ref_bin, str(C2_ELEMS), str(seconds / 2), str(CPU_THREADS)],
+                                     capture_output=True, text=True, timeout=seconds + 60)
+                if out.returncode == 0:
+                    r = json.loads(out.stdout.strip().splitlines()[-1])
+                    line["all_cores"] = {
+                        "value": round(r["gbps"], 3), "unit": "GB/s", "cores": r["threads"], "kind": "reference",
+                        "sample": f"same call, 64 MiB bucket cut into {r['threads']} slices, one thread each, "
+                                  f"{r['seconds']:.1f} s"}
+                return line
         except Exception:
             pass
     import numpy as np
@@ -162,6 +174,8 @@ def bench_bucket(args, cpu):
     }
     if cpu:
         line["gpu_vs_cpu"] = round(line["value"] / cpu["value"], 1)
+        if "all_cores" in cpu:
+            line["gpu_vs_cpu_all_cores"] = round(line["value"] / cpu["all_cores"]["value"], 1)
     if args.sweep:
         line["sweep"] = sweep(ca, torch, dev, stream)
     print(json.dumps(line), flush=True)

@@ -128,6 +128,18 @@ def test_c4_full_size_exact_int(gu, groups):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("b", [1, 2])
+def test_c3_full_size_bit_exact(gu, groups, b):
+    """C3 at full size: reduce-scatter, n=2, k=2, recvcount 2^25 fp32 (256 MiB send buffer per
+    rank), b in {1, 2}: bit-exact vs the oracle (fp32 data, U[-1,1))."""
+    n, k, recvcount = 2, 2, 1 << 25
+    sends = [po.fill(recvcount * n, "f32", po.PAT_UNIFORM, 0xC41A5EED, r) for r in range(n)]
+    got = run_local(gu, groups(n), "rs", sends, k, b, "f32", "sum")
+    ref = po.reduce_scatter_radix_batch(sends, k, b, "f32", "sum")
+    for r in range(n):
+        np.testing.assert_array_equal(got[r].view(np.uint32), ref[r].view(np.uint32))
+
+
 def test_c5_full_size_bf16_properties(gu, groups):
     """C5 geometry at full size (1 GiB bf16 per rank, 8 ranks, b=4, k=4): all ranks
     bit-identical, and within (n-1) bf16 ulps of the fp32 sum of the inputs."""
