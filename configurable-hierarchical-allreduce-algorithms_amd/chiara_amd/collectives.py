@@ -134,6 +134,9 @@ class Comm:
         """Pipeline depth (0 = automatic); results are bit-identical for every depth."""
         check(lib().chr_comm_set_slices(self._h, slices))
 
+    def set_balance(self, enable):
+        check(lib().chr_comm_set_balance(self._h, int(bool(enable))))
+
     def profile(self, enable=True):
         """Time every fused reduction launch of this communicator (HIP events)."""
         check(lib().chr_comm_profile(self._h, 1 if enable else 0))
@@ -180,6 +183,9 @@ class LocalGroup:
 
     def set_slices(self, slices):
         check(lib().chr_local_group_set_slices(self._h, slices))
+
+    def set_balance(self, enable):
+        check(lib().chr_local_group_set_balance(self._h, int(bool(enable))))
 
     def all_reduce_radix_batch(self, sendbufs, recvbufs, count, datatype, op, k, b):
         S = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in sendbufs])
@@ -281,12 +287,13 @@ def reduce_multi_ex(out, acc, ins, count, datatype, op, flags, stream=None):
 
 # ---- plan introspection (host only) --------------------------------------------------------------
 
-def describe_plan(mode, nranks, rank, k, b, count, slices=1):
-    n = lib().chr_plan_describe(mode, nranks, rank, k, b, count, slices, None, 0)
+def describe_plan(mode, nranks, rank, k, b, count, slices=1, balance=True):
+    bal = int(bool(balance))
+    n = lib().chr_plan_describe_ex(mode, nranks, rank, k, b, count, slices, bal, None, 0)
     if n < 0:
         raise ValueError("bad plan request")
     buf = ctypes.create_string_buffer(n + 1)
-    lib().chr_plan_describe(mode, nranks, rank, k, b, count, slices, buf, n + 1)
+    lib().chr_plan_describe_ex(mode, nranks, rank, k, b, count, slices, bal, buf, n + 1)
     return buf.value.decode()
 
 

@@ -158,7 +158,15 @@ bool is_device_ptr(const void* p) {
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
 }
 
-using PlanKey = std::tuple<int, int, int, int, uint64_t, int, int>;  // mode, rank, k, b, count, dtype size, slices
+using PlanKey = std::tuple<int, int, int, int, uint64_t, int, int, int>;  // mode, rank, k, b, count, dtype size, slices, balance
+
+int default_balance() {
+    static const int v = [] {
+        const char* e = std::getenv("CHR_BALANCE");
+        return e ? (std::atoi(e) != 0) : 1;
+    }();
+    return v;
+}
 
 // Pipeline depth: explicit setting, else CHR_SLICES, else by chunk size (schedule.cpp).
 int pick_slices(int setting, uint64_t count, int mode, int nranks, int b, size_t es) {
@@ -178,6 +186,7 @@ int pick_slices(int setting, uint64_t count, int mode, int nranks, int b, size_t
 struct chr_comm {
     int rank = 0, nranks = 0, device = 0;
     int slices = 0;  // 0 = auto
+    int balance = default_balance();
     ncclComm_t nccl = nullptr;
     hipStream_t stream = nullptr;
     DevBuf acc, stage, hsend, hrecv;
@@ -186,10 +195,11 @@ struct chr_comm {
 
     const Plan& plan(int mode, int k, int b, uint64_t count, size_t es) {
         const int P = pick_slices(slices, count, mode, nranks, b, es);
-        PlanKey key{mode, rank, k, b, count, (int)es, P};
+        PlanKey key{mode, rank, k, b, count, (int)es, P, balance};
         auto it = plans.find(key);
         if (it == plans.end())
-            it = plans.emplace(key, std::make_unique<Plan>(chr::build_plan((chr::Mode)mode, nranks, rank, k, b, count, P)))
+            it = plans.emplace(key, std::make_unique<Plan>(chr::build_plan((chr::Mode)mode, nranks, rank, k, b, count, P,
+                                                                           balance != 0)))
                      .first;
         return *it->second;
     }
@@ -198,9 +208,10 @@ struct chr_comm {
 struct chr_local_group {
     int nranks = 0, device = 0;
     int slices = 0;  // 0 = auto
+    int balance = default_balance();
     hipStream_t stream = nullptr;
     std::vector<DevBuf> acc, stage;
-    std::map<std::tuple<int, int, int, uint64_t, int, int>, std::vector<Plan>> plans;
+    std::map<std::tuple<int, int, int, uint64_t, int, int, int>, std::vector<Plan>> plans;
 };
 
 namespace {
@@ -283,11 +294,12 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
     if (!g || !sends || !recvs || !chr::valid_dtype_op(dtype, op)) return CHR_ERR_INVALID_ARG;
     const int n = g->nranks;
     const int depth = pick_slices(g->slices, count, mode, n, b, chr::dtype_size(dtype));
-    auto key = std::make_tuple(mode, k, b, (uint64_t)count, (int)chr::dtype_size(dtype), depth);
+    auto key = std::make_tuple(mode, k, b, (uint64_t)count, (int)chr::dtype_size(dtype), depth, g->balance);
     auto it = g->plans.find(key);
     if (it == g->plans.end()) {
         std::vector<Plan> v;
-        for (int r = 0; r < n; ++r) v.push_back(chr::build_plan((chr::Mode)mode, n, r, k, b, count, depth));
+        for (int r = 0; r < n; ++r)
+            v.push_back(chr::build_plan((chr::Mode)mode, n, r, k, b, count, depth, g->balance != 0));
         it = g->plans.emplace(key, std::move(v)).first;
     }
     const std::vector<Plan>& P = it->second;
@@ -433,6 +445,18 @@ int chr_comm_profile_read(chr_comm* c, double* reduce_ms, double* reduce_bytes, 
         c->prof.bytes = 0;
         c->prof.launches = 0;
     }
+    return CHR_SUCCESS;
+}
+
+int chr_comm_set_balance(chr_comm* c, int enable) {
+    if (!c) return CHR_ERR_INVALID_ARG;
+    c->balance = enable != 0;
+    return CHR_SUCCESS;
+}
+
+int chr_local_group_set_balance(chr_local_group* g, int enable) {
+    if (!g) return CHR_ERR_INVALID_ARG;
+    g->balance = enable != 0;
     return CHR_SUCCESS;
 }
 

@@ -120,7 +120,7 @@ LocalOp make_copy2d(Ref dst, Ref src, uint64_t width, uint64_t rows, uint64_t dp
     return op;
 }
 
-enum Logical { S_FOLD, S_PHASE, S_RETURN, S_LANE, S_DIST1, S_DIST2, S_SCATTER };
+enum Logical { S_FOLD, S_PHASE, S_RETURN, S_LANE, S_DIST1, S_DIST2, S_SCATTER, S_BPHASE, S_BLANE, S_BDIST };
 
 // One element-slice [lo, lo+len) of every chunk, laid out slice-major in ACC:
 // chunk position `pos` of slice p lives at acc_base + pos*len.
@@ -146,6 +146,7 @@ struct Builder {
         *len = o < e ? (uint64_t)(g.P[e] - g.P[o]) * c.len : 0;
     }
     const Recexch& x() const { return rx[lane]; }
+    bool b1() const { return g.b == 1; }
     bool participant() const { return rx[lane].step1_sendto == -1; }
 
     // Pieces of the distribute scatter: [lo, lo+len) cut into n-1 pieces, 64-element aligned.
@@ -155,6 +156,24 @@ struct Builder {
         *a = c.lo + cut((uint64_t)i);
         *l = cut((uint64_t)i + 1) - cut((uint64_t)i);
     }
+
+    // Balanced evaluation (single-phase geometries): the slice of every chunk is cut into n
+    // pieces, piece (j, Y) = index j*nnodes + Y, 64-element aligned; rank Y*b + j evaluates
+    // piece (j, Y) of every chunk.  Lane j's sub-piece = pieces (j, 0..nnodes-1), contiguous.
+    uint64_t bcut(const SliceCtx& c, uint64_t i) const {
+        const uint64_t np = (uint64_t)n;
+        return i >= np ? c.len : (c.len * i / np) / 64 * 64;
+    }
+    void bpiece(const SliceCtx& c, int j, int Y, uint64_t* a, uint64_t* l) const {
+        const uint64_t i = (uint64_t)j * g.nnodes + (uint64_t)Y;
+        *a = bcut(c, i);
+        *l = bcut(c, i + 1) - *a;
+    }
+    void bsub(const SliceCtx& c, int j, uint64_t* a, uint64_t* l) const {
+        *a = bcut(c, (uint64_t)j * g.nnodes);
+        *l = bcut(c, (uint64_t)(j + 1) * g.nnodes) - *a;
+    }
+    uint64_t acc_of(const SliceCtx& c, int N) const { return c.acc_base + chunk_pos(N) * c.len; }
 
     void emit(Logical kind, int ph, const SliceCtx& c, Step& s) {
         const uint64_t irc = g.irc, recvcount = g.recvcount;
@@ -268,6 +287,81 @@ struct Builder {
             }
             break;
         }
+        case S_BPHASE: {
+            // Phase 1 of chunk N is, in the reference, evaluated at lane L = N % b of every node:
+            // acc = L's data, then step2_nbrs[0][0..k-2] of L in order (:343-364).  Here lane j
+            // evaluates that same expression on its sub-piece of the chunk: it receives the
+            // other members' sub-piece j and reduces in L's operand order.
+            uint64_t a, len;
+            bsub(c, lane, &a, &len);
+            if (b1()) break;
+            for (int m = 0; m < g.b; ++m) {  // my sub-piece of m's lane to member m
+                if (m == lane) continue;
+                uint64_t ma, ml;
+                bsub(c, m, &ma, &ml);
+                for (int N = 0; N < g.nnodes && ml; ++N)
+                    s.sends.push_back({node * g.b + m, {BUF_ACC, acc_of(c, N) + ma}, ml});
+            }
+            if (!len) break;
+            for (int N = 0; N < g.nnodes; ++N) {
+                auto src = [&](int m) -> Ref {  // member m's sub-piece `lane` of chunk N, here
+                    if (m == lane) return {BUF_ACC, acc_of(c, N) + a};
+                    const int slot = (m < lane ? m : m - 1) * g.nnodes + N;
+                    return {BUF_STAGE, c.stage_base + (uint64_t)slot * c.len + a};
+                };
+                for (int m = 0; m < g.b; ++m)
+                    if (m != lane) s.recvs.push_back({node * g.b + m, src(m), len});
+                const int L = N % g.b;
+                std::vector<Ref> ins;
+                for (int i = 0; i < g.k - 1; ++i) ins.push_back(src(rx[L].step2_nbrs[0][i]));
+                s.post.push_back(make_reduce({BUF_ACC, acc_of(c, N) + a}, src(L), ins, len, 364));
+            }
+            break;
+        }
+        case S_BLANE: {
+            // Phase 2 of chunk N is evaluated at root node N in the reference: acc = node N's
+            // phase-1 value, then the other nodes' in stage order (:498-539).  Rank (Y, j)
+            // evaluates it on piece (j, Y), writing straight into recvbuf.
+            uint64_t a, len;
+            bpiece(c, lane, node, &a, &len);
+            for (int X = 0; X < g.nnodes; ++X) {  // my piece (lane, X) of every chunk to node X
+                if (X == node) continue;
+                uint64_t xa, xl;
+                bpiece(c, lane, X, &xa, &xl);
+                for (int N = 0; N < g.nnodes && xl; ++N)
+                    s.sends.push_back({X * g.b + lane, {BUF_ACC, acc_of(c, N) + xa}, xl});
+            }
+            if (!len) break;
+            for (int N = 0; N < g.nnodes; ++N) {
+                auto src = [&](int X) -> Ref {
+                    if (X == node) return {BUF_ACC, acc_of(c, N) + a};
+                    const int slot = (X < node ? X : X - 1) * g.nnodes + N;
+                    return {BUF_STAGE, c.stage_base + (uint64_t)slot * c.len + a};
+                };
+                for (int X = 0; X < g.nnodes; ++X)
+                    if (X != node) s.recvs.push_back({X * g.b + lane, src(X), len});
+                std::vector<Ref> ins;
+                for (int X = 0; X < g.nnodes; ++X)
+                    if (X != N) ins.push_back(src(X));
+                s.post.push_back(make_reduce({BUF_RECV, (uint64_t)N * irc + c.lo + a}, src(N), ins, len, 529));
+            }
+            break;
+        }
+        case S_BDIST: {  // allgather of the pieces: every rank's piece of every chunk to every rank
+            uint64_t a, len;
+            bpiece(c, lane, node, &a, &len);
+            for (int q = 0; q < n; ++q) {
+                if (q == me) continue;
+                uint64_t qa, ql;
+                bpiece(c, q % g.b, q / g.b, &qa, &ql);
+                for (int N = 0; N < g.nnodes; ++N) {
+                    const uint64_t base = (uint64_t)N * irc + c.lo;
+                    if (len) s.sends.push_back({q, {BUF_RECV, base + a}, len});
+                    if (ql) s.recvs.push_back({q, {BUF_RECV, base + qa}, ql});
+                }
+            }
+            break;
+        }
         case S_SCATTER: {  // reduce-scatter phase 3 (:572-627): owner -> every lane, direct
             const int owner = node * g.b + node % g.b;
             if (me == owner) {
@@ -297,7 +391,7 @@ int auto_slices(uint64_t irc_bytes) {
     return (int)std::max<uint64_t>(1, std::min<uint64_t>(8, s));
 }
 
-Plan build_plan(Mode mode, int n, int me, int k_in, int b, uint64_t count, int slices) {
+Plan build_plan(Mode mode, int n, int me, int k_in, int b, uint64_t count, int slices, bool balance) {
     if (is_mpich(mode)) return build_plan_mpich(mode, n, me, k_in, b, count);
     if (mode == MODE_ALLGATHER) return build_plan_allgather(n, me, k_in, b, count);
     Plan p;
@@ -353,15 +447,25 @@ Plan build_plan(Mode mode, int n, int me, int k_in, int b, uint64_t count, int s
     // Logical steps, identical on every rank (so super-step numbering agrees globally).
     std::vector<std::pair<Logical, int>> L;
     const bool folds = B.rx[0].rem > 0;  // non-participants exist in every group
+    // Balanced evaluation: one recexch phase (k == b after clamping) or none (b == 1), no
+    // fold, allreduce.  Same expressions, evaluated on 1/n of every chunk at every rank.
+    p.balanced = balance && mode == MODE_ALLREDUCE && n > 1 && !folds && g.nph <= 1;
+    if (p.balanced) {
+        if (g.nph == 1) L.push_back({S_BPHASE, 0});
+        L.push_back({S_BLANE, 0});
+        L.push_back({S_BDIST, 0});
+    }
     if (folds) L.push_back({S_FOLD, 0});
-    for (int ph = g.nph - 1; ph >= 0; --ph) L.push_back({S_PHASE, ph});
-    if (folds) L.push_back({S_RETURN, 0});
-    L.push_back({S_LANE, 0});
-    if (mode == MODE_ALLREDUCE) {
-        if (n > 1) L.push_back({S_DIST1, 0});
-        if (n > 2) L.push_back({S_DIST2, 0});
-    } else if (b > 1) {
-        L.push_back({S_SCATTER, 0});
+    if (!p.balanced) {
+        for (int ph = g.nph - 1; ph >= 0; --ph) L.push_back({S_PHASE, ph});
+        if (folds) L.push_back({S_RETURN, 0});
+        L.push_back({S_LANE, 0});
+        if (mode == MODE_ALLREDUCE) {
+            if (n > 1) L.push_back({S_DIST1, 0});
+            if (n > 2) L.push_back({S_DIST2, 0});
+        } else if (b > 1) {
+            L.push_back({S_SCATTER, 0});
+        }
     }
 
     // STAGE per element of slice length (max over the steps this rank can receive in).
@@ -375,6 +479,8 @@ Plan build_plan(Mode mode, int n, int me, int k_in, int b, uint64_t count, int s
     for (int l = 0; l < b; ++l) max_nrecvs = std::max(max_nrecvs, B.rx[l].step1_nrecvs);
     B.stage_per_elem = std::max<uint64_t>({(uint64_t)max_nrecvs * g.nnodes, (uint64_t)(g.k - 1) * max_region_chunks,
                                            (uint64_t)(g.nnodes - 1), 1});
+    if (p.balanced)  // (b-1) members' or (nnodes-1) nodes' pieces of every chunk
+        B.stage_per_elem = std::max<uint64_t>({(uint64_t)(b - 1) * g.nnodes, (uint64_t)(g.nnodes - 1) * g.nnodes, 1});
 
     // Element slices of every chunk (pipeline depth), 256-element aligned bounds.
     const uint64_t G = 256;
@@ -411,7 +517,8 @@ Plan build_plan(Mode mode, int n, int me, int k_in, int b, uint64_t count, int s
             const int ls = t - s;
             if (ls < 0 || ls >= S) continue;
             if (st.label.empty()) st.label = "t" + std::to_string(t);
-            static const char* names[] = {"fold", "phase", "return", "lane", "dist1", "dist2", "scatter"};
+            static const char* names[] = {"fold", "phase", "return", "lane", "dist1", "dist2", "scatter",
+                                          "bphase", "blane", "bdist"};
             st.label += std::string(st.label.size() > 0 ? "," : "") + names[L[ls].first] +
                         (L[ls].first == S_PHASE ? std::to_string(L[ls].second) : "") + "/s" + std::to_string(s);
             B.emit(L[ls].first, L[ls].second, sl[s], st);
@@ -435,7 +542,7 @@ std::string describe(const Plan& p) {
     o << "plan mode=" << (int)p.mode << " error=" << p.error << " nranks=" << g.nranks << " rank=" << p.rank
       << " k=" << g.k << " b=" << g.b << " recvcount=" << g.recvcount << " irc=" << g.irc << " send=" << p.send_elems
       << " recv=" << p.recv_elems << " acc=" << p.acc_elems << " stage=" << p.stage_elems
-      << " slices=" << p.slices << " steps=" << p.steps.size() << "\n";
+      << " slices=" << p.slices << " balanced=" << (p.balanced ? 1 : 0) << " steps=" << p.steps.size() << "\n";
     auto local = [&](const LocalOp& op) {
         if (op.kind == L_COPY) {
             o << "copy " << buf_name(op.dst.buf) << " " << op.dst.off << " " << buf_name(op.acc.buf) << " "

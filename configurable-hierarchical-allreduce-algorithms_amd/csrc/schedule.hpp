@@ -80,6 +80,7 @@ struct Geometry {
 struct Plan {
     int error = 0;  // chr_result
     int slices = 1;  // pipeline depth actually used
+    bool balanced = false;  // allreduce evaluated piecewise on every rank (see build_plan)
     Mode mode = MODE_ALLREDUCE;
     int rank = 0;
     Geometry g;
@@ -104,7 +105,10 @@ void recexch_count_offset(int nranks, int max_phases, int k, std::vector<int>* c
 // depth: every chunk is cut into that many element slices; slice s runs logical step
 // t-s in super-step t, so consecutive phases of different slices share an RCCL group.
 // The per-element reduction order is unchanged (results are bit-identical for any depth).
-Plan build_plan(Mode mode, int nranks, int rank, int k, int b, uint64_t count, int slices = 1);
+// balance: evaluate single-phase allreduce geometries piecewise on every rank (same
+// expressions, same bits; see schedule.cpp S_BPHASE/S_BLANE/S_BDIST).
+Plan build_plan(Mode mode, int nranks, int rank, int k, int b, uint64_t count, int slices = 1,
+                bool balance = true);
 int auto_slices(uint64_t irc_bytes);
 // MPICH baseline allreduces (count = elements per rank; aux = recexch single_phase_recv).
 Plan build_plan_mpich(Mode mode, int nranks, int rank, int k, int aux, uint64_t count);

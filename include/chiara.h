@@ -90,6 +90,13 @@ int chr_comm_stream(const chr_comm* comm, hipStream_t* stream);
  * busy at once).  0 = automatic (~64 MiB per slice message, up to 8; env CHR_SLICES).
  * Results are bit-identical for every depth. */
 int chr_comm_set_slices(chr_comm* comm, int slices);
+/* Balanced evaluation (default on; env CHR_BALANCE=0 turns the default off).  For allreduce
+ * geometries whose intra-group phase is one recexch phase (k == b after clamping) or none
+ * (b == 1), every rank evaluates 1/n of every chunk's reduction -- the same expression, in
+ * the same operand order, as the reference's single owner lane / root node -- instead of
+ * only the nnodes owner lanes doing all of it.  Same bytes per rank, same result bits; the
+ * busiest xGMI link carries less.  Other geometries are unaffected. */
+int chr_comm_set_balance(chr_comm* comm, int enable);
 /* Opt-in timing of the fused bucket-reduction launches of this communicator (HIP events
  * on its stream).  _read synchronises on the recorded launches and returns the summed
  * kernel milliseconds, the algorithmic bytes ((m+2)*n*sizeof(T) per launch) and the
@@ -140,6 +147,7 @@ int chr_local_group_create(chr_local_group** group, int nranks, int device);
 int chr_local_group_destroy(chr_local_group* group);
 int chr_local_group_stream(const chr_local_group* group, hipStream_t* stream);
 int chr_local_group_set_slices(chr_local_group* group, int slices);
+int chr_local_group_set_balance(chr_local_group* group, int enable);
 int chr_local_allreduce_radix_batch(chr_local_group* group, const void* const* sends,
                                     void* const* recvs, size_t count, chr_dtype dtype, chr_op op,
                                     int k, int b);
@@ -168,6 +176,9 @@ typedef enum {
 } chr_mode;
 long chr_plan_describe(chr_mode mode, int nranks, int rank, int k, int b, size_t count,
                        int slices, char* buf, size_t len);
+/* The same with the balanced-evaluation switch (chr_plan_describe uses balance = 1). */
+long chr_plan_describe_ex(chr_mode mode, int nranks, int rank, int k, int b, size_t count,
+                          int slices, int balance, char* buf, size_t len);
 
 /* ---- MPICH baseline allreduces (the ones testing/main.cpp benchmarks CHiArA against) --
  * Replace  int MPICH_Allreduce_ring(const char* sendbuf, char* recvbuf, int count,

@@ -58,8 +58,9 @@ def test_plan_errors_match_reference_preconditions():
 def test_plan_shape_c4():
     """C4 geometry (n=8, k=4, b=4): one recexch phase with k-1=3 concurrent neighbours,
     one fused 3-input reduction per active lane, 1-input lane reduction at the roots,
-    then the link-balanced distribute (scatter 1/7 pieces, forward)."""
-    p = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 1 << 20))
+    then the link-balanced distribute (scatter 1/7 pieces, forward).  Owner-lane evaluation
+    (balance off)."""
+    p = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 1 << 20, balance=False))
     assert p["header"]["k"] == 4 and p["header"]["steps"] == 4 and p["header"]["slices"] == 1
     ph = p["steps"][0]
     assert len(ph["recvs"]) == 3 and len(ph["sends"]) == 1
@@ -70,6 +71,19 @@ def test_plan_shape_c4():
     d1, d2 = p["steps"][2], p["steps"][3]
     assert len(d1["sends"]) == 7 and len(d1["recvs"]) == 1   # rank 0 owns chunk 0, gets a piece of chunk 1
     assert len(d2["sends"]) == 6 and len(d2["recvs"]) == 6  # forwards its piece of chunk 1, gets the rest
+
+
+def test_plan_shape_c4_balanced():
+    """Balanced C4: 3 steps; every rank exchanges with its 3 group peers (2 chunks each),
+    reduces 2 chunks x 3 inputs, then 1 piece per chunk with the other node, then allgathers."""
+    p = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 5, 4, 4, 1 << 20))
+    assert p["header"]["balanced"] == 1 and p["header"]["steps"] == 3
+    ph, lane, dist = p["steps"]
+    assert len(ph["sends"]) == 6 and len(ph["recvs"]) == 6
+    assert [len(op[4]) for op in ph["post"]] == [3, 3]
+    assert {x[0] for x in lane["sends"]} == {1} and [len(op[4]) for op in lane["post"]] == [1, 1]
+    assert all(op[1][0] == "RECV" for op in lane["post"])
+    assert len(dist["sends"]) == 14 and len(dist["recvs"]) == 14
 
 
 @pytest.mark.parametrize("slices", [2, 3, 5, 8])
@@ -92,10 +106,13 @@ def test_pipelined_plans_bit_exact(mode, n, k, b, slices):
 
 
 def test_pipelined_plan_structure():
-    p = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 8 * 4 * 4096, 4))
+    p = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 8 * 4 * 4096, 4, balance=False))
     assert p["header"]["slices"] == 4 and p["header"]["steps"] == 4 + 4 - 1
     # super-step 1 holds slice 0's lane reduce and slice 1's recexch phase in ONE group
     assert "lane/s0" in p["steps"][1]["label"] and "phase0/s1" in p["steps"][1]["label"]
+    q = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 8 * 4 * 4096, 4))
+    assert q["header"]["steps"] == 3 + 4 - 1
+    assert "blane/s0" in q["steps"][1]["label"] and "bphase/s1" in q["steps"][1]["label"]
 
 
 @pytest.mark.parametrize("n,k,b", [(8, 4, 4), (8, 2, 8), (16, 3, 4), (6, 5, 3), (12, 8, 2), (1, 2, 1)])
@@ -119,3 +136,51 @@ def test_allgather_plans(n, k, b):
 def test_allgather_plan_errors():
     assert plan_sim.load_plans(ca.MODE_ALLGATHER, 6, 2, 4, 8)[0]["header"]["error"] == 3
     assert plan_sim.load_plans(ca.MODE_ALLGATHER, 6, 1, 3, 8)[0]["header"]["error"] == 1
+
+
+@pytest.mark.parametrize("n,k,b", [(8, 4, 4), (8, 2, 2), (8, 8, 8), (8, 2, 1), (4, 4, 4), (2, 2, 2), (2, 2, 1),
+                                   (6, 3, 3), (12, 4, 4), (16, 4, 4), (9, 3, 3), (5, 2, 1)])
+@pytest.mark.parametrize("slices", [1, 3])
+def test_balanced_plans_bit_exact(n, k, b, slices):
+    """Balanced evaluation (every rank reduces 1/n of every chunk, same expressions) gives
+    the reference's bits, with and without pipelining, for SUM and the order-sensitive MAX."""
+    count = n * 1000 + n * 64
+    for dt, op, pat in (("f32", "sum", po.PAT_UNIFORM), ("bf16", "sum", po.PAT_UNIFORM), ("f32", "max", po.PAT_TIES)):
+        sends = [po.fill(count, dt, pat, 17, r) for r in range(n)]
+        want = po.allreduce_radix_batch(sends, k, b, dt, op)
+        plans = plan_sim.load_plans(ca.MODE_ALLREDUCE, n, k, b, count, slices, balance=True)
+        assert plans[0]["header"]["balanced"] == 1
+        got = plan_sim.execute(plans, sends, dt, op)
+        for r in range(n):
+            np.testing.assert_array_equal(got[r].view(np.uint8), want[r].view(np.uint8))
+
+
+def test_balance_only_where_single_phase():
+    hdr = lambda n, k, b: plan_sim.load_plans(ca.MODE_ALLREDUCE, n, k, b, n * 256)[0]["header"]["balanced"]
+    assert hdr(8, 4, 4) == 1 and hdr(8, 8, 8) == 1 and hdr(8, 2, 1) == 1
+    assert hdr(8, 2, 4) == 0 and hdr(8, 3, 4) == 0 and hdr(8, 4, 8) == 0  # multi-phase / fold
+    assert plan_sim.load_plans(ca.MODE_REDUCE_SCATTER, 8, 4, 4, 256)[0]["header"]["balanced"] == 0
+
+
+def _link_bytes(plans):
+    per_pair = {}
+    for r, p in enumerate(plans):
+        for st in p["steps"]:
+            for peer, _, cnt in st["sends"]:
+                per_pair[(r, peer)] = per_pair.get((r, peer), 0) + cnt
+    return per_pair
+
+
+def test_balanced_traffic_c4():
+    """C4 geometry (n=8, k=4, b=4): the same total bytes, every rank sending exactly the
+    allreduce minimum 2(n-1)/n of the buffer, and the busiest directed link carrying S/4 + S/8
+    instead of ~0.64 S."""
+    n, count = 8, 8 * 4096
+    bal = _link_bytes(plan_sim.load_plans(ca.MODE_ALLREDUCE, n, 4, 4, count, balance=True))
+    ref = _link_bytes(plan_sim.load_plans(ca.MODE_ALLREDUCE, n, 4, 4, count, balance=False))
+    per_rank = lambda d, r: sum(v for (a, _), v in d.items() if a == r)
+    assert sum(bal.values()) == sum(ref.values())
+    for r in range(n):  # balanced: every rank sends exactly the allreduce minimum
+        assert per_rank(bal, r) == 2 * (n - 1) * count // n
+    assert max(bal.values()) <= count // 4 + count // 8 + 64
+    assert max(ref.values()) > 0.6 * count
