@@ -178,7 +178,7 @@ def bench_bucket(args, cpu):
             line["gpu_vs_cpu_all_cores"] = round(line["value"] / cpu["all_cores"]["value"], 1)
     if args.sweep:
         line["sweep"] = sweep(ca, torch, dev, stream)
-    print(json.dumps(line), flush=True)
+    emit(line)
 
 
 def sweep(ca, torch, dev, stream):
@@ -254,7 +254,7 @@ def bench_e2e(args):
         ca.check(ca.all_reduce_radix_batch(d_send, d_recv, n, ca.FLOAT32, ca.SUM, comm, 2, 1))
     out["device_resident_ms"] = round((time.perf_counter() - t0) / 3 * 1e3, 3)
     comm.destroy()
-    print(json.dumps({"e2e": out}), flush=True)
+    emit({"e2e": out})
 
 
 # ---- N > 1: hierarchical allreduce over RCCL ---------------------------------------------------
@@ -343,7 +343,7 @@ def bench_allreduce(args):
         }
         if compare:
             line["compare"] = compare
-        print(json.dumps(line), flush=True)
+        emit(line)
     comm.destroy()
     dist.destroy_process_group()
 
@@ -403,7 +403,45 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
     return out
 
 
+class _StdoutToStderr:
+    """Route file descriptor 1 to stderr while libraries run (RCCL prints its init banner to
+    stdout); emit() writes the one JSON line to the real stdout."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def emit(self, text):
+        sys.stdout.flush()
+        os.write(self.saved, (text + "\n").encode())
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
+OUT = None  # set in main(): where the JSON line goes
+
+
+def emit(line):
+    text = json.dumps(line)
+    if OUT is not None:
+        OUT.emit(text)
+    else:
+        print(text, flush=True)
+
+
 def main():
+    global OUT
+    with _StdoutToStderr() as OUT:
+        _main()
+
+
+def _main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
