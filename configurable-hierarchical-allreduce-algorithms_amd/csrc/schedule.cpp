@@ -120,7 +120,8 @@ LocalOp make_copy2d(Ref dst, Ref src, uint64_t width, uint64_t rows, uint64_t dp
     return op;
 }
 
-enum Logical { S_FOLD, S_PHASE, S_RETURN, S_LANE, S_DIST1, S_DIST2, S_SCATTER, S_BPHASE, S_BLANE, S_BDIST };
+enum Logical { S_FOLD, S_PHASE, S_RETURN, S_LANE, S_DIST1, S_DIST2, S_SCATTER, S_BPHASE, S_BLANE, S_BDIST,
+               S_RPHASE, S_RLANE };
 
 // One element-slice [lo, lo+len) of every chunk, laid out slice-major in ACC:
 // chunk position `pos` of slice p lives at acc_base + pos*len.
@@ -362,6 +363,59 @@ struct Builder {
             }
             break;
         }
+        case S_RPHASE: {
+            // Balanced reduce-scatter: the output block of rank (Y, j) is sub-block j (recvcount
+            // elements of the IRC chunk) of chunk Y.  Phase 1 of every chunk N: lane j evaluates
+            // sub-block j in the owner lane's order (as S_BPHASE, pieces = recvcount blocks).
+            const uint64_t a = std::max(c.lo, (uint64_t)lane * recvcount);
+            const uint64_t e = std::min(c.lo + c.len, (uint64_t)(lane + 1) * recvcount);
+            for (int m = 0; m < g.b; ++m) {
+                if (m == lane) continue;
+                const uint64_t ma = std::max(c.lo, (uint64_t)m * recvcount);
+                const uint64_t me_ = std::min(c.lo + c.len, (uint64_t)(m + 1) * recvcount);
+                for (int N = 0; N < g.nnodes && ma < me_; ++N)
+                    s.sends.push_back({node * g.b + m, {BUF_ACC, acc_of(c, N) + (ma - c.lo)}, me_ - ma});
+            }
+            if (a >= e) break;
+            const uint64_t off = a - c.lo, len = e - a;
+            for (int N = 0; N < g.nnodes; ++N) {
+                auto src = [&](int m) -> Ref {
+                    if (m == lane) return {BUF_ACC, acc_of(c, N) + off};
+                    const int slot = (m < lane ? m : m - 1) * g.nnodes + N;
+                    return {BUF_STAGE, c.stage_base + (uint64_t)slot * c.len + off};
+                };
+                for (int m = 0; m < g.b; ++m)
+                    if (m != lane) s.recvs.push_back({node * g.b + m, src(m), len});
+                const int L = N % g.b;
+                std::vector<Ref> ins;
+                for (int i = 0; i < g.k - 1; ++i) ins.push_back(src(rx[L].step2_nbrs[0][i]));
+                s.post.push_back(make_reduce({BUF_ACC, acc_of(c, N) + off}, src(L), ins, len, 366));
+            }
+            break;
+        }
+        case S_RLANE: {
+            // Phase 2 of chunk N, sub-block j: at rank (N, j), root-node order (:498-552), written
+            // straight into recvbuf; every other node sends its sub-block j of chunk N there.
+            const uint64_t a = std::max(c.lo, (uint64_t)lane * recvcount);
+            const uint64_t e = std::min(c.lo + c.len, (uint64_t)(lane + 1) * recvcount);
+            if (a >= e) break;
+            const uint64_t off = a - c.lo, len = e - a;
+            for (int N = 0; N < g.nnodes; ++N)
+                if (N != node) s.sends.push_back({N * g.b + lane, {BUF_ACC, acc_of(c, N) + off}, len});
+            auto src = [&](int X) -> Ref {  // node X's phase-1 value of chunk `node`, sub-block lane
+                if (X == node) return {BUF_ACC, acc_of(c, node) + off};
+                const int slot = X < node ? X : X - 1;
+                return {BUF_STAGE, c.stage_base + (uint64_t)slot * c.len + off};
+            };
+            std::vector<Ref> ins;
+            for (int X = 0; X < g.nnodes; ++X) {
+                if (X == node) continue;
+                s.recvs.push_back({X * g.b + lane, src(X), len});
+                ins.push_back(src(X));
+            }
+            s.post.push_back(make_reduce({BUF_RECV, a - (uint64_t)lane * recvcount}, src(node), ins, len, 552));
+            break;
+        }
         case S_SCATTER: {  // reduce-scatter phase 3 (:572-627): owner -> every lane, direct
             const int owner = node * g.b + node % g.b;
             if (me == owner) {
@@ -448,12 +502,16 @@ Plan build_plan(Mode mode, int n, int me, int k_in, int b, uint64_t count, int s
     std::vector<std::pair<Logical, int>> L;
     const bool folds = B.rx[0].rem > 0;  // non-participants exist in every group
     // Balanced evaluation: one recexch phase (k == b after clamping) or none (b == 1), no
-    // fold, allreduce.  Same expressions, evaluated on 1/n of every chunk at every rank.
-    p.balanced = balance && mode == MODE_ALLREDUCE && n > 1 && !folds && g.nph <= 1;
-    if (p.balanced) {
+    // fold.  Same expressions, evaluated on 1/n of every chunk at every rank (allreduce), or
+    // on exactly the rank's own output block (reduce-scatter).
+    p.balanced = balance && n > 1 && !folds && g.nph <= 1;
+    if (p.balanced && mode == MODE_ALLREDUCE) {
         if (g.nph == 1) L.push_back({S_BPHASE, 0});
         L.push_back({S_BLANE, 0});
         L.push_back({S_BDIST, 0});
+    } else if (p.balanced) {  // reduce-scatter: each rank evaluates exactly its own block
+        if (g.nph == 1) L.push_back({S_RPHASE, 0});
+        L.push_back({S_RLANE, 0});
     }
     if (folds) L.push_back({S_FOLD, 0});
     if (!p.balanced) {
@@ -518,7 +576,7 @@ Plan build_plan(Mode mode, int n, int me, int k_in, int b, uint64_t count, int s
             if (ls < 0 || ls >= S) continue;
             if (st.label.empty()) st.label = "t" + std::to_string(t);
             static const char* names[] = {"fold", "phase", "return", "lane", "dist1", "dist2", "scatter",
-                                          "bphase", "blane", "bdist"};
+                                          "bphase", "blane", "bdist", "rphase", "rlane"};
             st.label += std::string(st.label.size() > 0 ? "," : "") + names[L[ls].first] +
                         (L[ls].first == S_PHASE ? std::to_string(L[ls].second) : "") + "/s" + std::to_string(s);
             B.emit(L[ls].first, L[ls].second, sl[s], st);

@@ -266,3 +266,21 @@ def test_balanced_equals_owner_lane_evaluation(gu, groups, n, k, b, dtype):
     for r in range(n):
         np.testing.assert_array_equal(outs[True][r].view(np.uint8), want[r].view(np.uint8))
         np.testing.assert_array_equal(outs[False][r].view(np.uint8), want[r].view(np.uint8))
+
+
+@pytest.mark.parametrize("n,k,b", [(2, 2, 2), (2, 2, 1), (8, 4, 4), (8, 8, 8)])
+def test_balanced_reduce_scatter_equals_owner_lane(gu, groups, n, k, b):
+    """Reduce-scatter: balanced (own block evaluated locally) and owner-lane plans, 4 MiB
+    blocks, both bit-exact vs the oracle."""
+    rc = (1 << 20) + 64
+    sends = [po.fill(rc * n, "f32", po.PAT_UNIFORM, 6, r) for r in range(n)]
+    want = po.reduce_scatter_radix_batch(sends, k, b, "f32", "sum")
+    g = groups(n)
+    try:
+        for bal in (True, False):
+            g.set_balance(bal)
+            got = run_local(gu, g, "rs", sends, k, b, "f32", "sum")
+            for r in range(n):
+                np.testing.assert_array_equal(got[r].view(np.uint32), want[r].view(np.uint32))
+    finally:
+        g.set_balance(True)

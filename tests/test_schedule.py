@@ -159,7 +159,8 @@ def test_balance_only_where_single_phase():
     hdr = lambda n, k, b: plan_sim.load_plans(ca.MODE_ALLREDUCE, n, k, b, n * 256)[0]["header"]["balanced"]
     assert hdr(8, 4, 4) == 1 and hdr(8, 8, 8) == 1 and hdr(8, 2, 1) == 1
     assert hdr(8, 2, 4) == 0 and hdr(8, 3, 4) == 0 and hdr(8, 4, 8) == 0  # multi-phase / fold
-    assert plan_sim.load_plans(ca.MODE_REDUCE_SCATTER, 8, 4, 4, 256)[0]["header"]["balanced"] == 0
+    assert plan_sim.load_plans(ca.MODE_REDUCE_SCATTER, 8, 4, 4, 256)[0]["header"]["balanced"] == 1
+    assert plan_sim.load_plans(ca.MODE_REDUCE_SCATTER, 8, 2, 4, 256)[0]["header"]["balanced"] == 0
 
 
 def _link_bytes(plans):
@@ -184,3 +185,28 @@ def test_balanced_traffic_c4():
         assert per_rank(bal, r) == 2 * (n - 1) * count // n
     assert max(bal.values()) <= count // 4 + count // 8 + 64
     assert max(ref.values()) > 0.6 * count
+
+
+@pytest.mark.parametrize("n,k,b", [(2, 2, 2), (2, 2, 1), (8, 4, 4), (8, 8, 8), (8, 2, 1), (6, 3, 3), (12, 4, 4),
+                                   (16, 2, 2)])
+@pytest.mark.parametrize("slices", [1, 3])
+def test_balanced_reduce_scatter_bit_exact(n, k, b, slices):
+    """Balanced reduce-scatter: rank (Y, j) evaluates exactly its own output block (sub-block j
+    of chunk Y) in the reference's operand order -- no scatter phase, same bits."""
+    rc = 64 * 7 + 3
+    for dt, op, pat in (("f32", "sum", po.PAT_UNIFORM), ("bf16", "sum", po.PAT_UNIFORM), ("f32", "max", po.PAT_TIES)):
+        sends = [po.fill(rc * n, dt, pat, 9, r) for r in range(n)]
+        want = po.reduce_scatter_radix_batch(sends, k, b, dt, op)
+        got = plan_sim.simulate(ca.MODE_REDUCE_SCATTER, sends, k, b, dt, op, slices=slices)
+        for r in range(n):
+            np.testing.assert_array_equal(got[r].view(np.uint8), want[r].view(np.uint8))
+
+
+def test_balanced_reduce_scatter_traffic_c3():
+    """C3 (n=2, k=2, b=2): each rank sends exactly the reduce-scatter minimum (n-1)/n of its
+    send buffer; the reference's lane 0 receives the whole buffer and scatters half back."""
+    n, rc = 2, 4096
+    bal = _link_bytes(plan_sim.load_plans(ca.MODE_REDUCE_SCATTER, n, 2, 2, rc, balance=True))
+    ref = _link_bytes(plan_sim.load_plans(ca.MODE_REDUCE_SCATTER, n, 2, 2, rc, balance=False))
+    assert bal == {(0, 1): rc, (1, 0): rc}
+    assert max(ref.values()) == 2 * rc and sum(ref.values()) == 3 * rc
