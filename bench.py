@@ -333,7 +333,7 @@ def bench_allreduce(args):
             "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
             "config": {"workload": f"all_reduce_radix_batch, {S >> 20} MiB per rank, k={k}, b={b}, RCCL p2p over "
                                    f"xGMI, device-resident", "k": k, "b": b, "count": count,
-                       "balanced_evaluation": bool(int(os.environ.get("CHR_BALANCE", "1"))),
+                       "schedule": os.environ.get("CHR_SCHEDULE", "flat"),
                        "parallelism": f"collective x{world}"},
             "algbw_GBps": round(algbw, 2), "busbw_GBps": round(busbw, 2),
             "xgmi_roofline": {"per_link_GBps": XGMI_LINK_GBPS, "aggregate_GBps": 7 * XGMI_LINK_GBPS,
@@ -369,7 +369,7 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
     """Context, not the metric: on the same buffers and ranks, (1) RCCL's own ncclAllReduce
     (torch.distributed nccl group), (2) the reference's MPICH ring baseline
     (testing/mpich_implementations/all_reduce/allreduce_ring.cpp) run on libchiara's executor and
-    (3) the metric's own schedule with balanced evaluation switched off (owner lanes reduce)."""
+    (3) the metric's arithmetic under the balanced and the reference-route schedules."""
     steps, warm = max(1, min(args.steps, 20)), 2
     S = count * (4 if dt == ca.FLOAT32 else 2)
     out = {"steps": steps}
@@ -392,14 +392,16 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
         ca.check(ca.MPICH_Allreduce_ring(send, recv, count, dt, ca.SUM, comm, async_op=True))
     out["mpich_ring_on_libchiara"] = entry(_timed_max(torch, dist, ring, steps, warm))
 
-    # the same radix/batch schedule with the reference's owner-lane evaluation (balance off)
-    def owner_lane():
+    # the same radix/batch arithmetic under the other two schedules (same bits, other routes)
+    def radix():
         ca.check(ca.all_reduce_radix_batch(send, recv, count, dt, ca.SUM, comm, k, b, async_op=True))
-    comm.set_balance(False)
-    try:
-        out["radix_batch_owner_lane"] = entry(_timed_max(torch, dist, owner_lane, steps, warm))
-    finally:
-        comm.set_balance(True)
+    for name, sch in (("radix_batch_balanced", ca.SCHEDULE_BALANCED), ("radix_batch_reference_route",
+                                                                      ca.SCHEDULE_REFERENCE)):
+        comm.set_schedule(sch)
+        try:
+            out[name] = entry(_timed_max(torch, dist, radix, steps, warm))
+        finally:
+            comm.set_schedule(ca.SCHEDULE_FLAT)
     return out
 
 

@@ -34,6 +34,7 @@ MODE_ALLREDUCE, MODE_REDUCE_SCATTER = 0, 1
 MODE_MPICH_RING, MODE_MPICH_RD, MODE_MPICH_RSAG, MODE_MPICH_RECEXCH = 2, 3, 4, 5
 MODE_MPICH_KRSAG, MODE_MPICH_RMULT = 6, 7
 MODE_ALLGATHER = 8
+SCHEDULE_REFERENCE, SCHEDULE_BALANCED, SCHEDULE_FLAT = 0, 1, 2
 REDUCE_RUNNING_FIRST = 1  # chr_reduce_multi_ex flag (MPICH_do_reduce operand order)
 
 
@@ -134,8 +135,10 @@ class Comm:
         """Pipeline depth (0 = automatic); results are bit-identical for every depth."""
         check(lib().chr_comm_set_slices(self._h, slices))
 
-    def set_balance(self, enable):
-        check(lib().chr_comm_set_balance(self._h, int(bool(enable))))
+    def set_schedule(self, schedule):
+        """SCHEDULE_REFERENCE / SCHEDULE_BALANCED / SCHEDULE_FLAT: where reductions are evaluated
+        (never what they compute)."""
+        check(lib().chr_comm_set_schedule(self._h, int(schedule)))
 
     def profile(self, enable=True):
         """Time every fused reduction launch of this communicator (HIP events)."""
@@ -184,8 +187,8 @@ class LocalGroup:
     def set_slices(self, slices):
         check(lib().chr_local_group_set_slices(self._h, slices))
 
-    def set_balance(self, enable):
-        check(lib().chr_local_group_set_balance(self._h, int(bool(enable))))
+    def set_schedule(self, schedule):
+        check(lib().chr_local_group_set_schedule(self._h, int(schedule)))
 
     def all_reduce_radix_batch(self, sendbufs, recvbufs, count, datatype, op, k, b):
         S = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in sendbufs])
@@ -287,8 +290,8 @@ def reduce_multi_ex(out, acc, ins, count, datatype, op, flags, stream=None):
 
 # ---- plan introspection (host only) --------------------------------------------------------------
 
-def describe_plan(mode, nranks, rank, k, b, count, slices=1, balance=True):
-    bal = int(bool(balance))
+def describe_plan(mode, nranks, rank, k, b, count, slices=1, schedule=None):
+    bal = SCHEDULE_FLAT if schedule is None else int(schedule)
     n = lib().chr_plan_describe_ex(mode, nranks, rank, k, b, count, slices, bal, None, 0)
     if n < 0:
         raise ValueError("bad plan request")

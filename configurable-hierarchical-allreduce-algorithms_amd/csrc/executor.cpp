@@ -158,12 +158,17 @@ bool is_device_ptr(const void* p) {
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
 }
 
-using PlanKey = std::tuple<int, int, int, int, uint64_t, int, int, int>;  // mode, rank, k, b, count, dtype size, slices, balance
+using PlanKey = std::tuple<int, int, int, int, uint64_t, int, int, int>;  // mode, rank, k, b, count, dtype size, slices, schedule
 
-int default_balance() {
+// CHR_SCHEDULE = reference | balanced | flat (or 0 / 1 / 2); default flat
+int default_schedule() {
     static const int v = [] {
-        const char* e = std::getenv("CHR_BALANCE");
-        return e ? (std::atoi(e) != 0) : 1;
+        const char* e = std::getenv("CHR_SCHEDULE");
+        if (!e) return (int)chr::SCHED_FLAT;
+        const std::string s(e);
+        if (s == "reference" || s == "0") return (int)chr::SCHED_REFERENCE;
+        if (s == "balanced" || s == "1") return (int)chr::SCHED_BALANCED;
+        return (int)chr::SCHED_FLAT;
     }();
     return v;
 }
@@ -186,7 +191,7 @@ int pick_slices(int setting, uint64_t count, int mode, int nranks, int b, size_t
 struct chr_comm {
     int rank = 0, nranks = 0, device = 0;
     int slices = 0;  // 0 = auto
-    int balance = default_balance();
+    int sched = default_schedule();
     ncclComm_t nccl = nullptr;
     hipStream_t stream = nullptr;
     DevBuf acc, stage, hsend, hrecv;
@@ -195,11 +200,11 @@ struct chr_comm {
 
     const Plan& plan(int mode, int k, int b, uint64_t count, size_t es) {
         const int P = pick_slices(slices, count, mode, nranks, b, es);
-        PlanKey key{mode, rank, k, b, count, (int)es, P, balance};
+        PlanKey key{mode, rank, k, b, count, (int)es, P, sched};
         auto it = plans.find(key);
         if (it == plans.end())
             it = plans.emplace(key, std::make_unique<Plan>(chr::build_plan((chr::Mode)mode, nranks, rank, k, b, count, P,
-                                                                           balance != 0)))
+                                                                           sched)))
                      .first;
         return *it->second;
     }
@@ -208,7 +213,7 @@ struct chr_comm {
 struct chr_local_group {
     int nranks = 0, device = 0;
     int slices = 0;  // 0 = auto
-    int balance = default_balance();
+    int sched = default_schedule();
     hipStream_t stream = nullptr;
     std::vector<DevBuf> acc, stage;
     std::map<std::tuple<int, int, int, uint64_t, int, int, int>, std::vector<Plan>> plans;
@@ -294,12 +299,12 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
     if (!g || !sends || !recvs || !chr::valid_dtype_op(dtype, op)) return CHR_ERR_INVALID_ARG;
     const int n = g->nranks;
     const int depth = pick_slices(g->slices, count, mode, n, b, chr::dtype_size(dtype));
-    auto key = std::make_tuple(mode, k, b, (uint64_t)count, (int)chr::dtype_size(dtype), depth, g->balance);
+    auto key = std::make_tuple(mode, k, b, (uint64_t)count, (int)chr::dtype_size(dtype), depth, g->sched);
     auto it = g->plans.find(key);
     if (it == g->plans.end()) {
         std::vector<Plan> v;
         for (int r = 0; r < n; ++r)
-            v.push_back(chr::build_plan((chr::Mode)mode, n, r, k, b, count, depth, g->balance != 0));
+            v.push_back(chr::build_plan((chr::Mode)mode, n, r, k, b, count, depth, g->sched));
         it = g->plans.emplace(key, std::move(v)).first;
     }
     const std::vector<Plan>& P = it->second;
@@ -448,15 +453,15 @@ int chr_comm_profile_read(chr_comm* c, double* reduce_ms, double* reduce_bytes, 
     return CHR_SUCCESS;
 }
 
-int chr_comm_set_balance(chr_comm* c, int enable) {
-    if (!c) return CHR_ERR_INVALID_ARG;
-    c->balance = enable != 0;
+int chr_comm_set_schedule(chr_comm* c, int schedule) {
+    if (!c || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_FLAT) return CHR_ERR_INVALID_ARG;
+    c->sched = schedule;
     return CHR_SUCCESS;
 }
 
-int chr_local_group_set_balance(chr_local_group* g, int enable) {
-    if (!g) return CHR_ERR_INVALID_ARG;
-    g->balance = enable != 0;
+int chr_local_group_set_schedule(chr_local_group* g, int schedule) {
+    if (!g || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_FLAT) return CHR_ERR_INVALID_ARG;
+    g->sched = schedule;
     return CHR_SUCCESS;
 }
 

@@ -4,6 +4,9 @@
 // line-for-line identical through phase 2).
 #include "schedule.hpp"
 
+#include <functional>
+#include <tuple>
+
 #include <algorithm>
 #include <cstdio>
 #include <sstream>
@@ -445,7 +448,10 @@ int auto_slices(uint64_t irc_bytes) {
     return (int)std::max<uint64_t>(1, std::min<uint64_t>(8, s));
 }
 
-Plan build_plan(Mode mode, int n, int me, int k_in, int b, uint64_t count, int slices, bool balance) {
+Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, int slices);
+
+Plan build_plan(Mode mode, int n, int me, int k_in, int b, uint64_t count, int slices, int sched) {
+    const bool balance = sched == SCHED_BALANCED;
     if (is_mpich(mode)) return build_plan_mpich(mode, n, me, k_in, b, count);
     if (mode == MODE_ALLGATHER) return build_plan_allgather(n, me, k_in, b, count);
     Plan p;
@@ -497,6 +503,10 @@ Plan build_plan(Mode mode, int n, int me, int k_in, int b, uint64_t count, int s
     p.recv_elems = mode == MODE_ALLREDUCE ? g.total : recvcount;
     p.acc_elems = g.total;
     if (g.total == 0) return p;
+    if (sched == SCHED_FLAT && n > 1) {
+        Plan f = build_plan_flat(mode, n, me, k_in, b, g, slices);
+        if (!f.error) return f;
+    }
 
     // Logical steps, identical on every rank (so super-step numbering agrees globally).
     std::vector<std::pair<Logical, int>> L;
@@ -505,6 +515,7 @@ Plan build_plan(Mode mode, int n, int me, int k_in, int b, uint64_t count, int s
     // fold.  Same expressions, evaluated on 1/n of every chunk at every rank (allreduce), or
     // on exactly the rank's own output block (reduce-scatter).
     p.balanced = balance && n > 1 && !folds && g.nph <= 1;
+    p.sched = p.balanced ? SCHED_BALANCED : SCHED_REFERENCE;
     if (p.balanced && mode == MODE_ALLREDUCE) {
         if (g.nph == 1) L.push_back({S_BPHASE, 0});
         L.push_back({S_BLANE, 0});
@@ -600,7 +611,8 @@ std::string describe(const Plan& p) {
     o << "plan mode=" << (int)p.mode << " error=" << p.error << " nranks=" << g.nranks << " rank=" << p.rank
       << " k=" << g.k << " b=" << g.b << " recvcount=" << g.recvcount << " irc=" << g.irc << " send=" << p.send_elems
       << " recv=" << p.recv_elems << " acc=" << p.acc_elems << " stage=" << p.stage_elems
-      << " slices=" << p.slices << " balanced=" << (p.balanced ? 1 : 0) << " steps=" << p.steps.size() << "\n";
+      << " slices=" << p.slices << " balanced=" << (p.balanced ? 1 : 0) << " schedule=" << p.sched
+      << " steps=" << p.steps.size() << "\n";
     auto local = [&](const LocalOp& op) {
         if (op.kind == L_COPY) {
             o << "copy " << buf_name(op.dst.buf) << " " << op.dst.off << " " << buf_name(op.acc.buf) << " "
@@ -1094,6 +1106,305 @@ Plan build_plan_allgather(int n, int me, int k, int b, uint64_t count) {
         for (size_t j = i; j < peers.size() && j < i + (size_t)(k - 1); ++j) {
             s.sends.push_back({peers[j].first, mine, count});
             s.recvs.push_back({peers[j].second, {BUF_RECV, (uint64_t)peers[j].second * count}, count});
+        }
+    }
+    return p;
+}
+
+}  // namespace chr
+
+// ==== flat schedule: the reference's arithmetic, the full xGMI mesh's communication ==========
+//
+// The radix/batch hierarchy fixes, for every element, an expression tree over the n ranks'
+// inputs (recexch phases in neighbour order, step-1 folds, lane reduction in stage order);
+// that tree is what makes the result bits.  Where it is evaluated is free.  build_plan_flat
+// extracts the tree of every chunk by executing the reference-order plans of all ranks
+// symbolically (expression ids instead of numbers, recvcount = 1), then emits:
+//   gather    every rank sends piece q of every chunk (allreduce) / block q (reduce-scatter)
+//             straight to rank q: all n-1 links at once, S/n per directed pair;
+//   evaluate  rank q evaluates the chunk's tree on its piece with the fused kernel, one launch
+//             per reference reduction op, operands in the reference's order;
+//   allgather (allreduce) the n result pieces to everyone, S/n per pair.
+// Every link carries 2S/n in all, the full-mesh optimum, for any (k, b).  Inputs are read in
+// place from SEND: no re-layout copy.
+namespace chr {
+namespace {
+
+struct SymNode {
+    int leaf = -1;  // >= 0: rank r's input element
+    int acc = -1;
+    std::vector<int> ins;
+    bool swap = false;
+};
+
+struct SymExec {
+    std::vector<SymNode> nodes;
+    std::vector<std::vector<std::vector<int>>> buf;  // [rank][Buf][elem] -> node id
+    const std::vector<Plan>& P;
+    explicit SymExec(const std::vector<Plan>& plans) : P(plans) {
+        const int n = (int)P.size();
+        for (int r = 0; r < n; ++r) nodes.push_back({r, -1, {}, false});
+        buf.resize(n);
+        for (int r = 0; r < n; ++r) {
+            buf[r].resize(4);
+            buf[r][BUF_SEND].assign(P[r].send_elems, r);
+            buf[r][BUF_RECV].assign(P[r].recv_elems, -1);
+            buf[r][BUF_ACC].assign(P[r].acc_elems, -1);
+            buf[r][BUF_STAGE].assign(P[r].stage_elems, -1);
+        }
+    }
+    int* at(int r, const Ref& x, uint64_t i) { return &buf[r][x.buf].at(x.off + i); }
+    void local(int r, const LocalOp& op) {
+        if (op.kind == L_COPY || op.kind == L_COPY2D) {
+            const uint64_t rows = op.kind == L_COPY2D ? op.rows : 1;
+            std::vector<int> tmp;
+            for (uint64_t row = 0; row < rows; ++row)
+                for (uint64_t i = 0; i < op.count; ++i) tmp.push_back(*at(r, op.acc, row * op.spitch + i));
+            size_t t = 0;
+            for (uint64_t row = 0; row < rows; ++row)
+                for (uint64_t i = 0; i < op.count; ++i) *at(r, op.dst, row * op.dpitch + i) = tmp[t++];
+            return;
+        }
+        std::vector<int> out(op.count);
+        for (uint64_t i = 0; i < op.count; ++i) {
+            const int a = *at(r, op.acc, i);
+            if (op.ins.empty()) {
+                out[i] = a;
+                continue;
+            }
+            SymNode nd;
+            nd.acc = a;
+            nd.swap = op.swap;
+            for (const Ref& x : op.ins) nd.ins.push_back(*at(r, x, i));
+            nodes.push_back(nd);
+            out[i] = (int)nodes.size() - 1;
+        }
+        for (uint64_t i = 0; i < op.count; ++i) *at(r, op.dst, i) = out[i];
+    }
+    bool run() {
+        const int n = (int)P.size();
+        for (int r = 0; r < n; ++r)
+            for (const LocalOp& op : P[r].pre) local(r, op);
+        const size_t ns = P[0].steps.size();
+        for (size_t si = 0; si < ns; ++si) {
+            std::vector<std::vector<char>> used(n);
+            for (int r = 0; r < n; ++r) used[r].assign(P[r].steps[si].sends.size(), 0);
+            std::vector<std::tuple<int, Ref, std::vector<int>>> land;
+            for (int r = 0; r < n; ++r)
+                for (const Xfer& rv : P[r].steps[si].recvs) {
+                    const auto& qs = P[rv.peer].steps[si].sends;
+                    size_t j = 0;
+                    while (j < qs.size() && (used[rv.peer][j] || qs[j].peer != r)) ++j;
+                    if (j == qs.size() || qs[j].count != rv.count) return false;
+                    used[rv.peer][j] = 1;
+                    std::vector<int> data(rv.count);
+                    for (uint64_t i = 0; i < rv.count; ++i) data[i] = *at(rv.peer, qs[j].ref, i);
+                    land.emplace_back(r, rv.ref, std::move(data));
+                }
+            for (auto& [r, ref, data] : land)
+                for (uint64_t i = 0; i < data.size(); ++i) *at(r, ref, i) = data[i];
+            for (int r = 0; r < n; ++r)
+                for (const LocalOp& op : P[r].steps[si].post) local(r, op);
+        }
+        return true;
+    }
+};
+
+// Evaluation program of one expression: internal nodes in dependency order.  Operand codes:
+// >= 0 leaf rank, < 0 temp ~t (result of program entry t).
+struct EvalOp {
+    int acc;
+    std::vector<int> ins;
+    bool swap;
+};
+
+bool eval_program(const std::vector<SymNode>& nodes, int root, int n, std::vector<EvalOp>* prog) {
+    std::vector<int> memo(nodes.size(), INT32_MIN);
+    std::vector<char> seen_leaf(n, 0);
+    bool ok = true;
+    std::function<int(int)> visit = [&](int id) -> int {
+        if (id < 0 || (size_t)id >= nodes.size()) {
+            ok = false;
+            return 0;
+        }
+        if (memo[id] != INT32_MIN) return memo[id];
+        const SymNode& nd = nodes[id];
+        if (nd.leaf >= 0) {
+            if (seen_leaf[nd.leaf]++) ok = false;  // every input exactly once
+            return memo[id] = nd.leaf;
+        }
+        EvalOp e;
+        e.acc = visit(nd.acc);
+        for (int c : nd.ins) e.ins.push_back(visit(c));
+        e.swap = nd.swap;
+        prog->push_back(e);
+        return memo[id] = ~(int)(prog->size() - 1);
+    };
+    const int top = visit(root);
+    for (int r = 0; r < n; ++r) ok = ok && seen_leaf[r] == 1;
+    return ok && top < 0;
+}
+
+}  // namespace
+
+Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, int slices) {
+    Plan p;
+    p.mode = mode;
+    p.rank = me;
+    p.g = g;
+    p.sched = SCHED_FLAT;
+    // 1. the reference-order plans of every rank at recvcount = 1, executed symbolically
+    const uint64_t cnt1 = mode == MODE_ALLREDUCE ? (uint64_t)n : 1;
+    std::vector<Plan> ref;
+    for (int r = 0; r < n; ++r) ref.push_back(build_plan(mode, n, r, k, b, cnt1, 1, SCHED_REFERENCE));
+    if (ref[0].error) {
+        p.error = ref[0].error;
+        return p;
+    }
+    SymExec X(ref);
+    if (!X.run()) {
+        p.error = 8;
+        return p;
+    }
+    const uint64_t irc1 = (uint64_t)b;  // IRC at recvcount 1
+    std::vector<std::vector<EvalOp>> progs;
+    if (mode == MODE_ALLREDUCE) {
+        for (int N = 0; N < g.nnodes; ++N) {
+            std::vector<EvalOp> pr;
+            for (int r = 0; r < n; ++r) {  // every rank holds the same expression for chunk N
+                std::vector<EvalOp> q;
+                if (!eval_program(X.nodes, X.buf[r][BUF_RECV][(uint64_t)N * irc1], n, &q)) {
+                    p.error = 8;
+                    return p;
+                }
+                if (r == 0) pr = q;
+            }
+            progs.push_back(pr);
+        }
+    } else {
+        std::vector<EvalOp> pr;
+        if (!eval_program(X.nodes, X.buf[me][BUF_RECV][0], n, &pr)) {
+            p.error = 8;
+            return p;
+        }
+        progs.push_back(pr);
+    }
+    size_t temps = 1;
+    for (const auto& pr : progs) temps = std::max(temps, pr.size());
+
+    // 2. slices and pieces
+    const uint64_t span = mode == MODE_ALLREDUCE ? g.irc : g.recvcount;  // sliced range
+    const uint64_t G = 256;
+    int P = slices;
+    if ((uint64_t)P > span / G) P = (int)std::max<uint64_t>(1, span / G);
+    p.slices = P;
+    p.send_elems = g.total;
+    p.recv_elems = mode == MODE_ALLREDUCE ? g.total : g.recvcount;
+    p.acc_elems = 0;
+    const int nchunks = mode == MODE_ALLREDUCE ? g.nnodes : 1;
+    const uint64_t slots = (uint64_t)(n - 1 + (int)temps) * (uint64_t)nchunks;
+    struct Sl {
+        uint64_t lo, len, stage, stride;
+    };
+    std::vector<Sl> sl(P);
+    uint64_t stage = 0;
+    for (int s2 = 0; s2 < P; ++s2) {
+        const uint64_t lo = s2 == 0 ? 0 : (span * s2 / P) / G * G;
+        const uint64_t hi = s2 == P - 1 ? span : (span * (s2 + 1) / P) / G * G;
+        const uint64_t len = hi - lo;
+        // slots: 64-element multiples, +64 for the per-chunk phase shift below
+        const uint64_t stride = ((mode == MODE_ALLREDUCE ? len / (uint64_t)n + 64 : len) + 127) / 64 * 64;
+        sl[s2] = {lo, len, stage, stride};
+        stage += slots * stride;
+    }
+    p.stage_elems = stage;
+    // piece q of a slice (allreduce): 64-element aligned cut into n
+    auto cut = [&](const Sl& c, uint64_t i) { return i >= (uint64_t)n ? c.len : (c.len * i / (uint64_t)n) / 64 * 64; };
+    auto piece = [&](const Sl& c, int q, uint64_t* a, uint64_t* l) {
+        *a = cut(c, (uint64_t)q);
+        *l = cut(c, (uint64_t)q + 1) - *a;
+    };
+    // position of my operand data for chunk N / my block, in the slice
+    auto own = [&](const Sl& c, int N, uint64_t a) -> Ref {  // my input, in place
+        if (mode == MODE_ALLREDUCE) return {BUF_SEND, (uint64_t)N * g.irc + c.lo + a};
+        return {BUF_SEND, (uint64_t)me * g.recvcount + c.lo};
+    };
+    // every operand of one evaluation congruent mod 64 elements with the in-place data, so the
+    // fused kernel takes its 16-B vector path whatever irc is
+    auto phase = [&](int N) -> uint64_t {
+        return mode == MODE_ALLREDUCE ? ((uint64_t)N * g.irc) % 64 : ((uint64_t)me * g.recvcount) % 64;
+    };
+    auto leaf_slot = [&](const Sl& c, int r, int N, uint64_t a) -> Ref {
+        const uint64_t idx = (uint64_t)(r < me ? r : r - 1) * (uint64_t)nchunks + (uint64_t)N;
+        (void)a;
+        return {BUF_STAGE, c.stage + idx * c.stride + phase(N)};
+    };
+    auto temp_slot = [&](const Sl& c, int t, int N) -> Ref {
+        const uint64_t idx = (uint64_t)(n - 1 + t) * (uint64_t)nchunks + (uint64_t)N;
+        return {BUF_STAGE, c.stage + idx * c.stride + phase(N)};
+    };
+
+    enum { F_GATHER, F_EVAL, F_DIST };
+    auto emit = [&](int kind, const Sl& c, Step& st) {
+        uint64_t a = 0, len = c.len;
+        if (mode == MODE_ALLREDUCE) piece(c, me, &a, &len);
+        if (kind == F_GATHER) {
+            for (int q = 0; q < n; ++q) {
+                if (q == me) continue;
+                if (mode == MODE_ALLREDUCE) {
+                    uint64_t qa, ql;
+                    piece(c, q, &qa, &ql);
+                    for (int N = 0; N < nchunks && ql; ++N)
+                        st.sends.push_back({q, {BUF_SEND, (uint64_t)N * g.irc + c.lo + qa}, ql});
+                } else if (c.len) {
+                    st.sends.push_back({q, {BUF_SEND, (uint64_t)q * g.recvcount + c.lo}, c.len});
+                }
+                for (int N = 0; N < nchunks && len; ++N) st.recvs.push_back({q, leaf_slot(c, q, N, a), len});
+            }
+            if (!len) return;
+            for (int N = 0; N < nchunks; ++N) {
+                const auto& pr = progs[mode == MODE_ALLREDUCE ? N : 0];
+                auto opnd = [&](int code) -> Ref {
+                    if (code >= 0) return code == me ? own(c, N, a) : leaf_slot(c, code, N, a);
+                    return temp_slot(c, ~code, N);
+                };
+                for (size_t t = 0; t < pr.size(); ++t) {
+                    const bool last = t + 1 == pr.size();
+                    Ref dst = last ? (mode == MODE_ALLREDUCE ? Ref{BUF_RECV, (uint64_t)N * g.irc + c.lo + a}
+                                                             : Ref{BUF_RECV, c.lo})
+                                   : temp_slot(c, (int)t, N);
+                    std::vector<Ref> ins;
+                    for (int x : pr[t].ins) ins.push_back(opnd(x));
+                    LocalOp op = make_reduce(dst, opnd(pr[t].acc), ins, len, 0);
+                    op.swap = pr[t].swap;
+                    st.post.push_back(op);
+                }
+            }
+        } else if (kind == F_DIST) {
+            for (int q = 0; q < n; ++q) {
+                if (q == me) continue;
+                uint64_t qa, ql;
+                piece(c, q, &qa, &ql);
+                for (int N = 0; N < nchunks; ++N) {
+                    const uint64_t base = (uint64_t)N * g.irc + c.lo;
+                    if (len) st.sends.push_back({q, {BUF_RECV, base + a}, len});
+                    if (ql) st.recvs.push_back({q, {BUF_RECV, base + qa}, ql});
+                }
+            }
+        }
+    };
+    std::vector<int> L{F_GATHER};
+    if (mode == MODE_ALLREDUCE) L.push_back(F_DIST);
+    const int S = (int)L.size();
+    p.steps.resize((size_t)(P + S - 1));
+    for (int t = 0; t < P + S - 1; ++t) {
+        Step& st = p.steps[t];
+        st.label = "t" + std::to_string(t);
+        for (int s2 = 0; s2 < P; ++s2) {
+            const int ls = t - s2;
+            if (ls < 0 || ls >= S) continue;
+            st.label += std::string(L[ls] == F_GATHER ? ",gather" : ",fdist") + "/s" + std::to_string(s2);
+            emit(L[ls], sl[s2], st);
         }
     }
     return p;

@@ -81,6 +81,7 @@ struct Plan {
     int error = 0;  // chr_result
     int slices = 1;  // pipeline depth actually used
     bool balanced = false;  // allreduce evaluated piecewise on every rank (see build_plan)
+    int sched = 0;          // Sched actually used
     Mode mode = MODE_ALLREDUCE;
     int rank = 0;
     Geometry g;
@@ -105,10 +106,14 @@ void recexch_count_offset(int nranks, int max_phases, int k, std::vector<int>* c
 // depth: every chunk is cut into that many element slices; slice s runs logical step
 // t-s in super-step t, so consecutive phases of different slices share an RCCL group.
 // The per-element reduction order is unchanged (results are bit-identical for any depth).
-// balance: evaluate single-phase allreduce geometries piecewise on every rank (same
-// expressions, same bits; see schedule.cpp S_BPHASE/S_BLANE/S_BDIST).
+// Where the reference's reductions are evaluated (the result bits never depend on it):
+//   SCHED_REFERENCE  at the reference's owner lanes / root nodes (its communication pattern)
+//   SCHED_BALANCED   single-phase geometries: every rank evaluates 1/n (schedule.cpp S_B*, S_R*)
+//   SCHED_FLAT       any geometry: expression trees extracted symbolically, leaves gathered
+//                    over the full mesh, evaluated at the piece's rank (build_plan_flat)
+enum Sched : int { SCHED_REFERENCE = 0, SCHED_BALANCED = 1, SCHED_FLAT = 2 };
 Plan build_plan(Mode mode, int nranks, int rank, int k, int b, uint64_t count, int slices = 1,
-                bool balance = true);
+                int sched = SCHED_FLAT);
 int auto_slices(uint64_t irc_bytes);
 // MPICH baseline allreduces (count = elements per rank; aux = recexch single_phase_recv).
 Plan build_plan_mpich(Mode mode, int nranks, int rank, int k, int aux, uint64_t count);

@@ -90,13 +90,20 @@ int chr_comm_stream(const chr_comm* comm, hipStream_t* stream);
  * busy at once).  0 = automatic (~64 MiB per slice message, up to 8; env CHR_SLICES).
  * Results are bit-identical for every depth. */
 int chr_comm_set_slices(chr_comm* comm, int slices);
-/* Balanced evaluation (default on; env CHR_BALANCE=0 turns the default off).  For allreduce
- * geometries whose intra-group phase is one recexch phase (k == b after clamping) or none
- * (b == 1), every rank evaluates 1/n of every chunk's reduction -- the same expression, in
- * the same operand order, as the reference's single owner lane / root node -- instead of
- * only the nnodes owner lanes doing all of it.  Same bytes per rank, same result bits; the
- * busiest xGMI link carries less.  Other geometries are unaffected. */
-int chr_comm_set_balance(chr_comm* comm, int enable);
+/* Where the radix/batch reductions are evaluated.  The result bits never depend on it: every
+ * element gets the reference's expression (recexch phases in neighbour order, folds, lane
+ * reduction in stage order) whatever the schedule.
+ *   CHR_SCHEDULE_REFERENCE  the reference's communication: owner lanes / root nodes reduce
+ *   CHR_SCHEDULE_BALANCED   single-phase geometries (k == b, or b == 1): each rank evaluates
+ *                           1/n of every chunk, hierarchical exchanges
+ *   CHR_SCHEDULE_FLAT       (default) any geometry: each rank gathers the n-1 other inputs of
+ *                           its piece directly over the xGMI mesh, evaluates the expression
+ *                           tree, then the pieces are allgathered; 2S/n per link in all
+ * Env CHR_SCHEDULE=reference|balanced|flat sets the default.  DESIGN.md §5. */
+#define CHR_SCHEDULE_REFERENCE 0
+#define CHR_SCHEDULE_BALANCED 1
+#define CHR_SCHEDULE_FLAT 2
+int chr_comm_set_schedule(chr_comm* comm, int schedule);
 /* Opt-in timing of the fused bucket-reduction launches of this communicator (HIP events
  * on its stream).  _read synchronises on the recorded launches and returns the summed
  * kernel milliseconds, the algorithmic bytes ((m+2)*n*sizeof(T) per launch) and the
@@ -147,7 +154,7 @@ int chr_local_group_create(chr_local_group** group, int nranks, int device);
 int chr_local_group_destroy(chr_local_group* group);
 int chr_local_group_stream(const chr_local_group* group, hipStream_t* stream);
 int chr_local_group_set_slices(chr_local_group* group, int slices);
-int chr_local_group_set_balance(chr_local_group* group, int enable);
+int chr_local_group_set_schedule(chr_local_group* group, int schedule);
 int chr_local_allreduce_radix_batch(chr_local_group* group, const void* const* sends,
                                     void* const* recvs, size_t count, chr_dtype dtype, chr_op op,
                                     int k, int b);
@@ -176,9 +183,9 @@ typedef enum {
 } chr_mode;
 long chr_plan_describe(chr_mode mode, int nranks, int rank, int k, int b, size_t count,
                        int slices, char* buf, size_t len);
-/* The same with the balanced-evaluation switch (chr_plan_describe uses balance = 1). */
+/* The same for a given CHR_SCHEDULE_* (chr_plan_describe describes CHR_SCHEDULE_FLAT). */
 long chr_plan_describe_ex(chr_mode mode, int nranks, int rank, int k, int b, size_t count,
-                          int slices, int balance, char* buf, size_t len);
+                          int slices, int schedule, char* buf, size_t len);
 
 /* ---- MPICH baseline allreduces (the ones testing/main.cpp benchmarks CHiArA against) --
  * Replace  int MPICH_Allreduce_ring(const char* sendbuf, char* recvbuf, int count,

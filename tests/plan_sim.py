@@ -11,8 +11,8 @@ import chiara_amd as ca
 import pyoracle as po
 
 
-def load_plans(mode, n, k, b, count, slices=1, balance=True):
-    return [ca.parse_plan(ca.describe_plan(mode, n, r, k, b, count, slices, balance)) for r in range(n)]
+def load_plans(mode, n, k, b, count, slices=1, schedule=None):
+    return [ca.parse_plan(ca.describe_plan(mode, n, r, k, b, count, slices, schedule)) for r in range(n)]
 
 
 class RankState:
@@ -94,10 +94,10 @@ def execute(plans, sends, dtype, rop, inplace=False):
     return [st.buf["RECV"] for st in states]
 
 
-def simulate(mode, sends, k, b, dtype, op, inplace=False, slices=1, balance=True):
+def simulate(mode, sends, k, b, dtype, op, inplace=False, slices=1, schedule=None):
     n = len(sends)
     count = sends[0].size // n if mode == ca.MODE_REDUCE_SCATTER else sends[0].size
-    plans = load_plans(mode, n, k, b, count, slices, balance)
+    plans = load_plans(mode, n, k, b, count, slices, schedule)
     if plans[0]["header"]["error"]:
         raise ValueError(f"plan error {plans[0]['header']['error']}")
     outs = execute(plans, sends, dtype, op, inplace)

@@ -246,26 +246,26 @@ def test_allgather_large_bit_exact(gu, groups, n, k, b, inplace):
 
 @pytest.mark.parametrize("n,k,b,dtype", [(8, 4, 4, "f32"), (8, 4, 4, "bf16"), (8, 8, 8, "f32"), (8, 2, 1, "f32"),
                                          (4, 4, 4, "f32"), (2, 2, 2, "f32")])
-def test_balanced_equals_owner_lane_evaluation(gu, groups, n, k, b, dtype):
-    """Balanced evaluation vs the reference's owner-lane evaluation, 8 MiB per rank, pipelined:
-    identical bits (and both equal the oracle)."""
+def test_schedules_bit_identical(gu, groups, n, k, b, dtype):
+    """Flat, balanced and reference-communication schedules, 8 MiB per rank, pipelined:
+    identical bits, all equal to the oracle."""
     count = (1 << 21) // (2 if dtype == "bf16" else 1) * 2
     count -= count % n
     sends = [po.fill(count, dtype, po.PAT_UNIFORM, 5, r) for r in range(n)]
     g = groups(n)
     outs = {}
     try:
-        for bal in (True, False):
-            g.set_balance(bal)
+        for sch in (ca.SCHEDULE_FLAT, ca.SCHEDULE_BALANCED, ca.SCHEDULE_REFERENCE):
+            g.set_schedule(sch)
             g.set_slices(3)
-            outs[bal] = run_local(gu, g, "ar", sends, k, b, dtype, "sum")
+            outs[sch] = run_local(gu, g, "ar", sends, k, b, dtype, "sum")
     finally:
-        g.set_balance(True)
+        g.set_schedule(ca.SCHEDULE_FLAT)
         g.set_slices(0)
     want = po.allreduce_radix_batch(sends, k, b, dtype, "sum")
     for r in range(n):
-        np.testing.assert_array_equal(outs[True][r].view(np.uint8), want[r].view(np.uint8))
-        np.testing.assert_array_equal(outs[False][r].view(np.uint8), want[r].view(np.uint8))
+        for sch in outs:
+            np.testing.assert_array_equal(outs[sch][r].view(np.uint8), want[r].view(np.uint8))
 
 
 @pytest.mark.parametrize("n,k,b", [(2, 2, 2), (2, 2, 1), (8, 4, 4), (8, 8, 8)])
@@ -277,10 +277,10 @@ def test_balanced_reduce_scatter_equals_owner_lane(gu, groups, n, k, b):
     want = po.reduce_scatter_radix_batch(sends, k, b, "f32", "sum")
     g = groups(n)
     try:
-        for bal in (True, False):
-            g.set_balance(bal)
+        for sch in (ca.SCHEDULE_FLAT, ca.SCHEDULE_BALANCED, ca.SCHEDULE_REFERENCE):
+            g.set_schedule(sch)
             got = run_local(gu, g, "rs", sends, k, b, "f32", "sum")
             for r in range(n):
                 np.testing.assert_array_equal(got[r].view(np.uint32), want[r].view(np.uint32))
     finally:
-        g.set_balance(True)
+        g.set_schedule(ca.SCHEDULE_FLAT)

@@ -60,7 +60,7 @@ def test_plan_shape_c4():
     one fused 3-input reduction per active lane, 1-input lane reduction at the roots,
     then the link-balanced distribute (scatter 1/7 pieces, forward).  Owner-lane evaluation
     (balance off)."""
-    p = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 1 << 20, balance=False))
+    p = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 1 << 20, schedule=ca.SCHEDULE_REFERENCE))
     assert p["header"]["k"] == 4 and p["header"]["steps"] == 4 and p["header"]["slices"] == 1
     ph = p["steps"][0]
     assert len(ph["recvs"]) == 3 and len(ph["sends"]) == 1
@@ -76,7 +76,7 @@ def test_plan_shape_c4():
 def test_plan_shape_c4_balanced():
     """Balanced C4: 3 steps; every rank exchanges with its 3 group peers (2 chunks each),
     reduces 2 chunks x 3 inputs, then 1 piece per chunk with the other node, then allgathers."""
-    p = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 5, 4, 4, 1 << 20))
+    p = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 5, 4, 4, 1 << 20, schedule=ca.SCHEDULE_BALANCED))
     assert p["header"]["balanced"] == 1 and p["header"]["steps"] == 3
     ph, lane, dist = p["steps"]
     assert len(ph["sends"]) == 6 and len(ph["recvs"]) == 6
@@ -106,11 +106,11 @@ def test_pipelined_plans_bit_exact(mode, n, k, b, slices):
 
 
 def test_pipelined_plan_structure():
-    p = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 8 * 4 * 4096, 4, balance=False))
+    p = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 8 * 4 * 4096, 4, schedule=ca.SCHEDULE_REFERENCE))
     assert p["header"]["slices"] == 4 and p["header"]["steps"] == 4 + 4 - 1
     # super-step 1 holds slice 0's lane reduce and slice 1's recexch phase in ONE group
     assert "lane/s0" in p["steps"][1]["label"] and "phase0/s1" in p["steps"][1]["label"]
-    q = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 8 * 4 * 4096, 4))
+    q = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 8 * 4 * 4096, 4, schedule=ca.SCHEDULE_BALANCED))
     assert q["header"]["steps"] == 3 + 4 - 1
     assert "blane/s0" in q["steps"][1]["label"] and "bphase/s1" in q["steps"][1]["label"]
 
@@ -148,7 +148,7 @@ def test_balanced_plans_bit_exact(n, k, b, slices):
     for dt, op, pat in (("f32", "sum", po.PAT_UNIFORM), ("bf16", "sum", po.PAT_UNIFORM), ("f32", "max", po.PAT_TIES)):
         sends = [po.fill(count, dt, pat, 17, r) for r in range(n)]
         want = po.allreduce_radix_batch(sends, k, b, dt, op)
-        plans = plan_sim.load_plans(ca.MODE_ALLREDUCE, n, k, b, count, slices, balance=True)
+        plans = plan_sim.load_plans(ca.MODE_ALLREDUCE, n, k, b, count, slices, schedule=ca.SCHEDULE_BALANCED)
         assert plans[0]["header"]["balanced"] == 1
         got = plan_sim.execute(plans, sends, dt, op)
         for r in range(n):
@@ -156,11 +156,13 @@ def test_balanced_plans_bit_exact(n, k, b, slices):
 
 
 def test_balance_only_where_single_phase():
-    hdr = lambda n, k, b: plan_sim.load_plans(ca.MODE_ALLREDUCE, n, k, b, n * 256)[0]["header"]["balanced"]
+    hdr = lambda n, k, b: plan_sim.load_plans(ca.MODE_ALLREDUCE, n, k, b, n * 256,
+                                              schedule=ca.SCHEDULE_BALANCED)[0]["header"]["balanced"]
     assert hdr(8, 4, 4) == 1 and hdr(8, 8, 8) == 1 and hdr(8, 2, 1) == 1
     assert hdr(8, 2, 4) == 0 and hdr(8, 3, 4) == 0 and hdr(8, 4, 8) == 0  # multi-phase / fold
-    assert plan_sim.load_plans(ca.MODE_REDUCE_SCATTER, 8, 4, 4, 256)[0]["header"]["balanced"] == 1
-    assert plan_sim.load_plans(ca.MODE_REDUCE_SCATTER, 8, 2, 4, 256)[0]["header"]["balanced"] == 0
+    rs = lambda k, b: plan_sim.load_plans(ca.MODE_REDUCE_SCATTER, 8, k, b, 256,
+                                          schedule=ca.SCHEDULE_BALANCED)[0]["header"]["balanced"]
+    assert rs(4, 4) == 1 and rs(2, 4) == 0
 
 
 def _link_bytes(plans):
@@ -177,8 +179,8 @@ def test_balanced_traffic_c4():
     allreduce minimum 2(n-1)/n of the buffer, and the busiest directed link carrying S/4 + S/8
     instead of ~0.64 S."""
     n, count = 8, 8 * 4096
-    bal = _link_bytes(plan_sim.load_plans(ca.MODE_ALLREDUCE, n, 4, 4, count, balance=True))
-    ref = _link_bytes(plan_sim.load_plans(ca.MODE_ALLREDUCE, n, 4, 4, count, balance=False))
+    bal = _link_bytes(plan_sim.load_plans(ca.MODE_ALLREDUCE, n, 4, 4, count, schedule=ca.SCHEDULE_BALANCED))
+    ref = _link_bytes(plan_sim.load_plans(ca.MODE_ALLREDUCE, n, 4, 4, count, schedule=ca.SCHEDULE_REFERENCE))
     per_rank = lambda d, r: sum(v for (a, _), v in d.items() if a == r)
     assert sum(bal.values()) == sum(ref.values())
     for r in range(n):  # balanced: every rank sends exactly the allreduce minimum
@@ -197,7 +199,8 @@ def test_balanced_reduce_scatter_bit_exact(n, k, b, slices):
     for dt, op, pat in (("f32", "sum", po.PAT_UNIFORM), ("bf16", "sum", po.PAT_UNIFORM), ("f32", "max", po.PAT_TIES)):
         sends = [po.fill(rc * n, dt, pat, 9, r) for r in range(n)]
         want = po.reduce_scatter_radix_batch(sends, k, b, dt, op)
-        got = plan_sim.simulate(ca.MODE_REDUCE_SCATTER, sends, k, b, dt, op, slices=slices)
+        got = plan_sim.simulate(ca.MODE_REDUCE_SCATTER, sends, k, b, dt, op, slices=slices,
+                                schedule=ca.SCHEDULE_BALANCED)
         for r in range(n):
             np.testing.assert_array_equal(got[r].view(np.uint8), want[r].view(np.uint8))
 
@@ -206,7 +209,45 @@ def test_balanced_reduce_scatter_traffic_c3():
     """C3 (n=2, k=2, b=2): each rank sends exactly the reduce-scatter minimum (n-1)/n of its
     send buffer; the reference's lane 0 receives the whole buffer and scatters half back."""
     n, rc = 2, 4096
-    bal = _link_bytes(plan_sim.load_plans(ca.MODE_REDUCE_SCATTER, n, 2, 2, rc, balance=True))
-    ref = _link_bytes(plan_sim.load_plans(ca.MODE_REDUCE_SCATTER, n, 2, 2, rc, balance=False))
+    bal = _link_bytes(plan_sim.load_plans(ca.MODE_REDUCE_SCATTER, n, 2, 2, rc, schedule=ca.SCHEDULE_BALANCED))
+    ref = _link_bytes(plan_sim.load_plans(ca.MODE_REDUCE_SCATTER, n, 2, 2, rc, schedule=ca.SCHEDULE_REFERENCE))
     assert bal == {(0, 1): rc, (1, 0): rc}
     assert max(ref.values()) == 2 * rc and sum(ref.values()) == 3 * rc
+
+
+@pytest.mark.parametrize("n,k,b", [(8, 4, 4), (8, 2, 4), (8, 3, 4), (8, 2, 2), (8, 4, 8), (8, 8, 8), (6, 5, 3),
+                                   (12, 3, 6), (16, 4, 4), (2, 2, 1)])
+def test_flat_traffic_is_full_mesh_optimal(n, k, b):
+    """Flat schedule, any geometry (multi-phase, fold, clamped k): every directed pair carries
+    2S/n (allreduce) or S/n (reduce-scatter) up to 64-element piece alignment, and the plan is
+    two / one steps deep."""
+    count = n * 64 * 64
+    ar = plan_sim.load_plans(ca.MODE_ALLREDUCE, n, k, b, count, schedule=ca.SCHEDULE_FLAT)
+    assert ar[0]["header"]["schedule"] == ca.SCHEDULE_FLAT and ar[0]["header"]["steps"] == 2
+    pair = _link_bytes(ar)
+    assert len(pair) == n * (n - 1)
+    assert max(pair.values()) - min(pair.values()) <= 2 * 64 * (n // b + 1)
+    assert sum(pair.values()) == 2 * (n - 1) * count
+    rc = 64 * 64
+    rs = plan_sim.load_plans(ca.MODE_REDUCE_SCATTER, n, k, b, rc, schedule=ca.SCHEDULE_FLAT)
+    assert set(_link_bytes(rs).values()) == {rc}
+
+
+@pytest.mark.parametrize("n,k,b", [(8, 2, 4), (8, 3, 4), (12, 3, 6), (9, 2, 3), (16, 4, 8), (6, 5, 3)])
+def test_flat_multi_phase_and_fold_bit_exact(n, k, b):
+    """Expression trees with several recexch phases and step-1 folds, evaluated by the flat
+    schedule (pipelined, in place and not): the reference's bits."""
+    count = n * 640
+    for dt, op, pat in (("f32", "sum", po.PAT_UNIFORM), ("f32", "min", po.PAT_TIES), ("bf16", "sum", po.PAT_UNIFORM)):
+        sends = [po.fill(count, dt, pat, 23, r) for r in range(n)]
+        want = po.allreduce_radix_batch(sends, k, b, dt, op)
+        for inplace in (False, True):
+            got = plan_sim.simulate(ca.MODE_ALLREDUCE, sends, k, b, dt, op, inplace=inplace, slices=2,
+                                    schedule=ca.SCHEDULE_FLAT)
+            for r in range(n):
+                np.testing.assert_array_equal(got[r].view(np.uint8), want[r].view(np.uint8))
+        rsends = [po.fill(count, dt, pat, 24, r) for r in range(n)]
+        rwant = po.reduce_scatter_radix_batch(rsends, k, b, dt, op)
+        rgot = plan_sim.simulate(ca.MODE_REDUCE_SCATTER, rsends, k, b, dt, op, slices=2, schedule=ca.SCHEDULE_FLAT)
+        for r in range(n):
+            np.testing.assert_array_equal(rgot[r].view(np.uint8), rwant[r].view(np.uint8))
