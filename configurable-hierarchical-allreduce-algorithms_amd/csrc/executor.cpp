@@ -386,7 +386,7 @@ int chr_comm_init_rank(chr_comm** out, int nranks, const chr_unique_id* id, int 
     c->nranks = nranks;
     c->device = device;
     hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamDefault);
     if (e != hipSuccess) return hip_code(e);
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof(u));
@@ -508,7 +508,7 @@ int chr_local_group_create(chr_local_group** out, int nranks, int device) {
     g->acc.resize(nranks);
     g->stage.resize(nranks);
     hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&g->stream, hipStreamDefault);
     if (e != hipSuccess) return hip_code(e);
     *out = g.release();
     return CHR_SUCCESS;

@@ -17,11 +17,17 @@ static void run_k_b(const Options& o, Ctx& c, std::ofstream& csv, int k, int cou
     MPI_Allgather(send.data(), count * (int)es, MPI_BYTE, ref.data(), count * (int)es, MPI_BYTE, MPI_COMM_WORLD);
     const bool dev = o.mem == "device";
     DevBuf dsend(dev ? count * es : 0), drecv(dev ? out_n * es : 0);
-    if (dev) (void)hipMemcpy(dsend.p, send.data(), count * es, hipMemcpyHostToDevice);
+    if (dev) {
+        (void)hipMemcpy(dsend.p, send.data(), count * es, hipMemcpyHostToDevice);
+        (void)hipDeviceSynchronize();
+    }
     const int reps = o.reps > 0 ? o.reps : 50;
     for (int rep = 0; rep < reps; ++rep) {
         std::fill(recv.begin(), recv.end(), 0);
-        if (dev) (void)hipMemset(drecv.p, 0, out_n * es);
+        if (dev) {
+            (void)hipMemset(drecv.p, 0, out_n * es);
+            (void)hipDeviceSynchronize();  // NULL-stream memset vs the comm's non-blocking stream
+        }
         MPI_Barrier(MPI_COMM_WORLD);
         const double t0 = MPI_Wtime();
         const int err = chr_allgather_radix_batch(dev ? dsend.p : send.data(), (size_t)count, dt,

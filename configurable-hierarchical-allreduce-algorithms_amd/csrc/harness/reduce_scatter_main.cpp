@@ -19,11 +19,17 @@ static void run_r_b(const Options& o, Ctx& c, std::ofstream& csv, const char* na
                              dt == CHR_BFLOAT16 ? c.bf16_sum : MPI_SUM, MPI_COMM_WORLD);
     const bool dev = o.mem == "device";
     DevBuf dsend(dev ? in_n * es : 0), drecv(dev ? count * es : 0);
-    if (dev) (void)hipMemcpy(dsend.p, send.data(), in_n * es, hipMemcpyHostToDevice);
+    if (dev) {
+        (void)hipMemcpy(dsend.p, send.data(), in_n * es, hipMemcpyHostToDevice);
+        (void)hipDeviceSynchronize();
+    }
     const int reps = o.reps > 0 ? o.reps : 20;
     for (int rep = 0; rep < reps; ++rep) {
         std::fill(recv.begin(), recv.end(), 0);
-        if (dev) (void)hipMemset(drecv.p, 0, count * es);
+        if (dev) {
+            (void)hipMemset(drecv.p, 0, count * es);
+            (void)hipDeviceSynchronize();  // NULL-stream memset vs the comm's non-blocking stream
+        }
         MPI_Barrier(MPI_COMM_WORLD);
         const double t0 = MPI_Wtime();
         const int err = chr_reduce_scatter_radix_batch(dev ? dsend.p : send.data(), dev ? drecv.p : recv.data(),

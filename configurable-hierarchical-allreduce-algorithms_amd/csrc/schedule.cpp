@@ -449,8 +449,60 @@ int auto_slices(uint64_t irc_bytes) {
 }
 
 Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, int slices);
+static Plan build_plan_impl(Mode mode, int n, int me, int k_in, int b, uint64_t count, int slices, int sched);
+
+// The fused kernel takes at most kPlanFanIn inputs per pass (kMaxFanIn, reduce_kernels.hip)
+// and chains longer folds through `dst`.  A later input that aliases `dst` -- the own leaf
+// read in place from SEND (== RECV under MPI_IN_PLACE), or recvbuf itself in MPICH's
+// running-value chains -- would then be read after it was overwritten.  Such reductions are
+// split: the leading inputs fold into a STAGE scratch region, the last <= kPlanFanIn inputs
+// are folded from there into `dst` in one pass.  Same association, same bits.
+static constexpr int kPlanFanIn = 8;
+
+static bool may_alias(const Ref& a, uint64_t na, const Ref& b, uint64_t nb) {
+    const bool io = (a.buf == BUF_SEND && b.buf == BUF_RECV) || (a.buf == BUF_RECV && b.buf == BUF_SEND);
+    if (io) return true;  // in place: SEND is RECV (offsets differ for allgather / reduce-scatter)
+    return a.buf == b.buf && a.off < b.off + nb && b.off < a.off + na;
+}
+
+static void split_wide_reductions(Plan& p) {
+    const uint64_t scratch = p.stage_elems;
+    uint64_t need = 0;
+    auto fix = [&](std::vector<LocalOp>& ops) {
+        std::vector<LocalOp> out;
+        for (LocalOp& op : ops) {
+            const size_t m = op.ins.size();
+            bool alias = false;
+            if (op.kind == L_REDUCE && m > (size_t)kPlanFanIn)
+                for (size_t j = kPlanFanIn; j < m; ++j) alias = alias || may_alias(op.ins[j], op.count, op.dst, op.count);
+            if (!alias) {
+                out.push_back(std::move(op));
+                continue;
+            }
+            const size_t r = (m - 1) % kPlanFanIn + 1;  // inputs of the final pass
+            LocalOp a = op, z = op;
+            a.dst = {BUF_STAGE, scratch};
+            a.ins.assign(op.ins.begin(), op.ins.end() - (long)r);
+            z.acc = {BUF_STAGE, scratch};
+            z.ins.assign(op.ins.end() - (long)r, op.ins.end());
+            need = std::max(need, op.count);
+            out.push_back(std::move(a));
+            out.push_back(std::move(z));
+        }
+        ops.swap(out);
+    };
+    fix(p.pre);
+    for (Step& st : p.steps) fix(st.post);
+    p.stage_elems += need;
+}
 
 Plan build_plan(Mode mode, int n, int me, int k_in, int b, uint64_t count, int slices, int sched) {
+    Plan p = build_plan_impl(mode, n, me, k_in, b, count, slices, sched);
+    if (!p.error) split_wide_reductions(p);
+    return p;
+}
+
+static Plan build_plan_impl(Mode mode, int n, int me, int k_in, int b, uint64_t count, int slices, int sched) {
     const bool balance = sched == SCHED_BALANCED;
     if (is_mpich(mode)) return build_plan_mpich(mode, n, me, k_in, b, count);
     if (mode == MODE_ALLGATHER) return build_plan_allgather(n, me, k_in, b, count);
@@ -1256,7 +1308,7 @@ Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, 
     // 1. the reference-order plans of every rank at recvcount = 1, executed symbolically
     const uint64_t cnt1 = mode == MODE_ALLREDUCE ? (uint64_t)n : 1;
     std::vector<Plan> ref;
-    for (int r = 0; r < n; ++r) ref.push_back(build_plan(mode, n, r, k, b, cnt1, 1, SCHED_REFERENCE));
+    for (int r = 0; r < n; ++r) ref.push_back(build_plan_impl(mode, n, r, k, b, cnt1, 1, SCHED_REFERENCE));
     if (ref[0].error) {
         p.error = ref[0].error;
         return p;

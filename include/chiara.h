@@ -83,7 +83,10 @@ int chr_comm_init_rank(chr_comm** comm, int nranks, const chr_unique_id* id, int
 int chr_comm_destroy(chr_comm* comm);
 int chr_comm_rank(const chr_comm* comm, int* rank);
 int chr_comm_size(const chr_comm* comm, int* nranks);
-/* The stream all of this communicator's collective work is enqueued on. */
+/* The stream all of this communicator's collective work is enqueued on.  It is a blocking
+ * stream: it orders after work on the legacy NULL stream (hipMemset, default-stream kernels),
+ * as an MPI caller expects.  Work that produces `send` on another non-blocking stream must be
+ * ordered before the call (hipStreamWaitEvent on this stream, or a synchronize). */
 int chr_comm_stream(const chr_comm* comm, hipStream_t* stream);
 /* Pipeline depth of the schedules: every chunk is cut into `slices` element slices and
  * consecutive phases of different slices share one RCCL group (different xGMI links

@@ -43,15 +43,23 @@ def run_local(st, op, dtype, rop):
     if kind == "copy":
         st.view(dst, n)[:] = st.view(acc, n).copy()
         return
-    a = st.view(acc, n).copy()
-    if kind == "reduce_sw":  # running value first: a = MPI_Reduce_local(a -> in, x -> inout)
-        for r in ins:
-            x = st.view(r, n).copy()
-            po.reduce_local(a, x, dtype, rop)
-            a = x
-    else:
-        po.reduce_multi(a, [st.view(r, n).copy() for r in ins], dtype, rop)
-    st.view(dst, n)[:] = a
+    # Model of the device launcher: at most FAN_IN inputs per pass; each pass reads its inputs
+    # and writes dst before the next pass reads (launch_reduce chains through dst).
+    cur = acc
+    for g0 in range(0, max(len(ins), 1), FAN_IN):
+        a = st.view(cur, n).copy()
+        grp = [st.view(r, n).copy() for r in ins[g0:g0 + FAN_IN]]
+        if kind == "reduce_sw":  # running value first: a = MPI_Reduce_local(a -> in, x -> inout)
+            for x in grp:
+                po.reduce_local(a, x, dtype, rop)
+                a = x
+        elif grp:
+            po.reduce_multi(a, grp, dtype, rop)
+        st.view(dst, n)[:] = a
+        cur = dst
+
+
+FAN_IN = 8  # kMaxFanIn in csrc/reduce_kernels.hip
 
 
 def execute(plans, sends, dtype, rop, inplace=False):

@@ -251,3 +251,38 @@ def test_flat_multi_phase_and_fold_bit_exact(n, k, b):
         rgot = plan_sim.simulate(ca.MODE_REDUCE_SCATTER, rsends, k, b, dt, op, slices=2, schedule=ca.SCHEDULE_FLAT)
         for r in range(n):
             np.testing.assert_array_equal(rgot[r].view(np.uint8), rwant[r].view(np.uint8))
+
+
+@pytest.mark.parametrize("schedule", [0, 1, 2])
+@pytest.mark.parametrize("n,k,b", [(12, 2, 1), (16, 3, 1), (16, 16, 16), (12, 12, 12), (10, 2, 1)])
+def test_wide_fan_in_in_place(schedule, n, k, b):
+    """Reductions with more than 8 inputs chain through dst on the device; an input that aliases
+    dst (the own leaf read in place) must be folded before dst is written (plans split such
+    reductions through STAGE scratch; plan_sim models the launcher's chaining)."""
+    count = n * 64
+    for dt, op, pat in (("f32", "sum", po.PAT_UNIFORM), ("f32", "min", po.PAT_TIES)):
+        sends = [po.fill(count, dt, pat, 31, r) for r in range(n)]
+        want = po.allreduce_radix_batch(sends, k, b, dt, op)
+        got = plan_sim.simulate(ca.MODE_ALLREDUCE, sends, k, b, dt, op, inplace=True, schedule=schedule)
+        for r in range(n):
+            np.testing.assert_array_equal(got[r].view(np.uint8), want[r].view(np.uint8))
+        rs = [po.fill(count, dt, pat, 32, r) for r in range(n)]
+        rwant = po.reduce_scatter_radix_batch(rs, k, b, dt, op)
+        rgot = plan_sim.simulate(ca.MODE_REDUCE_SCATTER, rs, k, b, dt, op, inplace=True, schedule=schedule)
+        for r in range(n):
+            np.testing.assert_array_equal(rgot[r].view(np.uint8), rwant[r].view(np.uint8))
+
+
+@pytest.mark.parametrize("algo,n,k", [("rx", 16, 13), ("rx", 12, 12), ("rm", 16, 16), ("rm", 12, 11),
+                                      ("krsag", 16, 12)])
+def test_wide_mpich_chains_in_place(algo, n, k):
+    """MPICH_do_reduce / recursive multiplying fold recvbuf into chains of k-1 > 8 operands."""
+    mode = {"rx": ca.MODE_MPICH_RECEXCH, "rm": ca.MODE_MPICH_RMULT, "krsag": ca.MODE_MPICH_KRSAG}[algo]
+    count = 300
+    for op, pat in (("sum", po.PAT_UNIFORM), ("max", po.PAT_TIES)):
+        sends = [po.fill(count, "f32", pat, 33, r) for r in range(n)]
+        want = po.mpich_allreduce(algo, sends, "f32", op, k=k)
+        for inplace in (False, True):
+            got = plan_sim.simulate(mode, sends, k, 0, "f32", op, inplace=inplace)
+            for r in range(n):
+                np.testing.assert_array_equal(got[r].view(np.uint8), want[r].view(np.uint8))
