@@ -323,6 +323,16 @@ def bench_allreduce(args):
                     "kernel": "chr::k_reduce_vec (fused bucket reductions inside the collective, busiest rank)",
                     "algorithmic_bytes_per_call": float(busiest[1]), "launches_per_call": int(busiest[2]),
                     "kernel_ms_per_call": round(float(busiest[0]), 4)}
+    # bytes on the busiest directed link of this schedule (max over ranks; slicing only splits messages)
+    sched = {"reference": 0, "0": 0, "balanced": 1, "1": 1}.get(os.environ.get("CHR_SCHEDULE", "flat"), 2)
+    plan = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, world, rank, k, b, count, 1, sched))
+    per_peer = {}
+    for st in plan["steps"]:
+        for peer, _, cnt in st["sends"]:
+            per_peer[peer] = per_peer.get(peer, 0) + cnt * es
+    lb = torch.tensor([float(max(per_peer.values()) if per_peer else 0)], dtype=torch.float64)
+    dist.all_reduce(lb, op=dist.ReduceOp.MAX)
+    link_bytes = int(lb.item())
     compare = None if args.no_compare else compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b,
                                                          world, dev)
     if rank == 0:
@@ -338,7 +348,11 @@ def bench_allreduce(args):
             "algbw_GBps": round(algbw, 2), "busbw_GBps": round(busbw, 2),
             "xgmi_roofline": {"per_link_GBps": XGMI_LINK_GBPS, "aggregate_GBps": 7 * XGMI_LINK_GBPS,
                               "busbw_frac_per_link": round(busbw / XGMI_LINK_GBPS, 4),
-                              "busbw_frac_aggregate": round(busbw / (7 * XGMI_LINK_GBPS), 4)},
+                              "busbw_frac_aggregate": round(busbw / (7 * XGMI_LINK_GBPS), 4),
+                              # schedule-aware bound: the compiled plan's busiest directed link
+                              "busiest_link_bytes": link_bytes,
+                              "link_bound_ms": round(link_bytes / (XGMI_LINK_GBPS * 1e9) * 1e3, 4),
+                              "frac": round(link_bytes / (XGMI_LINK_GBPS * 1e9) / (el / args.steps), 4)},
             "roofline": roofline, "cpu_baseline": None,
         }
         if compare:
