@@ -383,7 +383,8 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
     """Context, not the metric: on the same buffers and ranks, (1) RCCL's own ncclAllReduce
     (torch.distributed nccl group), (2) the reference's MPICH ring baseline
     (testing/mpich_implementations/all_reduce/allreduce_ring.cpp) run on libchiara's executor and
-    (3) the metric's arithmetic under the balanced and the reference-route schedules."""
+    (3) the metric's own schedule with the reductions on the transfer stream (no overlap) and
+    (4) its arithmetic under the balanced and the reference-route schedules."""
     steps, warm = max(1, min(args.steps, 20)), 2
     S = count * (4 if dt == ca.FLOAT32 else 2)
     out = {"steps": steps}
@@ -409,6 +410,11 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
     # the same radix/batch arithmetic under the other two schedules (same bits, other routes)
     def radix():
         ca.check(ca.all_reduce_radix_batch(send, recv, count, dt, ca.SUM, comm, k, b, async_op=True))
+    comm.set_overlap(False)
+    try:
+        out["radix_batch_no_overlap"] = entry(_timed_max(torch, dist, radix, steps, warm))
+    finally:
+        comm.set_overlap(True)
     for name, sch in (("radix_batch_balanced", ca.SCHEDULE_BALANCED), ("radix_batch_reference_route",
                                                                       ca.SCHEDULE_REFERENCE)):
         comm.set_schedule(sch)

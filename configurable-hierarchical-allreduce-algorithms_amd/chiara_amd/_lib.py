@@ -70,6 +70,7 @@ def _load():
         "chr_local_allreduce_mpich": ([vp, pp, pp, sz, i, i, i, i, i], i),
         "chr_allgather_radix_batch": ([vp, sz, i, vp, vp, i, i], i),
         "chr_comm_set_schedule": ([vp, i], i),
+        "chr_comm_set_overlap": ([vp, i], i),
         "chr_local_group_set_schedule": ([vp, i], i),
         "chr_plan_describe_ex": ([i, i, i, i, i, sz, i, i, ctypes.c_char_p, sz], ctypes.c_long),
         "chr_allgather_radix_batch_async": ([vp, sz, i, vp, vp, i, i], i),
@@ -100,6 +101,6 @@ EXPORTED = [
     "chr_local_allreduce_radix_batch", "chr_local_reduce_scatter_radix_batch", "chr_plan_describe", "chr_fill",
     "chr_error_string", "chr_abi_version", "chr_reduce_multi_ex", "chr_allreduce_mpich",
     "chr_allreduce_mpich_async", "chr_local_allreduce_mpich", "chr_allgather_radix_batch",
-    "chr_allgather_radix_batch_async", "chr_local_allgather_radix_batch", "chr_comm_set_schedule",
+    "chr_allgather_radix_batch_async", "chr_local_allgather_radix_batch", "chr_comm_set_schedule", "chr_comm_set_overlap",
     "chr_local_group_set_schedule", "chr_plan_describe_ex",
 ]

@@ -135,6 +135,10 @@ class Comm:
         """Pipeline depth (0 = automatic); results are bit-identical for every depth."""
         check(lib().chr_comm_set_slices(self._h, slices))
 
+    def set_overlap(self, enable):
+        """Reductions on a second stream, overlapped with the RCCL transfers (default on)."""
+        check(lib().chr_comm_set_overlap(self._h, int(bool(enable))))
+
     def set_schedule(self, schedule):
         """SCHEDULE_REFERENCE / SCHEDULE_BALANCED / SCHEDULE_FLAT: where reductions are evaluated
         (never what they compute)."""
@@ -324,7 +328,8 @@ def parse_plan(text):
         if tok[0] == "pre":
             plan["pre"].append(local(tok[1:]))
         elif tok[0] == "step":
-            cur = {"label": tok[2], "sends": [], "recvs": [], "post": []}
+            wait = int(tok[3].split("=")[1]) if len(tok) > 3 and tok[3].startswith("wait=") else -1
+            cur = {"label": tok[2], "wait": wait, "sends": [], "recvs": [], "post": []}
             plan["steps"].append(cur)
         elif tok[0] in ("send", "recv"):
             cur[tok[0] + "s"].append((int(tok[1]), (tok[2], int(tok[3])), int(tok[4])))

@@ -161,6 +161,15 @@ bool is_device_ptr(const void* p) {
 using PlanKey = std::tuple<int, int, int, int, uint64_t, int, int, int>;  // mode, rank, k, b, count, dtype size, slices, schedule
 
 // CHR_SCHEDULE = reference | balanced | flat (or 0 / 1 / 2); default flat
+// CHR_OVERLAP=0: local ops on the transfer stream (no compute/xGMI overlap); default 1
+int default_overlap() {
+    static const int v = [] {
+        const char* e = std::getenv("CHR_OVERLAP");
+        return e ? (std::atoi(e) != 0) : 1;
+    }();
+    return v;
+}
+
 int default_schedule() {
     static const int v = [] {
         const char* e = std::getenv("CHR_SCHEDULE");
@@ -192,8 +201,19 @@ struct chr_comm {
     int rank = 0, nranks = 0, device = 0;
     int slices = 0;  // 0 = auto
     int sched = default_schedule();
+    int overlap = default_overlap();
     ncclComm_t nccl = nullptr;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;   // RCCL transfers; the call completes on this stream
+    hipStream_t cstream = nullptr;  // local ops (reductions, copies) when overlapping
+    std::vector<hipEvent_t> events;  // pool: 2 per step
+    hipEvent_t event(size_t i) {
+        while (events.size() <= i) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+            events.push_back(e);
+        }
+        return events[i];
+    }
     DevBuf acc, stage, hsend, hrecv;
     ReduceProfile prof;
     std::map<PlanKey, std::unique_ptr<Plan>> plans;
@@ -230,7 +250,18 @@ int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int d
     int rc;
     for (const auto& op_ : p.pre)
         if ((rc = run_local(op_, B, dtype, op, c->stream, &c->prof))) return rc;
-    for (const chr::Step& s : p.steps) {
+    // Two streams: transfers on c->stream, local ops on c->cstream.  A step's transfers wait
+    // only for the local ops of step comm_wait (schedule.cpp analyze_deps); local ops wait
+    // for their own step's transfers.  The call ends with c->stream waiting for the last ops.
+    const bool two = c->overlap && c->cstream;
+    int waited = -1, last_comp = -1;
+    for (size_t t = 0; t < p.steps.size(); ++t) {
+        const chr::Step& s = p.steps[t];
+        if (two && s.comm_wait > waited) {
+            hipEvent_t e = c->event(2 * (size_t)s.comm_wait + 1);
+            if (!e || (rc = hip_code(hipStreamWaitEvent(c->stream, e, 0)))) return e ? rc : CHR_ERR_HIP;
+            waited = s.comm_wait;
+        }
         if (!s.sends.empty() || !s.recvs.empty()) {
             if ((rc = nccl_code(ncclGroupStart()))) return rc;
             for (const chr::Xfer& x : s.sends)
@@ -245,8 +276,23 @@ int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int d
                 }
             if ((rc = nccl_code(ncclGroupEnd()))) return rc;
         }
+        if (s.post.empty()) continue;
+        if (!two) {
+            for (const auto& op_ : s.post)
+                if ((rc = run_local(op_, B, dtype, op, c->stream, &c->prof))) return rc;
+            continue;
+        }
+        hipEvent_t ec = c->event(2 * t), ed = c->event(2 * t + 1);
+        if (!ec || !ed) return CHR_ERR_HIP;
+        if ((rc = hip_code(hipEventRecord(ec, c->stream))) || (rc = hip_code(hipStreamWaitEvent(c->cstream, ec, 0))))
+            return rc;
         for (const auto& op_ : s.post)
-            if ((rc = run_local(op_, B, dtype, op, c->stream, &c->prof))) return rc;
+            if ((rc = run_local(op_, B, dtype, op, c->cstream, &c->prof))) return rc;
+        if ((rc = hip_code(hipEventRecord(ed, c->cstream)))) return rc;
+        last_comp = (int)t;
+    }
+    if (two && last_comp > waited) {
+        if ((rc = hip_code(hipStreamWaitEvent(c->stream, c->event(2 * (size_t)last_comp + 1), 0)))) return rc;
     }
     return CHR_SUCCESS;
 }
@@ -387,12 +433,14 @@ int chr_comm_init_rank(chr_comm** out, int nranks, const chr_unique_id* id, int 
     c->device = device;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamDefault);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->cstream, hipStreamDefault);
     if (e != hipSuccess) return hip_code(e);
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof(u));
     int rc = nccl_code(ncclCommInitRank(&c->nccl, nranks, u, rank));
     if (rc) {
         (void)hipStreamDestroy(c->stream);
+        (void)hipStreamDestroy(c->cstream);
         return rc;
     }
     *out = c.release();
@@ -409,6 +457,9 @@ int chr_comm_destroy(chr_comm* c) {
     c->stage.release();
     c->hsend.release();
     c->hrecv.release();
+    if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+    for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
+    if (c->cstream) (void)hipStreamDestroy(c->cstream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return CHR_SUCCESS;
@@ -450,6 +501,12 @@ int chr_comm_profile_read(chr_comm* c, double* reduce_ms, double* reduce_bytes, 
         c->prof.bytes = 0;
         c->prof.launches = 0;
     }
+    return CHR_SUCCESS;
+}
+
+int chr_comm_set_overlap(chr_comm* c, int enable) {
+    if (!c) return CHR_ERR_INVALID_ARG;
+    c->overlap = enable != 0;
     return CHR_SUCCESS;
 }
 

@@ -496,9 +496,59 @@ static void split_wide_reductions(Plan& p) {
     p.stage_elems += need;
 }
 
+// Dependencies for two-stream execution (transfers on the comm stream, local ops on the
+// compute stream).  Regions are compared in one address space for SEND and RECV (they are the
+// same memory under MPI_IN_PLACE; a false conflict only costs overlap, never correctness).
+struct Region {
+    uint8_t buf;
+    uint64_t lo, hi;
+};
+static uint8_t space(uint8_t b) { return b == BUF_SEND ? (uint8_t)BUF_RECV : b; }
+static bool overlap(const Region& a, const Region& b) {
+    return space(a.buf) == space(b.buf) && a.lo < b.hi && b.lo < a.hi;
+}
+static void op_regions(const LocalOp& op, std::vector<Region>* rd, std::vector<Region>* wr) {
+    if (op.kind == L_COPY2D) {
+        for (uint64_t r = 0; r < op.rows; ++r) {
+            rd->push_back({op.acc.buf, op.acc.off + r * op.spitch, op.acc.off + r * op.spitch + op.count});
+            wr->push_back({op.dst.buf, op.dst.off + r * op.dpitch, op.dst.off + r * op.dpitch + op.count});
+        }
+        return;
+    }
+    rd->push_back({op.acc.buf, op.acc.off, op.acc.off + op.count});
+    for (const Ref& x : op.ins) rd->push_back({x.buf, x.off, x.off + op.count});
+    wr->push_back({op.dst.buf, op.dst.off, op.dst.off + op.count});
+}
+static void analyze_deps(Plan& p) {
+    const size_t ns = p.steps.size();
+    std::vector<std::vector<Region>> prd(ns), pwr(ns);
+    for (size_t u = 0; u < ns; ++u)
+        for (const LocalOp& op : p.steps[u].post) op_regions(op, &prd[u], &pwr[u]);
+    for (size_t t = 0; t < ns; ++t) {
+        std::vector<Region> crd, cwr;  // transfers: sends read, receives write
+        for (const Xfer& x : p.steps[t].sends) crd.push_back({x.ref.buf, x.ref.off, x.ref.off + x.count});
+        for (const Xfer& x : p.steps[t].recvs) cwr.push_back({x.ref.buf, x.ref.off, x.ref.off + x.count});
+        int w = -1;
+        for (size_t u = t; u-- > 0 && w < 0;) {
+            bool c = false;
+            for (const Region& a : pwr[u]) {
+                for (const Region& b : crd) c = c || overlap(a, b);  // RAW
+                for (const Region& b : cwr) c = c || overlap(a, b);  // WAW
+            }
+            for (const Region& a : prd[u])
+                for (const Region& b : cwr) c = c || overlap(a, b);  // WAR
+            if (c) w = (int)u;
+        }
+        p.steps[t].comm_wait = w;
+    }
+}
+
 Plan build_plan(Mode mode, int n, int me, int k_in, int b, uint64_t count, int slices, int sched) {
     Plan p = build_plan_impl(mode, n, me, k_in, b, count, slices, sched);
-    if (!p.error) split_wide_reductions(p);
+    if (!p.error) {
+        split_wide_reductions(p);
+        analyze_deps(p);
+    }
     return p;
 }
 
@@ -685,7 +735,7 @@ std::string describe(const Plan& p) {
     }
     for (size_t i = 0; i < p.steps.size(); ++i) {
         const Step& s = p.steps[i];
-        o << "step " << i << " " << (s.label.empty() ? "-" : s.label) << "\n";
+        o << "step " << i << " " << (s.label.empty() ? "-" : s.label) << " wait=" << s.comm_wait << "\n";
         for (const Xfer& x : s.sends)
             o << "send " << x.peer << " " << buf_name(x.ref.buf) << " " << x.ref.off << " " << x.count << "\n";
         for (const Xfer& x : s.recvs)
@@ -1445,20 +1495,19 @@ Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, 
             }
         }
     };
-    std::vector<int> L{F_GATHER};
-    if (mode == MODE_ALLREDUCE) L.push_back(F_DIST);
-    const int S = (int)L.size();
-    p.steps.resize((size_t)(P + S - 1));
-    for (int t = 0; t < P + S - 1; ++t) {
-        Step& st = p.steps[t];
-        st.label = "t" + std::to_string(t);
-        for (int s2 = 0; s2 < P; ++s2) {
-            const int ls = t - s2;
-            if (ls < 0 || ls >= S) continue;
-            st.label += std::string(L[ls] == F_GATHER ? ",gather" : ",fdist") + "/s" + std::to_string(s2);
-            emit(L[ls], sl[s2], st);
-        }
+    // Step order G0, G1, D0, G2, D1, ..., D(P-1): gather s+1 needs nothing from the evaluation
+    // of slice s, so with two streams it runs while slice s is reduced; allgather s follows it.
+    auto add = [&](int kind, int s2) {
+        p.steps.emplace_back();
+        Step& st = p.steps.back();
+        st.label = std::string(kind == F_GATHER ? "gather" : "fdist") + "/s" + std::to_string(s2);
+        emit(kind, sl[s2], st);
+    };
+    for (int s2 = 0; s2 < P; ++s2) {
+        add(F_GATHER, s2);
+        if (mode == MODE_ALLREDUCE && s2 > 0) add(F_DIST, s2 - 1);
     }
+    if (mode == MODE_ALLREDUCE) add(F_DIST, P - 1);
     return p;
 }
 

@@ -56,6 +56,10 @@ struct Step {
     std::vector<Xfer> sends, recvs;
     std::vector<LocalOp> post;
     std::string label;
+    // Two-stream execution: this step's transfers must wait for the local ops of step
+    // `comm_wait` (the latest earlier step whose ops touch what these transfers read or
+    // write); -1 = none.  Local ops always wait for their own step's transfers.
+    int comm_wait = -1;
 };
 
 enum Mode : int {

@@ -107,6 +107,11 @@ int chr_comm_set_slices(chr_comm* comm, int slices);
 #define CHR_SCHEDULE_BALANCED 1
 #define CHR_SCHEDULE_FLAT 2
 int chr_comm_set_schedule(chr_comm* comm, int schedule);
+/* Compute/xGMI overlap (default on; env CHR_OVERLAP=0): local reductions run on a second HIP
+ * stream, ordered against the RCCL transfers by events where the plan's data dependencies
+ * require it, so e.g. the flat schedule reduces slice s while slice s+1 is being gathered.
+ * The call still completes on chr_comm_stream. */
+int chr_comm_set_overlap(chr_comm* comm, int enable);
 /* Opt-in timing of the fused bucket-reduction launches of this communicator (HIP events
  * on its stream).  _read synchronises on the recorded launches and returns the summed
  * kernel milliseconds, the algorithmic bytes ((m+2)*n*sizeof(T) per launch) and the

@@ -42,8 +42,11 @@ def _worker(rank, world, port, cases, q):
     comm = ca.Comm.from_torch_distributed(device=0)
     dev = torch.device("cuda:0")
     try:
-        for (mode, k, b, count, dtype, host, slices) in cases:
+        for case in cases:
+            (mode, k, b, count, dtype, host, slices), extra = case[:7], case[7:]
             comm.set_slices(slices)
+            comm.set_schedule(extra[0] if extra else ca.SCHEDULE_FLAT)
+            comm.set_overlap(extra[1] if len(extra) > 1 else True)
             npdt = po.NP_DTYPES[dtype]
             cdt = {"f32": ca.FLOAT32, "bf16": ca.BFLOAT16, "i32": ca.INT32}[dtype]
             in_n = count * world if mode == "rs" else count
@@ -133,3 +136,15 @@ def test_rccl_mpich_baselines_world5_and_8():
 def test_rccl_allgather_world4_and_8():
     _run(4, [("ag", 2, 2, 1 << 16, "f32", False, 0), ("ag", 3, 4, 1001, "bf16", True, 0)])
     _run(8, [("ag", 4, 4, 1 << 18, "f32", False, 0), ("ag", 8, 2, 4097, "i32", False, 0)], timeout=600)
+
+
+def test_rccl_schedules_and_overlap_world4():
+    """The two-stream executor (overlap on/off) under all three schedules, allreduce and
+    reduce-scatter, 4 ranks over RCCL: bit-exact vs the oracle."""
+    cases = []
+    for sched in (0, 1, 2):
+        for ov in (True, False):
+            cases.append(("ar", 4, 4, 1 << 18, "f32", False, 4, sched, ov))
+            cases.append(("rs", 2, 2, 1 << 15, "f32", False, 3, sched, ov))
+    cases.append(("ar", 2, 4, 1 << 18, "bf16", False, 5, 2, True))  # multi-phase tree, flat
+    _run(4, cases, timeout=600)

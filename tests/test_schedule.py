@@ -286,3 +286,18 @@ def test_wide_mpich_chains_in_place(algo, n, k):
             got = plan_sim.simulate(mode, sends, k, 0, "f32", op, inplace=inplace)
             for r in range(n):
                 np.testing.assert_array_equal(got[r].view(np.uint8), want[r].view(np.uint8))
+
+
+def test_flat_overlap_dependencies():
+    """Two-stream execution: in the flat plan, gather s+1 never waits for the evaluation of slice
+    s (overlap), while allgather s waits exactly for it; wavefront plans wait step to step."""
+    p = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 1 << 24, 4))
+    labels = [st["label"] for st in p["steps"]]
+    assert labels == ["gather/s0", "gather/s1", "fdist/s0", "gather/s2", "fdist/s1", "gather/s3", "fdist/s2",
+                      "fdist/s3"]
+    waits = {st["label"]: st["wait"] for st in p["steps"]}
+    assert all(waits[f"gather/s{s}"] == -1 for s in range(4))
+    for s in range(4):
+        assert labels[waits[f"fdist/s{s}"]] == f"gather/s{s}"
+    r = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 1 << 24, 4, ca.SCHEDULE_REFERENCE))
+    assert [st["wait"] for st in r["steps"]][1:6] == [0, 1, 2, 3, 4]
