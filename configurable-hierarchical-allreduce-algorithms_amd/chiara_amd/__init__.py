@@ -15,6 +15,6 @@ from .collectives import (  # noqa: F401
     MPICH_Allreduce_recursive_doubling, MPICH_Allreduce_recursive_exchange,
     MPICH_Allreduce_reduce_scatter_allgather, MPICH_Allreduce_ring, all_reduce_radix_batch,
     allgather_radix_batch, check,
-    describe_plan, fill, get_unique_id, parse_plan, reduce_local, reduce_multi, reduce_multi_ex,
+    describe_plan, fill, get_unique_id, parse_plan, reduce_local, reduce_multi, reduce_multi_ex, reduce_tree,
     reduce_scatter_radix_batch,
 )

@@ -292,6 +292,15 @@ def reduce_multi_ex(out, acc, ins, count, datatype, op, flags, stream=None):
                                      _stream(stream))
 
 
+def reduce_tree(out, leaves, comb, swaps, count, datatype, op, stream=None):
+    """Fused expression tree (chr_reduce_tree): leaves pushed in order, comb[j] combines after
+    leaf j, swaps[c] = running value first for combine c."""
+    arr = (ctypes.c_void_p * max(1, len(leaves)))(*[_addr(x) for x in leaves])
+    cb = bytes(bytearray(comb))
+    sb = bytes(bytearray(swaps)) if swaps is not None else None
+    return lib().chr_reduce_tree(_addr(out), arr, len(leaves), cb, sb, count, datatype, op, _stream(stream))
+
+
 # ---- plan introspection (host only) --------------------------------------------------------------
 
 def describe_plan(mode, nranks, rank, k, b, count, slices=1, schedule=None):
@@ -320,6 +329,11 @@ def parse_plan(text):
                     [int(tok[6]), int(tok[7]), int(tok[8])])
         m = int(tok[6])
         ins = [(tok[7 + 2 * j], int(tok[8 + 2 * j])) for j in range(m)]
+        if tok[0] == "tree":  # leaves = [acc] + ins; then "c" comb... "s" swaps...
+            rest = tok[7 + 2 * m:]
+            si = rest.index("s")
+            prog = ([int(x) for x in rest[1:si]], [int(x) for x in rest[si + 1:]])
+            return ("tree", (tok[1], int(tok[2])), (tok[3], int(tok[4])), int(tok[5]), ins, prog)
         # "reduce_sw": running value first in every step (MPICH_do_reduce order)
         return (tok[0], (tok[1], int(tok[2])), (tok[3], int(tok[4])), int(tok[5]), ins)
 

@@ -59,6 +59,18 @@ int chr_reduce_multi_ex(void* out, const void* acc, const void* const* ins, int 
     return status(chr::launch_reduce(out, acc, ins, m, n, dtype, op, stream, (flags & CHR_REDUCE_RUNNING_FIRST) != 0));
 }
 
+int chr_reduce_tree(void* out, const void* const* leaves, int nleaves, const unsigned char* comb,
+                    const unsigned char* swaps, size_t n, chr_dtype dtype, chr_op op, hipStream_t stream) {
+    if (!chr::valid_dtype_op(dtype, op) || nleaves < 1 || !comb || !leaves) return CHR_ERR_INVALID_ARG;
+    uint32_t cb = 0, sb = 0;
+    if (!chr::tree_program_ok(nleaves, comb, swaps, &cb, &sb)) return CHR_ERR_UNSUPPORTED;
+    if (n == 0) return CHR_SUCCESS;
+    if (!out) return CHR_ERR_INVALID_ARG;
+    for (int j = 0; j < nleaves; ++j)
+        if (!leaves[j]) return CHR_ERR_INVALID_ARG;
+    return status(chr::launch_reduce_tree(out, leaves, nleaves, comb, swaps, n, dtype, op, stream));
+}
+
 int chr_fill(void* buf, size_t n, chr_dtype dtype, int pattern, uint64_t seed, int rank, uint64_t count_for_seq,
              hipStream_t stream) {
     if (!chr::dtype_size(dtype) || (pattern < 0 || pattern > 2)) return CHR_ERR_INVALID_ARG;

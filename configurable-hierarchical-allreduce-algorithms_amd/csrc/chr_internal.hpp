@@ -20,6 +20,14 @@ bool valid_dtype_op(int dtype, int op);
 hipError_t launch_reduce(void* out, const void* acc, const void* const* ins, int m, size_t n,
                          int dtype, int op, hipStream_t stream, bool running_first = false);
 
+// Fused expression tree (reduce_kernels.hip, k_reduce_tree): leaves in push order; comb[j] =
+// binary combines after pushing leaf j; swaps[c] = 1 if combine c takes the running value as
+// the `in` operand.  At most 8 leaves, stack depth 4 (tree_program_ok checks).
+hipError_t launch_reduce_tree(void* out, const void* const* leaves, int nl, const uint8_t* comb,
+                              const uint8_t* swaps, size_t n, int dtype, int op, hipStream_t stream);
+bool tree_program_ok(int nl, const uint8_t* comb, const uint8_t* swaps, uint32_t* comb_bits,
+                     uint32_t* swap_bits);
+
 hipError_t launch_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int rank,
                        uint64_t count_for_seq, hipStream_t stream);
 

@@ -128,20 +128,26 @@ int run_local(const chr::LocalOp& op, const Bufs& B, int dtype, int rop, hipStre
     if (op.kind == chr::L_COPY2D)
         return hip_code(hipMemcpy2DAsync(B.ptr(op.dst), op.dpitch * B.es, B.ptr(op.acc), op.spitch * B.es,
                                          op.count * B.es, op.rows, hipMemcpyDeviceToDevice, s));
-    std::vector<const void*> ins(op.ins.size());
-    for (size_t j = 0; j < op.ins.size(); ++j) ins[j] = B.ptr(op.ins[j]);
+    const bool tree = op.kind == chr::L_TREE;
+    std::vector<const void*> ins;
+    if (tree) ins.push_back(B.ptr(op.acc));  // leaf 0
+    for (const chr::Ref& r : op.ins) ins.push_back(B.ptr(r));
     const bool timed = prof && prof->on && !ins.empty();
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     if (timed) {
         ev = prof->take();
         (void)hipEventRecord(ev.first, s);
     }
-    const int rc = hip_code(chr::launch_reduce(B.ptr(op.dst), B.ptr(op.acc), ins.data(), (int)ins.size(), op.count,
-                                               dtype, rop, s, op.swap));
+    const int rc =
+        tree ? hip_code(chr::launch_reduce_tree(B.ptr(op.dst), ins.data(), (int)ins.size(), op.comb.data(),
+                                                op.swaps.empty() ? nullptr : op.swaps.data(), op.count, dtype, rop, s))
+             : hip_code(chr::launch_reduce(B.ptr(op.dst), B.ptr(op.acc), ins.data(), (int)ins.size(), op.count, dtype,
+                                           rop, s, op.swap));
     if (timed) {
         (void)hipEventRecord(ev.second, s);
         prof->pending.push_back(ev);
-        prof->bytes += (double)(ins.size() + 2) * op.count * B.es;
+        // algorithmic bytes: every operand read once, the result written once
+        prof->bytes += (double)(ins.size() + (tree ? 1 : 2)) * op.count * B.es;
         prof->launches += 1;
     }
     return rc;

@@ -25,14 +25,12 @@
 
 #include <cstdlib>
 
-#include "chr_internal.hpp"
+#include "reduce_common.hpp"
 
 namespace chr {
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kMaxFanIn = 8;
-constexpr int kBlock = 256;
 
 size_t dtype_size(int dtype) {
     switch (dtype) {
@@ -64,72 +62,6 @@ ReduceTuning& reduce_tuning() {
     return t;
 }
 
-// ---- element semantics -----------------------------------------------------------------
-
-__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
-__device__ __forceinline__ uint16_t f2bf(float f) {
-    uint32_t u = __float_as_uint(f);
-    if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x007FFFFFu)) return (uint16_t)((u >> 16) | 0x40u);
-    u += 0x7FFFu + ((u >> 16) & 1u);
-    return (uint16_t)(u >> 16);
-}
-
-template <int DT> struct DTy;
-template <> struct DTy<CHR_FLOAT32> { using T = float; };
-template <> struct DTy<CHR_FLOAT64> { using T = double; };
-template <> struct DTy<CHR_INT32> { using T = int32_t; };
-template <> struct DTy<CHR_BFLOAT16> { using T = uint16_t; };
-
-// Internal op codes for the running-value-first order of MPICH_do_reduce
-// (allreduce_recexch.cpp:147-186): each step is MPI_Reduce_local(running, next).  SUM and
-// PROD are bitwise commutative (IEEE add/mul, wrapping int, bf16 RNE of a commutative f32
-// op), so only MAX/MIN need their own instantiations (they differ on ties such as -0/+0
-// and on NaN compares).
-constexpr int kMaxSw = 6, kMinSw = 7;
-
-// MPI_Reduce_local(in = x, inout = y): MPICH 3.3.2's loop is inout = OP(inout, in) with
-// MAX(p, q) = p > q ? p : q (MPIR_OP_TYPE_REDUCE_CASE, a = inoutvec, b = invec), so MAX/MIN
-// keep the accumulator on ties and NaN compares.  kMaxSw/kMinSw: the running value is the
-// `in` operand and the result takes the place of the incoming buffer: OP(x, y).
-template <int DT, int OP>
-__device__ __forceinline__ typename DTy<DT>::T apply(typename DTy<DT>::T x, typename DTy<DT>::T y) {
-    if constexpr (DT == CHR_BFLOAT16) {
-        const float fx = bf2f(x), fy = bf2f(y);
-        if constexpr (OP == CHR_SUM) return f2bf(fy + fx);
-        else if constexpr (OP == CHR_PROD) return f2bf(fy * fx);
-        else if constexpr (OP == CHR_MAX) return fy > fx ? y : x;
-        else if constexpr (OP == CHR_MIN) return fy < fx ? y : x;
-        else if constexpr (OP == kMaxSw) return fx > fy ? x : y;
-        else return fx < fy ? x : y;
-    } else if constexpr (DT == CHR_INT32) {
-        if constexpr (OP == CHR_SUM) return (int32_t)((uint32_t)y + (uint32_t)x);
-        else if constexpr (OP == CHR_PROD) return (int32_t)((uint32_t)y * (uint32_t)x);
-        else if constexpr (OP == CHR_MAX || OP == kMaxSw) return y > x ? y : x;
-        else return y < x ? y : x;
-    } else {
-        if constexpr (OP == CHR_SUM) return y + x;
-        else if constexpr (OP == CHR_PROD) return y * x;
-        else if constexpr (OP == CHR_MAX) return y > x ? y : x;
-        else if constexpr (OP == CHR_MIN) return y < x ? y : x;
-        else if constexpr (OP == kMaxSw) return x > y ? x : y;
-        else return x < y ? x : y;
-    }
-}
-
-template <int DT, int OP>
-__device__ __forceinline__ u32x4 apply_vec(u32x4 in, u32x4 acc) {
-    using T = typename DTy<DT>::T;
-    constexpr int E = 16 / sizeof(T);
-    T a[E], b[E];
-    __builtin_memcpy(a, &in, 16);
-    __builtin_memcpy(b, &acc, 16);
-#pragma unroll
-    for (int e = 0; e < E; ++e) b[e] = apply<DT, OP>(a[e], b[e]);
-    u32x4 r;
-    __builtin_memcpy(&r, b, 16);
-    return r;
-}
-
 struct VecArgs {
     u32x4* out;
     const u32x4* acc;
@@ -137,16 +69,6 @@ struct VecArgs {
     size_t nvec;
 };
 
-template <bool NT>
-__device__ __forceinline__ u32x4 ld(const u32x4* p) {
-    if constexpr (NT) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-template <bool NT>
-__device__ __forceinline__ void st(u32x4* p, u32x4 v) {
-    if constexpr (NT) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
 
 // U vectors (16 B each) per lane per trip; all M+1 operands of the trip are loaded
 // before the first add so (M+1)*U*16 bytes per lane are in flight.  NT: non-temporal

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <sstream>
 
 namespace chr {
@@ -722,6 +723,15 @@ std::string describe(const Plan& p) {
         } else if (op.kind == L_COPY2D) {
             o << "copy2d " << buf_name(op.dst.buf) << " " << op.dst.off << " " << buf_name(op.acc.buf) << " "
               << op.acc.off << " " << op.count << " " << op.rows << " " << op.dpitch << " " << op.spitch << "\n";
+        } else if (op.kind == L_TREE) {
+            o << "tree " << buf_name(op.dst.buf) << " " << op.dst.off << " " << buf_name(op.acc.buf) << " "
+              << op.acc.off << " " << op.count << " " << op.ins.size();
+            for (const Ref& r : op.ins) o << " " << buf_name(r.buf) << " " << r.off;
+            o << " c";
+            for (uint8_t c : op.comb) o << " " << (int)c;
+            o << " s";
+            for (uint8_t w : op.swaps) o << " " << (int)w;
+            o << "\n";
         } else {
             o << (op.swap ? "reduce_sw " : "reduce ") << buf_name(op.dst.buf) << " " << op.dst.off << " " << buf_name(op.acc.buf) << " "
               << op.acc.off << " " << op.count << " " << op.ins.size();
@@ -1347,6 +1357,41 @@ bool eval_program(const std::vector<SymNode>& nodes, int root, int n, std::vecto
     return ok && top < 0;
 }
 
+// Post-order stack program of one expression for the fused tree kernel (chr_reduce_tree):
+// leaves in push order, comb[j] = combines right after leaf j, swaps per combine.  Every fold
+// acc (op) in_0 (op) in_1 ... becomes: program(acc), then per input program(in_i) + combine.
+bool tree_program(const std::vector<EvalOp>& pr, std::vector<int>* leaves, std::vector<uint8_t>* comb,
+                  std::vector<uint8_t>* swaps) {
+    if (pr.size() < 2) return false;  // a single fold is already one launch of k_reduce_vec
+    int depth = 0, maxd = 0;
+    bool ok = true;
+    std::function<void(int)> emit = [&](int code) {
+        if (code >= 0) {
+            leaves->push_back(code);
+            comb->push_back(0);
+            maxd = std::max(maxd, ++depth);
+            return;
+        }
+        const EvalOp& e = pr[~code];
+        emit(e.acc);
+        for (int x : e.ins) {
+            emit(x);
+            if (comb->back() >= 3) ok = false;
+            comb->back()++;
+            swaps->push_back(e.swap ? 1 : 0);
+            --depth;
+        }
+    };
+    emit(~(int)(pr.size() - 1));
+    return ok && depth == 1 && (int)leaves->size() <= kTreeMaxLeaves && maxd <= kTreeMaxDepth;
+}
+
+// CHR_TREE=0 evaluates flat expressions op by op (one k_reduce_vec launch per reference fold).
+bool tree_enabled() {
+    const char* e = std::getenv("CHR_TREE");
+    return !e || std::atoi(e) != 0;
+}
+
 }  // namespace
 
 Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, int slices) {
@@ -1391,8 +1436,20 @@ Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, 
         }
         progs.push_back(pr);
     }
+    // whole-tree programs (one fused launch per chunk) where the kernel's limits allow
+    struct TreeProg {
+        bool on = false;
+        std::vector<int> leaves;
+        std::vector<uint8_t> comb, swaps;
+    };
+    std::vector<TreeProg> tprog(progs.size());
+    const bool use_tree = tree_enabled();
     size_t temps = 1;
-    for (const auto& pr : progs) temps = std::max(temps, pr.size());
+    for (size_t i = 0; i < progs.size(); ++i) {
+        TreeProg& t = tprog[i];
+        t.on = use_tree && tree_program(progs[i], &t.leaves, &t.comb, &t.swaps);
+        if (!t.on) temps = std::max(temps, progs[i].size());
+    }
 
     // 2. slices and pieces
     const uint64_t span = mode == MODE_ALLREDUCE ? g.irc : g.recvcount;  // sliced range
@@ -1466,10 +1523,23 @@ Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, 
             if (!len) return;
             for (int N = 0; N < nchunks; ++N) {
                 const auto& pr = progs[mode == MODE_ALLREDUCE ? N : 0];
+                const TreeProg& tp = tprog[mode == MODE_ALLREDUCE ? N : 0];
                 auto opnd = [&](int code) -> Ref {
                     if (code >= 0) return code == me ? own(c, N, a) : leaf_slot(c, code, N, a);
                     return temp_slot(c, ~code, N);
                 };
+                if (tp.on) {
+                    LocalOp op;
+                    op.kind = L_TREE;
+                    op.dst = mode == MODE_ALLREDUCE ? Ref{BUF_RECV, (uint64_t)N * g.irc + c.lo + a} : Ref{BUF_RECV, c.lo};
+                    op.acc = opnd(tp.leaves[0]);
+                    for (size_t j = 1; j < tp.leaves.size(); ++j) op.ins.push_back(opnd(tp.leaves[j]));
+                    op.count = len;
+                    op.comb = tp.comb;
+                    op.swaps = tp.swaps;
+                    st.post.push_back(op);
+                    continue;
+                }
                 for (size_t t = 0; t < pr.size(); ++t) {
                     const bool last = t + 1 == pr.size();
                     Ref dst = last ? (mode == MODE_ALLREDUCE ? Ref{BUF_RECV, (uint64_t)N * g.irc + c.lo + a}

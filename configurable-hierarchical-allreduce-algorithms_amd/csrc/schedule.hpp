@@ -36,11 +36,15 @@ struct Xfer {
     uint64_t count;  // elements
 };
 
-enum LocalKind : uint8_t { L_COPY = 0, L_REDUCE = 1, L_COPY2D = 2 };
+enum LocalKind : uint8_t { L_COPY = 0, L_REDUCE = 1, L_COPY2D = 2, L_TREE = 3 };
 
 // L_REDUCE: dst = (...((acc op ins[0]) op ins[1])...) op ins[m-1]   (dst may equal acc)
 // L_COPY:   dst = acc                                    (count elements)
 // L_COPY2D: rows x count elements, row r: dst + r*dpitch <- acc + r*spitch
+// L_TREE:   dst = one whole expression tree (chr_reduce_tree): leaves acc, ins[0], ins[1], ...
+//           in push order; comb[j] combines after leaf j; swaps[c] per combine
+constexpr int kTreeMaxLeaves = 8;  // kMaxLeaves, reduce_tree.hip
+constexpr int kTreeMaxDepth = 4;   // kTreeDepth
 struct LocalOp {
     LocalKind kind;
     Ref dst;
@@ -50,6 +54,7 @@ struct LocalOp {
     int site;  // reference call site this op restates (line in all_reduce_radix_batch.cpp)
     uint64_t rows = 1, dpitch = 0, spitch = 0;
     bool swap = false;  // L_REDUCE: running value is the FIRST operand, OP(acc, in) (MPICH_do_reduce)
+    std::vector<uint8_t> comb, swaps;  // L_TREE program
 };
 
 struct Step {

@@ -73,6 +73,21 @@ int chr_reduce_multi(void* out, const void* acc, const void* const* ins, int m, 
 int chr_reduce_multi_ex(void* out, const void* acc, const void* const* ins, int m, size_t n,
                         chr_dtype dtype, chr_op op, int flags, hipStream_t stream);
 
+/* Fused expression tree: one HBM pass evaluating the nested MPI_Reduce_local calls that
+ * build one chunk's result across the reference's phases -- recexch folds
+ * (all_reduce_radix_batch.cpp:364, :446), step-1 folds (:332) and the lane reduction (:529);
+ * reduce_scatter_radix_batch.cpp:332, :366, :447, :552 -- with every intermediate kept in
+ * registers.  Post-order stack program: leaves[j] is pushed in order j = 0..nleaves-1; after
+ * leaf j, comb[j] combines follow.  A combine pops `in` and folds it into the value below
+ * (the running value): below = MPI_Reduce_local(in, below), or with swaps[c] != 0 (combine c
+ * in program order) MPI_Reduce_local(below, in) (MPICH_do_reduce order).  The program must
+ * leave exactly one value: sum(comb) == nleaves-1, comb[0] == 0.  Limits: 1 <= nleaves <= 8,
+ * stack depth <= 4 (CHR_ERR_UNSUPPORTED otherwise).  `out` may alias a leaf at the same
+ * element offset.  swaps may be NULL (all zero). */
+int chr_reduce_tree(void* out, const void* const* leaves, int nleaves, const unsigned char* comb,
+                    const unsigned char* swaps, size_t n, chr_dtype dtype, chr_op op,
+                    hipStream_t stream);
+
 /* ---- communicator (replaces MPI_Comm + MPI p2p: RCCL over xGMI) -------------------- */
 typedef struct chr_comm chr_comm;
 typedef struct { char internal[128]; } chr_unique_id; /* == ncclUniqueId */

@@ -9,6 +9,7 @@ import numpy as np
 
 import chiara_amd as ca
 import pyoracle as po
+import tree_util
 
 
 def load_plans(mode, n, k, b, count, slices=1, schedule=None):
@@ -32,8 +33,13 @@ class RankState:
 
 
 def run_local(st, op, dtype, rop):
-    kind, dst, acc, n, ins = op
+    kind, dst, acc, n, ins = op[:5]
     if n == 0:
+        return
+    if kind == "tree":  # chr_reduce_tree: post-order stack program over the leaves
+        comb, swaps = op[5]
+        leaves = [st.view(ref, n) for ref in [acc] + list(ins)]
+        st.view(dst, n)[:] = tree_util.tree_ref(leaves, comb, swaps, dtype, rop)
         return
     if kind == "copy2d":
         rows, dp, sp = ins

@@ -1,0 +1,99 @@
+"""Fused expression-tree kernel (chr_reduce_tree, csrc/reduce_tree.hip) vs the oracle.
+
+The reference op sequence a tree restates is the chain of MPI_Reduce_local calls that
+builds one chunk across phases (all_reduce_radix_batch.cpp:332, :364, :446, :529).  The
+CPU side evaluates the same post-order program with the oracle's MPI_Reduce_local
+restatement, one call per combine.  Bar: bit-exact for every dtype and op, including the
+running-value-first (swap) combines and ties/NaN data (pattern 2)."""
+import numpy as np
+import pytest
+
+import chiara_amd as ca
+import pyoracle as po
+from tree_util import random_program, tree_ref
+
+pytestmark = pytest.mark.gpu
+
+DT = {"f32": ca.FLOAT32, "f64": ca.FLOAT64, "i32": ca.INT32, "bf16": ca.BFLOAT16}
+OP = {"sum": ca.SUM, "prod": ca.PROD, "max": ca.MAX, "min": ca.MIN}
+
+
+@pytest.fixture(scope="module")
+def gu():
+    import gpu_util
+
+    return gpu_util
+
+
+def _bits(a):
+    return a.view({2: np.uint16, 4: np.uint32, 8: np.uint64}[a.itemsize])
+
+
+def _run(gu, dtype, op, comb, swaps, n, pattern=0, off=0, seed=11, inplace_leaf=None):
+    npdt = po.NP_DTYPES[dtype]
+    es = np.dtype(npdt).itemsize
+    nl = len(comb)
+    leaves = [po.fill(n, dtype, pattern, seed, r) for r in range(nl)]
+    if op == "prod" and dtype == "i32":
+        leaves = [(x % 5).astype(np.int32) for x in leaves]
+    d = []
+    for x in leaves:
+        t = gu.empty_dev((n + off) * es)
+        t[off * es:(off + n) * es] = gu.to_dev(x)
+        d.append(t)
+    if inplace_leaf is None:
+        out = gu.empty_dev((n + off) * es)
+    else:
+        out = d[inplace_leaf]
+    rc = ca.reduce_tree(out.data_ptr() + off * es, [t.data_ptr() + off * es for t in d], comb, swaps, n,
+                        DT[dtype], OP[op], gu.stream())
+    assert rc == 0
+    gu.sync()
+    got = gu.from_dev(out, npdt)[off:off + n]
+    ref = tree_ref(leaves, comb, swaps, dtype, op)
+    np.testing.assert_array_equal(_bits(got), _bits(ref))
+
+
+# the shapes the flat schedule emits at the BASELINE geometries (n=8)
+C4_TREE = ([0, 1, 1, 1, 0, 1, 1, 2], [0] * 7)       # k=4, b=4: fold4 + fold4, then lane fold
+K2B8_TREE = ([0, 1, 0, 2, 0, 1, 0, 3], [0] * 7)     # k=2, b=8: binary recexch, depth 4
+K4B8_TREE = ([0, 1, 1, 1, 0, 2, 1, 1], [0] * 7)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64", "i32", "bf16"])
+@pytest.mark.parametrize("op", ["sum", "prod", "max", "min"])
+@pytest.mark.parametrize("prog", [C4_TREE, K2B8_TREE, K4B8_TREE])
+def test_flat_shapes_all_dtypes_ops(gu, dtype, op, prog):
+    _run(gu, dtype, op, prog[0], prog[1], 100003, pattern=2 if op in ("max", "min") else 0)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_programs_with_swaps(gu, seed):
+    rng = np.random.default_rng(seed)
+    comb, swaps = random_program(rng, int(rng.integers(2, 9)))
+    for dtype in ("f32", "bf16"):
+        for op in ("sum", "max", "min"):
+            _run(gu, dtype, op, comb, swaps, 40000 + seed, pattern=2 if op != "sum" else 0, seed=seed)
+
+
+@pytest.mark.parametrize("n", [0, 1, 3, 7, 8, 9, 255, 1025, 2 * 256 * 4 * 2 + 5])
+def test_edge_sizes(gu, n):
+    for dt in ("f32", "bf16", "f64"):
+        _run(gu, dt, "sum", *C4_TREE, n)
+
+
+@pytest.mark.parametrize("off", [1, 2, 3])
+def test_misaligned(gu, off):
+    for dt in ("f32", "bf16", "i32"):
+        _run(gu, dt, "sum", *K2B8_TREE, 10007, off=off)
+
+
+def test_out_aliases_leaf(gu):
+    """MPI_IN_PLACE: the root is written over the rank's own leaf (same element offsets)."""
+    for leaf in (0, 3, 7):
+        _run(gu, "f32", "sum", *C4_TREE, 70001, inplace_leaf=leaf)
+
+
+def test_large_nt_path(gu):
+    """>= 128 MiB streamed per call takes the non-temporal instantiation."""
+    _run(gu, "f32", "sum", *C4_TREE, (16 << 20) + 7)

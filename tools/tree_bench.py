@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Fused expression tree vs one launch per fold, at the flat schedule's C4 evaluation shape.
+
+C4 (n=8, k=4, b=4): each rank evaluates, per chunk, ((l0 l1 l2 l3) (l4 l5 l6 l7)) -- two
+recexch folds of 4 (all_reduce_radix_batch.cpp:364) and the lane fold (:529).  Per-fold
+launches move 13 x piece bytes (two m=3 folds + one m=1 fold); the tree kernel 9 x.
+Prints one JSON line: time per evaluation and algorithmic GB/s of each form."""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "configurable-hierarchical-allreduce-algorithms_amd")]
+
+import torch  # noqa: E402
+
+import chiara_amd as ca  # noqa: E402
+
+COMB, SWAPS = [0, 1, 1, 1, 0, 1, 1, 2], [0] * 7
+
+
+def main():
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream(dev)
+    out = {}
+    for mib in (8, 64, 128):
+        n = (mib << 20) // 4
+        sets = max(1, min(8, (2048 << 20) // (11 * 4 * n)))
+        bufs = []
+        for si in range(sets):
+            leaves = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(8)]
+            for j, t in enumerate(leaves):
+                ca.fill(t, n, ca.FLOAT32, 0, 7, 8 * si + j, stream=s)
+            bufs.append((leaves, torch.empty(n, dtype=torch.float32, device=dev),
+                         torch.empty(n, dtype=torch.float32, device=dev), torch.empty(n, dtype=torch.float32, device=dev)))
+        reps = 40
+
+        def tree(i):
+            lv, o, _, _ = bufs[i % sets]
+            return ca.reduce_tree(o, lv, COMB, SWAPS, n, ca.FLOAT32, ca.SUM, s)
+
+        def folds(i):
+            lv, o, t0, t1 = bufs[i % sets]
+            rc = ca.reduce_multi(t0, lv[0], lv[1:4], n, ca.FLOAT32, ca.SUM, s)
+            rc |= ca.reduce_multi(t1, lv[4], lv[5:8], n, ca.FLOAT32, ca.SUM, s)
+            return rc | ca.reduce_multi(o, t0, [t1], n, ca.FLOAT32, ca.SUM, s)
+
+        res = {}
+        for name, fn, nbytes in (("tree", tree, 9 * 4 * n), ("folds", folds, 13 * 4 * n)):
+            for i in range(3):
+                assert fn(i) == 0
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record(s)
+            for i in range(reps):
+                fn(i)
+            e1.record(s)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / reps
+            res[name] = {"us": round(ms * 1e3, 2), "alg_GBps": round(nbytes / (ms * 1e-3) / 1e9, 1),
+                         "tree_bytes_GBps": round(9 * 4 * n / (ms * 1e-3) / 1e9, 1)}
+        lv, o, t0, t1 = bufs[0]
+        tree(0)
+        a = o.clone()
+        folds(0)
+        torch.cuda.synchronize()
+        res["bit_identical"] = bool(torch.equal(a.view(torch.int32), o.view(torch.int32)))
+        res["speedup"] = round(res["folds"]["us"] / res["tree"]["us"], 3)
+        out[f"piece_{mib}MiB"] = res
+        del bufs
+        torch.cuda.empty_cache()
+    print(json.dumps({"tree_vs_folds_c4": out}))
+
+
+if __name__ == "__main__":
+    main()
