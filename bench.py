@@ -324,7 +324,7 @@ def bench_allreduce(args):
                     "algorithmic_bytes_per_call": float(busiest[1]), "launches_per_call": int(busiest[2]),
                     "kernel_ms_per_call": round(float(busiest[0]), 4)}
     # bytes on the busiest directed link of this schedule (max over ranks; slicing only splits messages)
-    sched = {"reference": 0, "0": 0, "balanced": 1, "1": 1}.get(os.environ.get("CHR_SCHEDULE", "flat"), 2)
+    sched = {"reference": 0, "0": 0, "balanced": 1, "1": 1, "exact": 3, "3": 3}.get(os.environ.get("CHR_SCHEDULE", "flat"), 2)
     plan = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, world, rank, k, b, count, 1, sched))
     per_peer = {}
     for st in plan["steps"]:

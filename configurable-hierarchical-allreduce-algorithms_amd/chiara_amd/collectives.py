@@ -34,7 +34,7 @@ MODE_ALLREDUCE, MODE_REDUCE_SCATTER = 0, 1
 MODE_MPICH_RING, MODE_MPICH_RD, MODE_MPICH_RSAG, MODE_MPICH_RECEXCH = 2, 3, 4, 5
 MODE_MPICH_KRSAG, MODE_MPICH_RMULT = 6, 7
 MODE_ALLGATHER = 8
-SCHEDULE_REFERENCE, SCHEDULE_BALANCED, SCHEDULE_FLAT = 0, 1, 2
+SCHEDULE_REFERENCE, SCHEDULE_BALANCED, SCHEDULE_FLAT, SCHEDULE_EXACT = 0, 1, 2, 3
 REDUCE_RUNNING_FIRST = 1  # chr_reduce_multi_ex flag (MPICH_do_reduce operand order)
 
 
@@ -140,7 +140,7 @@ class Comm:
         check(lib().chr_comm_set_overlap(self._h, int(bool(enable))))
 
     def set_schedule(self, schedule):
-        """SCHEDULE_REFERENCE / SCHEDULE_BALANCED / SCHEDULE_FLAT: where reductions are evaluated
+        """SCHEDULE_REFERENCE / SCHEDULE_BALANCED / SCHEDULE_FLAT / SCHEDULE_EXACT: where reductions are evaluated
         (never what they compute)."""
         check(lib().chr_comm_set_schedule(self._h, int(schedule)))
 

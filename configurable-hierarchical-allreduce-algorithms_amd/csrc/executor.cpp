@@ -166,7 +166,7 @@ bool is_device_ptr(const void* p) {
 
 using PlanKey = std::tuple<int, int, int, int, uint64_t, int, int, int>;  // mode, rank, k, b, count, dtype size, slices, schedule
 
-// CHR_SCHEDULE = reference | balanced | flat (or 0 / 1 / 2); default flat
+// CHR_SCHEDULE = reference | balanced | flat | exact (or 0 / 1 / 2 / 3); default flat
 // CHR_OVERLAP=0: local ops on the transfer stream (no compute/xGMI overlap); default 1
 int default_overlap() {
     static const int v = [] {
@@ -183,6 +183,7 @@ int default_schedule() {
         const std::string s(e);
         if (s == "reference" || s == "0") return (int)chr::SCHED_REFERENCE;
         if (s == "balanced" || s == "1") return (int)chr::SCHED_BALANCED;
+        if (s == "exact" || s == "3") return (int)chr::SCHED_EXACT;
         return (int)chr::SCHED_FLAT;
     }();
     return v;
@@ -517,13 +518,13 @@ int chr_comm_set_overlap(chr_comm* c, int enable) {
 }
 
 int chr_comm_set_schedule(chr_comm* c, int schedule) {
-    if (!c || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_FLAT) return CHR_ERR_INVALID_ARG;
+    if (!c || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_EXACT) return CHR_ERR_INVALID_ARG;
     c->sched = schedule;
     return CHR_SUCCESS;
 }
 
 int chr_local_group_set_schedule(chr_local_group* g, int schedule) {
-    if (!g || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_FLAT) return CHR_ERR_INVALID_ARG;
+    if (!g || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_EXACT) return CHR_ERR_INVALID_ARG;
     g->sched = schedule;
     return CHR_SUCCESS;
 }

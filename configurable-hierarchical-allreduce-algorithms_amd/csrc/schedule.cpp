@@ -125,7 +125,7 @@ LocalOp make_copy2d(Ref dst, Ref src, uint64_t width, uint64_t rows, uint64_t dp
 }
 
 enum Logical { S_FOLD, S_PHASE, S_RETURN, S_LANE, S_DIST1, S_DIST2, S_SCATTER, S_BPHASE, S_BLANE, S_BDIST,
-               S_RPHASE, S_RLANE };
+               S_RPHASE, S_RLANE, S_BCAST, S_AG, S_KSCAT };
 
 // One element-slice [lo, lo+len) of every chunk, laid out slice-major in ACC:
 // chunk position `pos` of slice p lives at acc_base + pos*len.
@@ -141,6 +141,70 @@ struct Builder {
     std::vector<Recexch> rx;
     std::vector<int> cnt, off;
     uint64_t stage_per_elem = 0;  // STAGE elements needed per element of slice length
+    // SCHED_EXACT (unsliced): the reference's own phases 3-4 message for message.
+    bool exact = false;
+    int k_in = 0;            // k as passed: the reference sizes its allgather / scatter loops with it
+    uint64_t ex_bc = 0;      // STAGE: bcast landing, one IRC per stage (tmp_results, :552-568)
+    uint64_t ex_tmp = 0;     // STAGE: Bruck buffers (tmp_recvbuf, :582-756) / RS scatter buffer (:572-627)
+    int nph_ag = 0;          // allgather / scatter phases (:274-277; RS :271-275), unclamped k
+    // left-over k-Bruck (nu_count != 0, :645-756): my receives / sends per phase, in IRC units
+    struct LeftMsg {
+        bool send;
+        int peer_lane;
+        uint64_t off, cnt;
+    };
+    std::vector<std::vector<LeftMsg>> left;
+
+    // Restatement of the left-over Bruck's bookkeeping (all_reduce_radix_batch.cpp:645-742):
+    // active[] / send_sizes[][] evolve identically on every rank; each rank's receives land at
+    // its running `received` offset, its sends always start at offset 0.
+    void plan_left() {
+        const int b = g.b, k = g.k, nu = g.nu;
+        left.assign(nph_ag, {});
+        if (!nu) return;
+        std::vector<int> active(b);
+        std::vector<std::vector<long long>> ss(nph_ag + 1, std::vector<long long>(b, 0));
+        for (int l = 0; l < b; ++l) {
+            active[l] = l < nu ? 0 : -1;
+            ss[0][l] = l < nu ? 1 : 0;
+        }
+        long long delta = 1;
+        for (int i = 0; i < nph_ag; ++i) {
+            long long received = ss[i][lane];
+            for (int j = 1; j < k; ++j) {
+                if (delta * j >= b) {
+                    for (int l = 0; l < b; ++l) {
+                        if (active[l] == i) active[l] = i + 1;
+                        ss[i + 1][l] += ss[i][l];
+                    }
+                    break;
+                }
+                const int isrc = (int)((lane + delta * j) % b);
+                const int idst = (int)((b + (lane - delta * j) % b) % b);
+                long long sz = std::min(ss[i][isrc], (long long)nu - received);
+                if (active[isrc] == i && sz > 0) {
+                    left[i].push_back({false, isrc, (uint64_t)received, (uint64_t)sz});
+                    received += sz;
+                }
+                sz = std::min(ss[i][lane], (long long)nu - (ss[i][idst] + ss[i + 1][idst]));
+                if (active[lane] == i && sz > 0) left[i].push_back({true, idst, 0, (uint64_t)sz});
+                for (int l = 0; l < b; ++l) {
+                    if (active[l] == i) {
+                        const int t = (int)((b + (l - delta * j) % b) % b);
+                        active[t] = active[t] != i ? i + 1 : i;
+                        ss[i + 1][t] += ss[i][l];
+                        if (j == k - 1) active[l] = i + 1;
+                    }
+                    if (j == k - 1) ss[i + 1][l] += ss[i][l];
+                }
+            }
+            delta *= k;
+        }
+    }
+    Ref tmp_stage(int stg) const {  // Bruck buffer of stage stg (stg == nstages: the left-over part)
+        if (lane == 0 || (stg == g.nstages && lane >= g.nu)) return {BUF_RECV, (uint64_t)stg * g.b * g.irc};
+        return {BUF_STAGE, ex_tmp + (uint64_t)stg * g.b * g.irc};
+    }
 
     uint64_t chunk_pos(int N) const { return (uint64_t)g.P[N % g.b] + (uint64_t)(N / g.b); }
     // Region of lane blocks [o, o+c) of one slice, in elements.
@@ -250,6 +314,17 @@ struct Builder {
                 if (mode == MODE_ALLREDUCE) {
                     // reduce straight into the chunk's final place in recvbuf
                     s.post.push_back(make_reduce({BUF_RECV, (uint64_t)R * irc + c.lo}, {BUF_ACC, mine}, ins, c.len, 529));
+                } else if (exact) {
+                    s.post.push_back(make_reduce({BUF_ACC, mine}, {BUF_ACC, mine}, ins, c.len, 552));
+                    // root re-layout (reduce_scatter_radix_batch.cpp:572-579): block real_slot of the
+                    // chunk to normalized slot (real_slot - root_local) mod b; root_local == lane here
+                    const uint64_t rc = recvcount;
+                    const Ref t{BUF_STAGE, ex_tmp};
+                    s.post.push_back(make_copy(t, {BUF_ACC, mine + (uint64_t)lane * rc}, (uint64_t)(g.b - lane) * rc, 575));
+                    if (lane)
+                        s.post.push_back(make_copy({BUF_STAGE, ex_tmp + (uint64_t)(g.b - lane) * rc}, {BUF_ACC, mine},
+                                                   (uint64_t)lane * rc, 575));
+                    if (nph_ag == 0) s.post.push_back(make_copy({BUF_RECV, 0}, t, rc, 625));  // b == 1: shift 0
                 } else {
                     s.post.push_back(make_reduce({BUF_ACC, mine}, {BUF_ACC, mine}, ins, c.len, 552));
                     // own sub-block (reduce_scatter_radix_batch.cpp:572-579, :625-627)
@@ -418,6 +493,96 @@ struct Builder {
                 ins.push_back(src(X));
             }
             s.post.push_back(make_reduce({BUF_RECV, a - (uint64_t)lane * recvcount}, src(node), ins, len, 552));
+            break;
+        }
+        case S_BCAST: {  // allreduce allgather phase 1 (:552-568): lane root -> same lane of every node
+            for (int stg = 0; stg * g.b < g.nnodes; ++stg) {
+                const int N = stg * g.b + lane;  // chunk of my lane in this stage
+                if (N >= g.nnodes) continue;
+                const Ref bc{BUF_STAGE, ex_bc + (uint64_t)stg * irc};
+                if (node == N) {
+                    s.post.push_back(make_copy(bc, {BUF_RECV, (uint64_t)N * irc}, irc, 558));
+                    for (int j = 0; j < g.nnodes; ++j)
+                        if (j != node) s.sends.push_back({j * g.b + lane, {BUF_RECV, (uint64_t)N * irc}, irc});  // :564
+                } else {
+                    s.recvs.push_back({N * g.b + lane, bc, irc});  // :555
+                }
+            }
+            // each stage's own chunk to slot 0 of its Bruck buffer (:591, :645-647)
+            for (int stg = 0; stg < g.nstages; ++stg)
+                s.post.push_back(make_copy(tmp_stage(stg), {BUF_STAGE, ex_bc + (uint64_t)stg * irc}, irc, 591));
+            if (g.nu && lane < g.nu)
+                s.post.push_back(make_copy(tmp_stage(g.nstages), {BUF_STAGE, ex_bc + (uint64_t)g.nstages * irc}, irc, 646));
+            break;
+        }
+        case S_AG: {  // allreduce allgather phase 2 (:587-756): k-port Bruck inside the node, phase ph
+            const int b = g.b, k = g.k;
+            long long delta = 1;
+            for (int i = 0; i < ph; ++i) delta *= k;
+            const bool last = ph == nph_ag - 1;
+            const int p_of_k = x().p_of_k;
+            for (int stg = 0; stg < g.nstages; ++stg) {  // full stages (:587-640)
+                const Ref t = tmp_stage(stg);
+                for (int j = 1; j < k; ++j) {
+                    if (delta * j >= b) break;
+                    const int dst = (int)((b + (lane - delta * j) % b) % b) + node * b;
+                    const int src = (int)((lane + delta * j) % b) + node * b;
+                    long long cnt = delta;  // in IRC units (:604-617)
+                    if (last && p_of_k != b) {
+                        const long long left_cnt = b - delta * j;
+                        cnt = j == k - 1 ? left_cnt : std::min(cnt, left_cnt);
+                    }
+                    s.recvs.push_back({src, {t.buf, t.off + (uint64_t)(j * delta) * irc}, (uint64_t)cnt * irc});  // :620
+                    s.sends.push_back({dst, t, (uint64_t)cnt * irc});                                           // :623
+                }
+                if (last && lane != 0) {  // rotation into recvbuf (:627-637)
+                    const uint64_t base = (uint64_t)stg * b * irc;
+                    s.post.push_back(make_copy({BUF_RECV, base}, {t.buf, t.off + (uint64_t)(b - lane) * irc},
+                                               (uint64_t)lane * irc, 629));
+                    s.post.push_back(make_copy({BUF_RECV, base + (uint64_t)lane * irc}, t, (uint64_t)(b - lane) * irc, 633));
+                }
+            }
+            if (g.nu) {  // left-over chunks (:645-756)
+                const Ref t = tmp_stage(g.nstages);
+                for (const LeftMsg& m : left[ph]) {
+                    if (m.send) s.sends.push_back({node * b + m.peer_lane, {t.buf, t.off + m.off * irc}, m.cnt * irc});
+                    else s.recvs.push_back({node * b + m.peer_lane, {t.buf, t.off + m.off * irc}, m.cnt * irc});
+                }
+                if (last && lane != 0 && lane < g.nu) {  // :745-754
+                    const uint64_t base = (uint64_t)g.nstages * b * irc;
+                    s.post.push_back(make_copy({BUF_RECV, base}, {t.buf, t.off + (uint64_t)(g.nu - lane) * irc},
+                                               (uint64_t)lane * irc, 747));
+                    s.post.push_back(make_copy({BUF_RECV, base + (uint64_t)lane * irc}, t, (uint64_t)(g.nu - lane) * irc,
+                                               751));
+                }
+            }
+            break;
+        }
+        case S_KSCAT: {  // reduce-scatter k-nomial scatter inside the node (:584-627), phase ph
+            const int b = g.b, k = g.k;
+            const uint64_t rc = recvcount;
+            const int root_local = node % b, shift = (lane - root_local + b) % b;
+            // delta: k_in^(nph-1) in the first phase, then divided by the clamped k (:271-275, :621)
+            long long delta = 1;
+            for (int i = 0; i < nph_ag; ++i) delta *= k_in;
+            delta /= k_in;
+            for (int q = nph_ag - 1; q > ph; --q) delta = q > 0 ? delta / k : delta;
+            const long long group = delta * k, gstart = (shift / group) * group;
+            const long long bend = std::min<long long>(gstart + group, b), offs = shift - gstart;
+            if (offs == 0) {
+                for (int j = 1; j < k; ++j) {
+                    const long long child = gstart + j * delta;
+                    if (child >= bend) break;
+                    const long long sub = std::min(delta, bend - child);
+                    const int dst = node * b + (int)((child + root_local) % b);
+                    s.sends.push_back({dst, {BUF_STAGE, ex_tmp + (uint64_t)child * rc}, (uint64_t)sub * rc});  // :603
+                }
+            } else if (offs % delta == 0 && offs < group) {
+                const int src = node * b + (int)((gstart + root_local) % b);
+                const long long sub = std::min<long long>(delta, bend - shift);
+                s.recvs.push_back({src, {BUF_STAGE, ex_tmp + (uint64_t)shift * rc}, (uint64_t)sub * rc});  // :615
+            }
+            if (ph == 0) s.post.push_back(make_copy({BUF_RECV, 0}, {BUF_STAGE, ex_tmp + (uint64_t)shift * rc}, rc, 625));
             break;
         }
         case S_SCATTER: {  // reduce-scatter phase 3 (:572-627): owner -> every lane, direct
@@ -618,7 +783,14 @@ static Plan build_plan_impl(Mode mode, int n, int me, int k_in, int b, uint64_t 
     // fold.  Same expressions, evaluated on 1/n of every chunk at every rank (allreduce), or
     // on exactly the rank's own output block (reduce-scatter).
     p.balanced = balance && n > 1 && !folds && g.nph <= 1;
-    p.sched = p.balanced ? SCHED_BALANCED : SCHED_REFERENCE;
+    p.sched = p.balanced ? SCHED_BALANCED : sched == SCHED_EXACT ? SCHED_EXACT : SCHED_REFERENCE;
+    B.exact = sched == SCHED_EXACT;
+    if (B.exact) {
+        B.k_in = k_in;
+        for (int t = b - 1; t > 0; t /= k_in) ++B.nph_ag;  // :274-277 / RS :271-275 (k before clamping)
+        slices = 1;  // the reference's messages are whole chunks
+        if (mode == MODE_ALLREDUCE) B.plan_left();
+    }
     if (p.balanced && mode == MODE_ALLREDUCE) {
         if (g.nph == 1) L.push_back({S_BPHASE, 0});
         L.push_back({S_BLANE, 0});
@@ -632,7 +804,14 @@ static Plan build_plan_impl(Mode mode, int n, int me, int k_in, int b, uint64_t 
         for (int ph = g.nph - 1; ph >= 0; --ph) L.push_back({S_PHASE, ph});
         if (folds) L.push_back({S_RETURN, 0});
         L.push_back({S_LANE, 0});
-        if (mode == MODE_ALLREDUCE) {
+        if (B.exact && mode == MODE_ALLREDUCE) {  // bcast + k-port Bruck (:552-756)
+            if (n > 1) {
+                L.push_back({S_BCAST, 0});
+                for (int ph = 0; ph < B.nph_ag; ++ph) L.push_back({S_AG, ph});
+            }
+        } else if (B.exact) {  // k-nomial scatter, highest phase first (:584-622)
+            for (int ph = B.nph_ag - 1; ph >= 0; --ph) L.push_back({S_KSCAT, ph});
+        } else if (mode == MODE_ALLREDUCE) {
             if (n > 1) L.push_back({S_DIST1, 0});
             if (n > 2) L.push_back({S_DIST2, 0});
         } else if (b > 1) {
@@ -666,6 +845,11 @@ static Plan build_plan_impl(Mode mode, int n, int me, int k_in, int b, uint64_t 
         sl[s] = {lo, hi - lo, lo * (uint64_t)g.nnodes, lo * B.stage_per_elem};
     }
     p.stage_elems = g.irc * B.stage_per_elem;
+    if (B.exact) {  // bcast landing + Bruck buffers (allreduce) / scatter buffer (reduce-scatter)
+        B.ex_bc = p.stage_elems;
+        B.ex_tmp = B.ex_bc + (mode == MODE_ALLREDUCE ? (uint64_t)(g.nstages + 1) * g.irc : 0);
+        p.stage_elems = B.ex_tmp + (mode == MODE_ALLREDUCE ? g.total : g.irc);
+    }
 
     // pre: SEND -> ACC, slice-major and block-major (:306-312 copy, re-laid out)
     for (const SliceCtx& c : sl) {
@@ -690,9 +874,11 @@ static Plan build_plan_impl(Mode mode, int n, int me, int k_in, int b, uint64_t 
             if (ls < 0 || ls >= S) continue;
             if (st.label.empty()) st.label = "t" + std::to_string(t);
             static const char* names[] = {"fold", "phase", "return", "lane", "dist1", "dist2", "scatter",
-                                          "bphase", "blane", "bdist", "rphase", "rlane"};
-            st.label += std::string(st.label.size() > 0 ? "," : "") + names[L[ls].first] +
-                        (L[ls].first == S_PHASE ? std::to_string(L[ls].second) : "") + "/s" + std::to_string(s);
+                                          "bphase", "blane", "bdist", "rphase", "rlane", "bcast", "bruck", "kscat"};
+            const Logical lk = L[ls].first;
+            st.label += std::string(st.label.size() > 0 ? "," : "") + names[lk] +
+                        (lk == S_PHASE || lk == S_AG || lk == S_KSCAT ? std::to_string(L[ls].second) : "") + "/s" +
+                        std::to_string(s);
             B.emit(L[ls].first, L[ls].second, sl[s], st);
         }
     }

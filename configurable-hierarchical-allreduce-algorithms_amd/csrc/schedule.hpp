@@ -120,7 +120,9 @@ void recexch_count_offset(int nranks, int max_phases, int k, std::vector<int>* c
 //   SCHED_BALANCED   single-phase geometries: every rank evaluates 1/n (schedule.cpp S_B*, S_R*)
 //   SCHED_FLAT       any geometry: expression trees extracted symbolically, leaves gathered
 //                    over the full mesh, evaluated at the piece's rank (build_plan_flat)
-enum Sched : int { SCHED_REFERENCE = 0, SCHED_BALANCED = 1, SCHED_FLAT = 2 };
+//   SCHED_EXACT      the reference's messages end to end, unsliced: REFERENCE's phases 0-2, then
+//                    its bcast + k-port Bruck allgather (S_BCAST, S_AG) / k-nomial scatter (S_KSCAT)
+enum Sched : int { SCHED_REFERENCE = 0, SCHED_BALANCED = 1, SCHED_FLAT = 2, SCHED_EXACT = 3 };
 Plan build_plan(Mode mode, int nranks, int rank, int k, int b, uint64_t count, int slices = 1,
                 int sched = SCHED_FLAT);
 int auto_slices(uint64_t irc_bytes);

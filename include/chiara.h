@@ -111,16 +111,24 @@ int chr_comm_set_slices(chr_comm* comm, int slices);
 /* Where the radix/batch reductions are evaluated.  The result bits never depend on it: every
  * element gets the reference's expression (recexch phases in neighbour order, folds, lane
  * reduction in stage order) whatever the schedule.
- *   CHR_SCHEDULE_REFERENCE  the reference's communication: owner lanes / root nodes reduce
+ *   CHR_SCHEDULE_REFERENCE  the reference's reductions at its owner lanes / root nodes, its
+ *                           recexch exchanges; results spread by a link-balanced distribute
  *   CHR_SCHEDULE_BALANCED   single-phase geometries (k == b, or b == 1): each rank evaluates
  *                           1/n of every chunk, hierarchical exchanges
  *   CHR_SCHEDULE_FLAT       (default) any geometry: each rank gathers the n-1 other inputs of
  *                           its piece directly over the xGMI mesh, evaluates the expression
  *                           tree, then the pieces are allgathered; 2S/n per link in all
- * Env CHR_SCHEDULE=reference|balanced|flat sets the default.  DESIGN.md §5. */
+ *   CHR_SCHEDULE_EXACT      the reference's communication pattern end to end, unsliced:
+ *                           phases 0-2 as REFERENCE, then its inter-node bcast + intra-node
+ *                           k-port Bruck allgather with rotation (all_reduce_radix_batch.cpp
+ *                           :552-756), or its k-nomial scatter (reduce_scatter_radix_batch.cpp
+ *                           :572-627); per GPU pair the same bytes as the reference
+ *                           (tests/golden/msg_trace.json).  For multi-node shapes.
+ * Env CHR_SCHEDULE=reference|balanced|flat|exact sets the default.  DESIGN.md §5. */
 #define CHR_SCHEDULE_REFERENCE 0
 #define CHR_SCHEDULE_BALANCED 1
 #define CHR_SCHEDULE_FLAT 2
+#define CHR_SCHEDULE_EXACT 3
 int chr_comm_set_schedule(chr_comm* comm, int schedule);
 /* Compute/xGMI overlap (default on; env CHR_OVERLAP=0): local reductions run on a second HIP
  * stream, ordered against the RCCL transfers by events where the plan's data dependencies

@@ -34,10 +34,11 @@ def _worker(rank, world, port, cases, q):
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        for (mode, k, b, count, dtype, slices) in cases:
+        for case in cases:
+            (mode, k, b, count, dtype, slices), sched = case[:6], (case[6] if len(case) > 6 else None)
             in_n = count if mode == ca.MODE_ALLREDUCE else count * world
             send = po.fill(in_n, dtype, 0, 99, rank)
-            plan = ca.parse_plan(ca.describe_plan(mode, world, rank, k, b, count, slices))
+            plan = ca.parse_plan(ca.describe_plan(mode, world, rank, k, b, count, slices, sched))
             st = plan_sim.RankState(plan, send, None, dtype)
             for op in plan["pre"]:
                 plan_sim.run_local(st, op, dtype, "sum")
@@ -84,7 +85,9 @@ def test_gloo_world2():
 
     _run(2, [(ca.MODE_ALLREDUCE, 2, 1, 2 * 1000, "f32", 1), (ca.MODE_ALLREDUCE, 2, 2, 2 * 1000, "f32", 1),
              (ca.MODE_REDUCE_SCATTER, 2, 1, 4096, "f32", 1), (ca.MODE_REDUCE_SCATTER, 2, 2, 4096, "bf16", 1),
-             (ca.MODE_ALLREDUCE, 2, 2, 2 * 4096, "f32", 4), (ca.MODE_REDUCE_SCATTER, 2, 1, 4096, "f32", 3)])
+             (ca.MODE_ALLREDUCE, 2, 2, 2 * 4096, "f32", 4), (ca.MODE_REDUCE_SCATTER, 2, 1, 4096, "f32", 3),
+             (ca.MODE_ALLREDUCE, 2, 2, 2 * 1000, "f32", 1, ca.SCHEDULE_EXACT),
+             (ca.MODE_REDUCE_SCATTER, 2, 2, 4096, "f32", 1, ca.SCHEDULE_EXACT)])
 
 
 @pytest.mark.slow
@@ -93,4 +96,6 @@ def test_gloo_world4():
 
     _run(4, [(ca.MODE_ALLREDUCE, 4, 4, 4 * 333, "f32", 1), (ca.MODE_ALLREDUCE, 2, 2, 4 * 333, "bf16", 1),
              (ca.MODE_ALLREDUCE, 3, 4, 4 * 100, "f32", 1), (ca.MODE_REDUCE_SCATTER, 2, 4, 50, "f32", 1),
-             (ca.MODE_ALLREDUCE, 4, 4, 4 * 2048, "f32", 3), (ca.MODE_REDUCE_SCATTER, 2, 2, 1500, "bf16", 2)])
+             (ca.MODE_ALLREDUCE, 4, 4, 4 * 2048, "f32", 3), (ca.MODE_REDUCE_SCATTER, 2, 2, 1500, "bf16", 2),
+             (ca.MODE_ALLREDUCE, 2, 4, 4 * 333, "f32", 1, ca.SCHEDULE_EXACT),
+             (ca.MODE_REDUCE_SCATTER, 4, 4, 50, "f32", 1, ca.SCHEDULE_EXACT)])

@@ -83,6 +83,27 @@ def test_local_group_matches_reference_golden(gu, groups, golden):
     assert not bad, f"{len(bad)} device/reference mismatches, e.g. {bad[:5]}"
 
 
+def test_local_group_exact_schedule_matches_reference_golden(gu, groups, golden):
+    """The exact schedule (reference messages end to end) on the device, every radix/batch golden case."""
+    cases, _ = golden
+    bad = []
+    for c in cases:
+        if c["mode"] == "ag":
+            continue
+        n = c["n"]
+        in_n = c["count"] * n if c["mode"] == "rs" else c["count"]
+        sends = [po.fill(in_n, c["dtype"], c["pattern"], c["seed"], r) for r in range(n)]
+        g = groups(n)
+        g.set_schedule(ca.SCHEDULE_EXACT)
+        try:
+            outs = run_local(gu, g, c["mode"], sends, c["k"], c["b"], c["dtype"], c["op"], bool(c["inplace"]))
+        finally:
+            g.set_schedule(ca.SCHEDULE_FLAT)
+        if hashlib.sha256(b"".join(o.tobytes() for o in outs)).hexdigest() != c["sha256"]:
+            bad.append(c["id"])
+    assert not bad, f"{len(bad)} device/reference mismatches, e.g. {bad[:5]}"
+
+
 @pytest.mark.parametrize("mode,n,k,b,dtype", [
     ("ar", 8, 4, 4, "f32"), ("ar", 8, 4, 4, "bf16"), ("ar", 8, 2, 2, "f32"), ("ar", 8, 3, 4, "bf16"),
     ("ar", 8, 2, 4, "bf16"), ("ar", 8, 4, 8, "f32"), ("rs", 2, 2, 1, "f32"), ("rs", 2, 2, 2, "f32"),
@@ -247,15 +268,15 @@ def test_allgather_large_bit_exact(gu, groups, n, k, b, inplace):
 @pytest.mark.parametrize("n,k,b,dtype", [(8, 4, 4, "f32"), (8, 4, 4, "bf16"), (8, 8, 8, "f32"), (8, 2, 1, "f32"),
                                          (4, 4, 4, "f32"), (2, 2, 2, "f32")])
 def test_schedules_bit_identical(gu, groups, n, k, b, dtype):
-    """Flat, balanced and reference-communication schedules, 8 MiB per rank, pipelined:
-    identical bits, all equal to the oracle."""
+    """Flat, balanced, reference-communication and exact (the reference's messages end to end,
+    unsliced) schedules, 8 MiB per rank: identical bits, all equal to the oracle."""
     count = (1 << 21) // (2 if dtype == "bf16" else 1) * 2
     count -= count % n
     sends = [po.fill(count, dtype, po.PAT_UNIFORM, 5, r) for r in range(n)]
     g = groups(n)
     outs = {}
     try:
-        for sch in (ca.SCHEDULE_FLAT, ca.SCHEDULE_BALANCED, ca.SCHEDULE_REFERENCE):
+        for sch in (ca.SCHEDULE_FLAT, ca.SCHEDULE_BALANCED, ca.SCHEDULE_REFERENCE, ca.SCHEDULE_EXACT):
             g.set_schedule(sch)
             g.set_slices(3)
             outs[sch] = run_local(gu, g, "ar", sends, k, b, dtype, "sum")
@@ -277,7 +298,7 @@ def test_balanced_reduce_scatter_equals_owner_lane(gu, groups, n, k, b):
     want = po.reduce_scatter_radix_batch(sends, k, b, "f32", "sum")
     g = groups(n)
     try:
-        for sch in (ca.SCHEDULE_FLAT, ca.SCHEDULE_BALANCED, ca.SCHEDULE_REFERENCE):
+        for sch in (ca.SCHEDULE_FLAT, ca.SCHEDULE_BALANCED, ca.SCHEDULE_REFERENCE, ca.SCHEDULE_EXACT):
             g.set_schedule(sch)
             got = run_local(gu, g, "rs", sends, k, b, "f32", "sum")
             for r in range(n):

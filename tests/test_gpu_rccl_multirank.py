@@ -139,12 +139,20 @@ def test_rccl_allgather_world4_and_8():
 
 
 def test_rccl_schedules_and_overlap_world4():
-    """The two-stream executor (overlap on/off) under all three schedules, allreduce and
+    """The two-stream executor (overlap on/off) under all four schedules, allreduce and
     reduce-scatter, 4 ranks over RCCL: bit-exact vs the oracle."""
     cases = []
-    for sched in (0, 1, 2):
+    for sched in (0, 1, 2, 3):
         for ov in (True, False):
             cases.append(("ar", 4, 4, 1 << 18, "f32", False, 4, sched, ov))
             cases.append(("rs", 2, 2, 1 << 15, "f32", False, 3, sched, ov))
     cases.append(("ar", 2, 4, 1 << 18, "bf16", False, 5, 2, True))  # multi-phase tree, flat
     _run(4, cases, timeout=600)
+
+
+def test_rccl_exact_schedule_world8():
+    """The reference's own messages end to end (bcast + left-over k-Bruck at C4; k-nomial
+    scatter for reduce-scatter), 8 ranks over RCCL: bit-exact vs the oracle."""
+    _run(8, [("ar", 4, 4, 1 << 18, "f32", False, 0, 3, True), ("ar", 2, 8, 8 * 1001, "bf16", False, 0, 3, True),
+             ("ar", 2, 2, 1 << 16, "f32", True, 0, 3, False), ("rs", 4, 8, 1 << 14, "f32", False, 0, 3, True),
+             ("rs", 2, 4, 999, "f32", False, 0, 3, True)], timeout=600)
