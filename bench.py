@@ -320,7 +320,7 @@ def bench_allreduce(args):
         ach = float(busiest[1]) / (float(busiest[0]) * 1e-3) / 1e9
         roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
-                    "kernel": "chr::k_reduce_vec (fused bucket reductions inside the collective, busiest rank)",
+                    "kernel": "chr::k_reduce_tree / k_reduce_vec (fused reductions inside the collective, busiest rank)",
                     "algorithmic_bytes_per_call": float(busiest[1]), "launches_per_call": int(busiest[2]),
                     "kernel_ms_per_call": round(float(busiest[0]), 4)}
     # bytes on the busiest directed link of this schedule (max over ranks; slicing only splits messages)
@@ -383,8 +383,9 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
     """Context, not the metric: on the same buffers and ranks, (1) RCCL's own ncclAllReduce
     (torch.distributed nccl group), (2) the reference's MPICH ring baseline
     (testing/mpich_implementations/all_reduce/allreduce_ring.cpp) run on libchiara's executor and
-    (3) the metric's own schedule with the reductions on the transfer stream (no overlap) and
-    (4) its arithmetic under the balanced and the reference-route schedules."""
+    (3) the metric's own schedule with the reductions on the transfer stream (no overlap),
+    (4) its arithmetic under the balanced, reference-route and exact (the reference's messages
+    end to end) schedules and (5) the flat schedule at pipeline depths 1, 2 and 4."""
     steps, warm = max(1, min(args.steps, 20)), 2
     S = count * (4 if dt == ca.FLOAT32 else 2)
     out = {"steps": steps}
@@ -415,13 +416,21 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
         out["radix_batch_no_overlap"] = entry(_timed_max(torch, dist, radix, steps, warm))
     finally:
         comm.set_overlap(True)
-    for name, sch in (("radix_batch_balanced", ca.SCHEDULE_BALANCED), ("radix_batch_reference_route",
-                                                                      ca.SCHEDULE_REFERENCE)):
+    for name, sch in (("radix_batch_balanced", ca.SCHEDULE_BALANCED),
+                      ("radix_batch_reference_route", ca.SCHEDULE_REFERENCE),
+                      ("radix_batch_exact_reference_messages", ca.SCHEDULE_EXACT)):
         comm.set_schedule(sch)
         try:
             out[name] = entry(_timed_max(torch, dist, radix, steps, warm))
         finally:
             comm.set_schedule(ca.SCHEDULE_FLAT)
+    # pipeline depth of the metric's own (flat) schedule: automatic is 8 slices at 1 GiB
+    for P in (1, 2, 4):
+        comm.set_slices(P)
+        try:
+            out[f"radix_batch_flat_slices{P}"] = entry(_timed_max(torch, dist, radix, steps, warm))
+        finally:
+            comm.set_slices(0)
     return out
 
 
