@@ -295,6 +295,7 @@ def bench_allreduce(args):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ca.check(ca.all_reduce_radix_batch(send, recv, count, dt, ca.SUM, comm, k, b, async_op=True))
+    t_enq = time.perf_counter() - t0  # host time to enqueue every call (RCCL groups, launches, events)
     torch.cuda.synchronize()
     dist.barrier()
     el = time.perf_counter() - t0
@@ -346,6 +347,8 @@ def bench_allreduce(args):
                        "schedule": os.environ.get("CHR_SCHEDULE", "flat"),
                        "parallelism": f"collective x{world}"},
             "algbw_GBps": round(algbw, 2), "busbw_GBps": round(busbw, 2),
+            # rank 0's host enqueue time per call: close to ms_per_step would mean host-bound
+            "host_enqueue_ms_per_call": round(t_enq / args.steps * 1e3, 4),
             "xgmi_roofline": {"per_link_GBps": XGMI_LINK_GBPS, "aggregate_GBps": 7 * XGMI_LINK_GBPS,
                               "busbw_frac_per_link": round(busbw / XGMI_LINK_GBPS, 4),
                               "busbw_frac_aggregate": round(busbw / (7 * XGMI_LINK_GBPS), 4),
