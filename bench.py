@@ -388,7 +388,8 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
     (testing/mpich_implementations/all_reduce/allreduce_ring.cpp) run on libchiara's executor and
     (3) the metric's own schedule with the reductions on the transfer stream (no overlap),
     (4) its arithmetic under the balanced, reference-route and exact (the reference's messages
-    end to end) schedules and (5) the flat schedule at pipeline depths 1, 2 and 4."""
+    end to end) schedules, (5) the flat schedule at pipeline depths 1, 2 and 4 and (6) the other
+    multi-GPU BASELINE configs, C3 and C5 (baseline_configs)."""
     steps, warm = max(1, min(args.steps, 20)), 2
     S = count * (4 if dt == ca.FLOAT32 else 2)
     out = {"steps": steps}
@@ -434,6 +435,47 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
             out[f"radix_batch_flat_slices{P}"] = entry(_timed_max(torch, dist, radix, steps, warm))
         finally:
             comm.set_slices(0)
+    out.update(baseline_configs(args, ca, torch, dist, comm, world, dev, steps, warm))
+    return out
+
+
+def baseline_configs(args, ca, torch, dist, comm, world, dev, steps, warm):
+    """The other multi-GPU BASELINE configs at this world size, default schedule, same run:
+    C3 (fp32 reduce-scatter, radix 2, 256 MiB send buffer; b = 1 and 2) and C5 (bf16 allreduce,
+    b = 4 ("4x2": 4 ranks per group x 2 groups), k = 4, 1 GiB, compute/xGMI overlap) at 8 ranks."""
+    out = {}
+    try:
+        rs_send = (256 << 20) // 4  # elements in the send buffer
+        rc = rs_send // world
+        s_rs = torch.empty(rc * world * 4, dtype=torch.uint8, device=dev)
+        r_rs = torch.empty(rc * 4, dtype=torch.uint8, device=dev)
+        ca.check(ca.fill(s_rs, rc * world, ca.FLOAT32, 0, SEED, int(os.environ["RANK"]), stream=comm.stream))
+        for b in sorted({1, 2} & {d for d in range(1, world + 1) if world % d == 0}):
+            def rs():
+                ca.check(ca.reduce_scatter_radix_batch(s_rs, r_rs, rc, ca.FLOAT32, ca.SUM, comm, 2, b, async_op=True))
+            el = _timed_max(torch, dist, rs, steps, warm)
+            algbw = rc * world * 4 * steps / el / 1e9  # nccl-tests: send-buffer bytes / time
+            out[f"c3_reduce_scatter_fp32_k2_b{b}_256MiB"] = {
+                "algbw_GBps": round(algbw, 2), "busbw_GBps": round(algbw * (world - 1) / world, 2),
+                "ms_per_call": round(el / steps * 1e3, 4)}
+        del s_rs, r_rs
+        if world == 8:
+            cnt = (1 << 30) // 2
+            s5 = torch.empty(cnt * 2, dtype=torch.uint8, device=dev)
+            r5 = torch.empty(cnt * 2, dtype=torch.uint8, device=dev)
+            ca.check(ca.fill(s5, cnt, ca.BFLOAT16, 0, SEED, int(os.environ["RANK"]), stream=comm.stream))
+
+            def c5():
+                ca.check(ca.all_reduce_radix_batch(s5, r5, cnt, ca.BFLOAT16, ca.SUM, comm, 4, 4, async_op=True))
+            el = _timed_max(torch, dist, c5, steps, warm)
+            algbw = cnt * 2 * steps / el / 1e9
+            out["c5_allreduce_bf16_k4_b4_1GiB"] = {
+                "algbw_GBps": round(algbw, 2), "busbw_GBps": round(algbw * 2 * (world - 1) / world, 2),
+                "ms_per_call": round(el / steps * 1e3, 4)}
+            del s5, r5
+    except Exception as e:  # context only: never fail the metric line for it
+        out["baseline_configs_error"] = str(e)[:200]
+    torch.cuda.empty_cache()
     return out
 
 
