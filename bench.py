@@ -96,6 +96,33 @@ def cpu_baseline(seconds):
                       f"{calls} calls in {dt:.1f} s, 1 thread (nproc={os.cpu_count()})"}
 
 
+def cpu_baseline_collective(world, k, b, gpu_bytes_per_rank):
+    """N>1: the REAL reference all_reduce_radix_batch (oracle/_ref/ref_timer: the reference file
+    compiled unchanged against MPICH) on `world` host cores, one MPI rank per core, same (k, b).
+    Bounded sample: 64 MiB fp32 per rank instead of 1 GiB (the reference takes ~3 s per 1 GiB call
+    at 8 ranks), 3 calls, max over ranks.  Same value definition as the GPU line."""
+    exe = os.path.join(REPO, "oracle", "_ref", "ref_timer")
+    mpiexec = "/opt/conda/bin/mpiexec"
+    if not (os.path.exists(exe) and os.path.exists(mpiexec)):
+        return None
+    elems = (1 << 24) - (1 << 24) % world
+    reps = 3
+    try:
+        out = subprocess.run([mpiexec, "-bind-to", "core", "-n", str(world), exe, "ar", str(k), str(b), str(elems),
+                              str(reps)], capture_output=True, text=True, timeout=300)
+        if out.returncode != 0:
+            return None
+        r = json.loads(out.stdout.strip().splitlines()[-1])
+    except Exception:
+        return None
+    t = r["seconds_per_call"]
+    return {"value": round(world * elems * 4 / t / 1e9, 3), "unit": "GB/s", "cores": world, "kind": "reference",
+            "sample": f"reference all_reduce_radix_batch (all_reduce_radix_batch.cpp compiled unchanged, MPICH 3.3.2), "
+                      f"{world} ranks bound to {world} host cores, k={k}, b={b}, {elems * 4 >> 20} MiB fp32 per rank "
+                      f"(bounded sample of the {gpu_bytes_per_rank >> 20} MiB per rank workload), {reps} calls, max over ranks: "
+                      f"{t * 1e3:.1f} ms per call (nproc={os.cpu_count()})"}
+
+
 def pmc_traffic(kernel_key):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if any."""
     path = os.path.join(REPO, "profiles", "pmc_latest.json")
@@ -336,6 +363,12 @@ def bench_allreduce(args):
     link_bytes = int(lb.item())
     compare = None if args.no_compare else compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b,
                                                          world, dev)
+    # the reference CPU+MPI path on this box's host cores, after every GPU timing (rank 0 runs
+    # it; the other ranks wait at the barrier)
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_collective(world, k, b, S)
+    dist.barrier()
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(world * S * args.steps / el / 1e9, 2), "unit": "GB/s",
@@ -356,8 +389,10 @@ def bench_allreduce(args):
                               "busiest_link_bytes": link_bytes,
                               "link_bound_ms": round(link_bytes / (XGMI_LINK_GBPS * 1e9) * 1e3, 4),
                               "frac": round(link_bytes / (XGMI_LINK_GBPS * 1e9) / (el / args.steps), 4)},
-            "roofline": roofline, "cpu_baseline": None,
+            "roofline": roofline, "cpu_baseline": cpu,
         }
+        if cpu:
+            line["gpu_vs_cpu"] = round(line["value"] / cpu["value"], 1)
         if compare:
             line["compare"] = compare
         emit(line)
