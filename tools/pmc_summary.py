@@ -6,7 +6,7 @@ gfx950 correction from MI355X_MICROARCH.md §HBM: FETCH_SIZE counts 128-B reques
 wide (16 B/lane) coalesced streaming read as 64 B.  Collected in separate passes (TCC
 slots: FETCH_SIZE costs 3, WRITE_SIZE 2).
 
-usage: tools/pmc_summary.py <pmc_FETCH_SIZE dir> <pmc_WRITE_SIZE dir> <kernel key> <alg bytes> [out.json]
+usage: tools/pmc_summary.py <pmc_FETCH_SIZE dir> <pmc_WRITE_SIZE dir> <kernel key> <alg bytes> [out.json] [kernel name needle]
 """
 import csv
 import glob
@@ -26,10 +26,11 @@ def per_launch(d, counter, needle):
 
 def main():
     fdir, wdir, key, alg = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
-    out = sys.argv[5] if len(sys.argv) > 5 else os.path.join(os.path.dirname(__file__), "..", "profiles",
+    out = sys.argv[5] if len(sys.argv) > 5 and sys.argv[5] != "-" else os.path.join(os.path.dirname(__file__), "..", "profiles",
                                                                "pmc_latest.json")
-    fetch_kb, nf, ff = per_launch(fdir, "FETCH_SIZE", "k_reduce_vec")
-    write_kb, nw, wf = per_launch(wdir, "WRITE_SIZE", "k_reduce_vec")
+    needle = sys.argv[6] if len(sys.argv) > 6 else "k_reduce_vec"
+    fetch_kb, nf, ff = per_launch(fdir, "FETCH_SIZE", needle)
+    write_kb, nw, wf = per_launch(wdir, "WRITE_SIZE", needle)
     read_b = fetch_kb * 1024 * 2
     write_b = write_kb * 1024
     try:
