@@ -338,7 +338,14 @@ def bench_allreduce(args):
     ca.check(ca.all_reduce_radix_batch(send, recv, count, dt, ca.SUM, comm, k, b, async_op=True))
     torch.cuda.synchronize()
     red_ms, red_bytes, red_n = comm.profile_read()
+    phases = comm.profile_phases()  # transfer ms per plan phase (DEBUG_MODE phase timers' analogue)
     comm.profile(False)
+    allph = [None] * world
+    dist.all_gather_object(allph, phases)
+    phases_ms = {}
+    for ph in allph:  # max over ranks, per phase
+        for nm, v in ph.items():
+            phases_ms[nm] = round(max(phases_ms.get(nm, 0.0), v), 4)
     stats = torch.tensor([red_ms, red_bytes, float(red_n)], dtype=torch.float64)
     gathered = [torch.zeros_like(stats) for _ in range(world)]
     dist.all_gather(gathered, stats)
@@ -390,6 +397,8 @@ def bench_allreduce(args):
                               "link_bound_ms": round(link_bytes / (XGMI_LINK_GBPS * 1e9) * 1e3, 4),
                               "frac": round(link_bytes / (XGMI_LINK_GBPS * 1e9) / (el / args.steps), 4)},
             "roofline": roofline, "cpu_baseline": cpu,
+            # one profiled call (overlap on): transfer ms per plan phase, max over ranks
+            "phase_transfer_ms": phases_ms,
         }
         if cpu:
             line["gpu_vs_cpu"] = round(line["value"] / cpu["value"], 1)

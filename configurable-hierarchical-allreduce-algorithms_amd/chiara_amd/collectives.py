@@ -145,7 +145,7 @@ class Comm:
         check(lib().chr_comm_set_schedule(self._h, int(schedule)))
 
     def profile(self, enable=True):
-        """Time every fused reduction launch of this communicator (HIP events)."""
+        """Time every fused reduction launch and every step's RCCL group of this communicator (HIP events)."""
         check(lib().chr_comm_profile(self._h, 1 if enable else 0))
 
     def profile_read(self, reset=True):
@@ -154,6 +154,19 @@ class Comm:
         check(lib().chr_comm_profile_read(self._h, ctypes.byref(ms), ctypes.byref(by), ctypes.byref(n),
                                           1 if reset else 0))
         return ms.value, by.value, n.value
+
+    def profile_phases(self, reset=True):
+        """{phase: transfer milliseconds} of the steps since the last reset (profiling on)."""
+        n = lib().chr_comm_profile_phases(self._h, None, 0, 0)
+        if n < 0:
+            raise ChiaraError(1, "profile_phases")
+        buf = ctypes.create_string_buffer(n + 1)
+        lib().chr_comm_profile_phases(self._h, buf, n + 1, 1 if reset else 0)
+        out = {}
+        for ln in buf.value.decode().splitlines():
+            name, ms = ln.rsplit(" ", 1)
+            out[name] = float(ms)
+        return out
 
     @property
     def stream(self):

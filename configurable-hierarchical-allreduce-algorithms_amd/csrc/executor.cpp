@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cctype>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -86,6 +87,11 @@ struct ReduceProfile {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, spare;
     double ms = 0, bytes = 0;
     long launches = 0;
+    // per-phase transfer time (the reference's DEBUG_MODE phase timers, all_reduce_radix_batch.cpp
+    // :228-232, :480-489, :542-548, :572-578, :758-764): events around each step's RCCL group on
+    // the transfer stream, summed per phase name (the step label without slice suffixes)
+    std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> steps_pending;
+    std::map<std::string, double> phase_ms;
     std::pair<hipEvent_t, hipEvent_t> take() {
         if (!spare.empty()) {
             auto e = spare.back();
@@ -105,6 +111,32 @@ struct ReduceProfile {
             spare.push_back(e);
         }
         pending.clear();
+        for (auto& s : steps_pending) {
+            float t = 0;
+            if (hipEventSynchronize(s.second.second) == hipSuccess &&
+                hipEventElapsedTime(&t, s.second.first, s.second.second) == hipSuccess)
+                phase_ms[s.first] += t;
+            spare.push_back(s.second);
+        }
+        steps_pending.clear();
+    }
+    // "t3,phase0/s0,lane/s1" -> "phase0+lane"; "gather/s2" -> "gather"
+    static std::string phase_of(const std::string& label) {
+        std::string out, tok;
+        auto flush = [&]() {
+            const size_t slash = tok.find('/');
+            std::string name = tok.substr(0, slash);
+            if (!name.empty() && !(name[0] == 't' && name.size() > 1 && std::isdigit((unsigned char)name[1]))) {
+                if (out.find(name) == std::string::npos) out += (out.empty() ? "" : "+") + name;
+            }
+            tok.clear();
+        };
+        for (char ch : label) {
+            if (ch == ',') flush();
+            else tok += ch;
+        }
+        flush();
+        return out.empty() ? "step" : out;
     }
     void release() {
         drain();
@@ -269,6 +301,12 @@ int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int d
             if (!e || (rc = hip_code(hipStreamWaitEvent(c->stream, e, 0)))) return e ? rc : CHR_ERR_HIP;
             waited = s.comm_wait;
         }
+        const bool timed = c->prof.on && (!s.sends.empty() || !s.recvs.empty());
+        std::pair<hipEvent_t, hipEvent_t> sev{nullptr, nullptr};
+        if (timed) {
+            sev = c->prof.take();
+            (void)hipEventRecord(sev.first, c->stream);
+        }
         if (!s.sends.empty() || !s.recvs.empty()) {
             if ((rc = nccl_code(ncclGroupStart()))) return rc;
             for (const chr::Xfer& x : s.sends)
@@ -282,6 +320,10 @@ int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int d
                     return rc;
                 }
             if ((rc = nccl_code(ncclGroupEnd()))) return rc;
+        }
+        if (timed) {
+            (void)hipEventRecord(sev.second, c->stream);
+            c->prof.steps_pending.push_back({ReduceProfile::phase_of(s.label), sev});
         }
         if (s.post.empty()) continue;
         if (!two) {
@@ -509,6 +551,25 @@ int chr_comm_profile_read(chr_comm* c, double* reduce_ms, double* reduce_bytes, 
         c->prof.launches = 0;
     }
     return CHR_SUCCESS;
+}
+
+long chr_comm_profile_phases(chr_comm* c, char* buf, size_t len, int reset) {
+    if (!c) return -1;
+    (void)hipSetDevice(c->device);
+    c->prof.drain();
+    std::string s;
+    char line[160];
+    for (const auto& kv : c->prof.phase_ms) {
+        std::snprintf(line, sizeof line, "%s %.6f\n", kv.first.c_str(), kv.second);
+        s += line;
+    }
+    if (buf && len) {
+        const size_t n = s.size() < len - 1 ? s.size() : len - 1;
+        std::memcpy(buf, s.data(), n);
+        buf[n] = '\0';
+    }
+    if (reset) c->prof.phase_ms.clear();
+    return (long)s.size();
 }
 
 int chr_comm_set_overlap(chr_comm* c, int enable) {

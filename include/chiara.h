@@ -142,6 +142,13 @@ int chr_comm_set_overlap(chr_comm* comm, int enable);
 int chr_comm_profile(chr_comm* comm, int enable);
 int chr_comm_profile_read(chr_comm* comm, double* reduce_ms, double* reduce_bytes, long* launches,
                           int reset);
+/* Per-phase transfer time while profiling: HIP events around every step's RCCL group on the
+ * transfer stream, summed per phase (the plan step's label without slice suffixes, e.g.
+ * "gather", "fdist", "phase0+lane", "bruck1").  The analogue of the reference's DEBUG_MODE
+ * phase timers (all_reduce_radix_batch.cpp:228-232, :480-489, :542-548, :572-578, :758-764).
+ * Writes "name milliseconds" lines into buf (NUL-terminated, truncated to len) and returns the
+ * full text length; reset != 0 clears the sums. */
+long chr_comm_profile_phases(chr_comm* comm, char* buf, size_t len, int reset);
 
 /* ---- schedule boundary ----------------------------------------------------------------
  * Replaces  int all_reduce_radix_batch(char* sendbuf, char* recvbuf, int count,
