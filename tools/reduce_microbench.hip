@@ -601,6 +601,136 @@ static void focus4_m(size_t bytes, int sets, int rounds) {
     free_sets(S);
 }
 
+// ---- focus5: m = 1 streaming variants not covered above (all nt loads + nt stores) ----------
+// k_pipe: persistent grid, software pipelined: the loads of trip t+1 are issued before trip t's
+// add and store, so reads and writes of neighbouring trips overlap inside each wave.
+template <int U, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_pipe(Args a) {
+    const size_t stride = (size_t)gridDim.x * BLOCK * U;
+    size_t base = (size_t)blockIdx.x * BLOCK * U + threadIdx.x;
+    if (base + (size_t)(U - 1) * BLOCK >= a.nvec) return;  // focus5 sizes are whole trips
+    f32x4 acc[U], x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        acc[u] = __builtin_nontemporal_load(&a.acc[base + (size_t)u * BLOCK]);
+        x[u] = __builtin_nontemporal_load(&a.ins[0][base + (size_t)u * BLOCK]);
+    }
+    for (;;) {
+        const size_t next = base + stride;
+        const bool more = next + (size_t)(U - 1) * BLOCK < a.nvec;
+        f32x4 acc2[U], x2[U];
+        if (more) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                acc2[u] = __builtin_nontemporal_load(&a.acc[next + (size_t)u * BLOCK]);
+                x2[u] = __builtin_nontemporal_load(&a.ins[0][next + (size_t)u * BLOCK]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) __builtin_nontemporal_store(x[u] + acc[u], &a.out[base + (size_t)u * BLOCK]);
+        if (!more) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            acc[u] = acc2[u];
+            x[u] = x2[u];
+        }
+        base = next;
+    }
+}
+
+// k_map: one trip per workgroup, nt, with the workgroup -> address mapping varied.
+//   MAP 0: identity;  1: XCD-contiguous (workgroups dispatch round-robin over the 8 XCDs, so
+//   b -> (b % 8) * (G / 8) + b / 8 gives each XCD one contiguous eighth of the bucket);
+//   2: reversed;  3: input loaded before the accumulator.
+template <int U, int MAP>
+__global__ __launch_bounds__(256) void k_map(Args a) {
+    const unsigned G = gridDim.x, b = blockIdx.x;
+    const unsigned bb = MAP == 1 ? (b % 8) * (G / 8) + b / 8 : MAP == 2 ? G - 1 - b : b;
+    const size_t base = (size_t)bb * 256 * U + threadIdx.x;
+    f32x4 acc[U], x[U];
+    if (MAP == 3) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = __builtin_nontemporal_load(&a.ins[0][base + (size_t)u * 256]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] = __builtin_nontemporal_load(&a.acc[base + (size_t)u * 256]);
+    } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] = __builtin_nontemporal_load(&a.acc[base + (size_t)u * 256]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = __builtin_nontemporal_load(&a.ins[0][base + (size_t)u * 256]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) __builtin_nontemporal_store(x[u] + acc[u], &a.out[base + (size_t)u * 256]);
+}
+
+static void focus5(size_t bytes, int sets, int rounds) {
+    const size_t nvec = bytes / 16;
+    Sets S = make_sets(1, nvec, sets);
+    const int reps = 200;
+    auto args_for = [&](int i) {
+        Args a{};
+        auto& b = S.bufs[i % sets];
+        a.out = b[0];
+        a.acc = b[0];
+        a.ins[0] = b[1];
+        a.nvec = nvec;
+        return a;
+    };
+    char tag[64];
+    std::snprintf(tag, sizeof tag, " sets=%d", sets);
+    auto product = [&]() {
+        double us = time_launches([&](int i) {
+            Args a = args_for(i);
+            const void* ins[1] = {a.ins[0]};
+            chr_reduce_multi(a.out, a.acc, ins, 1, a.nvec * 4, CHR_FLOAT32, CHR_SUM, 0);
+        }, reps);
+        report((std::string("libchiara chr_reduce_multi") + tag).c_str(), 1, bytes, us);
+    };
+    for (int r = 0; r < rounds; ++r) {
+        product();
+#define P(U, BL, G, NAME)                                                                                     \
+    {                                                                                                         \
+        double us = time_launches([&](int i) { hipLaunchKernelGGL((k_pipe<U, BL>), dim3(G), dim3(BL), 0, 0, args_for(i)); }, reps); \
+        report((std::string(NAME) + tag).c_str(), 1, bytes, us);                                              \
+    }
+        P(4, 256, 256, "pipe U4 B256 G256");
+        P(4, 256, 512, "pipe U4 B256 G512");
+        P(4, 256, 1024, "pipe U4 B256 G1024");
+        P(2, 256, 1024, "pipe U2 B256 G1024");
+        P(2, 256, 2048, "pipe U2 B256 G2048");
+        P(4, 512, 512, "pipe U4 B512 G512");
+        P(2, 1024, 512, "pipe U2 B1024 G512");
+#undef P
+#define M_(U, MAP, NAME)                                                                                      \
+    {                                                                                                         \
+        const int G = (int)(nvec / (256 * U));                                                                \
+        double us = time_launches([&](int i) { hipLaunchKernelGGL((k_map<U, MAP>), dim3(G), dim3(256), 0, 0, args_for(i)); }, reps); \
+        report((std::string(NAME) + tag).c_str(), 1, bytes, us);                                              \
+    }
+        M_(4, 0, "map U4 identity");
+        M_(4, 1, "map U4 xcd-contiguous");
+        M_(4, 2, "map U4 reversed");
+        M_(4, 3, "map U4 input-first");
+        M_(8, 0, "map U8 identity");
+        M_(8, 1, "map U8 xcd-contiguous");
+#undef M_
+#define R(U, BL, NAME)                                                                                        \
+    {                                                                                                         \
+        const int G = (int)((nvec + (size_t)BL * U - 1) / ((size_t)BL * U));                                  \
+        double us = time_launches([&](int i) { hipLaunchKernelGGL((k_reg<1, U, BL, true, true, true>), dim3(G), dim3(BL), 0, 0, args_for(i)); }, reps); \
+        report((std::string(NAME) + tag).c_str(), 1, bytes, us);                                              \
+    }
+        R(4, 512, "reg NT U4 B512");
+        R(2, 1024, "reg NT U2 B1024");
+        R(4, 1024, "reg NT U4 B1024");
+#undef R
+        product();
+        std::printf("--\n");
+    }
+    free_sets(S);
+}
+
 // correctness spot check of every variant family against a host sum
 static void check() {
     const size_t nvec = (1 << 20) + 37;
@@ -643,6 +773,29 @@ static void check() {
     reset();
     hipLaunchKernelGGL((k_buf<1, 4, 1, 0, 0>), dim3(777), dim3(256), 0, 0, a);
     verify("buf");
+    {  // whole-trip variants: a multiple of 1024 vectors
+        Args w = a;
+        w.nvec = (nvec / 8192) * 8192;
+        const size_t keep = nvec;
+        auto verify_n = [&](const char* name) {
+            std::vector<f32x4> r(keep);
+            CK(hipMemcpy(r.data(), d0, keep * 16, hipMemcpyDeviceToHost));
+            for (size_t i = 0; i < keep; ++i)
+                for (int c = 0; c < 4; ++c) {
+                    const float want = i < w.nvec ? h0[i][c] + h1[i][c] : h0[i][c];
+                    if (r[i][c] != want) {
+                        std::printf("CHECK FAIL %s at %zu\n", name, i);
+                        std::exit(2);
+                    }
+                }
+        };
+        reset();
+        hipLaunchKernelGGL((k_pipe<4, 256>), dim3(3), dim3(256), 0, 0, w);
+        verify_n("pipe");
+        reset();
+        hipLaunchKernelGGL((k_map<4, 1>), dim3((unsigned)(w.nvec / 1024)), dim3(256), 0, 0, w);
+        verify_n("map-xcd");
+    }
     CK(hipFree(d0));
     CK(hipFree(d1));
     std::printf("variant correctness: ok\n");
@@ -698,6 +851,10 @@ int main(int argc, char** argv) {
     check();
     if (argc > 1 && std::string(argv[1]) == "layout") {
         layout_mode();
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus5") {
+        focus5(64 << 20, 16, 3);
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus4") {
