@@ -18,9 +18,11 @@
 //    +15-40 % over plain accesses; plain stays faster on small, cache-warm calls);
 //  * no LDS: a pure stream has no reuse, and staging through LDS (global_load_lds) was
 //    measured null-to-negative for this regime (profiles/);
-//  * no XCD remap: no inter-workgroup reuse, so L2 placement cannot matter;
+//  * no XCD remap: no inter-workgroup reuse; an XCD-contiguous workgroup map measured 0.88x
+//    (HBM wants every XCD spread over all addresses, profiles/r01/microbench_focus5.txt);
 //  * IEEE semantics kept bit-exact with the CPU oracle: no fast-math, selects (not
-//    v_max) for MAX/MIN, int32 wraps, bf16 = f32 op then RNE per step with NaN kept.
+//    v_max) for MAX/MIN, int32 wraps, bf16 = f32 op then RNE per step with NaN kept
+//    (v_cvt_pk_bf16_f32, reduce_common.hpp).
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -28,7 +30,6 @@
 #include "reduce_common.hpp"
 
 namespace chr {
-
 
 constexpr int kMaxFanIn = 8;
 
@@ -68,7 +69,6 @@ struct VecArgs {
     const u32x4* ins[kMaxFanIn];
     size_t nvec;
 };
-
 
 // U vectors (16 B each) per lane per trip; all M+1 operands of the trip are loaded
 // before the first add so (M+1)*U*16 bytes per lane are in flight.  NT: non-temporal
