@@ -48,3 +48,15 @@ def test_no_cpu_fallback_for_compute():
 
     h = ctypes.c_void_p()
     assert g(ctypes.byref(h), 2, 0) == 6  # CHR_ERR_NO_DEVICE
+
+
+def test_profile_phases_rejects_null_comm():
+    assert ca.lib().chr_comm_profile_phases(None, None, 0, 0) == -1
+
+
+def test_reduce_tree_rejects_bad_args_without_device():
+    import ctypes
+
+    leaves = (ctypes.c_void_p * 2)(0x1000, 0x2000)
+    assert ca.lib().chr_reduce_tree(0x3000, leaves, 2, bytes([0, 1]), None, 0, 9, ca.SUM, None) == 1  # bad dtype
+    assert ca.lib().chr_reduce_tree(0x3000, None, 2, bytes([0, 1]), None, 0, ca.FLOAT32, ca.SUM, None) == 1

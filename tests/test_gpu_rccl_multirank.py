@@ -156,3 +156,56 @@ def test_rccl_exact_schedule_world8():
     _run(8, [("ar", 4, 4, 1 << 18, "f32", False, 0, 3, True), ("ar", 2, 8, 8 * 1001, "bf16", False, 0, 3, True),
              ("ar", 2, 2, 1 << 16, "f32", True, 0, 3, False), ("rs", 4, 8, 1 << 14, "f32", False, 0, 3, True),
              ("rs", 2, 4, 999, "f32", False, 0, 3, True)], timeout=600)
+
+
+def _phase_worker(rank, world, port, q):
+    os.environ["NCCL_HOSTID"] = f"chiara-test-host-{rank}"
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    os.environ.setdefault("NCCL_IB_DISABLE", "1")
+    sys.path[:0] = [HERE, os.path.join(REPO, "oracle"),
+                    os.path.join(REPO, "configurable-hierarchical-allreduce-algorithms_amd")]
+    import torch
+    import torch.distributed as dist
+
+    import chiara_amd as ca
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    comm = ca.Comm.from_torch_distributed(device=0)
+    try:
+        count = 1 << 16
+        send = torch.ones(count, dtype=torch.float32, device="cuda:0")
+        recv = torch.zeros(count, dtype=torch.float32, device="cuda:0")
+        out = {}
+        for name, sch in (("flat", ca.SCHEDULE_FLAT), ("exact", ca.SCHEDULE_EXACT)):
+            comm.set_schedule(sch)
+            comm.profile(True)
+            ca.check(ca.all_reduce_radix_batch(send, recv, count, ca.FLOAT32, ca.SUM, comm, 4, 4))
+            comm.profile_read()
+            out[name] = comm.profile_phases()
+            comm.profile(False)
+        q.put((rank, out, float(recv[7].item())))
+    finally:
+        comm.destroy()
+        dist.destroy_process_group()
+
+
+def test_rccl_profile_phases_world4():
+    """chr_comm_profile_phases: per-phase transfer times named after the plan's phases."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_phase_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    alive = [p for p in procs if p.is_alive()]
+    for p in alive:
+        p.kill()
+    assert not alive and all(p.exitcode == 0 for p in procs)
+    for _ in range(4):
+        rank, out, v = q.get()
+        assert v == 4.0
+        assert set(out["flat"]) == {"gather", "fdist"}, out
+        assert all(ms > 0 for ms in out["flat"].values())
+        assert any(k.startswith("bruck") for k in out["exact"]) and "bcast" not in out["exact"], out
