@@ -34,7 +34,7 @@ MODE_ALLREDUCE, MODE_REDUCE_SCATTER = 0, 1
 MODE_MPICH_RING, MODE_MPICH_RD, MODE_MPICH_RSAG, MODE_MPICH_RECEXCH = 2, 3, 4, 5
 MODE_MPICH_KRSAG, MODE_MPICH_RMULT = 6, 7
 MODE_ALLGATHER = 8
-SCHEDULE_REFERENCE, SCHEDULE_BALANCED, SCHEDULE_FLAT, SCHEDULE_EXACT = 0, 1, 2, 3
+SCHEDULE_REFERENCE, SCHEDULE_BALANCED, SCHEDULE_FLAT, SCHEDULE_EXACT, SCHEDULE_FLAT_AG = 0, 1, 2, 3, 4
 REDUCE_RUNNING_FIRST = 1  # chr_reduce_multi_ex flag (MPICH_do_reduce operand order)
 
 
@@ -356,10 +356,12 @@ def parse_plan(text):
             plan["pre"].append(local(tok[1:]))
         elif tok[0] == "step":
             wait = int(tok[3].split("=")[1]) if len(tok) > 3 and tok[3].startswith("wait=") else -1
-            cur = {"label": tok[2], "wait": wait, "sends": [], "recvs": [], "post": []}
+            cur = {"label": tok[2], "wait": wait, "sends": [], "recvs": [], "allgathers": [], "post": []}
             plan["steps"].append(cur)
         elif tok[0] in ("send", "recv"):
             cur[tok[0] + "s"].append((int(tok[1]), (tok[2], int(tok[3])), int(tok[4])))
+        elif tok[0] == "allgather":  # in-place collective: (region ref, elements per rank)
+            cur["allgathers"].append(((tok[1], int(tok[2])), int(tok[3])))
         else:
             cur["post"].append(local(tok))
     return plan

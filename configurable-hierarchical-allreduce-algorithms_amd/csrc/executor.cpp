@@ -198,7 +198,7 @@ bool is_device_ptr(const void* p) {
 
 using PlanKey = std::tuple<int, int, int, int, uint64_t, int, int, int>;  // mode, rank, k, b, count, dtype size, slices, schedule
 
-// CHR_SCHEDULE = reference | balanced | flat | exact (or 0 / 1 / 2 / 3); default flat
+// CHR_SCHEDULE = reference | balanced | flat | exact | flat_ag (or 0 .. 4); default flat
 // CHR_OVERLAP=0: local ops on the transfer stream (no compute/xGMI overlap); default 1
 int default_overlap() {
     static const int v = [] {
@@ -216,6 +216,7 @@ int default_schedule() {
         if (s == "reference" || s == "0") return (int)chr::SCHED_REFERENCE;
         if (s == "balanced" || s == "1") return (int)chr::SCHED_BALANCED;
         if (s == "exact" || s == "3") return (int)chr::SCHED_EXACT;
+        if (s == "flat_ag" || s == "4") return (int)chr::SCHED_FLAT_AG;
         return (int)chr::SCHED_FLAT;
     }();
     return v;
@@ -301,7 +302,8 @@ int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int d
             if (!e || (rc = hip_code(hipStreamWaitEvent(c->stream, e, 0)))) return e ? rc : CHR_ERR_HIP;
             waited = s.comm_wait;
         }
-        const bool timed = c->prof.on && (!s.sends.empty() || !s.recvs.empty());
+        const bool xfers = !s.sends.empty() || !s.recvs.empty() || !s.allgathers.empty();
+        const bool timed = c->prof.on && xfers;
         std::pair<hipEvent_t, hipEvent_t> sev{nullptr, nullptr};
         if (timed) {
             sev = c->prof.take();
@@ -319,6 +321,18 @@ int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int d
                     (void)ncclGroupEnd();
                     return rc;
                 }
+            if ((rc = nccl_code(ncclGroupEnd()))) return rc;
+        }
+        if (!s.allgathers.empty()) {  // in place: my block already sits at ref + rank*count
+            if ((rc = nccl_code(ncclGroupStart()))) return rc;
+            for (const chr::Coll& x : s.allgathers) {
+                char* base = B.ptr(x.ref);
+                if ((rc = nccl_code(ncclAllGather(base + (size_t)c->rank * x.count * es, base, x.count * es, ncclUint8,
+                                                  c->nccl, c->stream)))) {
+                    (void)ncclGroupEnd();
+                    return rc;
+                }
+            }
             if ((rc = nccl_code(ncclGroupEnd()))) return rc;
         }
         if (timed) {
@@ -451,6 +465,17 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
                     std::fprintf(stderr, "[chiara] plan mismatch: unmatched send step %zu rank %d\n", si, r);
                     return CHR_ERR_UNSUPPORTED;
                 }
+        // allgather collectives: every rank's block r to every other rank, same region
+        for (size_t ci = 0; ci < P[0].steps[si].allgathers.size(); ++ci)
+            for (int r = 0; r < n; ++r)
+                for (int q = 0; q < n; ++q) {
+                    if (q == r) continue;
+                    const chr::Coll& x = P[r].steps[si].allgathers[ci];
+                    const size_t off = (size_t)q * x.count * es;
+                    if ((e = hipMemcpyAsync(B[r].ptr(x.ref) + off, B[q].ptr(P[q].steps[si].allgathers[ci].ref) + off,
+                                            x.count * es, hipMemcpyDeviceToDevice, g->stream)) != hipSuccess)
+                        return hip_code(e);
+                }
         for (int r = 0; r < n; ++r)
             for (const auto& op_ : P[r].steps[si].post)
                 if ((rc = run_local(op_, B[r], dtype, op, g->stream))) return rc;
@@ -579,13 +604,13 @@ int chr_comm_set_overlap(chr_comm* c, int enable) {
 }
 
 int chr_comm_set_schedule(chr_comm* c, int schedule) {
-    if (!c || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_EXACT) return CHR_ERR_INVALID_ARG;
+    if (!c || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_FLAT_AG) return CHR_ERR_INVALID_ARG;
     c->sched = schedule;
     return CHR_SUCCESS;
 }
 
 int chr_local_group_set_schedule(chr_local_group* g, int schedule) {
-    if (!g || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_EXACT) return CHR_ERR_INVALID_ARG;
+    if (!g || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_FLAT_AG) return CHR_ERR_INVALID_ARG;
     g->sched = schedule;
     return CHR_SUCCESS;
 }

@@ -614,7 +614,7 @@ int auto_slices(uint64_t irc_bytes) {
     return (int)std::max<uint64_t>(1, std::min<uint64_t>(8, s));
 }
 
-Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, int slices);
+Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, int slices, bool coll_ag = false);
 static Plan build_plan_impl(Mode mode, int n, int me, int k_in, int b, uint64_t count, int slices, int sched);
 
 // The fused kernel takes at most kPlanFanIn inputs per pass (kMaxFanIn, reduce_kernels.hip)
@@ -694,6 +694,10 @@ static void analyze_deps(Plan& p) {
         std::vector<Region> crd, cwr;  // transfers: sends read, receives write
         for (const Xfer& x : p.steps[t].sends) crd.push_back({x.ref.buf, x.ref.off, x.ref.off + x.count});
         for (const Xfer& x : p.steps[t].recvs) cwr.push_back({x.ref.buf, x.ref.off, x.ref.off + x.count});
+        for (const Coll& x : p.steps[t].allgathers) {
+            crd.push_back({x.ref.buf, x.ref.off + (uint64_t)p.rank * x.count, x.ref.off + (uint64_t)(p.rank + 1) * x.count});
+            cwr.push_back({x.ref.buf, x.ref.off, x.ref.off + (uint64_t)p.g.nranks * x.count});
+        }
         int w = -1;
         for (size_t u = t; u-- > 0 && w < 0;) {
             bool c = false;
@@ -771,8 +775,8 @@ static Plan build_plan_impl(Mode mode, int n, int me, int k_in, int b, uint64_t 
     p.recv_elems = mode == MODE_ALLREDUCE ? g.total : recvcount;
     p.acc_elems = g.total;
     if (g.total == 0) return p;
-    if (sched == SCHED_FLAT && n > 1) {
-        Plan f = build_plan_flat(mode, n, me, k_in, b, g, slices);
+    if ((sched == SCHED_FLAT || sched == SCHED_FLAT_AG) && n > 1) {
+        Plan f = build_plan_flat(mode, n, me, k_in, b, g, slices, sched == SCHED_FLAT_AG);
         if (!f.error) return f;
     }
 
@@ -936,6 +940,8 @@ std::string describe(const Plan& p) {
             o << "send " << x.peer << " " << buf_name(x.ref.buf) << " " << x.ref.off << " " << x.count << "\n";
         for (const Xfer& x : s.recvs)
             o << "recv " << x.peer << " " << buf_name(x.ref.buf) << " " << x.ref.off << " " << x.count << "\n";
+        for (const Coll& x : s.allgathers)
+            o << "allgather " << buf_name(x.ref.buf) << " " << x.ref.off << " " << x.count << "\n";
         for (const LocalOp& op : s.post) local(op);
     }
     return o.str();
@@ -1580,12 +1586,12 @@ bool tree_enabled() {
 
 }  // namespace
 
-Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, int slices) {
+Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, int slices, bool coll_ag) {
     Plan p;
     p.mode = mode;
     p.rank = me;
     p.g = g;
-    p.sched = SCHED_FLAT;
+    p.sched = coll_ag ? SCHED_FLAT_AG : SCHED_FLAT;
     // 1. the reference-order plans of every rank at recvcount = 1, executed symbolically
     const uint64_t cnt1 = mode == MODE_ALLREDUCE ? (uint64_t)n : 1;
     std::vector<Plan> ref;
@@ -1739,6 +1745,17 @@ Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, 
                 }
             }
         } else if (kind == F_DIST) {
+            // equal pieces (every BASELINE size): one in-place ncclAllGather per chunk
+            bool equal = coll_ag;
+            for (int q = 1; q < n && equal; ++q) {
+                uint64_t qa, ql;
+                piece(c, q, &qa, &ql);
+                equal = ql == len && qa == (uint64_t)q * len;
+            }
+            if (equal && len) {
+                for (int N = 0; N < nchunks; ++N) st.allgathers.push_back({{BUF_RECV, (uint64_t)N * g.irc + c.lo}, len});
+                return;
+            }
             for (int q = 0; q < n; ++q) {
                 if (q == me) continue;
                 uint64_t qa, ql;

@@ -57,8 +57,16 @@ struct LocalOp {
     std::vector<uint8_t> comb, swaps;  // L_TREE program
 };
 
+// In-place allgather collective (ncclAllGather) over a region of `nranks * count` elements
+// at `ref`: rank r contributes [ref + r*count, +count) and receives every other block.
+struct Coll {
+    Ref ref;
+    uint64_t count;  // elements per rank
+};
+
 struct Step {
     std::vector<Xfer> sends, recvs;
+    std::vector<Coll> allgathers;  // issued after the step's p2p group
     std::vector<LocalOp> post;
     std::string label;
     // Two-stream execution: this step's transfers must wait for the local ops of step
@@ -122,7 +130,9 @@ void recexch_count_offset(int nranks, int max_phases, int k, std::vector<int>* c
 //                    over the full mesh, evaluated at the piece's rank (build_plan_flat)
 //   SCHED_EXACT      the reference's messages end to end, unsliced: REFERENCE's phases 0-2, then
 //                    its bcast + k-port Bruck allgather (S_BCAST, S_AG) / k-nomial scatter (S_KSCAT)
-enum Sched : int { SCHED_REFERENCE = 0, SCHED_BALANCED = 1, SCHED_FLAT = 2, SCHED_EXACT = 3 };
+//   SCHED_FLAT_AG    SCHED_FLAT with the allgather phase on RCCL's ncclAllGather collective
+//                    (pure data movement, so the bits are unchanged) where the pieces are equal
+enum Sched : int { SCHED_REFERENCE = 0, SCHED_BALANCED = 1, SCHED_FLAT = 2, SCHED_EXACT = 3, SCHED_FLAT_AG = 4 };
 Plan build_plan(Mode mode, int nranks, int rank, int k, int b, uint64_t count, int slices = 1,
                 int sched = SCHED_FLAT);
 int auto_slices(uint64_t irc_bytes);

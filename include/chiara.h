@@ -124,11 +124,15 @@ int chr_comm_set_slices(chr_comm* comm, int slices);
  *                           :552-756), or its k-nomial scatter (reduce_scatter_radix_batch.cpp
  *                           :572-627); per GPU pair the same bytes as the reference
  *                           (tests/golden/msg_trace.json).  For multi-node shapes.
- * Env CHR_SCHEDULE=reference|balanced|flat|exact sets the default.  DESIGN.md §5. */
+ *   CHR_SCHEDULE_FLAT_AG    FLAT with its allgather phase on RCCL's ncclAllGather collective
+ *                           (in place, one per chunk) where the pieces are equal; data
+ *                           movement only, so identical bits
+ * Env CHR_SCHEDULE=reference|balanced|flat|exact|flat_ag sets the default.  DESIGN.md §5. */
 #define CHR_SCHEDULE_REFERENCE 0
 #define CHR_SCHEDULE_BALANCED 1
 #define CHR_SCHEDULE_FLAT 2
 #define CHR_SCHEDULE_EXACT 3
+#define CHR_SCHEDULE_FLAT_AG 4
 int chr_comm_set_schedule(chr_comm* comm, int schedule);
 /* Compute/xGMI overlap (default on; env CHR_OVERLAP=0): local reductions run on a second HIP
  * stream, ordered against the RCCL transfers by events where the plan's data dependencies

@@ -102,6 +102,15 @@ def execute(plans, sends, dtype, rop, inplace=False):
         assert all(all(u) for u in used), f"unmatched send in step {si}"
         for r, ref, data in payload:
             states[r].view(ref, data.size)[:] = data
+        for ci in range(len(plans[0]["steps"][si].get("allgathers", []))):  # in-place allgather collectives
+            blocks = []
+            for r in range(n):
+                (buf, off), cnt = plans[r]["steps"][si]["allgathers"][ci]
+                blocks.append(states[r].view((buf, off + r * cnt), cnt).copy())
+            for r in range(n):
+                (buf, off), cnt = plans[r]["steps"][si]["allgathers"][ci]
+                for q in range(n):
+                    states[r].view((buf, off + q * cnt), cnt)[:] = blocks[q]
         for r in range(n):
             for op in plans[r]["steps"][si]["post"]:
                 run_local(states[r], op, dtype, rop)

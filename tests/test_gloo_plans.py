@@ -54,6 +54,12 @@ def _worker(rank, world, port, cases, q):
                     r.wait()
                 for ref, n, t in landing:
                     st.view(ref, n)[:] = t.numpy().view(send.dtype)
+                for (buf, off), cnt in s.get("allgathers", []):  # in-place allgather collective
+                    mine = torch.from_numpy(st.view((buf, off + rank * cnt), cnt).copy().view(np.uint8))
+                    parts = [torch.empty_like(mine) for _ in range(world)]
+                    dist.all_gather(parts, mine)
+                    for src in range(world):
+                        st.view((buf, off + src * cnt), cnt)[:] = parts[src].numpy().view(send.dtype)
                 for op in s["post"]:
                     plan_sim.run_local(st, op, dtype, "sum")
             out = st.buf["RECV"][: (count if mode == ca.MODE_ALLREDUCE else count)]
@@ -87,7 +93,8 @@ def test_gloo_world2():
              (ca.MODE_REDUCE_SCATTER, 2, 1, 4096, "f32", 1), (ca.MODE_REDUCE_SCATTER, 2, 2, 4096, "bf16", 1),
              (ca.MODE_ALLREDUCE, 2, 2, 2 * 4096, "f32", 4), (ca.MODE_REDUCE_SCATTER, 2, 1, 4096, "f32", 3),
              (ca.MODE_ALLREDUCE, 2, 2, 2 * 1000, "f32", 1, ca.SCHEDULE_EXACT),
-             (ca.MODE_REDUCE_SCATTER, 2, 2, 4096, "f32", 1, ca.SCHEDULE_EXACT)])
+             (ca.MODE_REDUCE_SCATTER, 2, 2, 4096, "f32", 1, ca.SCHEDULE_EXACT),
+             (ca.MODE_ALLREDUCE, 2, 2, 2 * 4096, "f32", 3, ca.SCHEDULE_FLAT_AG)])
 
 
 @pytest.mark.slow
@@ -98,4 +105,5 @@ def test_gloo_world4():
              (ca.MODE_ALLREDUCE, 3, 4, 4 * 100, "f32", 1), (ca.MODE_REDUCE_SCATTER, 2, 4, 50, "f32", 1),
              (ca.MODE_ALLREDUCE, 4, 4, 4 * 2048, "f32", 3), (ca.MODE_REDUCE_SCATTER, 2, 2, 1500, "bf16", 2),
              (ca.MODE_ALLREDUCE, 2, 4, 4 * 333, "f32", 1, ca.SCHEDULE_EXACT),
-             (ca.MODE_REDUCE_SCATTER, 4, 4, 50, "f32", 1, ca.SCHEDULE_EXACT)])
+             (ca.MODE_REDUCE_SCATTER, 4, 4, 50, "f32", 1, ca.SCHEDULE_EXACT),
+             (ca.MODE_ALLREDUCE, 4, 4, 4 * 4096, "bf16", 2, ca.SCHEDULE_FLAT_AG)])

@@ -276,7 +276,8 @@ def test_schedules_bit_identical(gu, groups, n, k, b, dtype):
     g = groups(n)
     outs = {}
     try:
-        for sch in (ca.SCHEDULE_FLAT, ca.SCHEDULE_BALANCED, ca.SCHEDULE_REFERENCE, ca.SCHEDULE_EXACT):
+        for sch in (ca.SCHEDULE_FLAT, ca.SCHEDULE_BALANCED, ca.SCHEDULE_REFERENCE, ca.SCHEDULE_EXACT,
+                    ca.SCHEDULE_FLAT_AG):
             g.set_schedule(sch)
             g.set_slices(3)
             outs[sch] = run_local(gu, g, "ar", sends, k, b, dtype, "sum")

@@ -301,3 +301,31 @@ def test_flat_overlap_dependencies():
         assert labels[waits[f"fdist/s{s}"]] == f"gather/s{s}"
     r = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 1 << 24, 4, ca.SCHEDULE_REFERENCE))
     assert [st["wait"] for st in r["steps"]][1:6] == [0, 1, 2, 3, 4]
+
+
+@pytest.mark.parametrize("n,k,b,dt,slices", [(8, 4, 4, "f32", 2), (8, 2, 8, "bf16", 3), (4, 4, 4, "f32", 1),
+                                             (2, 2, 1, "f64", 2), (6, 2, 3, "f32", 1)])
+def test_flat_rccl_allgather_variant(n, k, b, dt, slices):
+    """SCHEDULE_FLAT_AG: the flat plan with its allgather phase as in-place ncclAllGather
+    collectives (equal pieces) -- same bits as the oracle."""
+    cnt = n * 64 * 8
+    sends = [po.fill(cnt, dt, 0, 55, r) for r in range(n)]
+    plans = plan_sim.load_plans(ca.MODE_ALLREDUCE, n, k, b, cnt, slices, schedule=ca.SCHEDULE_FLAT_AG)
+    # slices whose pieces are equal use the collective (with 3 slices some are unequal: p2p)
+    assert any(st["allgathers"] and not st["sends"] for st in plans[0]["steps"] if st["label"].startswith("fdist"))
+    got = plan_sim.simulate(ca.MODE_ALLREDUCE, sends, k, b, dt, "sum", slices=slices, schedule=ca.SCHEDULE_FLAT_AG)
+    ref = po.allreduce_radix_batch(sends, k, b, dt, "sum")
+    for r in range(n):
+        np.testing.assert_array_equal(got[r].view(np.uint8), ref[r].view(np.uint8))
+
+
+def test_flat_rccl_allgather_unequal_pieces_fall_back_to_p2p():
+    n = 8
+    cnt = n * 100  # irc pieces are not equal: that slice's allgather stays point-to-point
+    plans = plan_sim.load_plans(ca.MODE_ALLREDUCE, n, 4, 4, cnt, 1, schedule=ca.SCHEDULE_FLAT_AG)
+    assert not any(st["allgathers"] for st in plans[0]["steps"])
+    sends = [po.fill(cnt, "f32", 0, 56, r) for r in range(n)]
+    got = plan_sim.simulate(ca.MODE_ALLREDUCE, sends, 4, 4, "f32", "sum", schedule=ca.SCHEDULE_FLAT_AG)
+    ref = po.allreduce_radix_batch(sends, 4, 4, "f32", "sum")
+    for r in range(n):
+        np.testing.assert_array_equal(got[r].view(np.uint32), ref[r].view(np.uint32))
