@@ -127,9 +127,11 @@ def test_baseline_geometries_vs_oracle(gu, groups, mode, n, k, b, dtype, slices)
         np.testing.assert_array_equal(got[r], ref[r])
 
 
-def test_c4_full_size_exact_int(gu, groups):
+@pytest.mark.parametrize("schedule", ["flat", "exact", "flat_ag", "reference"])
+def test_c4_full_size_exact_int(gu, groups, schedule):
     """C4 at full size (1 GiB per rank, 8 ranks, k=4, b=4) with the reference harness's
-    int32 pattern rank*count+i: every rank must hold sum_r (r*count + i) exactly."""
+    int32 pattern rank*count+i: every rank must hold sum_r (r*count + i) exactly, under the
+    default schedule and the reference-message (exact), RCCL-allgather and reference routes."""
     import torch
 
     n, k, b, count = 8, 4, 4, 1 << 28
@@ -139,7 +141,12 @@ def test_c4_full_size_exact_int(gu, groups):
         assert ca.fill(s, count, ca.INT32, 1, 0, r, count, gu.stream()) == 0
     recvs = [torch.empty(count, dtype=torch.int32, device=gu.DEV) for _ in range(n)]
     gu.sync()
-    assert g.all_reduce_radix_batch(sends, recvs, count, ca.INT32, ca.SUM, k, b) == 0
+    g.set_schedule({"flat": ca.SCHEDULE_FLAT, "exact": ca.SCHEDULE_EXACT, "flat_ag": ca.SCHEDULE_FLAT_AG,
+                    "reference": ca.SCHEDULE_REFERENCE}[schedule])
+    try:
+        assert g.all_reduce_radix_batch(sends, recvs, count, ca.INT32, ca.SUM, k, b) == 0
+    finally:
+        g.set_schedule(ca.SCHEDULE_FLAT)
     i = torch.arange(count, dtype=torch.int64, device=gu.DEV)
     expect = ((count * (n * (n - 1) // 2) + n * i) & 0xFFFFFFFF).to(torch.int64)
     expect = torch.where(expect >= 2**31, expect - 2**32, expect).to(torch.int32)
