@@ -313,3 +313,35 @@ def test_balanced_reduce_scatter_equals_owner_lane(gu, groups, n, k, b):
                 np.testing.assert_array_equal(got[r].view(np.uint32), want[r].view(np.uint32))
     finally:
         g.set_schedule(ca.SCHEDULE_FLAT)
+
+
+SCHEDULES = {"flat": ca.SCHEDULE_FLAT, "balanced": ca.SCHEDULE_BALANCED, "reference": ca.SCHEDULE_REFERENCE,
+             "exact": ca.SCHEDULE_EXACT, "flat_ag": ca.SCHEDULE_FLAT_AG}
+
+
+@pytest.mark.parametrize("schedule", sorted(SCHEDULES))
+def test_tiny_ragged_and_empty_every_schedule(gu, groups, schedule):
+    """Edge sizes under every schedule: one element per rank, odd per-rank counts, reduce-scatter
+    recvcount 1/3/5, and count 0 (a no-op returning success): bit-exact vs the oracle."""
+    g8 = groups(8)
+    g6 = groups(6)
+    for g in (g8, g6):
+        g.set_schedule(SCHEDULES[schedule])
+    try:
+        for n, g, k, b in ((8, g8, 4, 4), (8, g8, 2, 8), (8, g8, 3, 2), (6, g6, 2, 3), (6, g6, 4, 6)):
+            for per in (1, 3, 5):
+                for mode in ("ar", "rs"):
+                    count = per * n if mode == "ar" else per
+                    in_n = count if mode == "ar" else count * n
+                    sends = [po.fill(in_n, "f32", 0, 17, r) for r in range(n)]
+                    got = run_local(gu, g, mode, sends, k, b, "f32", "sum")
+                    f = po.allreduce_radix_batch if mode == "ar" else po.reduce_scatter_radix_batch
+                    want = f(sends, k, b, "f32", "sum")
+                    for r in range(n):
+                        np.testing.assert_array_equal(got[r].view(np.uint32), want[r].view(np.uint32))
+            d = [gu.empty_dev(16) for _ in range(n)]
+            assert g.all_reduce_radix_batch(d, d, 0, ca.FLOAT32, ca.SUM, k, b) == 0
+            assert g.reduce_scatter_radix_batch(d, d, 0, ca.FLOAT32, ca.SUM, k, b) == 0
+    finally:
+        for g in (g8, g6):
+            g.set_schedule(ca.SCHEDULE_FLAT)

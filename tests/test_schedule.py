@@ -329,3 +329,21 @@ def test_flat_rccl_allgather_unequal_pieces_fall_back_to_p2p():
     ref = po.allreduce_radix_batch(sends, 4, 4, "f32", "sum")
     for r in range(n):
         np.testing.assert_array_equal(got[r].view(np.uint32), ref[r].view(np.uint32))
+
+
+@pytest.mark.parametrize("schedule", [ca.SCHEDULE_REFERENCE, ca.SCHEDULE_BALANCED, ca.SCHEDULE_FLAT, ca.SCHEDULE_EXACT,
+                                      ca.SCHEDULE_FLAT_AG])
+def test_tiny_and_ragged_sizes_every_schedule(schedule):
+    """One element per rank, odd per-rank counts, reduce-scatter recvcount 1/3/5: plans of every
+    schedule reproduce the oracle bit-exactly (the GPU twin is in test_gpu_collectives.py)."""
+    for n, k, b in ((8, 4, 4), (8, 2, 8), (8, 3, 2), (6, 2, 3), (6, 4, 6)):
+        for per in (1, 3, 5):
+            for mode in (ca.MODE_ALLREDUCE, ca.MODE_REDUCE_SCATTER):
+                count = per * n if mode == ca.MODE_ALLREDUCE else per
+                in_n = count if mode == ca.MODE_ALLREDUCE else count * n
+                sends = [po.fill(in_n, "f32", 0, 17, r) for r in range(n)]
+                got = plan_sim.simulate(mode, sends, k, b, "f32", "sum", schedule=schedule)
+                f = po.allreduce_radix_batch if mode == ca.MODE_ALLREDUCE else po.reduce_scatter_radix_batch
+                want = f(sends, k, b, "f32", "sum")
+                for r in range(n):
+                    np.testing.assert_array_equal(got[r].view(np.uint32), want[r].view(np.uint32))
