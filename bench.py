@@ -359,7 +359,8 @@ def bench_allreduce(args):
                     "algorithmic_bytes_per_call": float(busiest[1]), "launches_per_call": int(busiest[2]),
                     "kernel_ms_per_call": round(float(busiest[0]), 4)}
     # bytes on the busiest directed link of this schedule (max over ranks; slicing only splits messages)
-    sched = {"reference": 0, "0": 0, "balanced": 1, "1": 1, "exact": 3, "3": 3, "flat_ag": 4, "4": 4}.get(os.environ.get("CHR_SCHEDULE", "flat"), 2)
+    sched = {"reference": 0, "0": 0, "balanced": 1, "1": 1, "exact": 3, "3": 3, "flat_ag": 4, "4": 4, "flat_seq": 5,
+             "5": 5}.get(os.environ.get("CHR_SCHEDULE", "flat"), 2)
     plan = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, world, rank, k, b, count, 1, sched))
     per_peer = {}
     for st in plan["steps"]:
@@ -467,7 +468,8 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
     for name, sch in (("radix_batch_balanced", ca.SCHEDULE_BALANCED),
                       ("radix_batch_reference_route", ca.SCHEDULE_REFERENCE),
                       ("radix_batch_exact_reference_messages", ca.SCHEDULE_EXACT),
-                      ("radix_batch_flat_rccl_allgather", ca.SCHEDULE_FLAT_AG)):
+                      ("radix_batch_flat_rccl_allgather", ca.SCHEDULE_FLAT_AG),
+                      ("radix_batch_flat_separate_groups", ca.SCHEDULE_FLAT_SEQ)):
         comm.set_schedule(sch)
         try:
             out[name] = entry(_timed_max(torch, dist, radix, steps, warm))

@@ -34,7 +34,7 @@ MODE_ALLREDUCE, MODE_REDUCE_SCATTER = 0, 1
 MODE_MPICH_RING, MODE_MPICH_RD, MODE_MPICH_RSAG, MODE_MPICH_RECEXCH = 2, 3, 4, 5
 MODE_MPICH_KRSAG, MODE_MPICH_RMULT = 6, 7
 MODE_ALLGATHER = 8
-SCHEDULE_REFERENCE, SCHEDULE_BALANCED, SCHEDULE_FLAT, SCHEDULE_EXACT, SCHEDULE_FLAT_AG = 0, 1, 2, 3, 4
+SCHEDULE_REFERENCE, SCHEDULE_BALANCED, SCHEDULE_FLAT, SCHEDULE_EXACT, SCHEDULE_FLAT_AG, SCHEDULE_FLAT_SEQ = 0, 1, 2, 3, 4, 5
 REDUCE_RUNNING_FIRST = 1  # chr_reduce_multi_ex flag (MPICH_do_reduce operand order)
 
 

@@ -198,7 +198,7 @@ bool is_device_ptr(const void* p) {
 
 using PlanKey = std::tuple<int, int, int, int, uint64_t, int, int, int>;  // mode, rank, k, b, count, dtype size, slices, schedule
 
-// CHR_SCHEDULE = reference | balanced | flat | exact | flat_ag (or 0 .. 4); default flat
+// CHR_SCHEDULE = reference | balanced | flat | exact | flat_ag | flat_seq (or 0 .. 5); default flat
 // CHR_OVERLAP=0: local ops on the transfer stream (no compute/xGMI overlap); default 1
 int default_overlap() {
     static const int v = [] {
@@ -217,6 +217,7 @@ int default_schedule() {
         if (s == "balanced" || s == "1") return (int)chr::SCHED_BALANCED;
         if (s == "exact" || s == "3") return (int)chr::SCHED_EXACT;
         if (s == "flat_ag" || s == "4") return (int)chr::SCHED_FLAT_AG;
+        if (s == "flat_seq" || s == "5") return (int)chr::SCHED_FLAT_SEQ;
         return (int)chr::SCHED_FLAT;
     }();
     return v;
@@ -604,13 +605,13 @@ int chr_comm_set_overlap(chr_comm* c, int enable) {
 }
 
 int chr_comm_set_schedule(chr_comm* c, int schedule) {
-    if (!c || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_FLAT_AG) return CHR_ERR_INVALID_ARG;
+    if (!c || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_FLAT_SEQ) return CHR_ERR_INVALID_ARG;
     c->sched = schedule;
     return CHR_SUCCESS;
 }
 
 int chr_local_group_set_schedule(chr_local_group* g, int schedule) {
-    if (!g || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_FLAT_AG) return CHR_ERR_INVALID_ARG;
+    if (!g || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_FLAT_SEQ) return CHR_ERR_INVALID_ARG;
     g->sched = schedule;
     return CHR_SUCCESS;
 }

@@ -614,7 +614,8 @@ int auto_slices(uint64_t irc_bytes) {
     return (int)std::max<uint64_t>(1, std::min<uint64_t>(8, s));
 }
 
-Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, int slices, bool coll_ag = false);
+Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, int slices, bool coll_ag = false,
+                     bool merge = true);
 static Plan build_plan_impl(Mode mode, int n, int me, int k_in, int b, uint64_t count, int slices, int sched);
 
 // The fused kernel takes at most kPlanFanIn inputs per pass (kMaxFanIn, reduce_kernels.hip)
@@ -775,8 +776,8 @@ static Plan build_plan_impl(Mode mode, int n, int me, int k_in, int b, uint64_t 
     p.recv_elems = mode == MODE_ALLREDUCE ? g.total : recvcount;
     p.acc_elems = g.total;
     if (g.total == 0) return p;
-    if ((sched == SCHED_FLAT || sched == SCHED_FLAT_AG) && n > 1) {
-        Plan f = build_plan_flat(mode, n, me, k_in, b, g, slices, sched == SCHED_FLAT_AG);
+    if ((sched == SCHED_FLAT || sched == SCHED_FLAT_AG || sched == SCHED_FLAT_SEQ) && n > 1) {
+        Plan f = build_plan_flat(mode, n, me, k_in, b, g, slices, sched == SCHED_FLAT_AG, sched != SCHED_FLAT_SEQ);
         if (!f.error) return f;
     }
 
@@ -1586,12 +1587,12 @@ bool tree_enabled() {
 
 }  // namespace
 
-Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, int slices, bool coll_ag) {
+Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, int slices, bool coll_ag, bool merge) {
     Plan p;
     p.mode = mode;
     p.rank = me;
     p.g = g;
-    p.sched = coll_ag ? SCHED_FLAT_AG : SCHED_FLAT;
+    p.sched = coll_ag ? SCHED_FLAT_AG : merge ? SCHED_FLAT : SCHED_FLAT_SEQ;
     // 1. the reference-order plans of every rank at recvcount = 1, executed symbolically
     const uint64_t cnt1 = mode == MODE_ALLREDUCE ? (uint64_t)n : 1;
     std::vector<Plan> ref;
@@ -1768,14 +1769,34 @@ Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, 
             }
         }
     };
-    // Step order G0, G1, D0, G2, D1, ..., D(P-1): gather s+1 needs nothing from the evaluation
-    // of slice s, so with two streams it runs while slice s is reduced; allgather s follows it.
     auto add = [&](int kind, int s2) {
         p.steps.emplace_back();
         Step& st = p.steps.back();
         st.label = std::string(kind == F_GATHER ? "gather" : "fdist") + "/s" + std::to_string(s2);
         emit(kind, sl[s2], st);
     };
+    if (merge && mode == MODE_ALLREDUCE) {
+        // One RCCL group per step t: gather of slice t together with the allgather of slice t-2.
+        // Slice t-2 was reduced (compute stream) while step t-1's group was on the links, so the
+        // group rarely waits; the two flows share every link at once, and a call has P + 2
+        // groups instead of 2P (fewer launch / drain bubbles).
+        for (int t = 0; t < P + 2; ++t) {
+            p.steps.emplace_back();
+            Step& st = p.steps.back();
+            if (t < P) {
+                st.label = "gather/s" + std::to_string(t);
+                emit(F_GATHER, sl[t], st);
+            }
+            if (t >= 2 && t - 2 < P) {
+                st.label += std::string(st.label.empty() ? "" : ",") + "fdist/s" + std::to_string(t - 2);
+                emit(F_DIST, sl[t - 2], st);
+            }
+            if (st.label.empty()) p.steps.pop_back();
+        }
+        return p;
+    }
+    // Step order G0, G1, D0, G2, D1, ..., D(P-1): gather s+1 needs nothing from the evaluation
+    // of slice s, so with two streams it runs while slice s is reduced; allgather s follows it.
     for (int s2 = 0; s2 < P; ++s2) {
         add(F_GATHER, s2);
         if (mode == MODE_ALLREDUCE && s2 > 0) add(F_DIST, s2 - 1);

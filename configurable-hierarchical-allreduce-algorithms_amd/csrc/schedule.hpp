@@ -132,7 +132,11 @@ void recexch_count_offset(int nranks, int max_phases, int k, std::vector<int>* c
 //                    its bcast + k-port Bruck allgather (S_BCAST, S_AG) / k-nomial scatter (S_KSCAT)
 //   SCHED_FLAT_AG    SCHED_FLAT with the allgather phase on RCCL's ncclAllGather collective
 //                    (pure data movement, so the bits are unchanged) where the pieces are equal
-enum Sched : int { SCHED_REFERENCE = 0, SCHED_BALANCED = 1, SCHED_FLAT = 2, SCHED_EXACT = 3, SCHED_FLAT_AG = 4 };
+//   SCHED_FLAT_SEQ   SCHED_FLAT with gather and allgather in separate RCCL groups (2P groups per
+//                    call instead of P + 2; the ordering before the merged groups)
+enum Sched : int {
+    SCHED_REFERENCE = 0, SCHED_BALANCED = 1, SCHED_FLAT = 2, SCHED_EXACT = 3, SCHED_FLAT_AG = 4, SCHED_FLAT_SEQ = 5
+};
 Plan build_plan(Mode mode, int nranks, int rank, int k, int b, uint64_t count, int slices = 1,
                 int sched = SCHED_FLAT);
 int auto_slices(uint64_t irc_bytes);

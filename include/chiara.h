@@ -127,12 +127,15 @@ int chr_comm_set_slices(chr_comm* comm, int slices);
  *   CHR_SCHEDULE_FLAT_AG    FLAT with its allgather phase on RCCL's ncclAllGather collective
  *                           (in place, one per chunk) where the pieces are equal; data
  *                           movement only, so identical bits
- * Env CHR_SCHEDULE=reference|balanced|flat|exact|flat_ag sets the default.  DESIGN.md §5. */
+ *   CHR_SCHEDULE_FLAT_SEQ   FLAT with its gather and allgather in separate RCCL groups (FLAT
+ *                           merges the gather of slice t with the allgather of slice t-2)
+ * Env CHR_SCHEDULE=reference|balanced|flat|exact|flat_ag|flat_seq sets the default.  DESIGN.md §5. */
 #define CHR_SCHEDULE_REFERENCE 0
 #define CHR_SCHEDULE_BALANCED 1
 #define CHR_SCHEDULE_FLAT 2
 #define CHR_SCHEDULE_EXACT 3
 #define CHR_SCHEDULE_FLAT_AG 4
+#define CHR_SCHEDULE_FLAT_SEQ 5
 int chr_comm_set_schedule(chr_comm* comm, int schedule);
 /* Compute/xGMI overlap (default on; env CHR_OVERLAP=0): local reductions run on a second HIP
  * stream, ordered against the RCCL transfers by events where the plan's data dependencies

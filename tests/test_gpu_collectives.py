@@ -284,7 +284,7 @@ def test_schedules_bit_identical(gu, groups, n, k, b, dtype):
     outs = {}
     try:
         for sch in (ca.SCHEDULE_FLAT, ca.SCHEDULE_BALANCED, ca.SCHEDULE_REFERENCE, ca.SCHEDULE_EXACT,
-                    ca.SCHEDULE_FLAT_AG):
+                    ca.SCHEDULE_FLAT_AG, ca.SCHEDULE_FLAT_SEQ):
             g.set_schedule(sch)
             g.set_slices(3)
             outs[sch] = run_local(gu, g, "ar", sends, k, b, dtype, "sum")
@@ -316,7 +316,7 @@ def test_balanced_reduce_scatter_equals_owner_lane(gu, groups, n, k, b):
 
 
 SCHEDULES = {"flat": ca.SCHEDULE_FLAT, "balanced": ca.SCHEDULE_BALANCED, "reference": ca.SCHEDULE_REFERENCE,
-             "exact": ca.SCHEDULE_EXACT, "flat_ag": ca.SCHEDULE_FLAT_AG}
+             "exact": ca.SCHEDULE_EXACT, "flat_ag": ca.SCHEDULE_FLAT_AG, "flat_seq": ca.SCHEDULE_FLAT_SEQ}
 
 
 @pytest.mark.parametrize("schedule", sorted(SCHEDULES))

@@ -139,10 +139,10 @@ def test_rccl_allgather_world4_and_8():
 
 
 def test_rccl_schedules_and_overlap_world4():
-    """The two-stream executor (overlap on/off) under all five schedules, allreduce and
+    """The two-stream executor (overlap on/off) under all six schedules, allreduce and
     reduce-scatter, 4 ranks over RCCL: bit-exact vs the oracle."""
     cases = []
-    for sched in (0, 1, 2, 3, 4):
+    for sched in (0, 1, 2, 3, 4, 5):
         for ov in (True, False):
             cases.append(("ar", 4, 4, 1 << 18, "f32", False, 4, sched, ov))
             cases.append(("rs", 2, 2, 1 << 15, "f32", False, 3, sched, ov))

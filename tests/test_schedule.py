@@ -288,10 +288,21 @@ def test_wide_mpich_chains_in_place(algo, n, k):
                 np.testing.assert_array_equal(got[r].view(np.uint8), want[r].view(np.uint8))
 
 
-def test_flat_overlap_dependencies():
-    """Two-stream execution: in the flat plan, gather s+1 never waits for the evaluation of slice
-    s (overlap), while allgather s waits exactly for it; wavefront plans wait step to step."""
+def test_flat_merged_groups_and_dependencies():
+    """Default flat plan: one RCCL group per step holds the gather of slice t and the allgather
+    of slice t-2 (P + 2 groups); each step waits exactly for the evaluation of slice t-2, which
+    ran while step t-1 was on the links."""
     p = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 1 << 24, 4))
+    labels = [st["label"] for st in p["steps"]]
+    assert labels == ["gather/s0", "gather/s1", "gather/s2,fdist/s0", "gather/s3,fdist/s1", "fdist/s2", "fdist/s3"]
+    assert [st["wait"] for st in p["steps"]] == [-1, -1, 0, 1, 2, 3]
+
+
+def test_flat_overlap_dependencies():
+    """Two-stream execution: in the flat_seq plan (separate groups), gather s+1 never waits for
+    the evaluation of slice s (overlap), while allgather s waits exactly for it; wavefront plans
+    wait step to step."""
+    p = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 1 << 24, 4, ca.SCHEDULE_FLAT_SEQ))
     labels = [st["label"] for st in p["steps"]]
     assert labels == ["gather/s0", "gather/s1", "fdist/s0", "gather/s2", "fdist/s1", "gather/s3", "fdist/s2",
                       "fdist/s3"]
@@ -332,7 +343,7 @@ def test_flat_rccl_allgather_unequal_pieces_fall_back_to_p2p():
 
 
 @pytest.mark.parametrize("schedule", [ca.SCHEDULE_REFERENCE, ca.SCHEDULE_BALANCED, ca.SCHEDULE_FLAT, ca.SCHEDULE_EXACT,
-                                      ca.SCHEDULE_FLAT_AG])
+                                      ca.SCHEDULE_FLAT_AG, ca.SCHEDULE_FLAT_SEQ])
 def test_tiny_and_ragged_sizes_every_schedule(schedule):
     """One element per rank, odd per-rank counts, reduce-scatter recvcount 1/3/5: plans of every
     schedule reproduce the oracle bit-exactly (the GPU twin is in test_gpu_collectives.py)."""
