@@ -11,6 +11,7 @@ import shutil
 import subprocess
 
 import pytest
+from plot_pipeline import COLUMNS, plotter_frame
 
 pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -35,12 +36,23 @@ def _run(binary, args, n, tmp_path, where=("oracle", "_ref")):
         return list(csv.DictReader(f))
 
 
+def _plots(tmp_path, collective):
+    """the CSV goes through the reference plotters' data stage unchanged."""
+    path = [os.path.join(tmp_path, f) for f in os.listdir(tmp_path) if f.endswith(".csv")][0]
+    with open(path) as f:
+        assert f.readline().strip().split(",") == COLUMNS
+    for agg in ("median", "min", "mean"):  # median_best / minimum_best / avg_best plotters
+        wide, best, speedup = plotter_frame(path, collective, agg)
+        assert best.notna().all().all() and (speedup > 0).all().all()
+
+
 def test_reference_allreduce_harness_on_mi355x(tmp_path):
     rows = _run("ref_harness_allreduce", ["3", "--overwrite", "b=4", "base=64"], 4, tmp_path)
     ours = [r for r in rows if r["algorithm_name"] == "all_reduce_radix_batch"]
     assert len(ours) == 3 * 2 * 50  # n_iter x k in {2,3} x 50 reps
     assert {r["k"] for r in ours} == {"2", "3"}
     assert all(r["is_correct"] == "1" for r in rows)
+    _plots(tmp_path, "allreduce")
 
 
 def test_reference_reduce_scatter_harness_on_mi355x(tmp_path):
@@ -48,6 +60,7 @@ def test_reference_reduce_scatter_harness_on_mi355x(tmp_path):
     ours = [r for r in rows if r["algorithm_name"] == "reduce_scatter_radix_batch"]
     assert len(ours) == 2 * 2 * 20
     assert all(r["is_correct"] == "1" for r in rows)
+    _plots(tmp_path, "reduce_scatter")
 
 
 def test_reference_mpich_baseline_harness_on_mi355x(tmp_path):
@@ -67,22 +80,24 @@ def test_reference_allgather_harness_on_mi355x(tmp_path):
     ours = [r for r in rows if r["algorithm_name"] == "allgather_radix_batch"]
     assert ours and {r["k"] for r in ours} == {"2", "3"}
     assert all(r["is_correct"] == "1" for r in rows)
+    _plots(tmp_path, "allgather")
 
 
 BIN = ("configurable-hierarchical-allreduce-algorithms_amd", "bin")
 
 
-@pytest.mark.parametrize("binary,args,n,name", [
+@pytest.mark.parametrize("binary,args,n,name,coll", [
     ("chiara_allreduce", ["2", "--overwrite", "b=4", "base=4096", "mem=device", "dtype=f32", "reps=5"], 8,
-     "all_reduce_radix_batch"),
+     "all_reduce_radix_batch", "allreduce"),
     ("chiara_reduce_scatter", ["2", "--overwrite", "b=4", "base=1000", "mem=device", "reps=5"], 4,
-     "reduce_scatter_radix_batch"),
+     "reduce_scatter_radix_batch", "reduce_scatter"),
     ("chiara_allgather", ["3", "--overwrite", "b=4", "base=100", "mem=device", "dtype=bf16", "reps=5"], 8,
-     "allgather_radix_batch"),
+     "allgather_radix_batch", "allgather"),
 ])
-def test_own_harnesses_device_resident(tmp_path, binary, args, n, name):
+def test_own_harnesses_device_resident(tmp_path, binary, args, n, name, coll):
     """csrc/harness: the reference CLI/CSV with the HBM-resident extension (mem=device)."""
     rows = _run(binary, args, n, tmp_path, where=BIN)
     ours = [r for r in rows if r["algorithm_name"] == name]
     bad = [r for r in rows if r["is_correct"] != "1"]
     assert ours and not bad, bad[:5]
+    _plots(tmp_path, coll)
