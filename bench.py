@@ -194,7 +194,7 @@ def bench_bucket(args, cpu):
                    "buffer_sets": NSETS, "parallelism": "replicas"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "kernel": "chr::k_reduce_vec<f32,SUM,M=1,U=4,NT>", "algorithmic_bytes_per_launch": bytes_per_step,
+                     "kernel": "chr::k_reduce_vec<f32,SUM,M=1,U=4,NT,ACC0,64 threads>", "algorithmic_bytes_per_launch": bytes_per_step,
                      "avg_kernel_ms": round(avg_kern_ms, 5)},
         "cpu_baseline": cpu,
         "host_wall_s": round(wall, 4),

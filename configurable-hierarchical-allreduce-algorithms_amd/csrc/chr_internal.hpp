@@ -37,9 +37,12 @@ hipError_t launch_fill(void* buf, size_t n, int dtype, int pattern, uint64_t see
 //   CHR_REDUCE_NT_MIN_BYTES  bytes streamed by one call from which NT is used (128 MiB)
 //   CHR_REDUCE_ACC0          0 / 1 forces the first accumulator slot nt / default policy
 //                            under NT; unset = default policy for m >= 2 or large buckets
-//   CHR_REDUCE_ACC0_MIN_BYTES  bucket size from which m = 1 uses it too (512 MiB)
+//   CHR_REDUCE_ACC0_MIN_BYTES  bucket size from which m = 1 uses it too (0: always)
+//   CHR_REDUCE_BLOCK         threads per workgroup of the vector kernels: 64 or 256;
+//                            unset = 64 for NT calls, 256 otherwise
 struct ReduceTuning {
     int max_blocks;
+    int block;
     int nt_mode;
     size_t nt_min_bytes;
     int acc0_mode;

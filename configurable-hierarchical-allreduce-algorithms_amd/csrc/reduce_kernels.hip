@@ -12,10 +12,13 @@
 // and the accumulator, write the result), ~0.1-0.5 FLOP/byte: no MFMA.  Design:
 //  * one 16-byte global_load_dwordx4 per lane per operand (1 KiB per wave-instruction),
 //    U independent vectors per lane in flight (ILP) with every operand's loads issued
-//    before the first add, 256-thread workgroups, one trip per workgroup (the full grid
-//    measured faster than a capped grid-stride grid on large buckets);
+//    before the first add, one trip per workgroup (the full grid measured faster than a
+//    capped grid-stride grid on large buckets);
 //  * non-temporal loads and stores for calls that stream >= 128 MiB (HBM-cold buckets
 //    +15-40 % over plain accesses; plain stays faster on small, cache-warm calls);
+//  * workgroup size by regime: one wave (64 threads) for the streaming (nt) calls, +3 % on
+//    the 64 MiB m=1 bucket and up to +5 % for m >= 3 (profiles/r01/block_ab_*); 256 threads
+//    for the small cache-warm calls, where one-wave workgroups lose up to 5 %;
 //  * no LDS: a pure stream has no reuse, and staging through LDS (global_load_lds) was
 //    measured null-to-negative for this regime (profiles/);
 //  * no XCD remap: no inter-workgroup reuse; an XCD-contiguous workgroup map measured 0.88x
@@ -57,7 +60,9 @@ ReduceTuning& reduce_tuning() {
         s = std::getenv("CHR_REDUCE_ACC0");   // 0 / 1 / unset = by fan-in and size
         r.acc0_mode = s ? std::atoi(s) : -1;
         s = std::getenv("CHR_REDUCE_ACC0_MIN_BYTES");
-        r.acc0_min_bytes = s ? (size_t)std::atoll(s) : (size_t)512 << 20;
+        r.acc0_min_bytes = s ? (size_t)std::atoll(s) : 0;
+        s = std::getenv("CHR_REDUCE_BLOCK");  // 64 / 256 / unset = by policy (launch_vec_m)
+        r.block = s ? (std::atoi(s) == 64 ? 64 : 256) : 0;
         return r;
     }();
     return t;
@@ -76,24 +81,25 @@ struct VecArgs {
 // the caches hold: +15-40 % on HBM-cold buckets.  ACC0: under NT, the FIRST of the U
 // accumulator vectors keeps the default policy (in place, a quarter of the write-backs then
 // go through the Infinity Cache): per-slot policy sweep
-// (profiles/r01/microbench_focus4_slot_policy.txt) +15 % at 1 GiB m=1, +3-5 % for m>=2,
-// -2 % for 64 MiB m=1, where launch_vec_m keeps every slot nt; making ALL accumulator
-// slots temporal thrashes the cache (-7 %).  Slot 0 is peeled so that the two policies
+// (profiles/r01/microbench_focus4_slot_policy.txt) +15 % at 1 GiB m=1, +3-5 % for m>=2 with
+// 256-thread workgroups; with one-wave workgroups it also gains on the 64 MiB m=1 bucket
+// (6 440-6 464 vs 6 041-6 052 GB/s all-nt, profiles/r01/block_ab_bench.txt), so it is used for
+// every nt call; making ALL accumulator slots temporal thrashes the cache (-7 %).  Slot 0 is peeled so that the two policies
 // are separate instructions (a select between a plain and an nt load of one address is
 // merged by LLVM, dropping the nt bit).
-template <int DT, int OP, int M, int U, bool NT, bool ACC0>
-__global__ __launch_bounds__(kBlock) void k_reduce_vec(VecArgs a) {
-    const size_t stride = (size_t)gridDim.x * kBlock * U;
-    for (size_t base = (size_t)blockIdx.x * kBlock * U + threadIdx.x; base < a.nvec; base += stride) {
-        if (base + (size_t)(U - 1) * kBlock < a.nvec) {
+template <int DT, int OP, int M, int U, bool NT, bool ACC0, int BL>
+__global__ __launch_bounds__(BL) void k_reduce_vec(VecArgs a) {
+    const size_t stride = (size_t)gridDim.x * BL * U;
+    for (size_t base = (size_t)blockIdx.x * BL * U + threadIdx.x; base < a.nvec; base += stride) {
+        if (base + (size_t)(U - 1) * BL < a.nvec) {
             u32x4 acc[U], x[M][U];
             acc[0] = ld<NT && !ACC0>(&a.acc[base]);
 #pragma unroll
-            for (int u = 1; u < U; ++u) acc[u] = ld<NT>(&a.acc[base + (size_t)u * kBlock]);
+            for (int u = 1; u < U; ++u) acc[u] = ld<NT>(&a.acc[base + (size_t)u * BL]);
 #pragma unroll
             for (int j = 0; j < M; ++j)
 #pragma unroll
-                for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&a.ins[j][base + (size_t)u * kBlock]);
+                for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&a.ins[j][base + (size_t)u * BL]);
             // Keep every load of the trip ahead of the first add: without this the
             // scheduler interleaves the first add (and its vmcnt(0)) between the loads.
             __builtin_amdgcn_sched_barrier(0);
@@ -102,10 +108,10 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(VecArgs a) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) acc[u] = apply_vec<DT, OP>(x[j][u], acc[u]);
 #pragma unroll
-            for (int u = 0; u < U; ++u) st<NT>(&a.out[base + (size_t)u * kBlock], acc[u]);
+            for (int u = 0; u < U; ++u) st<NT>(&a.out[base + (size_t)u * BL], acc[u]);
         } else {
             for (int u = 0; u < U; ++u) {
-                const size_t i = base + (size_t)u * kBlock;
+                const size_t i = base + (size_t)u * BL;
                 if (i >= a.nvec) break;
                 u32x4 acc = a.acc[i];
 #pragma unroll
@@ -139,23 +145,32 @@ __global__ __launch_bounds__(kBlock) void k_reduce_scalar(ScalarArgs a) {
 
 // ---- host launchers ----------------------------------------------------------------------
 
+template <int DT, int OP, int M, int BL>
+static hipError_t launch_vec_mb(const VecArgs& a, bool nt, bool acc0, hipStream_t s) {
+    constexpr int U = M <= 2 ? 4 : 2;
+    const size_t trips = (a.nvec + (size_t)BL * U - 1) / ((size_t)BL * U);
+    const size_t cap = reduce_tuning().max_blocks > 0 ? (size_t)reduce_tuning().max_blocks : trips;
+    const int grid = (int)(trips < cap ? trips : cap);
+    if (!nt)
+        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, false, false, BL>), dim3(grid), dim3(BL), 0, s, a);
+    else if (acc0)
+        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, true, BL>), dim3(grid), dim3(BL), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, false, BL>), dim3(grid), dim3(BL), 0, s, a);
+    return hipGetLastError();
+}
+
+// Policy (profiles/r01/block_ab_*): calls that stream >= 128 MiB run non-temporal with
+// one-wave workgroups and the first accumulator slot temporal (ACC0); smaller, cache-warm
+// calls keep plain accesses and 256-thread workgroups.
 template <int DT, int OP, int M>
 static hipError_t launch_vec_m(const VecArgs& a, hipStream_t s) {
-    constexpr int U = M <= 2 ? 4 : 2;
     const ReduceTuning& t = reduce_tuning();
-    const size_t trips = (a.nvec + (size_t)kBlock * U - 1) / ((size_t)kBlock * U);
-    const size_t cap = t.max_blocks > 0 ? (size_t)t.max_blocks : trips;
-    const int grid = (int)(trips < cap ? trips : cap);
     const size_t call_bytes = (size_t)(M + 2) * a.nvec * 16;
     const bool nt = t.nt_mode == 1 || (t.nt_mode < 0 && call_bytes >= t.nt_min_bytes);
     const bool acc0 = t.acc0_mode == 1 || (t.acc0_mode < 0 && (M >= 2 || a.nvec * 16 >= t.acc0_min_bytes));
-    if (!nt)
-        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, false, false>), dim3(grid), dim3(kBlock), 0, s, a);
-    else if (acc0)
-        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, true>), dim3(grid), dim3(kBlock), 0, s, a);
-    else
-        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, false>), dim3(grid), dim3(kBlock), 0, s, a);
-    return hipGetLastError();
+    const int bl = t.block ? t.block : nt ? 64 : 256;
+    return bl == 64 ? launch_vec_mb<DT, OP, M, 64>(a, nt, acc0, s) : launch_vec_mb<DT, OP, M, 256>(a, nt, acc0, s);
 }
 
 template <int DT, int OP>

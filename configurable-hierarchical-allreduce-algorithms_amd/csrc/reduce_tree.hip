@@ -88,24 +88,24 @@ struct ScalarOp {
 
 // U vectors per lane per trip for NL leaves: every leaf load of the trip is issued before
 // the first combine (NL * U <= 16 loads of 16 B in flight per lane).
-template <int DT, int OP, int NL, int U, bool NT>
-__global__ __launch_bounds__(kBlock) void k_reduce_tree(TreeArgs a) {
-    const size_t stride = (size_t)gridDim.x * kBlock * U;
-    for (size_t base = (size_t)blockIdx.x * kBlock * U + threadIdx.x; base < a.nvec; base += stride) {
-        if (base + (size_t)(U - 1) * kBlock < a.nvec) {
+template <int DT, int OP, int NL, int U, bool NT, int BL>
+__global__ __launch_bounds__(BL) void k_reduce_tree(TreeArgs a) {
+    const size_t stride = (size_t)gridDim.x * BL * U;
+    for (size_t base = (size_t)blockIdx.x * BL * U + threadIdx.x; base < a.nvec; base += stride) {
+        if (base + (size_t)(U - 1) * BL < a.nvec) {
             u32x4 x[NL][U];
 #pragma unroll
             for (int j = 0; j < NL; ++j)
 #pragma unroll
-                for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&a.leaves[j][base + (size_t)u * kBlock]);
+                for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&a.leaves[j][base + (size_t)u * BL]);
             __builtin_amdgcn_sched_barrier(0);
             u32x4 r[U];
             tree_eval<u32x4, NL, U, VecOp<DT, OP>>(x, r, a.comb, a.swaps);
 #pragma unroll
-            for (int u = 0; u < U; ++u) st<NT>(&a.out[base + (size_t)u * kBlock], r[u]);
+            for (int u = 0; u < U; ++u) st<NT>(&a.out[base + (size_t)u * BL], r[u]);
         } else {
             for (int u = 0; u < U; ++u) {
-                const size_t i = base + (size_t)u * kBlock;
+                const size_t i = base + (size_t)u * BL;
                 if (i >= a.nvec) break;
                 u32x4 x[NL][1];
 #pragma unroll
@@ -139,6 +139,17 @@ __global__ __launch_bounds__(kBlock) void k_reduce_tree_scalar(TreeScalarArgs a)
     }
 }
 
+template <int DT, int OP, int NL, int BL>
+static hipError_t launch_tree_vec(const TreeArgs& a, bool nt, hipStream_t s) {
+    constexpr int U = NL <= 4 ? 4 : 2;
+    const size_t trips = (a.nvec + (size_t)BL * U - 1) / ((size_t)BL * U);
+    const size_t cap = reduce_tuning().max_blocks > 0 ? (size_t)reduce_tuning().max_blocks : trips;
+    const int grid = (int)(trips < cap ? trips : cap);
+    if (nt) hipLaunchKernelGGL((k_reduce_tree<DT, OP, NL, U, true, BL>), dim3(grid), dim3(BL), 0, s, a);
+    else hipLaunchKernelGGL((k_reduce_tree<DT, OP, NL, U, false, BL>), dim3(grid), dim3(BL), 0, s, a);
+    return hipGetLastError();
+}
+
 template <int DT, int OP, int NL>
 static hipError_t launch_tree_nl(const TreeArgs& a, const TreeScalarArgs* sa, hipStream_t s) {
     if (sa) {
@@ -147,16 +158,12 @@ static hipError_t launch_tree_nl(const TreeArgs& a, const TreeScalarArgs* sa, hi
         hipLaunchKernelGGL((k_reduce_tree_scalar<DT, OP, NL>), dim3(grid), dim3(kBlock), 0, s, *sa);
         return hipGetLastError();
     }
-    constexpr int U = NL <= 4 ? 4 : 2;
+    // same policy as launch_vec_m: streaming calls (>= 128 MiB) nt with one-wave workgroups
     const ReduceTuning& t = reduce_tuning();
-    const size_t trips = (a.nvec + (size_t)kBlock * U - 1) / ((size_t)kBlock * U);
-    const size_t cap = t.max_blocks > 0 ? (size_t)t.max_blocks : trips;
-    const int grid = (int)(trips < cap ? trips : cap);
     const size_t call_bytes = (size_t)(a.nl + 1) * a.nvec * 16;
     const bool nt = t.nt_mode == 1 || (t.nt_mode < 0 && call_bytes >= t.nt_min_bytes);
-    if (nt) hipLaunchKernelGGL((k_reduce_tree<DT, OP, NL, U, true>), dim3(grid), dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL((k_reduce_tree<DT, OP, NL, U, false>), dim3(grid), dim3(kBlock), 0, s, a);
-    return hipGetLastError();
+    const int bl = t.block ? t.block : nt ? 64 : 256;
+    return bl == 64 ? launch_tree_vec<DT, OP, NL, 64>(a, nt, s) : launch_tree_vec<DT, OP, NL, 256>(a, nt, s);
 }
 
 template <int DT, int OP>

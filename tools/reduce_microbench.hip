@@ -731,6 +731,102 @@ static void focus5(size_t bytes, int sets, int rounds) {
     free_sets(S);
 }
 
+// ---- focus6: the achievable ceiling for this traffic mix, and small workgroups ----------------
+// k_rd: R read streams (nt), no store unless a sum hits a sentinel no random input produces, so
+// the loads cannot be removed.  k_wr: W nt store streams of a constant.  Together they say what
+// 2 reads + 1 write per element can reach on this HBM, which bounds the m = 1 kernel better
+// than the 8 TB/s spec.
+template <int R>
+__global__ __launch_bounds__(256) void k_rd(Args a, float sentinel) {
+    const size_t base = (size_t)blockIdx.x * 256 * 4 + threadIdx.x;
+    f32x4 x[R][4];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            x[r][u] = __builtin_nontemporal_load(r == 0 ? &a.acc[base + (size_t)u * 256] : &a.ins[r - 1][base + (size_t)u * 256]);
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 s = x[0][0];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (r || u) s += x[r][u];
+    if (s[0] == sentinel && s[1] == sentinel) a.out[base] = s;
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void k_wr(Args a, float v) {
+    const size_t base = (size_t)blockIdx.x * 256 * 4 + threadIdx.x;
+    f32x4 c = {v, v + 1.f, v + 2.f, v + 3.f};
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            __builtin_nontemporal_store(c, (w == 0 ? a.out : (f32x4*)a.ins[w - 1]) + base + (size_t)u * 256);
+}
+
+static void report_moved(const char* name, double moved_bytes, double us) {
+    const double gbps = moved_bytes / (us * 1e-6) / 1e9;
+    std::printf("%-34s moved=%7.1f MiB  %9.2f us  %8.1f GB/s  %.3f of 8 TB/s\n", name, moved_bytes / (1 << 20), us,
+                gbps, gbps / 8000.0);
+    std::fflush(stdout);
+}
+
+static void focus6(size_t bytes, int sets, int rounds) {
+    const size_t nvec = bytes / 16;
+    Sets S = make_sets(1, nvec, sets);
+    const int reps = 200;
+    const int G = (int)(nvec / 1024);
+    auto args_for = [&](int i) {
+        Args a{};
+        auto& b = S.bufs[i % sets];
+        a.out = b[0];
+        a.acc = b[0];
+        a.ins[0] = b[1];
+        a.nvec = nvec;
+        return a;
+    };
+    char tag[64];
+    std::snprintf(tag, sizeof tag, " sets=%d", sets);
+    for (int r = 0; r < rounds; ++r) {
+        double us = time_launches([&](int i) {
+            Args a = args_for(i);
+            const void* ins[1] = {a.ins[0]};
+            chr_reduce_multi(a.out, a.acc, ins, 1, a.nvec * 4, CHR_FLOAT32, CHR_SUM, 0);
+        }, reps);
+        report_moved((std::string("product 2R+1W") + tag).c_str(), 3.0 * bytes, us);
+        const double t_prod = us;
+        us = time_launches([&](int i) { hipLaunchKernelGGL(k_rd<2>, dim3(G), dim3(256), 0, 0, args_for(i), 1e30f); }, reps);
+        report_moved((std::string("read-only 2R") + tag).c_str(), 2.0 * bytes, us);
+        const double t_rd = us;
+        us = time_launches([&](int i) { hipLaunchKernelGGL(k_rd<1>, dim3(G), dim3(256), 0, 0, args_for(i), 1e30f); }, reps);
+        report_moved((std::string("read-only 1R") + tag).c_str(), 1.0 * bytes, us);
+        us = time_launches([&](int i) { hipLaunchKernelGGL(k_wr<1>, dim3(G), dim3(256), 0, 0, args_for(i), (float)i); }, reps);
+        report_moved((std::string("write-only 1W") + tag).c_str(), 1.0 * bytes, us);
+        const double t_wr = us;
+        us = time_launches([&](int i) { hipLaunchKernelGGL(k_wr<2>, dim3(G), dim3(256), 0, 0, args_for(i), (float)i); }, reps);
+        report_moved((std::string("write-only 2W") + tag).c_str(), 2.0 * bytes, us);
+        std::printf("serial bound (2R time + 1W time) = %.2f us -> %.1f GB/s; product at %.3f of it\n", t_rd + t_wr,
+                    3.0 * bytes / ((t_rd + t_wr) * 1e-6) / 1e9, (t_rd + t_wr) / t_prod);
+#define R(U, BL, NAME)                                                                                        \
+    {                                                                                                         \
+        const int Gr = (int)((nvec + (size_t)BL * U - 1) / ((size_t)BL * U));                                 \
+        double u_ = time_launches([&](int i) { hipLaunchKernelGGL((k_reg<1, U, BL, true, true, true>), dim3(Gr), dim3(BL), 0, 0, args_for(i)); }, reps); \
+        report((std::string(NAME) + tag).c_str(), 1, bytes, u_);                                              \
+    }
+        R(4, 256, "reg NT U4 B256");
+        R(4, 128, "reg NT U4 B128");
+        R(8, 128, "reg NT U8 B128");
+        R(4, 64, "reg NT U4 B64");
+        R(8, 64, "reg NT U8 B64");
+        R(16, 64, "reg NT U16 B64");
+#undef R
+        std::printf("--\n");
+    }
+    free_sets(S);
+}
+
 // correctness spot check of every variant family against a host sum
 static void check() {
     const size_t nvec = (1 << 20) + 37;
@@ -851,6 +947,11 @@ int main(int argc, char** argv) {
     check();
     if (argc > 1 && std::string(argv[1]) == "layout") {
         layout_mode();
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus6") {
+        focus6(64 << 20, 16, 2);
+        focus6(1024ull << 20, 2, 1);
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus5") {
