@@ -333,6 +333,17 @@ def bench_allreduce(args):
     recv = torch.empty(count * es, dtype=torch.uint8, device=dev)
     ca.check(ca.fill(send, count, dt, 0, SEED, rank, stream=stream))
     torch.cuda.synchronize()
+    # The metric runs CHR_SCHEDULE_AUTO (unless CHR_SCHEDULE names one): the first call for these
+    # arguments times FLAT / FLAT_SEQ / FLAT_AG at several pipeline depths, the ranks agree on the
+    # slowest rank's times and every later call uses the fastest.  That setup call (plan compile,
+    # scratch, tuning) runs here, before warmup and outside the timed region, like communicator init.
+    sched_env = os.environ.get("CHR_SCHEDULE")
+    metric_sched = ca.SCHEDULE_AUTO if sched_env in (None, "auto", "6") else None
+    if metric_sched is not None:
+        comm.set_schedule(metric_sched)
+    ca.check(ca.all_reduce_radix_batch(send, recv, count, dt, ca.SUM, comm, k, b))
+    tuned = comm.tuned_schedule(ca.MODE_ALLREDUCE, count, dt, k, b) if metric_sched is not None else None
+    sched_names = {0: "reference", 1: "balanced", 2: "flat", 3: "exact", 4: "flat_ag", 5: "flat_seq"}
     for _ in range(args.warmup):
         ca.check(ca.all_reduce_radix_batch(send, recv, count, dt, ca.SUM, comm, k, b, async_op=True))
     torch.cuda.synchronize()
@@ -378,8 +389,11 @@ def bench_allreduce(args):
                     "algorithmic_bytes_per_call": float(busiest[1]), "launches_per_call": int(busiest[2]),
                     "kernel_ms_per_call": round(float(busiest[0]), 4)}
     # bytes on the busiest directed link of this schedule (max over ranks; slicing only splits messages)
-    sched = {"reference": 0, "0": 0, "balanced": 1, "1": 1, "exact": 3, "3": 3, "flat_ag": 4, "4": 4, "flat_seq": 5,
-             "5": 5}.get(os.environ.get("CHR_SCHEDULE", "flat"), 2)
+    if tuned is not None:
+        sched = tuned[0]
+    else:
+        sched = {"reference": 0, "0": 0, "balanced": 1, "1": 1, "exact": 3, "3": 3, "flat_ag": 4, "4": 4,
+                 "flat_seq": 5, "5": 5}.get(sched_env or "flat", 2)
     plan = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, world, rank, k, b, count, 1, sched))
     per_peer = {}
     for st in plan["steps"]:
@@ -389,7 +403,7 @@ def bench_allreduce(args):
     dist.all_reduce(lb, op=dist.ReduceOp.MAX)
     link_bytes = int(lb.item())
     compare = None if args.no_compare else compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b,
-                                                         world, dev)
+                                                         world, dev, metric_sched)
     # the reference CPU+MPI path on this box's host cores, after every GPU timing (rank 0 runs
     # it; the other ranks wait at the barrier)
     cpu = None
@@ -404,7 +418,8 @@ def bench_allreduce(args):
             "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
             "config": {"workload": f"all_reduce_radix_batch, {S >> 20} MiB per rank, k={k}, b={b}, RCCL p2p over "
                                    f"xGMI, device-resident", "k": k, "b": b, "count": count,
-                       "schedule": os.environ.get("CHR_SCHEDULE", "flat"),
+                       "schedule": (f"auto -> {sched_names.get(tuned[0], tuned[0])}, {tuned[1]} slices" if tuned
+                                    else sched_env or "flat"),
                        "parallelism": f"collective x{world}"},
             "algbw_GBps": round(algbw, 2), "busbw_GBps": round(busbw, 2),
             # rank 0's host enqueue time per call: close to ms_per_step would mean host-bound
@@ -446,7 +461,7 @@ def _timed_max(torch, dist, fn, steps, warmup):
     return float(t.item())
 
 
-def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, world, dev):
+def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, world, dev, metric_sched=None):
     """Context, not the metric: on the same buffers and ranks, (1) RCCL's own ncclAllReduce
     (torch.distributed nccl group), (2) the reference's MPICH ring baseline
     (testing/mpich_implementations/all_reduce/allreduce_ring.cpp) run on libchiara's executor and
@@ -476,7 +491,9 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
         ca.check(ca.MPICH_Allreduce_ring(send, recv, count, dt, ca.SUM, comm, async_op=True))
     out["mpich_ring_on_libchiara"] = entry(_timed_max(torch, dist, ring, steps, warm))
 
-    # the same radix/batch arithmetic under the other two schedules (same bits, other routes)
+    # the same radix/batch arithmetic under the other schedules (same bits, other routes)
+    restore = ca.SCHEDULE_FLAT if metric_sched is None else metric_sched
+
     def radix():
         ca.check(ca.all_reduce_radix_batch(send, recv, count, dt, ca.SUM, comm, k, b, async_op=True))
     comm.set_overlap(False)
@@ -484,7 +501,8 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
         out["radix_batch_no_overlap"] = entry(_timed_max(torch, dist, radix, steps, warm))
     finally:
         comm.set_overlap(True)
-    for name, sch in (("radix_batch_balanced", ca.SCHEDULE_BALANCED),
+    for name, sch in (("radix_batch_flat", ca.SCHEDULE_FLAT),
+                      ("radix_batch_balanced", ca.SCHEDULE_BALANCED),
                       ("radix_batch_reference_route", ca.SCHEDULE_REFERENCE),
                       ("radix_batch_exact_reference_messages", ca.SCHEDULE_EXACT),
                       ("radix_batch_flat_rccl_allgather", ca.SCHEDULE_FLAT_AG),
@@ -493,14 +511,18 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
         try:
             out[name] = entry(_timed_max(torch, dist, radix, steps, warm))
         finally:
-            comm.set_schedule(ca.SCHEDULE_FLAT)
-    # pipeline depth of the metric's own (flat) schedule: automatic is 8 slices at 1 GiB
-    for P in (1, 2, 4):
-        comm.set_slices(P)
-        try:
-            out[f"radix_batch_flat_slices{P}"] = entry(_timed_max(torch, dist, radix, steps, warm))
-        finally:
-            comm.set_slices(0)
+            comm.set_schedule(restore)
+    # pipeline depth of the flat schedule: automatic is 8 slices at 1 GiB
+    comm.set_schedule(ca.SCHEDULE_FLAT)
+    try:
+        for P in (1, 2, 4):
+            comm.set_slices(P)
+            try:
+                out[f"radix_batch_flat_slices{P}"] = entry(_timed_max(torch, dist, radix, steps, warm))
+            finally:
+                comm.set_slices(0)
+    finally:
+        comm.set_schedule(restore)
     out.update(baseline_configs(args, ca, torch, dist, comm, world, dev, steps, warm))
     return out
 

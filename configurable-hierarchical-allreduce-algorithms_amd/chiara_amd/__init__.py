@@ -10,7 +10,7 @@ from .collectives import (  # noqa: F401
     MODE_ALLGATHER, MODE_ALLREDUCE, MODE_MPICH_KRSAG, MODE_MPICH_RD, MODE_MPICH_RECEXCH, MODE_MPICH_RING,
     MODE_MPICH_RMULT, MODE_MPICH_RSAG, MPICH_Allreduce_k_reduce_scatter_allgather,
     MPICH_Allreduce_recursive_multiplying,
-    MODE_REDUCE_SCATTER, PROD, REDUCE_RUNNING_FIRST, SCHEDULE_BALANCED, SCHEDULE_EXACT, SCHEDULE_FLAT, SCHEDULE_FLAT_AG, SCHEDULE_FLAT_SEQ,
+    MODE_REDUCE_SCATTER, PROD, REDUCE_RUNNING_FIRST, SCHEDULE_BALANCED, SCHEDULE_EXACT, SCHEDULE_FLAT, SCHEDULE_FLAT_AG, SCHEDULE_FLAT_SEQ, SCHEDULE_AUTO,
     SCHEDULE_REFERENCE,
     SUCCESS, SUM, Comm, LocalGroup,
     MPICH_Allreduce_recursive_doubling, MPICH_Allreduce_recursive_exchange,

@@ -35,6 +35,7 @@ MODE_MPICH_RING, MODE_MPICH_RD, MODE_MPICH_RSAG, MODE_MPICH_RECEXCH = 2, 3, 4, 5
 MODE_MPICH_KRSAG, MODE_MPICH_RMULT = 6, 7
 MODE_ALLGATHER = 8
 SCHEDULE_REFERENCE, SCHEDULE_BALANCED, SCHEDULE_FLAT, SCHEDULE_EXACT, SCHEDULE_FLAT_AG, SCHEDULE_FLAT_SEQ = 0, 1, 2, 3, 4, 5
+SCHEDULE_AUTO = 6  # measured choice among FLAT / FLAT_SEQ / FLAT_AG and the pipeline depth (Comm only)
 REDUCE_RUNNING_FIRST = 1  # chr_reduce_multi_ex flag (MPICH_do_reduce operand order)
 
 
@@ -140,9 +141,16 @@ class Comm:
         check(lib().chr_comm_set_overlap(self._h, int(bool(enable))))
 
     def set_schedule(self, schedule):
-        """SCHEDULE_REFERENCE / SCHEDULE_BALANCED / SCHEDULE_FLAT / SCHEDULE_EXACT: where reductions are evaluated
-        (never what they compute)."""
+        """SCHEDULE_REFERENCE / SCHEDULE_BALANCED / SCHEDULE_FLAT / SCHEDULE_EXACT / SCHEDULE_FLAT_AG /
+        SCHEDULE_FLAT_SEQ / SCHEDULE_AUTO: where reductions are evaluated (never what they compute)."""
         check(lib().chr_comm_set_schedule(self._h, int(schedule)))
+
+    def tuned_schedule(self, mode, count, datatype, k, b):
+        """(schedule, slices) SCHEDULE_AUTO kept for a collective already called with these arguments,
+        or None."""
+        sc, sl = ctypes.c_int(), ctypes.c_int()
+        rc = lib().chr_comm_tuned_schedule(self._h, mode, count, datatype, k, b, ctypes.byref(sc), ctypes.byref(sl))
+        return (sc.value, sl.value) if rc == SUCCESS else None
 
     def profile(self, enable=True):
         """Time every fused reduction launch and every step's RCCL group of this communicator (HIP events)."""

@@ -198,7 +198,7 @@ bool is_device_ptr(const void* p) {
 
 using PlanKey = std::tuple<int, int, int, int, uint64_t, int, int, int>;  // mode, rank, k, b, count, dtype size, slices, schedule
 
-// CHR_SCHEDULE = reference | balanced | flat | exact | flat_ag | flat_seq (or 0 .. 5); default flat
+// CHR_SCHEDULE = reference | balanced | flat | exact | flat_ag | flat_seq | auto (or 0 .. 6); default flat
 // CHR_OVERLAP=0: local ops on the transfer stream (no compute/xGMI overlap); default 1
 int default_overlap() {
     static const int v = [] {
@@ -218,6 +218,7 @@ int default_schedule() {
         if (s == "exact" || s == "3") return (int)chr::SCHED_EXACT;
         if (s == "flat_ag" || s == "4") return (int)chr::SCHED_FLAT_AG;
         if (s == "flat_seq" || s == "5") return (int)chr::SCHED_FLAT_SEQ;
+        if (s == "auto" || s == "6") return CHR_SCHEDULE_AUTO;
         return (int)chr::SCHED_FLAT;
     }();
     return v;
@@ -259,13 +260,16 @@ struct chr_comm {
     ReduceProfile prof;
     std::map<PlanKey, std::unique_ptr<Plan>> plans;
 
-    const Plan& plan(int mode, int k, int b, uint64_t count, size_t es) {
-        const int P = pick_slices(slices, count, mode, nranks, b, es);
-        PlanKey key{mode, rank, k, b, count, (int)es, P, sched};
+    // CHR_SCHEDULE_AUTO: (mode, count, element size, k, b, slices setting, overlap) -> (schedule, depth)
+    std::map<std::tuple<int, uint64_t, int, int, int, int, int>, std::pair<int, int>> tuned;
+
+    const Plan& plan(int mode, int k, int b, uint64_t count, size_t es, int sched_, int slices_) {
+        const int P = pick_slices(slices_, count, mode, nranks, b, es);
+        PlanKey key{mode, rank, k, b, count, (int)es, P, sched_};
         auto it = plans.find(key);
         if (it == plans.end())
             it = plans.emplace(key, std::make_unique<Plan>(chr::build_plan((chr::Mode)mode, nranks, rank, k, b, count, P,
-                                                                           sched)))
+                                                                           sched_)))
                      .first;
         return *it->second;
     }
@@ -274,7 +278,7 @@ struct chr_comm {
 struct chr_local_group {
     int nranks = 0, device = 0;
     int slices = 0;  // 0 = auto
-    int sched = default_schedule();
+    int sched = default_schedule() == CHR_SCHEDULE_AUTO ? (int)chr::SCHED_FLAT : default_schedule();  // no tuning
     hipStream_t stream = nullptr;
     std::vector<DevBuf> acc, stage;
     std::map<std::tuple<int, int, int, uint64_t, int, int, int>, std::vector<Plan>> plans;
@@ -361,10 +365,9 @@ int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int d
     return CHR_SUCCESS;
 }
 
-int collective(chr_comm* c, int mode, const void* send, void* recv, size_t count, int dtype, int op, int k, int b,
-               bool sync) {
-    if (!c || !chr::valid_dtype_op(dtype, op)) return CHR_ERR_INVALID_ARG;
-    const Plan& p = c->plan(mode, k, b, count, chr::dtype_size(dtype));
+int run_collective(chr_comm* c, int sched, int slices, int mode, const void* send, void* recv, size_t count, int dtype,
+                   int op, int k, int b, bool sync) {
+    const Plan& p = c->plan(mode, k, b, count, chr::dtype_size(dtype), sched, slices);
     if (p.error) return p.error;
     if (p.g.total == 0) return CHR_SUCCESS;
     if (!recv) return CHR_ERR_INVALID_ARG;
@@ -402,6 +405,117 @@ int collective(chr_comm* c, int mode, const void* send, void* recv, size_t count
         (e = hipMemcpyAsync(recv, drecv, p.recv_elems * es, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
         return hip_code(e);
     return hip_code(hipStreamSynchronize(c->stream));
+}
+
+// CHR_SCHEDULE_AUTO.  The single-node schedules FLAT, FLAT_SEQ and FLAT_AG move the same bits
+// over the same full-mesh traffic (2S/n per link) but differ in how RCCL groups and collectives
+// share the links, and the pipeline depth trades overlap against per-group latency; which is
+// fastest is a property of the machine, so on the first device-resident call for a given
+// (collective, count, dtype, k, b) every candidate runs TUNE_REPS timed calls, the ranks agree on
+// the slowest rank's time per candidate (one ncclAllReduce(max), so every rank picks the same
+// one) and the fastest is kept for every later call.  Each tuning call is a complete collective;
+// an in-place call is tuned on temporary copies so the caller's data is reduced exactly once.
+constexpr int TUNE_REPS = 3;
+
+int tune_schedule(chr_comm* c, int mode, const void* send, void* recv, size_t count, int dtype, int op, int k, int b,
+                  int* sched_out, int* slices_out) {
+    *sched_out = chr::SCHED_FLAT;
+    *slices_out = c->slices;
+    if (chr::is_mpich(mode) || mode == chr::MODE_ALLGATHER || c->nranks < 2) return CHR_SUCCESS;
+    const size_t es = chr::dtype_size(dtype);
+    const bool inplace = send == CHR_IN_PLACE;
+    const void* input = inplace ? (const void*)recv : send;
+    if (!input || !recv || !is_device_ptr(input) || !is_device_ptr(recv)) return CHR_SUCCESS;  // host-staged: FLAT
+    auto key = std::make_tuple(mode, (uint64_t)count, (int)es, k, b, c->slices, c->overlap);
+    auto it = c->tuned.find(key);
+    if (it != c->tuned.end()) {
+        *sched_out = it->second.first;
+        *slices_out = it->second.second;
+        return CHR_SUCCESS;
+    }
+    const Plan& p0 = c->plan(mode, k, b, count, es, chr::SCHED_FLAT, c->slices);
+    if (p0.error) return p0.error;
+    std::vector<std::pair<int, int>> cand;
+    std::vector<int> depths;
+    const int pa = pick_slices(c->slices, count, mode, c->nranks, b, es);
+    for (int d = pa; d >= 1; d /= 2) {
+        depths.push_back(d);
+        if (c->slices > 0) break;  // an explicit depth is kept
+    }
+    for (int sc : {(int)chr::SCHED_FLAT, (int)chr::SCHED_FLAT_SEQ, (int)chr::SCHED_FLAT_AG})
+        for (int d : depths) cand.push_back({sc, d});
+    // in place: tune on copies (the collective would otherwise reduce the caller's data again)
+    void* tsend = nullptr;
+    void* trecv = nullptr;
+    const void* s_arg = send;
+    void* r_arg = recv;
+    hipError_t e = hipSuccess;
+    if (inplace) {
+        if ((e = hipMalloc(&tsend, p0.send_elems * es)) != hipSuccess ||
+            (e = hipMalloc(&trecv, p0.recv_elems * es)) != hipSuccess ||
+            (e = hipMemcpyAsync(tsend, recv, p0.send_elems * es, hipMemcpyDeviceToDevice, c->stream)) != hipSuccess) {
+            (void)hipFree(tsend);
+            (void)hipFree(trecv);
+            return hip_code(e);
+        }
+        s_arg = tsend;
+        r_arg = trecv;
+    }
+    std::vector<float> ms(cand.size(), 0.f);
+    int rc = CHR_SUCCESS;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if ((e = hipEventCreate(&e0)) != hipSuccess || (e = hipEventCreate(&e1)) != hipSuccess) rc = hip_code(e);
+    for (size_t i = 0; i < cand.size() && !rc; ++i) {
+        const int sc = cand[i].first, d = cand[i].second;
+        // untimed first call: plan compile, scratch growth, RCCL connection setup
+        if ((rc = run_collective(c, sc, d, mode, s_arg, r_arg, count, dtype, op, k, b, true))) break;
+        if ((rc = hip_code(hipEventRecord(e0, c->stream)))) break;
+        for (int r = 0; r < TUNE_REPS && !rc; ++r)
+            rc = run_collective(c, sc, d, mode, s_arg, r_arg, count, dtype, op, k, b, false);
+        if (rc || (rc = hip_code(hipEventRecord(e1, c->stream))) || (rc = hip_code(hipEventSynchronize(e1)))) break;
+        rc = hip_code(hipEventElapsedTime(&ms[i], e0, e1));
+    }
+    float* dms = nullptr;
+    if (!rc && (rc = hip_code(hipMalloc(&dms, ms.size() * sizeof(float)))) == CHR_SUCCESS) {
+        if (!(rc = hip_code(hipMemcpyAsync(dms, ms.data(), ms.size() * sizeof(float), hipMemcpyHostToDevice,
+                                           c->stream))) &&
+            !(rc = nccl_code(ncclAllReduce(dms, dms, ms.size(), ncclFloat32, ncclMax, c->nccl, c->stream))) &&
+            !(rc = hip_code(hipMemcpyAsync(ms.data(), dms, ms.size() * sizeof(float), hipMemcpyDeviceToHost,
+                                           c->stream))))
+            rc = hip_code(hipStreamSynchronize(c->stream));
+    }
+    (void)hipFree(dms);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (inplace) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(tsend);
+        (void)hipFree(trecv);
+    }
+    if (rc) return rc;
+    size_t best = 0;
+    for (size_t i = 1; i < cand.size(); ++i)
+        if (ms[i] < ms[best]) best = i;
+    if (std::getenv("CHR_TUNE_VERBOSE") && c->rank == 0)
+        for (size_t i = 0; i < cand.size(); ++i)
+            std::fprintf(stderr, "[chiara] tune mode %d count %zu: schedule %d slices %d  %.3f ms%s\n", mode, count,
+                         cand[i].first, cand[i].second, ms[i] / TUNE_REPS, i == best ? "  <- kept" : "");
+    c->tuned[key] = cand[best];
+    *sched_out = cand[best].first;
+    *slices_out = cand[best].second;
+    return CHR_SUCCESS;
+}
+
+int collective(chr_comm* c, int mode, const void* send, void* recv, size_t count, int dtype, int op, int k, int b,
+               bool sync) {
+    if (!c || !chr::valid_dtype_op(dtype, op)) return CHR_ERR_INVALID_ARG;
+    int sched = c->sched, slices = c->slices;
+    if (sched == CHR_SCHEDULE_AUTO) {
+        if (hipSetDevice(c->device) != hipSuccess) return CHR_ERR_HIP;
+        int rc = tune_schedule(c, mode, send, recv, count, dtype, op, k, b, &sched, &slices);
+        if (rc) return rc;
+    }
+    return run_collective(c, sched, slices, mode, send, recv, count, dtype, op, k, b, sync);
 }
 
 int local_collective(chr_local_group* g, int mode, const void* const* sends, void* const* recvs, size_t count,
@@ -605,8 +719,19 @@ int chr_comm_set_overlap(chr_comm* c, int enable) {
 }
 
 int chr_comm_set_schedule(chr_comm* c, int schedule) {
-    if (!c || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_FLAT_SEQ) return CHR_ERR_INVALID_ARG;
+    if (!c || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_AUTO) return CHR_ERR_INVALID_ARG;
     c->sched = schedule;
+    return CHR_SUCCESS;
+}
+
+int chr_comm_tuned_schedule(const chr_comm* c, int mode, size_t count, chr_dtype dtype, int k, int b, int* schedule,
+                            int* slices) {
+    if (!c || !schedule || !slices || !chr::valid_dtype_op(dtype, CHR_SUM)) return CHR_ERR_INVALID_ARG;
+    auto it = c->tuned.find(std::make_tuple(mode, (uint64_t)count, (int)chr::dtype_size(dtype), k, b, c->slices,
+                                            c->overlap));
+    if (it == c->tuned.end()) return CHR_ERR_INVALID_ARG;
+    *schedule = it->second.first;
+    *slices = it->second.second;
     return CHR_SUCCESS;
 }
 

@@ -129,14 +129,25 @@ int chr_comm_set_slices(chr_comm* comm, int slices);
  *                           movement only, so identical bits
  *   CHR_SCHEDULE_FLAT_SEQ   FLAT with its gather and allgather in separate RCCL groups (FLAT
  *                           merges the gather of slice t with the allgather of slice t-2)
- * Env CHR_SCHEDULE=reference|balanced|flat|exact|flat_ag|flat_seq sets the default.  DESIGN.md §5. */
+ * Env CHR_SCHEDULE=reference|balanced|flat|exact|flat_ag|flat_seq|auto sets the default.  DESIGN.md §5. */
 #define CHR_SCHEDULE_REFERENCE 0
 #define CHR_SCHEDULE_BALANCED 1
 #define CHR_SCHEDULE_FLAT 2
 #define CHR_SCHEDULE_EXACT 3
 #define CHR_SCHEDULE_FLAT_AG 4
 #define CHR_SCHEDULE_FLAT_SEQ 5
+/*   CHR_SCHEDULE_AUTO       chooses among FLAT, FLAT_SEQ and FLAT_AG and the pipeline depth by
+ *                           measurement: on the first device-resident call for a (collective,
+ *                           count, dtype, k, b) every candidate runs a few complete collectives,
+ *                           the ranks agree on the slowest rank's times (one ncclAllReduce) and
+ *                           the fastest is kept.  Same bits as every other schedule.  Host-staged
+ *                           calls and the other collectives use FLAT. */
+#define CHR_SCHEDULE_AUTO 6
 int chr_comm_set_schedule(chr_comm* comm, int schedule);
+/* What CHR_SCHEDULE_AUTO chose for a collective already called with these arguments
+ * (mode: 0 allreduce_radix_batch, 1 reduce_scatter_radix_batch; count as passed). */
+int chr_comm_tuned_schedule(const chr_comm* comm, int mode, size_t count, chr_dtype dtype, int k, int b, int* schedule,
+                            int* slices);
 /* Compute/xGMI overlap (default on; env CHR_OVERLAP=0): local reductions run on a second HIP
  * stream, ordered against the RCCL transfers by events where the plan's data dependencies
  * require it, so e.g. the flat schedule reduces slice s while slice s+1 is being gathered.

@@ -47,6 +47,7 @@ def _worker(rank, world, port, cases, q):
             comm.set_slices(slices)
             comm.set_schedule(extra[0] if extra else ca.SCHEDULE_FLAT)
             comm.set_overlap(extra[1] if len(extra) > 1 else True)
+            inplace = len(extra) > 2 and extra[2]
             npdt = po.NP_DTYPES[dtype]
             cdt = {"f32": ca.FLOAT32, "bf16": ca.BFLOAT16, "i32": ca.INT32}[dtype]
             in_n = count * world if mode == "rs" else count
@@ -55,6 +56,9 @@ def _worker(rank, world, port, cases, q):
             x = po.fill(in_n, dtype, pat, 4242, rank)
             if host:
                 send, out = x, np.zeros(out_n, dtype=npdt)
+            elif inplace:  # MPI_IN_PLACE: the input sits in the receive buffer
+                out_t = torch.from_numpy(x.view(np.uint8).copy()).to(dev)
+                send = ca.IN_PLACE
             else:
                 send = torch.from_numpy(x.view(np.uint8).copy()).to(dev)
                 out_t = torch.zeros(out_n * x.itemsize, dtype=torch.uint8, device=dev)
@@ -83,8 +87,15 @@ def _worker(rank, world, port, cases, q):
                 rc = fn(send, dst, count, cdt, ca.SUM, comm)
                 ref = po.mpich_allreduce(mode, allx, dtype, "sum")[rank]
             if not host:
-                out = out_t.cpu().numpy().view(npdt)
-            q.put((rank, mode, k, b, rc, bool(np.array_equal(out.view(np.uint8), ref.view(np.uint8)))))
+                out = out_t.cpu().numpy().view(npdt)[:out_n]
+            ok = bool(np.array_equal(out.view(np.uint8), ref.view(np.uint8)))
+            if extra and extra[0] == ca.SCHEDULE_AUTO and mode in ("ar", "rs"):
+                # device calls keep a measured choice; host-staged ones run FLAT untuned
+                tuned = comm.tuned_schedule(ca.MODE_ALLREDUCE if mode == "ar" else ca.MODE_REDUCE_SCATTER, count, cdt,
+                                            k, b)
+                ok = ok and ((tuned is None) == host)
+                ok = ok and (tuned is None or tuned[0] in (ca.SCHEDULE_FLAT, ca.SCHEDULE_FLAT_SEQ, ca.SCHEDULE_FLAT_AG))
+            q.put((rank, mode, k, b, rc, ok))
     finally:
         comm.destroy()
         dist.destroy_process_group()
@@ -147,6 +158,19 @@ def test_rccl_schedules_and_overlap_world4():
             cases.append(("ar", 4, 4, 1 << 18, "f32", False, 4, sched, ov))
             cases.append(("rs", 2, 2, 1 << 15, "f32", False, 3, sched, ov))
     cases.append(("ar", 2, 4, 1 << 18, "bf16", False, 5, 2, True))  # multi-phase tree, flat
+    _run(4, cases, timeout=600)
+
+
+def test_rccl_auto_schedule_world4():
+    """CHR_SCHEDULE_AUTO over RCCL: the first call per argument set times FLAT / FLAT_SEQ /
+    FLAT_AG at several pipeline depths and every rank keeps the same one (a disagreement would
+    hang); the result of the tuning call and of the cached later call is bit-exact vs the
+    oracle, in place (tuned on copies: the caller's data is reduced once) and host-staged."""
+    A = 6  # SCHEDULE_AUTO
+    cases = [("ar", 4, 4, 1 << 18, "f32", False, 0, A, True), ("ar", 4, 4, 1 << 18, "f32", False, 0, A, True),
+             ("ar", 2, 2, 1 << 16, "bf16", False, 0, A, True, True), ("ar", 2, 2, 1 << 16, "bf16", False, 0, A, True, True),
+             ("rs", 2, 2, 1 << 15, "f32", False, 0, A, True), ("rs", 4, 4, 4000, "f32", False, 0, A, True, True),
+             ("ar", 4, 4, 1 << 14, "f32", True, 0, A, True), ("ar", 2, 4, 8 * 1001, "bf16", False, 3, A, False)]
     _run(4, cases, timeout=600)
 
 
