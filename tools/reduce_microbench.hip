@@ -827,6 +827,50 @@ static void focus6(size_t bytes, int sets, int rounds) {
     free_sets(S);
 }
 
+// ---- focus7: vectors per lane (U) for fan-in m >= 3 with one-wave workgroups -----------------
+// k_reg's slot-0 accumulator load is plain (LLVM merges it with the tail path's), i.e. the
+// product's ACC0 policy, which the product uses for every m >= 2 call.
+template <int M>
+static void focus7_m(size_t bytes, int sets, int rounds) {
+    const size_t nvec = bytes / 16;
+    Sets S = make_sets(M, nvec, sets);
+    const int reps = 100;
+    auto args_for = [&](int i) {
+        Args a{};
+        auto& b = S.bufs[i % sets];
+        a.out = b[0];
+        a.acc = b[0];
+        for (int j = 0; j < M; ++j) a.ins[j] = b[j + 1];
+        a.nvec = nvec;
+        return a;
+    };
+    char tag[64];
+    std::snprintf(tag, sizeof tag, " sets=%d", sets);
+    for (int r = 0; r < rounds; ++r) {
+        double us = time_launches([&](int i) {
+            Args a = args_for(i);
+            const void* ins[8];
+            for (int j = 0; j < M; ++j) ins[j] = a.ins[j];
+            chr_reduce_multi(a.out, a.acc, ins, M, a.nvec * 4, CHR_FLOAT32, CHR_SUM, 0);
+        }, reps);
+        report((std::string("libchiara chr_reduce_multi") + tag).c_str(), M, bytes, us);
+#define R(U, BL, NAME)                                                                                        \
+    {                                                                                                         \
+        const int Gr = (int)((nvec + (size_t)BL * U - 1) / ((size_t)BL * U));                                 \
+        double u_ = time_launches([&](int i) { hipLaunchKernelGGL((k_reg<M, U, BL, true, true, true>), dim3(Gr), dim3(BL), 0, 0, args_for(i)); }, reps); \
+        report((std::string(NAME) + tag).c_str(), M, bytes, u_);                                              \
+    }
+        R(1, 64, "reg NT U1 B64");
+        R(2, 64, "reg NT U2 B64");
+        R(4, 64, "reg NT U4 B64");
+        R(2, 128, "reg NT U2 B128");
+        R(2, 256, "reg NT U2 B256");
+#undef R
+        std::printf("--\n");
+    }
+    free_sets(S);
+}
+
 // correctness spot check of every variant family against a host sum
 static void check() {
     const size_t nvec = (1 << 20) + 37;
@@ -947,6 +991,13 @@ int main(int argc, char** argv) {
     check();
     if (argc > 1 && std::string(argv[1]) == "layout") {
         layout_mode();
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus7") {
+        focus7_m<3>(64 << 20, 8, 2);
+        focus7_m<3>(256 << 20, 2, 1);
+        focus7_m<7>(64 << 20, 4, 2);
+        focus7_m<7>(16 << 20, 16, 1);
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus6") {
