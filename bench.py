@@ -523,8 +523,35 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
                 comm.set_slices(0)
     finally:
         comm.set_schedule(restore)
+    out["small_messages"] = small_messages(ca, torch, dist, comm, dt, k, b, world, dev)
     out.update(baseline_configs(args, ca, torch, dist, comm, world, dev, steps, warm))
     return out
+
+
+def small_messages(ca, torch, dist, comm, dt, k, b, world, dev):
+    """Latency of blocking calls (the reference harness's pattern) at small buffers, issued eagerly
+    and replayed from captured HIP graphs (chr_comm_set_graphs): us per call, max over ranks."""
+    es = 4 if dt == ca.FLOAT32 else 2
+    res = {}
+    try:
+        for nbytes in (4 << 10, 256 << 10, 4 << 20):
+            count = nbytes // es - (nbytes // es) % world
+            s = torch.empty(count * es, dtype=torch.uint8, device=dev)
+            r = torch.empty(count * es, dtype=torch.uint8, device=dev)
+            ca.check(ca.fill(s, count, dt, 0, SEED, int(os.environ["RANK"]), stream=comm.stream))
+            row = {}
+            for name, g in (("eager_us", False), ("graph_us", True)):
+                comm.set_graphs(g)
+                try:
+                    el = _timed_max(torch, dist, lambda: ca.check(ca.all_reduce_radix_batch(s, r, count, dt, ca.SUM, comm,
+                                                                                             k, b)), 50, 3)
+                finally:
+                    comm.set_graphs(False)
+                row[name] = round(el / 50 * 1e6, 1)
+            res[f"{nbytes >> 10}KiB"] = row
+    except Exception as e:  # context only
+        res["error"] = str(e)[:200]
+    return res
 
 
 def baseline_configs(args, ca, torch, dist, comm, world, dev, steps, warm):

@@ -145,6 +145,10 @@ class Comm:
         SCHEDULE_FLAT_SEQ / SCHEDULE_AUTO: where reductions are evaluated (never what they compute)."""
         check(lib().chr_comm_set_schedule(self._h, int(schedule)))
 
+    def set_graphs(self, enable):
+        """Replay device-resident collectives from captured HIP graphs (one per plan and buffers)."""
+        check(lib().chr_comm_set_graphs(self._h, int(bool(enable))))
+
     def tuned_schedule(self, mode, count, datatype, k, b):
         """(schedule, slices) SCHEDULE_AUTO kept for a collective already called with these arguments,
         or None."""

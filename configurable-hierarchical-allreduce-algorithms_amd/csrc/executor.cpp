@@ -208,6 +208,15 @@ int default_overlap() {
     return v;
 }
 
+// CHR_GRAPHS=1: device-resident collectives replay a captured HIP graph per (plan, buffers)
+int default_graphs() {
+    static const int v = [] {
+        const char* e = std::getenv("CHR_GRAPHS");
+        return e ? (std::atoi(e) != 0) : 0;
+    }();
+    return v;
+}
+
 int default_schedule() {
     static const int v = [] {
         const char* e = std::getenv("CHR_SCHEDULE");
@@ -260,6 +269,14 @@ struct chr_comm {
     ReduceProfile prof;
     std::map<PlanKey, std::unique_ptr<Plan>> plans;
 
+    // HIP graph replay (chr_comm_set_graphs): one executable graph per (plan, send, recv, dtype, op, overlap),
+    // dropped whenever the scratch buffers they point into are reallocated
+    int graphs = default_graphs();
+    std::map<std::tuple<const Plan*, const void*, void*, int, int, int>, hipGraphExec_t> gexec;
+    void drop_graphs() {
+        for (auto& kv : gexec) (void)hipGraphExecDestroy(kv.second);
+        gexec.clear();
+    }
     // CHR_SCHEDULE_AUTO: (mode, count, element size, k, b, slices setting, overlap) -> (schedule, depth)
     std::map<std::tuple<int, uint64_t, int, int, int, int, int>, std::pair<int, int>> tuned;
 
@@ -365,6 +382,41 @@ int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int d
     return CHR_SUCCESS;
 }
 
+// Graph replay of a device-resident call.  A plan's whole enqueue -- RCCL groups on the transfer
+// stream, reductions and copies forked onto the compute stream and joined back by events -- is
+// captured once per (plan, buffers) and replayed with one hipGraphLaunch: the host cost of a call
+// drops from the RCCL group calls, launches and event records of every step to one launch, which
+// is what bounds small messages.  Scratch is sized before capture (no allocation inside it); if
+// that grows a buffer, every cached graph is dropped (they point into the old one).
+int launch_graph(chr_comm* c, const Plan& p, const void* send, void* recv, int dtype, int op) {
+    const size_t es = chr::dtype_size(dtype);
+    const void* acc0 = c->acc.p;
+    const void* stage0 = c->stage.p;
+    hipError_t e = c->acc.reserve(p.acc_elems * es, c->stream);
+    if (e == hipSuccess) e = c->stage.reserve(p.stage_elems * es, c->stream);
+    if (e != hipSuccess) return hip_code(e);
+    if (c->acc.p != acc0 || c->stage.p != stage0) c->drop_graphs();
+    auto key = std::make_tuple(&p, send, recv, dtype, op, c->overlap);
+    auto it = c->gexec.find(key);
+    if (it == c->gexec.end()) {
+        if (!c->event(2 * p.steps.size() + 1)) return CHR_ERR_HIP;  // the event pool, created outside the capture
+        if ((e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal)) != hipSuccess) return hip_code(e);
+        const int rc = enqueue_rccl(c, p, send, recv, dtype, op);
+        hipGraph_t g = nullptr;
+        e = hipStreamEndCapture(c->stream, &g);
+        if (rc || e != hipSuccess) {
+            if (g) (void)hipGraphDestroy(g);
+            return rc ? rc : hip_code(e);
+        }
+        hipGraphExec_t x = nullptr;
+        e = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (e != hipSuccess) return hip_code(e);
+        it = c->gexec.emplace(key, x).first;
+    }
+    return hip_code(hipGraphLaunch(it->second, c->stream));
+}
+
 int run_collective(chr_comm* c, int sched, int slices, int mode, const void* send, void* recv, size_t count, int dtype,
                    int op, int k, int b, bool sync) {
     const Plan& p = c->plan(mode, k, b, count, chr::dtype_size(dtype), sched, slices);
@@ -381,7 +433,8 @@ int run_collective(chr_comm* c, int sched, int slices, int mode, const void* sen
     if (e != hipSuccess) return hip_code(e);
     const bool dev_in = is_device_ptr(input), dev_out = is_device_ptr(recv);
     if (dev_in && dev_out) {
-        int rc = enqueue_rccl(c, p, input, recv, dtype, op);
+        int rc = c->graphs && !c->prof.on ? launch_graph(c, p, input, recv, dtype, op)
+                                          : enqueue_rccl(c, p, input, recv, dtype, op);
         if (rc || !sync) return rc;
         return hip_code(hipStreamSynchronize(c->stream));
     }
@@ -640,6 +693,7 @@ int chr_comm_destroy(chr_comm* c) {
     if (!c) return CHR_SUCCESS;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    c->drop_graphs();
     c->prof.release();
     if (c->nccl) (void)ncclCommDestroy(c->nccl);
     c->acc.release();
@@ -721,6 +775,16 @@ int chr_comm_set_overlap(chr_comm* c, int enable) {
 int chr_comm_set_schedule(chr_comm* c, int schedule) {
     if (!c || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_AUTO) return CHR_ERR_INVALID_ARG;
     c->sched = schedule;
+    return CHR_SUCCESS;
+}
+
+int chr_comm_set_graphs(chr_comm* c, int enable) {
+    if (!c) return CHR_ERR_INVALID_ARG;
+    if (!enable && c->stream) {
+        (void)hipStreamSynchronize(c->stream);
+        c->drop_graphs();
+    }
+    c->graphs = enable != 0;
     return CHR_SUCCESS;
 }
 

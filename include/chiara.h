@@ -153,6 +153,12 @@ int chr_comm_tuned_schedule(const chr_comm* comm, int mode, size_t count, chr_dt
  * require it, so e.g. the flat schedule reduces slice s while slice s+1 is being gathered.
  * The call still completes on chr_comm_stream. */
 int chr_comm_set_overlap(chr_comm* comm, int enable);
+/* HIP graph replay (default off; env CHR_GRAPHS=1): a device-resident collective is captured once
+ * per (plan, send, recv, dtype, op) -- its RCCL groups, fused reductions and copies on both streams
+ * -- and later calls with the same arguments replay it with one hipGraphLaunch.  Cuts the host
+ * cost per call to one launch (small messages are bound by it).  Buffers must stay allocated
+ * while graphs that name them may be replayed; disabling drops every cached graph.  Same bits. */
+int chr_comm_set_graphs(chr_comm* comm, int enable);
 /* Opt-in timing of the fused bucket-reduction launches of this communicator (HIP events
  * on its stream).  _read synchronises on the recorded launches and returns the summed
  * kernel milliseconds, the algorithmic bytes ((m+2)*n*sizeof(T) per launch) and the

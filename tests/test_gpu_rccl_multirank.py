@@ -233,3 +233,74 @@ def test_rccl_profile_phases_world4():
         assert set(out["flat"]) == {"gather", "fdist"}, out
         assert all(ms > 0 for ms in out["flat"].values())
         assert any(k.startswith("bruck") for k in out["exact"]) and "bcast" not in out["exact"], out
+
+
+def _graph_worker(rank, world, port, q):
+    os.environ["NCCL_HOSTID"] = f"chiara-test-host-{rank}"
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    os.environ.setdefault("NCCL_IB_DISABLE", "1")
+    sys.path[:0] = [HERE, os.path.join(REPO, "oracle"),
+                    os.path.join(REPO, "configurable-hierarchical-allreduce-algorithms_amd")]
+    import torch
+    import torch.distributed as dist
+
+    import chiara_amd as ca
+    import pyoracle as po
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    comm = ca.Comm.from_torch_distributed(device=0)
+    dev = torch.device("cuda:0")
+    comm.set_graphs(True)
+    try:
+        # (mode, k, b, count, dtype, slices, schedule, overlap): every call after the first replays the
+        # graph captured for these buffers, so each round refills the same send buffer with new data
+        for mode, k, b, count, dtype, slices, sched, ov in (
+                ("ar", 4, 4, 1 << 16, "f32", 4, ca.SCHEDULE_FLAT, True),
+                ("ar", 2, 4, 8 * 1001, "bf16", 2, ca.SCHEDULE_REFERENCE, True),
+                ("rs", 2, 2, 1 << 14, "f32", 3, ca.SCHEDULE_FLAT_SEQ, False),
+                ("ar", 4, 4, 1 << 15, "f32", 0, ca.SCHEDULE_AUTO, True)):
+            comm.set_slices(slices)
+            comm.set_schedule(sched)
+            comm.set_overlap(ov)
+            cdt = {"f32": ca.FLOAT32, "bf16": ca.BFLOAT16}[dtype]
+            in_n = count * world if mode == "rs" else count
+            es = 4 if dtype == "f32" else 2
+            send = torch.empty(in_n * es, dtype=torch.uint8, device=dev)
+            out_t = torch.empty(count * es, dtype=torch.uint8, device=dev)
+            for rnd in range(3):
+                seed = 777 + rnd
+                send.copy_(torch.from_numpy(po.fill(in_n, dtype, 0, seed, rank).view(np.uint8).copy()))
+                fn = ca.all_reduce_radix_batch if mode == "ar" else ca.reduce_scatter_radix_batch
+                rc = fn(send, out_t, count, cdt, ca.SUM, comm, k, b)
+                allx = [po.fill(in_n, dtype, 0, seed, r) for r in range(world)]
+                f = po.allreduce_radix_batch if mode == "ar" else po.reduce_scatter_radix_batch
+                ref = f(allx, k, b, dtype, "sum")[rank]
+                out = out_t.cpu().numpy()
+                q.put((rank, mode, k, b, rc, bool(np.array_equal(out, ref.view(np.uint8)))))
+    finally:
+        comm.set_graphs(False)
+        comm.destroy()
+        dist.destroy_process_group()
+
+
+def test_rccl_graph_replay_world4():
+    """chr_comm_set_graphs: the captured plan (RCCL groups + reductions on two streams) replays
+    bit-exact vs the oracle on new data in the same buffers, for flat / reference / flat_seq
+    (overlap off) / AUTO plans, allreduce and reduce-scatter."""
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_graph_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    alive = [p for p in procs if p.is_alive()]
+    for p in alive:
+        p.kill()
+    assert not alive, "RCCL graph test hung"
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = [q.get() for _ in range(world * 4 * 3)]
+    bad = [r for r in res if r[4] != 0 or not r[5]]
+    assert not bad, bad
