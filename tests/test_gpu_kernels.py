@@ -124,6 +124,16 @@ def test_bucket_sizes_1k_to_1g(gu, nbytes):
         _check_multi(gu, "f32", "sum", 3, n, seed=12)
 
 
+@pytest.mark.parametrize("dtype,op,m,nbytes,off", [("f32", "sum", 1, 64 << 20, 1), ("bf16", "max", 3, 48 << 20, 0),
+                                                    ("f64", "sum", 7, 16 << 20, 3), ("i32", "prod", 2, 48 << 20, 2),
+                                                    ("bf16", "sum", 1, 64 << 20, 5)])
+def test_streaming_path_ragged(gu, dtype, op, m, nbytes, off):
+    """Calls that stream >= 128 MiB take the nt / one-wave / ACC0 instantiation: ragged counts and
+    misaligned heads there too (scalar head and tail around the vector body)."""
+    es = np.dtype(po.NP_DTYPES[dtype]).itemsize
+    _check_multi(gu, dtype, op, m, nbytes // es + 12345, off, seed=21)
+
+
 def test_invalid_args(gu):
     assert ca.reduce_local(0, 0, 0, ca.FLOAT32, ca.SUM) == 0  # n == 0 is a no-op
     assert ca.reduce_local(0, 0, 5, ca.FLOAT32, ca.SUM) == 1
