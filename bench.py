@@ -21,6 +21,10 @@ import subprocess
 import sys
 import time
 
+# RCCL / cross-process device memory on this host driver need dmabuf IPC:
+# set before torch or HIP is loaded, so every rank's runtime starts with it.
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.join(REPO, "configurable-hierarchical-allreduce-algorithms_amd")
 sys.path[:0] = [PKG_DIR, os.path.join(REPO, "oracle")]
@@ -96,16 +100,19 @@ def cpu_baseline(seconds):
                       f"{calls} calls in {dt:.1f} s, 1 thread (nproc={os.cpu_count()})"}
 
 
-def cpu_baseline_collective(world, k, b, gpu_bytes_per_rank):
+def cpu_baseline_collective(world, k, b, gpu_count, gpu_es):
     """N>1: the REAL reference all_reduce_radix_batch (oracle/_ref/ref_timer: the reference file
     compiled unchanged against MPICH) on `world` host cores, one MPI rank per core, same (k, b).
-    Bounded sample: 64 MiB fp32 per rank instead of 1 GiB (the reference takes ~3 s per 1 GiB call
-    at 8 ranks), 3 calls, max over ranks.  Same value definition as the GPU line."""
+    Bounded sample: at most 64 MiB fp32 per rank (the reference takes ~3 s per 1 GiB call at 8
+    ranks), 3 calls, max over ranks.  Same value definition as the GPU line."""
     exe = os.path.join(REPO, "oracle", "_ref", "ref_timer")
     mpiexec = "/opt/conda/bin/mpiexec"
     if not (os.path.exists(exe) and os.path.exists(mpiexec)):
         return None
-    elems = (1 << 24) - (1 << 24) % world
+    elems = min(gpu_count, 1 << 24)
+    elems -= elems % world
+    if elems <= 0:
+        return None
     reps = 3
     try:
         out = subprocess.run([mpiexec, "-bind-to", "core", "-n", str(world), exe, "ar", str(k), str(b), str(elems),
@@ -116,11 +123,14 @@ def cpu_baseline_collective(world, k, b, gpu_bytes_per_rank):
     except Exception:
         return None
     t = r["seconds_per_call"]
+    whole = elems == gpu_count and gpu_es == 4
+    what = ("the whole per-rank workload" if whole else
+            f"a bounded sample of the {gpu_count * gpu_es / 2**20:g} MiB per rank workload, "
+            f"{elems / gpu_count * 100:.3g} % of its elements" + ("" if gpu_es == 4 else ", in fp32"))
     return {"value": round(world * elems * 4 / t / 1e9, 3), "unit": "GB/s", "cores": world, "kind": "reference",
             "sample": f"reference all_reduce_radix_batch (all_reduce_radix_batch.cpp compiled unchanged, MPICH 3.3.2), "
-                      f"{world} ranks bound to {world} host cores, k={k}, b={b}, {elems * 4 >> 20} MiB fp32 per rank "
-                      f"(bounded sample of the {gpu_bytes_per_rank >> 20} MiB per rank workload), {reps} calls, max over ranks: "
-                      f"{t * 1e3:.1f} ms per call (nproc={os.cpu_count()})"}
+                      f"{world} ranks bound to {world} host cores, k={k}, b={b}, {elems * 4 / 2**20:g} MiB fp32 per rank "
+                      f"({what}), {reps} calls, max over ranks: {t * 1e3:.1f} ms per call (nproc={os.cpu_count()})"}
 
 
 def pmc_traffic(kernel_key):
@@ -162,7 +172,11 @@ def bench_bucket(args, cpu):
         s = i % NSETS
         return ca.reduce_local(ins[s], accs[s], n, ca.FLOAT32, ca.SUM, stream)
 
-    for i in range(args.warmup):
+    # Untimed warmup: at least one launch per buffer set, so every set has been streamed by the
+    # kernel (and the clocks have left idle) before timing, whatever --warmup is; the working set
+    # stays 2 GiB, 8x the Infinity Cache, so the timed launches still stream from HBM.
+    touch = max(args.warmup, 2 * NSETS)
+    for i in range(touch):
         ca.check(step(i))
     torch.cuda.synchronize()
     # Timed region: HIP events on the launch stream around K back-to-back launches of the
@@ -191,7 +205,7 @@ def bench_bucket(args, cpu):
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": "C2 bucket reduction: k=2 (m=1 incoming bucket), 64 MiB fp32 per bucket, "
                                "device-resident, MPI_Reduce_local semantics", "bucket_bytes": 4 * n, "m": 1,
-                   "buffer_sets": NSETS, "parallelism": "replicas"},
+                   "buffer_sets": NSETS, "untimed_launches": touch, "parallelism": "replicas"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "kernel": "chr::k_reduce_vec<f32,SUM,M=1,U=4,NT,ACC0,64 threads>", "algorithmic_bytes_per_launch": bytes_per_step,
@@ -408,7 +422,7 @@ def bench_allreduce(args):
     # it; the other ranks wait at the barrier)
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
-        cpu = cpu_baseline_collective(world, k, b, S)
+        cpu = cpu_baseline_collective(world, k, b, count, es)
     dist.barrier()
     if rank == 0:
         line = {

@@ -25,6 +25,7 @@ BFLOAT16 = 3
 # ops (chr_op)
 SUM, PROD, MAX, MIN = 0, 1, 2, 3
 SUCCESS = 0
+ERR_RCCL, ERR_TIMEOUT, ERR_ABORTED = 5, 9, 10
 IN_PLACE = object()  # MPI_IN_PLACE analogue
 _IN_PLACE_PTR = 1     # CHR_IN_PLACE
 
@@ -148,6 +149,23 @@ class Comm:
     def set_graphs(self, enable):
         """Replay device-resident collectives from captured HIP graphs (one per plan and buffers)."""
         check(lib().chr_comm_set_graphs(self._h, int(bool(enable))))
+
+    def set_timeout(self, timeout_ms):
+        """Blocking calls give up after timeout_ms (0 = never): the communicator is aborted and
+        ERR_TIMEOUT returned, so a lost peer is an error code instead of a hang."""
+        check(lib().chr_comm_set_timeout(self._h, int(timeout_ms)))
+
+    def abort(self):
+        """Abort the RCCL communicator (ncclCommAbort); later calls return ERR_ABORTED."""
+        check(lib().chr_comm_abort(self._h))
+
+    def synchronize(self):
+        """Wait for this communicator's enqueued work under the timeout; returns the status code."""
+        return lib().chr_comm_synchronize(self._h)
+
+    @property
+    def aborted(self):
+        return bool(lib().chr_comm_is_aborted(self._h))
 
     def tuned_schedule(self, mode, count, datatype, k, b):
         """(schedule, slices) SCHEDULE_AUTO kept for a collective already called with these arguments,

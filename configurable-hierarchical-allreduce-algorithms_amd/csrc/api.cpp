@@ -22,6 +22,8 @@ const char* chr_error_string(int code) {
     case CHR_ERR_NO_DEVICE: return "no HIP device";
     case CHR_ERR_OUT_OF_MEMORY: return "out of device memory";
     case CHR_ERR_UNSUPPORTED: return "unsupported";
+    case CHR_ERR_TIMEOUT: return "call timed out; communicator aborted";
+    case CHR_ERR_ABORTED: return "communicator aborted by an earlier failure";
     default: return "unknown error";
     }
 }

@@ -14,12 +14,14 @@
 #include <rccl/rccl.h>
 
 #include <cctype>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -120,24 +122,6 @@ struct ReduceProfile {
         }
         steps_pending.clear();
     }
-    // "t3,phase0/s0,lane/s1" -> "phase0+lane"; "gather/s2" -> "gather"
-    static std::string phase_of(const std::string& label) {
-        std::string out, tok;
-        auto flush = [&]() {
-            const size_t slash = tok.find('/');
-            std::string name = tok.substr(0, slash);
-            if (!name.empty() && !(name[0] == 't' && name.size() > 1 && std::isdigit((unsigned char)name[1]))) {
-                if (out.find(name) == std::string::npos) out += (out.empty() ? "" : "+") + name;
-            }
-            tok.clear();
-        };
-        for (char ch : label) {
-            if (ch == ',') flush();
-            else tok += ch;
-        }
-        flush();
-        return out.empty() ? "step" : out;
-    }
     void release() {
         drain();
         for (auto& e : spare) {
@@ -217,6 +201,16 @@ int default_graphs() {
     return v;
 }
 
+// CHR_TIMEOUT_MS: blocking calls give up after this many milliseconds (0 = wait forever, the
+// default); see chr_comm_set_timeout
+int default_timeout_ms() {
+    static const int v = [] {
+        const char* e = std::getenv("CHR_TIMEOUT_MS");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
+
 int default_schedule() {
     static const int v = [] {
         const char* e = std::getenv("CHR_SCHEDULE");
@@ -269,6 +263,20 @@ struct chr_comm {
     ReduceProfile prof;
     std::map<PlanKey, std::unique_ptr<Plan>> plans;
 
+    // Failure handling.  A call that fails after it has posted RCCL operations, or that times
+    // out, aborts the RCCL communicator (ncclCommAbort: its kernels exit, peers see the closed
+    // connections) instead of leaving peers posted; every later call then returns
+    // CHR_ERR_ABORTED and chr_comm_destroy skips ncclCommDestroy, which could block on a wedged
+    // communicator.  The reference has no such path: under MPI_ERRORS_ARE_FATAL an error aborts
+    // the job, and a lost peer is a hang.
+    int timeout_ms = default_timeout_ms();
+    bool failed = false;
+    void abort_comm() {
+        if (nccl) (void)ncclCommAbort(nccl);
+        nccl = nullptr;
+        failed = true;
+    }
+
     // HIP graph replay (chr_comm_set_graphs): one executable graph per (plan, send, recv, dtype, op, overlap),
     // dropped whenever the scratch buffers they point into are reallocated
     int graphs = default_graphs();
@@ -276,6 +284,17 @@ struct chr_comm {
     void drop_graphs() {
         for (auto& kv : gexec) (void)hipGraphExecDestroy(kv.second);
         gexec.clear();
+    }
+    // The only way scratch grows: whichever path reserves it (eager, graph capture, host-staged,
+    // profiled, tuning), a reallocation drops every cached graph, since they point into the old
+    // buffers.  reserve() synchronises the stream first, so no replay is still running.
+    hipError_t reserve_scratch(size_t acc_bytes, size_t stage_bytes) {
+        const void* a0 = acc.p;
+        const void* s0 = stage.p;
+        hipError_t e = acc.reserve(acc_bytes, stream);
+        if (e == hipSuccess) e = stage.reserve(stage_bytes, stream);
+        if (acc.p != a0 || stage.p != s0) drop_graphs();
+        return e;
     }
     // CHR_SCHEDULE_AUTO: (mode, count, element size, k, b, slices setting, overlap) -> (schedule, depth)
     std::map<std::tuple<int, uint64_t, int, int, int, int, int>, std::pair<int, int>> tuned;
@@ -303,10 +322,21 @@ struct chr_local_group {
 
 namespace {
 
+int enqueue_plan(chr_comm* c, const Plan& p, const void* send, void* recv, int dtype, int op, bool* posted);
+
+// Enqueues a whole plan.  A failure after the first RCCL operation was posted aborts the
+// communicator: peers may already be waiting on this rank's messages.
 int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int dtype, int op) {
+    if (c->failed) return CHR_ERR_ABORTED;
+    bool posted = false;
+    const int rc = enqueue_plan(c, p, send, recv, dtype, op, &posted);
+    if (rc && posted) c->abort_comm();
+    return rc;
+}
+
+int enqueue_plan(chr_comm* c, const Plan& p, const void* send, void* recv, int dtype, int op, bool* posted) {
     const size_t es = chr::dtype_size(dtype);
-    hipError_t e = c->acc.reserve(p.acc_elems * es, c->stream);
-    if (e == hipSuccess) e = c->stage.reserve(p.stage_elems * es, c->stream);
+    hipError_t e = c->reserve_scratch(p.acc_elems * es, p.stage_elems * es);
     if (e != hipSuccess) return hip_code(e);
     Bufs B{(const char*)send, (char*)recv, (char*)c->acc.p, (char*)c->stage.p, es};
     int rc;
@@ -331,6 +361,7 @@ int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int d
             sev = c->prof.take();
             (void)hipEventRecord(sev.first, c->stream);
         }
+        if (xfers) *posted = true;
         if (!s.sends.empty() || !s.recvs.empty()) {
             if ((rc = nccl_code(ncclGroupStart()))) return rc;
             for (const chr::Xfer& x : s.sends)
@@ -359,7 +390,7 @@ int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int d
         }
         if (timed) {
             (void)hipEventRecord(sev.second, c->stream);
-            c->prof.steps_pending.push_back({ReduceProfile::phase_of(s.label), sev});
+            c->prof.steps_pending.push_back({chr::phase_name(s.label), sev});
         }
         if (s.post.empty()) continue;
         if (!two) {
@@ -390,12 +421,8 @@ int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int d
 // that grows a buffer, every cached graph is dropped (they point into the old one).
 int launch_graph(chr_comm* c, const Plan& p, const void* send, void* recv, int dtype, int op) {
     const size_t es = chr::dtype_size(dtype);
-    const void* acc0 = c->acc.p;
-    const void* stage0 = c->stage.p;
-    hipError_t e = c->acc.reserve(p.acc_elems * es, c->stream);
-    if (e == hipSuccess) e = c->stage.reserve(p.stage_elems * es, c->stream);
+    hipError_t e = c->reserve_scratch(p.acc_elems * es, p.stage_elems * es);
     if (e != hipSuccess) return hip_code(e);
-    if (c->acc.p != acc0 || c->stage.p != stage0) c->drop_graphs();
     auto key = std::make_tuple(&p, send, recv, dtype, op, c->overlap);
     auto it = c->gexec.find(key);
     if (it == c->gexec.end()) {
@@ -414,7 +441,50 @@ int launch_graph(chr_comm* c, const Plan& p, const void* send, void* recv, int d
         if (e != hipSuccess) return hip_code(e);
         it = c->gexec.emplace(key, x).first;
     }
-    return hip_code(hipGraphLaunch(it->second, c->stream));
+    const int rc = hip_code(hipGraphLaunch(it->second, c->stream));
+    if (rc) c->abort_comm();  // the replay may have been partly submitted
+    return rc;
+}
+
+// Blocking completion of a call on the communicator stream.  With a timeout set, the stream is
+// polled, and RCCL's asynchronous error state with it (a peer that died or closed its
+// connections); on timeout or error the communicator is aborted, so a lost peer becomes an
+// error code on every surviving rank instead of a hang.
+int wait_call(chr_comm* c) {
+    if (c->timeout_ms <= 0) return hip_code(hipStreamSynchronize(c->stream));
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    const auto limit = t0 + std::chrono::milliseconds(c->timeout_ms);
+    auto next_check = t0;
+    for (int spin = 0;; ++spin) {
+        const hipError_t q = hipStreamQuery(c->stream);
+        if (q == hipSuccess) return CHR_SUCCESS;
+        if (q != hipErrorNotReady) {
+            c->abort_comm();
+            return hip_code(q);
+        }
+        const auto now = clk::now();
+        if (now >= next_check) {  // RCCL's own error state, every millisecond
+            ncclResult_t ae = ncclSuccess;
+            if (c->nccl && ncclCommGetAsyncError(c->nccl, &ae) == ncclSuccess && ae != ncclSuccess &&
+                ae != ncclInProgress) {
+                c->abort_comm();
+                (void)hipStreamSynchronize(c->stream);
+                return CHR_ERR_RCCL;
+            }
+            next_check = now + std::chrono::milliseconds(1);
+        }
+        if (now >= limit) {
+            if (std::getenv("CHR_DEBUG"))
+                std::fprintf(stderr, "[chiara] rank %d: call timed out after %d ms, aborting the communicator\n",
+                             c->rank, c->timeout_ms);
+            c->abort_comm();  // RCCL kernels poll the abort flag and exit
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipStreamSynchronize(c->cstream);
+            return CHR_ERR_TIMEOUT;
+        }
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
 }
 
 int run_collective(chr_comm* c, int sched, int slices, int mode, const void* send, void* recv, size_t count, int dtype,
@@ -436,7 +506,7 @@ int run_collective(chr_comm* c, int sched, int slices, int mode, const void* sen
         int rc = c->graphs && !c->prof.on ? launch_graph(c, p, input, recv, dtype, op)
                                           : enqueue_rccl(c, p, input, recv, dtype, op);
         if (rc || !sync) return rc;
-        return hip_code(hipStreamSynchronize(c->stream));
+        return wait_call(c);
     }
     if (!sync) return CHR_ERR_UNSUPPORTED;  // async needs device-resident buffers
     // Host-memory contract of the reference: stage through HBM (PCIe H2D / D2H).
@@ -457,7 +527,7 @@ int run_collective(chr_comm* c, int sched, int slices, int mode, const void* sen
     if (!dev_out &&
         (e = hipMemcpyAsync(recv, drecv, p.recv_elems * es, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
         return hip_code(e);
-    return hip_code(hipStreamSynchronize(c->stream));
+    return wait_call(c);
 }
 
 // CHR_SCHEDULE_AUTO.  The single-node schedules FLAT, FLAT_SEQ and FLAT_AG move the same bits
@@ -468,17 +538,35 @@ int run_collective(chr_comm* c, int sched, int slices, int mode, const void* sen
 // the slowest rank's time per candidate (one ncclAllReduce(max), so every rank picks the same
 // one) and the fastest is kept for every later call.  Each tuning call is a complete collective;
 // an in-place call is tuned on temporary copies so the caller's data is reduced exactly once.
+//
+// Tuning is collective, so every decision that could differ between ranks is agreed on first:
+// whether this call can be tuned (device-resident buffers, the temporaries allocated) is one
+// ncclAllReduce(min) over the ranks, and a call no rank can tune runs FLAT untuned on every rank.
+// The cache is then identical on every rank, and a cached choice applies to later calls of the
+// same arguments whatever memory their buffers are in.  A candidate that fails after posting
+// RCCL operations aborts the communicator (enqueue_rccl); peers with a timeout (chr_comm_set_timeout)
+// then return an error instead of waiting.
 constexpr int TUNE_REPS = 3;
+
+int agree_min(chr_comm* c, int mine, int* all) {
+    int* d = nullptr;
+    int rc = hip_code(hipMalloc(&d, sizeof(int)));
+    if (!rc) rc = hip_code(hipMemcpyAsync(d, &mine, sizeof(int), hipMemcpyHostToDevice, c->stream));
+    if (!rc) rc = nccl_code(ncclAllReduce(d, d, 1, ncclInt32, ncclMin, c->nccl, c->stream));
+    if (!rc) rc = hip_code(hipMemcpyAsync(all, d, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    if (!rc) rc = wait_call(c);
+    else c->abort_comm();
+    (void)hipFree(d);
+    return rc;
+}
 
 int tune_schedule(chr_comm* c, int mode, const void* send, void* recv, size_t count, int dtype, int op, int k, int b,
                   int* sched_out, int* slices_out) {
     *sched_out = chr::SCHED_FLAT;
     *slices_out = c->slices;
     if (chr::is_mpich(mode) || mode == chr::MODE_ALLGATHER || c->nranks < 2) return CHR_SUCCESS;
+    if (c->failed) return CHR_ERR_ABORTED;
     const size_t es = chr::dtype_size(dtype);
-    const bool inplace = send == CHR_IN_PLACE;
-    const void* input = inplace ? (const void*)recv : send;
-    if (!input || !recv || !is_device_ptr(input) || !is_device_ptr(recv)) return CHR_SUCCESS;  // host-staged: FLAT
     auto key = std::make_tuple(mode, (uint64_t)count, (int)es, k, b, c->slices, c->overlap);
     auto it = c->tuned.find(key);
     if (it != c->tuned.end()) {
@@ -487,7 +575,34 @@ int tune_schedule(chr_comm* c, int mode, const void* send, void* recv, size_t co
         return CHR_SUCCESS;
     }
     const Plan& p0 = c->plan(mode, k, b, count, es, chr::SCHED_FLAT, c->slices);
-    if (p0.error) return p0.error;
+    if (p0.error) return p0.error;  // a function of the arguments only: the same on every rank
+    if (p0.g.total == 0) return CHR_SUCCESS;
+    const bool inplace = send == CHR_IN_PLACE;
+    const void* input = inplace ? (const void*)recv : send;
+    // in place: tune on copies (the collective would otherwise reduce the caller's data again)
+    void* tsend = nullptr;
+    void* trecv = nullptr;
+    const void* s_arg = send;
+    void* r_arg = recv;
+    int ok = input && recv && is_device_ptr(input) && is_device_ptr(recv);
+    if (ok && inplace) {
+        ok = hipMalloc(&tsend, p0.send_elems * es) == hipSuccess && hipMalloc(&trecv, p0.recv_elems * es) == hipSuccess &&
+             hipMemcpyAsync(tsend, recv, p0.send_elems * es, hipMemcpyDeviceToDevice, c->stream) == hipSuccess;
+        (void)hipGetLastError();
+        s_arg = tsend;
+        r_arg = trecv;
+    }
+    auto release = [&]() {
+        if (tsend || trecv) (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(tsend);
+        (void)hipFree(trecv);
+    };
+    int all = 0;
+    int rc = agree_min(c, ok, &all);
+    if (rc || !all) {  // host-staged somewhere, or an allocation failed somewhere: FLAT, untuned
+        release();
+        return rc;
+    }
     std::vector<std::pair<int, int>> cand;
     std::vector<int> depths;
     const int pa = pick_slices(c->slices, count, mode, c->nranks, b, es);
@@ -497,27 +612,13 @@ int tune_schedule(chr_comm* c, int mode, const void* send, void* recv, size_t co
     }
     for (int sc : {(int)chr::SCHED_FLAT, (int)chr::SCHED_FLAT_SEQ, (int)chr::SCHED_FLAT_AG})
         for (int d : depths) cand.push_back({sc, d});
-    // in place: tune on copies (the collective would otherwise reduce the caller's data again)
-    void* tsend = nullptr;
-    void* trecv = nullptr;
-    const void* s_arg = send;
-    void* r_arg = recv;
-    hipError_t e = hipSuccess;
-    if (inplace) {
-        if ((e = hipMalloc(&tsend, p0.send_elems * es)) != hipSuccess ||
-            (e = hipMalloc(&trecv, p0.recv_elems * es)) != hipSuccess ||
-            (e = hipMemcpyAsync(tsend, recv, p0.send_elems * es, hipMemcpyDeviceToDevice, c->stream)) != hipSuccess) {
-            (void)hipFree(tsend);
-            (void)hipFree(trecv);
-            return hip_code(e);
-        }
-        s_arg = tsend;
-        r_arg = trecv;
-    }
     std::vector<float> ms(cand.size(), 0.f);
-    int rc = CHR_SUCCESS;
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if ((e = hipEventCreate(&e0)) != hipSuccess || (e = hipEventCreate(&e1)) != hipSuccess) rc = hip_code(e);
+    hipError_t e = hipSuccess;
+    if ((e = hipEventCreate(&e0)) != hipSuccess || (e = hipEventCreate(&e1)) != hipSuccess) {
+        rc = hip_code(e);
+        c->abort_comm();  // the peers are about to start the candidates
+    }
     for (size_t i = 0; i < cand.size() && !rc; ++i) {
         const int sc = cand[i].first, d = cand[i].second;
         // untimed first call: plan compile, scratch growth, RCCL connection setup
@@ -525,9 +626,10 @@ int tune_schedule(chr_comm* c, int mode, const void* send, void* recv, size_t co
         if ((rc = hip_code(hipEventRecord(e0, c->stream)))) break;
         for (int r = 0; r < TUNE_REPS && !rc; ++r)
             rc = run_collective(c, sc, d, mode, s_arg, r_arg, count, dtype, op, k, b, false);
-        if (rc || (rc = hip_code(hipEventRecord(e1, c->stream))) || (rc = hip_code(hipEventSynchronize(e1)))) break;
+        if (rc || (rc = hip_code(hipEventRecord(e1, c->stream))) || (rc = wait_call(c))) break;
         rc = hip_code(hipEventElapsedTime(&ms[i], e0, e1));
     }
+    if (rc && !c->failed) c->abort_comm();  // a local failure mid-tuning: the peers are still in it
     float* dms = nullptr;
     if (!rc && (rc = hip_code(hipMalloc(&dms, ms.size() * sizeof(float)))) == CHR_SUCCESS) {
         if (!(rc = hip_code(hipMemcpyAsync(dms, ms.data(), ms.size() * sizeof(float), hipMemcpyHostToDevice,
@@ -535,16 +637,15 @@ int tune_schedule(chr_comm* c, int mode, const void* send, void* recv, size_t co
             !(rc = nccl_code(ncclAllReduce(dms, dms, ms.size(), ncclFloat32, ncclMax, c->nccl, c->stream))) &&
             !(rc = hip_code(hipMemcpyAsync(ms.data(), dms, ms.size() * sizeof(float), hipMemcpyDeviceToHost,
                                            c->stream))))
-            rc = hip_code(hipStreamSynchronize(c->stream));
+            rc = wait_call(c);
+        if (rc && !c->failed) c->abort_comm();
+    } else if (rc == CHR_ERR_OUT_OF_MEMORY && !c->failed) {
+        c->abort_comm();
     }
     (void)hipFree(dms);
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
-    if (inplace) {
-        (void)hipStreamSynchronize(c->stream);
-        (void)hipFree(tsend);
-        (void)hipFree(trecv);
-    }
+    release();
     if (rc) return rc;
     size_t best = 0;
     for (size_t i = 1; i < cand.size(); ++i)
@@ -562,6 +663,7 @@ int tune_schedule(chr_comm* c, int mode, const void* send, void* recv, size_t co
 int collective(chr_comm* c, int mode, const void* send, void* recv, size_t count, int dtype, int op, int k, int b,
                bool sync) {
     if (!c || !chr::valid_dtype_op(dtype, op)) return CHR_ERR_INVALID_ARG;
+    if (c->failed) return CHR_ERR_ABORTED;
     int sched = c->sched, slices = c->slices;
     if (sched == CHR_SCHEDULE_AUTO) {
         if (hipSetDevice(c->device) != hipSuccess) return CHR_ERR_HIP;
@@ -695,7 +797,7 @@ int chr_comm_destroy(chr_comm* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->drop_graphs();
     c->prof.release();
-    if (c->nccl) (void)ncclCommDestroy(c->nccl);
+    if (c->nccl) (void)ncclCommDestroy(c->nccl);  // an aborted communicator was released by ncclCommAbort
     c->acc.release();
     c->stage.release();
     c->hsend.release();
@@ -719,6 +821,30 @@ int chr_comm_size(const chr_comm* c, int* n) {
     *n = c->nranks;
     return CHR_SUCCESS;
 }
+
+int chr_comm_set_timeout(chr_comm* c, int timeout_ms) {
+    if (!c || timeout_ms < 0) return CHR_ERR_INVALID_ARG;
+    c->timeout_ms = timeout_ms;
+    return CHR_SUCCESS;
+}
+
+int chr_comm_abort(chr_comm* c) {
+    if (!c) return CHR_ERR_INVALID_ARG;
+    (void)hipSetDevice(c->device);
+    c->abort_comm();
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+    return CHR_SUCCESS;
+}
+
+int chr_comm_synchronize(chr_comm* c) {
+    if (!c) return CHR_ERR_INVALID_ARG;
+    if (c->failed) return CHR_ERR_ABORTED;
+    if (hipSetDevice(c->device) != hipSuccess) return CHR_ERR_HIP;
+    return wait_call(c);
+}
+
+int chr_comm_is_aborted(const chr_comm* c) { return c && c->failed ? 1 : 0; }
 
 int chr_comm_set_slices(chr_comm* c, int slices) {
     if (!c || slices < 0) return CHR_ERR_INVALID_ARG;

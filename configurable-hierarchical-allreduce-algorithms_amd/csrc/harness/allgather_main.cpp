@@ -13,7 +13,7 @@ static void run_k_b(const Options& o, Ctx& c, std::ofstream& csv, int k, int cou
     const chr_dtype dt = to_chr(o.dtype);
     const size_t es = esize(dt), out_n = (size_t)count * c.nprocs;
     std::vector<char> send, ref(out_n * es), recv(out_n * es);
-    fill_seq(send, count, dt, c.rank, count);
+    fill_input(send, count, dt, c.rank, count, o.pattern);
     MPI_Allgather(send.data(), count * (int)es, MPI_BYTE, ref.data(), count * (int)es, MPI_BYTE, MPI_COMM_WORLD);
     const bool dev = o.mem == "device";
     DevBuf dsend(dev ? count * es : 0), drecv(dev ? out_n * es : 0);
@@ -50,7 +50,7 @@ static void run_standard(const Options& o, Ctx& c, std::ofstream& csv, int count
     const chr_dtype dt = to_chr(o.dtype);
     const size_t es = esize(dt), out_n = (size_t)count * c.nprocs;
     std::vector<char> send, ref(out_n * es), recv(out_n * es);
-    fill_seq(send, count, dt, c.rank, count);
+    fill_input(send, count, dt, c.rank, count, o.pattern);
     MPI_Allgather(send.data(), count * (int)es, MPI_BYTE, ref.data(), count * (int)es, MPI_BYTE, MPI_COMM_WORLD);
     const int reps = o.reps > 0 ? o.reps : 50;
     for (int rep = 0; rep < reps; ++rep) {

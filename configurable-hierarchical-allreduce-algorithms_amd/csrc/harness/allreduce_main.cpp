@@ -14,9 +14,11 @@ static void run_k2(const Options& o, Ctx& c, std::ofstream& csv, const char* nam
     const chr_dtype dt = to_chr(o.dtype);
     const size_t es = esize(dt);
     std::vector<char> send, ref(count * es), recv(count * es);
-    fill_seq(send, count, dt, c.rank, count);
+    fill_input(send, count, dt, c.rank, count, o.pattern);
     MPI_Allreduce(send.data(), ref.data(), count, dt == CHR_BFLOAT16 ? c.bf16 : mpi_type(dt),
                   dt == CHR_BFLOAT16 ? c.bf16_sum : MPI_SUM, MPI_COMM_WORLD);
+    std::vector<double> sumabs(count);
+    MPI_Allreduce(abs_values(send, count, dt).data(), sumabs.data(), count, MPI_DOUBLE, MPI_SUM, MPI_COMM_WORLD);
     const bool dev = o.mem == "device";
     DevBuf dsend(dev ? count * es : 0), drecv(dev ? count * es : 0);
     if (dev) {
@@ -37,7 +39,7 @@ static void run_k2(const Options& o, Ctx& c, std::ofstream& csv, const char* nam
         MPI_Barrier(MPI_COMM_WORLD);
         const double t1 = MPI_Wtime();
         if (dev) (void)hipMemcpy(recv.data(), drecv.p, count * es, hipMemcpyDeviceToHost);
-        const bool correct = err == CHR_SUCCESS && check_correctness(recv, ref, count, dt, c.nprocs);
+        const bool correct = err == CHR_SUCCESS && check_correctness(recv, ref, sumabs, count, dt, c.nprocs);
         if (err != CHR_SUCCESS && c.rank == 0 && rep == 0)
             std::fprintf(stderr, "%s k=%d b=%d count=%d: %s\n", name, k, o.b, count, chr_error_string(err));
         if (c.rank == 0)
@@ -51,8 +53,10 @@ static void run_no_k(const Options& o, Ctx& c, std::ofstream& csv, int count) {
     if (dt == CHR_BFLOAT16) return;
     const size_t es = esize(dt);
     std::vector<char> send, recv(count * es), ref(count * es);
-    fill_seq(send, count, dt, c.rank, count);
+    fill_input(send, count, dt, c.rank, count, o.pattern);
     MPI_Allreduce(send.data(), ref.data(), count, mpi_type(dt), MPI_SUM, MPI_COMM_WORLD);
+    std::vector<double> sumabs(count);
+    MPI_Allreduce(abs_values(send, count, dt).data(), sumabs.data(), count, MPI_DOUBLE, MPI_SUM, MPI_COMM_WORLD);
     const int reps = o.reps > 0 ? o.reps : 50;
     for (int rep = 0; rep < reps; ++rep) {
         std::fill(recv.begin(), recv.end(), 0);
@@ -61,7 +65,7 @@ static void run_no_k(const Options& o, Ctx& c, std::ofstream& csv, int count) {
         const int err = MPI_Allreduce(send.data(), recv.data(), count, mpi_type(dt), MPI_SUM, MPI_COMM_WORLD);
         MPI_Barrier(MPI_COMM_WORLD);
         const double t1 = MPI_Wtime();
-        const bool correct = err == MPI_SUCCESS && check_correctness(recv, ref, count, dt, c.nprocs);
+        const bool correct = err == MPI_SUCCESS && check_correctness(recv, ref, sumabs, count, dt, c.nprocs);
         if (c.rank == 0)
             csv << "MPICH_allreduce,0,0," << c.nprocs << "," << count / c.nprocs << "," << (t1 - t0) << ","
                 << (correct ? 1 : 0) << "\n" << std::flush;

@@ -14,9 +14,12 @@ static void run_r_b(const Options& o, Ctx& c, std::ofstream& csv, const char* na
     const size_t es = esize(dt);
     const size_t in_n = (size_t)count * c.nprocs;
     std::vector<char> send, ref(count * es), recv(count * es);
-    fill_seq(send, in_n, dt, c.rank, in_n);  // rank*(count*nprocs)+i (main.cpp:45-46)
+    fill_input(send, in_n, dt, c.rank, in_n, o.pattern);  // seq: rank*(count*nprocs)+i (main.cpp:45-46)
     MPI_Reduce_scatter_block(send.data(), ref.data(), count, dt == CHR_BFLOAT16 ? c.bf16 : mpi_type(dt),
                              dt == CHR_BFLOAT16 ? c.bf16_sum : MPI_SUM, MPI_COMM_WORLD);
+    std::vector<double> sumabs(count);
+    MPI_Reduce_scatter_block(abs_values(send, in_n, dt).data(), sumabs.data(), count, MPI_DOUBLE, MPI_SUM,
+                             MPI_COMM_WORLD);
     const bool dev = o.mem == "device";
     DevBuf dsend(dev ? in_n * es : 0), drecv(dev ? count * es : 0);
     if (dev) {
@@ -37,7 +40,7 @@ static void run_r_b(const Options& o, Ctx& c, std::ofstream& csv, const char* na
         MPI_Barrier(MPI_COMM_WORLD);
         const double t1 = MPI_Wtime();
         if (dev) (void)hipMemcpy(recv.data(), drecv.p, count * es, hipMemcpyDeviceToHost);
-        const int ok_local = (err == CHR_SUCCESS && check_correctness(recv, ref, count, dt, c.nprocs)) ? 1 : 0;
+        const int ok_local = (err == CHR_SUCCESS && check_correctness(recv, ref, sumabs, count, dt, c.nprocs)) ? 1 : 0;
         int ok = 0;
         MPI_Allreduce(&ok_local, &ok, 1, MPI_INT, MPI_MIN, MPI_COMM_WORLD);
         double el = t1 - t0, el_max = 0;
@@ -54,8 +57,11 @@ static void run_standard(const Options& o, Ctx& c, std::ofstream& csv, int count
     const size_t es = esize(dt);
     const size_t in_n = (size_t)count * c.nprocs;
     std::vector<char> send, recv(count * es), ref(count * es);
-    fill_seq(send, in_n, dt, c.rank, in_n);
+    fill_input(send, in_n, dt, c.rank, in_n, o.pattern);
     MPI_Reduce_scatter_block(send.data(), ref.data(), count, mpi_type(dt), MPI_SUM, MPI_COMM_WORLD);
+    std::vector<double> sumabs(count);
+    MPI_Reduce_scatter_block(abs_values(send, in_n, dt).data(), sumabs.data(), count, MPI_DOUBLE, MPI_SUM,
+                             MPI_COMM_WORLD);
     const int reps = o.reps > 0 ? o.reps : 20;
     for (int rep = 0; rep < reps; ++rep) {
         MPI_Barrier(MPI_COMM_WORLD);
@@ -63,7 +69,7 @@ static void run_standard(const Options& o, Ctx& c, std::ofstream& csv, int count
         const int err = MPI_Reduce_scatter_block(send.data(), recv.data(), count, mpi_type(dt), MPI_SUM, MPI_COMM_WORLD);
         MPI_Barrier(MPI_COMM_WORLD);
         const double t1 = MPI_Wtime();
-        const int ok_local = (err == MPI_SUCCESS && check_correctness(recv, ref, count, dt, c.nprocs)) ? 1 : 0;
+        const int ok_local = (err == MPI_SUCCESS && check_correctness(recv, ref, sumabs, count, dt, c.nprocs)) ? 1 : 0;
         int ok = 0;
         MPI_Allreduce(&ok_local, &ok, 1, MPI_INT, MPI_MIN, MPI_COMM_WORLD);
         double el = t1 - t0, el_max = 0;

@@ -8,6 +8,7 @@
 #include <tuple>
 
 #include <algorithm>
+#include <cctype>
 #include <cstdio>
 #include <cstdlib>
 #include <sstream>
@@ -897,6 +898,29 @@ static const char* buf_name(uint8_t b) {
     case BUF_ACC: return "ACC";
     default: return "STAGE";
     }
+}
+
+// "t3,phase0/s0,lane/s1" -> "phase0+lane"; "gather/s2" -> "gather".  Names are compared as
+// whole tokens ("gather" after "allgather" is a phase of its own).
+std::string phase_name(const std::string& label) {
+    std::vector<std::string> names;
+    std::string tok;
+    auto flush = [&]() {
+        const std::string name = tok.substr(0, tok.find('/'));
+        tok.clear();
+        if (name.empty() || (name[0] == 't' && name.size() > 1 && std::isdigit((unsigned char)name[1]))) return;
+        for (const auto& n : names)
+            if (n == name) return;
+        names.push_back(name);
+    };
+    for (char ch : label) {
+        if (ch == ',') flush();
+        else tok += ch;
+    }
+    flush();
+    std::string out;
+    for (const auto& n : names) out += (out.empty() ? "" : "+") + n;
+    return out.empty() ? "step" : out;
 }
 
 std::string describe(const Plan& p) {

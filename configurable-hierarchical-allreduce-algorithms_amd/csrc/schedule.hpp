@@ -144,5 +144,8 @@ int auto_slices(uint64_t irc_bytes);
 Plan build_plan_mpich(Mode mode, int nranks, int rank, int k, int aux, uint64_t count);
 Plan build_plan_allgather(int nranks, int rank, int k, int b, uint64_t sendcount);
 std::string describe(const Plan& p);
+// Phase of a step label for the per-phase timers: slice suffixes and super-step tags dropped,
+// distinct phase names joined by '+' ("t3,phase0/s0,lane/s1" -> "phase0+lane").
+std::string phase_name(const std::string& label);
 
 }  // namespace chr

@@ -43,7 +43,10 @@ typedef enum {
     CHR_ERR_RCCL = 5,
     CHR_ERR_NO_DEVICE = 6,
     CHR_ERR_OUT_OF_MEMORY = 7,
-    CHR_ERR_UNSUPPORTED = 8
+    CHR_ERR_UNSUPPORTED = 8,
+    CHR_ERR_TIMEOUT = 9,     /* a blocking call exceeded chr_comm_set_timeout; the communicator was
+                                aborted (ncclCommAbort) */
+    CHR_ERR_ABORTED = 10     /* the communicator was aborted by an earlier failure or chr_comm_abort */
 } chr_result;
 
 /* MPI_IN_PLACE analogue (all_reduce_radix_batch.cpp:234, :306-321): pass as `send`. */
@@ -95,7 +98,22 @@ typedef struct { char internal[128]; } chr_unique_id; /* == ncclUniqueId */
 int chr_get_unique_id(chr_unique_id* id);
 /* One rank per process (or thread), one MI355X per rank.  Collective across `nranks`. */
 int chr_comm_init_rank(chr_comm** comm, int nranks, const chr_unique_id* id, int rank, int device);
+/* Releases the communicator.  On an aborted communicator this never blocks. */
 int chr_comm_destroy(chr_comm* comm);
+/* Failure handling (the reference relies on MPI_ERRORS_ARE_FATAL; a lost peer is a hang there).
+ * A call that fails after posting RCCL operations aborts the communicator (ncclCommAbort) instead
+ * of leaving its peers posted; every later call returns CHR_ERR_ABORTED.
+ * chr_comm_set_timeout: blocking calls (and chr_comm_synchronize) poll the stream and RCCL's
+ * asynchronous error state and give up after timeout_ms milliseconds, aborting the communicator
+ * and returning CHR_ERR_TIMEOUT (or CHR_ERR_RCCL for a reported error); 0 = wait forever (the
+ * default; env CHR_TIMEOUT_MS).  Tuning calls of CHR_SCHEDULE_AUTO use it too.
+ * chr_comm_abort: abort on purpose (the MPI_Abort analogue for this communicator); peers then
+ * get an error from their pending or next calls if they set a timeout.
+ * chr_comm_synchronize: wait for the communicator's enqueued (_async) work under the timeout. */
+int chr_comm_set_timeout(chr_comm* comm, int timeout_ms);
+int chr_comm_abort(chr_comm* comm);
+int chr_comm_synchronize(chr_comm* comm);
+int chr_comm_is_aborted(const chr_comm* comm);
 int chr_comm_rank(const chr_comm* comm, int* rank);
 int chr_comm_size(const chr_comm* comm, int* nranks);
 /* The stream all of this communicator's collective work is enqueued on.  It is a blocking

@@ -42,6 +42,15 @@ static bool op_in_bounds(const Plan& p, const LocalOp& op) {
 
 int main(int argc, char** argv) {
     const int max_n = argc > 1 ? std::atoi(argv[1]) : 16;  // the CPU test runs a reduced grid
+    // per-phase timer names (chr_comm_profile_phases): whole-token de-duplication
+    const std::pair<const char*, const char*> names[] = {
+        {"t3,phase0/s0,lane/s1", "phase0+lane"}, {"gather/s2", "gather"}, {"allgather/s0,gather/s1", "allgather+gather"},
+        {"phase01/s0,phase0/s1", "phase01+phase0"}, {"t12", "step"}, {"bruck1,bruck1/s3", "bruck1"}};
+    for (const auto& nm : names)
+        if (phase_name(nm.first) != nm.second) {
+            std::fprintf(stderr, "FAIL phase_name(%s) = %s, want %s\n", nm.first, phase_name(nm.first).c_str(), nm.second);
+            ++g_bad;
+        }
     long plans = 0;
     const int modes[] = {MODE_ALLREDUCE, MODE_REDUCE_SCATTER, MODE_ALLGATHER, MODE_MPICH_RING, MODE_MPICH_RD,
                          MODE_MPICH_RSAG, MODE_MPICH_RECEXCH, MODE_MPICH_KRSAG, MODE_MPICH_RMULT};
