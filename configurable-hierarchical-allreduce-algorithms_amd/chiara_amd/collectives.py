@@ -22,14 +22,23 @@ FLOAT32 = FLOAT = 0
 FLOAT64 = DOUBLE = 1
 INT32 = INT = 2
 BFLOAT16 = 3
-# ops (chr_op)
+INT8 = SIGNED_CHAR = 4
+UINT8 = UNSIGNED_CHAR = BYTE = 5
+INT16 = SHORT = 6
+UINT16 = UNSIGNED_SHORT = 7
+UINT32 = UNSIGNED = 8
+INT64 = LONG = LONG_LONG = 9
+UINT64 = UNSIGNED_LONG = 10
+# ops (chr_op): MPI's predefined ops; the logical and bitwise ones on integer types only
 SUM, PROD, MAX, MIN = 0, 1, 2, 3
+LAND, LOR, LXOR, BAND, BOR, BXOR = 4, 5, 6, 7, 8, 9
 SUCCESS = 0
 ERR_RCCL, ERR_TIMEOUT, ERR_ABORTED = 5, 9, 10
 IN_PLACE = object()  # MPI_IN_PLACE analogue
 _IN_PLACE_PTR = 1     # CHR_IN_PLACE
 
-DTYPE_SIZE = {FLOAT32: 4, FLOAT64: 8, INT32: 4, BFLOAT16: 2}
+DTYPE_SIZE = {FLOAT32: 4, FLOAT64: 8, INT32: 4, BFLOAT16: 2, INT8: 1, UINT8: 1, INT16: 2, UINT16: 2, UINT32: 4,
+              INT64: 8, UINT64: 8}
 MODE_ALLREDUCE, MODE_REDUCE_SCATTER = 0, 1
 # MPICH baselines (testing/mpich_implementations/all_reduce/), chr_mode numbering
 MODE_MPICH_RING, MODE_MPICH_RD, MODE_MPICH_RSAG, MODE_MPICH_RECEXCH = 2, 3, 4, 5
@@ -395,3 +404,6 @@ def parse_plan(text):
         else:
             cur["post"].append(local(tok))
     return plan
+
+
+__all__ = [_n for _n in dir() if not _n.startswith("_") and _n not in ("ctypes", "os", "lib", "UniqueId")]

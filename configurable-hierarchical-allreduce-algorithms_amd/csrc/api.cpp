@@ -75,7 +75,7 @@ int chr_reduce_tree(void* out, const void* const* leaves, int nleaves, const uns
 
 int chr_fill(void* buf, size_t n, chr_dtype dtype, int pattern, uint64_t seed, int rank, uint64_t count_for_seq,
              hipStream_t stream) {
-    if (!chr::dtype_size(dtype) || (pattern < 0 || pattern > 2)) return CHR_ERR_INVALID_ARG;
+    if (!chr::dtype_size(dtype) || (pattern < 0 || pattern > 3)) return CHR_ERR_INVALID_ARG;
     if (n == 0) return CHR_SUCCESS;
     if (!buf) return CHR_ERR_INVALID_ARG;
     return status(chr::launch_fill(buf, n, dtype, pattern, seed, rank, count_for_seq, stream));

@@ -12,6 +12,8 @@ namespace chr {
 
 size_t dtype_size(int dtype);
 bool valid_dtype_op(int dtype, int op);
+// The kernel instantiation (type, op) that computes (dtype, op) bit-exactly (reduce_kernels.hip).
+void canon_op(int dtype, int op, bool running_first, int* kdt, int* kop);
 
 // Fused bucket reduction: out = (...((acc op ins[0]) op ins[1])...) op ins[m-1], each step
 // MPI_Reduce_local(ins[j], acc) = OP(ins[j], acc); with running_first each step is

@@ -4,6 +4,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "chr_internal.hpp"
 
 namespace chr {
@@ -31,13 +33,23 @@ template <> struct DTy<CHR_FLOAT32> { using T = float; };
 template <> struct DTy<CHR_FLOAT64> { using T = double; };
 template <> struct DTy<CHR_INT32> { using T = int32_t; };
 template <> struct DTy<CHR_BFLOAT16> { using T = uint16_t; };
+template <> struct DTy<CHR_INT8> { using T = int8_t; };
+template <> struct DTy<CHR_UINT8> { using T = uint8_t; };
+template <> struct DTy<CHR_INT16> { using T = int16_t; };
+template <> struct DTy<CHR_UINT16> { using T = uint16_t; };
+template <> struct DTy<CHR_UINT32> { using T = uint32_t; };
+template <> struct DTy<CHR_INT64> { using T = int64_t; };
+template <> struct DTy<CHR_UINT64> { using T = uint64_t; };
+
+template <int DT>
+constexpr bool is_float_dt() { return DT == CHR_FLOAT32 || DT == CHR_FLOAT64 || DT == CHR_BFLOAT16; }
 
 // Internal op codes for the running-value-first order of MPICH_do_reduce
 // (allreduce_recexch.cpp:147-186): each step is MPI_Reduce_local(running, next).  SUM and
 // PROD are bitwise commutative (IEEE add/mul, wrapping int, bf16 RNE of a commutative f32
 // op), so only MAX/MIN need their own instantiations (they differ on ties such as -0/+0
 // and on NaN compares).
-constexpr int kMaxSw = 6, kMinSw = 7;
+constexpr int kMaxSw = 16, kMinSw = 17;
 
 // MPI_Reduce_local(in = x, inout = y): MPICH 3.3.2's loop is inout = OP(inout, in) with
 // MAX(p, q) = p > q ? p : q (MPIR_OP_TYPE_REDUCE_CASE, a = inoutvec, b = invec), so MAX/MIN
@@ -53,11 +65,23 @@ __device__ __forceinline__ typename DTy<DT>::T apply(typename DTy<DT>::T x, type
         else if constexpr (OP == CHR_MIN) return fy < fx ? y : x;
         else if constexpr (OP == kMaxSw) return fx > fy ? x : y;
         else return fx < fy ? x : y;
-    } else if constexpr (DT == CHR_INT32) {
-        if constexpr (OP == CHR_SUM) return (int32_t)((uint32_t)y + (uint32_t)x);
-        else if constexpr (OP == CHR_PROD) return (int32_t)((uint32_t)y * (uint32_t)x);
+    } else if constexpr (!is_float_dt<DT>()) {
+        // integers (MPICH's C loops): wrapping SUM/PROD (computed unsigned, at least 32 bits wide,
+        // so no signed overflow and no promotion surprises), MAX/MIN (ties are bitwise equal, so
+        // the swapped orders coincide), logical ops with a 0/1 result, bitwise ops
+        using T = typename DTy<DT>::T;
+        using UT = std::make_unsigned_t<T>;
+        using W = std::conditional_t<(sizeof(T) < 4), uint32_t, UT>;
+        if constexpr (OP == CHR_SUM) return (T)(UT)((W)(UT)y + (W)(UT)x);
+        else if constexpr (OP == CHR_PROD) return (T)(UT)((W)(UT)y * (W)(UT)x);
         else if constexpr (OP == CHR_MAX || OP == kMaxSw) return y > x ? y : x;
-        else return y < x ? y : x;
+        else if constexpr (OP == CHR_MIN || OP == kMinSw) return y < x ? y : x;
+        else if constexpr (OP == CHR_LAND) return (T)((y != 0) && (x != 0));
+        else if constexpr (OP == CHR_LOR) return (T)((y != 0) || (x != 0));
+        else if constexpr (OP == CHR_LXOR) return (T)((y != 0) != (x != 0));
+        else if constexpr (OP == CHR_BAND) return (T)(y & x);
+        else if constexpr (OP == CHR_BOR) return (T)(y | x);
+        else return (T)(y ^ x);
     } else {
         if constexpr (OP == CHR_SUM) return y + x;
         else if constexpr (OP == CHR_PROD) return y * x;
@@ -70,6 +94,10 @@ __device__ __forceinline__ typename DTy<DT>::T apply(typename DTy<DT>::T x, type
 
 template <int DT, int OP>
 __device__ __forceinline__ u32x4 apply_vec(u32x4 in, u32x4 acc) {
+    // bitwise ops do not see element boundaries: whole dwords
+    if constexpr (OP == CHR_BAND) return acc & in;
+    if constexpr (OP == CHR_BOR) return acc | in;
+    if constexpr (OP == CHR_BXOR) return acc ^ in;
     if constexpr (DT == CHR_BFLOAT16 && (OP == CHR_SUM || OP == CHR_PROD)) {
         // two bf16 per dword: widen by shift / mask, one f32 op each, one packed RNE convert
         u32x4 r;

@@ -30,11 +30,9 @@
 
 #include <cstdlib>
 
-#include "reduce_common.hpp"
+#include "reduce_vec.hpp"
 
 namespace chr {
-
-constexpr int kMaxFanIn = 8;
 
 size_t dtype_size(int dtype) {
     switch (dtype) {
@@ -42,11 +40,53 @@ size_t dtype_size(int dtype) {
     case CHR_FLOAT64: return 8;
     case CHR_INT32: return 4;
     case CHR_BFLOAT16: return 2;
+    case CHR_INT8: case CHR_UINT8: return 1;
+    case CHR_INT16: case CHR_UINT16: return 2;
+    case CHR_UINT32: return 4;
+    case CHR_INT64: case CHR_UINT64: return 8;
     default: return 0;
     }
 }
 
-bool valid_dtype_op(int dtype, int op) { return dtype_size(dtype) != 0 && op >= CHR_SUM && op <= CHR_MIN; }
+static bool is_float_dtype(int dtype) {
+    return dtype == CHR_FLOAT32 || dtype == CHR_FLOAT64 || dtype == CHR_BFLOAT16;
+}
+
+// MPI's predefined-op/type table as MPICH's MPI_Reduce_local applies it: SUM/PROD/MAX/MIN on
+// every type, the logical and bitwise ops on the integer types only.
+bool valid_dtype_op(int dtype, int op) {
+    if (!dtype_size(dtype)) return false;
+    if (op >= CHR_SUM && op <= CHR_MIN) return true;
+    return op >= CHR_LAND && op <= CHR_BXOR && !is_float_dtype(dtype);
+}
+
+// The kernel instantiation that computes (dtype, op).  Signedness only matters to MAX/MIN:
+// wrapping SUM/PROD, the logical and the bitwise ops give the same bits on the unsigned type of
+// the same width (int32's kernels serve uint32 there).  running_first (MPICH_do_reduce order)
+// changes MAX/MIN results only for floating types (ties of -0/+0, NaN compares).
+void canon_op(int dtype, int op, bool running_first, int* kdt, int* kop) {
+    *kop = op;
+    if (is_float_dtype(dtype)) {
+        *kdt = dtype;
+        if (running_first && (op == CHR_MAX || op == CHR_MIN)) *kop = op == CHR_MAX ? kMaxSw : kMinSw;
+        return;
+    }
+    if (op == CHR_MAX || op == CHR_MIN) {
+        *kdt = dtype;
+        return;
+    }
+    switch (dtype_size(dtype)) {
+    case 1: *kdt = CHR_UINT8; break;
+    case 2: *kdt = CHR_UINT16; break;
+    case 4: *kdt = CHR_INT32; break;
+    default: *kdt = CHR_UINT64; break;
+    }
+}
+
+// kernel types compiled in this translation unit (all tuning variants); the rest: reduce_int.hip
+static bool in_core_tu(int kdt, int kop) {
+    return is_float_dtype(kdt) || (kdt == CHR_INT32 && kop >= CHR_SUM && kop <= CHR_MIN);
+}
 
 ReduceTuning& reduce_tuning() {
     static ReduceTuning t = [] {
@@ -68,161 +108,45 @@ ReduceTuning& reduce_tuning() {
     return t;
 }
 
-struct VecArgs {
-    u32x4* out;
-    const u32x4* acc;
-    const u32x4* ins[kMaxFanIn];
-    size_t nvec;
-};
-
-// U vectors (16 B each) per lane per trip; all M+1 operands of the trip are loaded
-// before the first add so (M+1)*U*16 bytes per lane are in flight.  NT: non-temporal
-// loads and stores (global_load/store_dwordx4 ... nt) for calls that stream far more than
-// the caches hold: +15-40 % on HBM-cold buckets.  ACC0: under NT, the FIRST of the U
-// accumulator vectors keeps the default policy (in place, a quarter of the write-backs then
-// go through the Infinity Cache): per-slot policy sweep
-// (profiles/r01/microbench_focus4_slot_policy.txt) +15 % at 1 GiB m=1, +3-5 % for m>=2 with
-// 256-thread workgroups; with one-wave workgroups it also gains on the 64 MiB m=1 bucket
-// (6 440-6 464 vs 6 041-6 052 GB/s all-nt, profiles/r01/block_ab_bench.txt), so it is used for
-// every nt call; making ALL accumulator slots temporal thrashes the cache (-7 %).  Slot 0 is peeled so that the two policies
-// are separate instructions (a select between a plain and an nt load of one address is
-// merged by LLVM, dropping the nt bit).
-template <int DT, int OP, int M, int U, bool NT, bool ACC0, int BL>
-__global__ __launch_bounds__(BL) void k_reduce_vec(VecArgs a) {
-    const size_t stride = (size_t)gridDim.x * BL * U;
-    for (size_t base = (size_t)blockIdx.x * BL * U + threadIdx.x; base < a.nvec; base += stride) {
-        if (base + (size_t)(U - 1) * BL < a.nvec) {
-            u32x4 acc[U], x[M][U];
-            acc[0] = ld<NT && !ACC0>(&a.acc[base]);
-#pragma unroll
-            for (int u = 1; u < U; ++u) acc[u] = ld<NT>(&a.acc[base + (size_t)u * BL]);
-#pragma unroll
-            for (int j = 0; j < M; ++j)
-#pragma unroll
-                for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&a.ins[j][base + (size_t)u * BL]);
-            // Keep every load of the trip ahead of the first add: without this the
-            // scheduler interleaves the first add (and its vmcnt(0)) between the loads.
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int j = 0; j < M; ++j)
-#pragma unroll
-                for (int u = 0; u < U; ++u) acc[u] = apply_vec<DT, OP>(x[j][u], acc[u]);
-#pragma unroll
-            for (int u = 0; u < U; ++u) st<NT>(&a.out[base + (size_t)u * BL], acc[u]);
-        } else {
-            for (int u = 0; u < U; ++u) {
-                const size_t i = base + (size_t)u * BL;
-                if (i >= a.nvec) break;
-                u32x4 acc = a.acc[i];
-#pragma unroll
-                for (int j = 0; j < M; ++j) acc = apply_vec<DT, OP>(a.ins[j][i], acc);
-                a.out[i] = acc;
-            }
-        }
-    }
-}
-
-struct ScalarArgs {
-    void* out;
-    const void* acc;
-    const void* ins[kMaxFanIn];
-    int m;
-    size_t n;
-};
-
-// Any alignment (odd sizes / offsets): one element per lane per trip.
-template <int DT, int OP>
-__global__ __launch_bounds__(kBlock) void k_reduce_scalar(ScalarArgs a) {
-    using T = typename DTy<DT>::T;
-    T* out = (T*)a.out;
-    const T* acc = (const T*)a.acc;
-    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < a.n; i += (size_t)gridDim.x * kBlock) {
-        T v = acc[i];
-        for (int j = 0; j < a.m; ++j) v = apply<DT, OP>(((const T*)a.ins[j])[i], v);
-        out[i] = v;
-    }
-}
-
 // ---- host launchers ----------------------------------------------------------------------
-
-template <int DT, int OP, int M, int BL>
-static hipError_t launch_vec_mb(const VecArgs& a, bool nt, bool acc0, hipStream_t s) {
-    constexpr int U = M <= 2 ? 4 : 2;
-    const size_t trips = (a.nvec + (size_t)BL * U - 1) / ((size_t)BL * U);
-    const size_t cap = reduce_tuning().max_blocks > 0 ? (size_t)reduce_tuning().max_blocks : trips;
-    const int grid = (int)(trips < cap ? trips : cap);
-    if (!nt)
-        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, false, false, BL>), dim3(grid), dim3(BL), 0, s, a);
-    else if (acc0)
-        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, true, BL>), dim3(grid), dim3(BL), 0, s, a);
-    else
-        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, false, BL>), dim3(grid), dim3(BL), 0, s, a);
-    return hipGetLastError();
-}
-
-// Policy (profiles/r01/block_ab_*): calls that stream >= 128 MiB run non-temporal with
-// one-wave workgroups and the first accumulator slot temporal (ACC0); smaller, cache-warm
-// calls keep plain accesses and 256-thread workgroups.
-template <int DT, int OP, int M>
-static hipError_t launch_vec_m(const VecArgs& a, hipStream_t s) {
-    const ReduceTuning& t = reduce_tuning();
-    const size_t call_bytes = (size_t)(M + 2) * a.nvec * 16;
-    const bool nt = t.nt_mode == 1 || (t.nt_mode < 0 && call_bytes >= t.nt_min_bytes);
-    const bool acc0 = t.acc0_mode == 1 || (t.acc0_mode < 0 && (M >= 2 || a.nvec * 16 >= t.acc0_min_bytes));
-    const int bl = t.block ? t.block : nt ? 64 : 256;
-    return bl == 64 ? launch_vec_mb<DT, OP, M, 64>(a, nt, acc0, s) : launch_vec_mb<DT, OP, M, 256>(a, nt, acc0, s);
-}
-
-template <int DT, int OP>
-static hipError_t launch_vec_op(const VecArgs& a, int m, hipStream_t s) {
-    switch (m) {
-    case 1: return launch_vec_m<DT, OP, 1>(a, s);
-    case 2: return launch_vec_m<DT, OP, 2>(a, s);
-    case 3: return launch_vec_m<DT, OP, 3>(a, s);
-    case 4: return launch_vec_m<DT, OP, 4>(a, s);
-    case 5: return launch_vec_m<DT, OP, 5>(a, s);
-    case 6: return launch_vec_m<DT, OP, 6>(a, s);
-    case 7: return launch_vec_m<DT, OP, 7>(a, s);
-    case 8: return launch_vec_m<DT, OP, 8>(a, s);
-    default: return hipErrorInvalidValue;
-    }
-}
 
 template <int DT>
 static hipError_t launch_vec_dt(const VecArgs& a, int m, int op, hipStream_t s) {
     switch (op) {
-    case CHR_SUM: return launch_vec_op<DT, CHR_SUM>(a, m, s);
-    case CHR_PROD: return launch_vec_op<DT, CHR_PROD>(a, m, s);
-    case CHR_MAX: return launch_vec_op<DT, CHR_MAX>(a, m, s);
-    case CHR_MIN: return launch_vec_op<DT, CHR_MIN>(a, m, s);
+    case CHR_SUM: return launch_vec_op<DT, CHR_SUM, true>(a, m, s);
+    case CHR_PROD: return launch_vec_op<DT, CHR_PROD, true>(a, m, s);
+    case CHR_MAX: return launch_vec_op<DT, CHR_MAX, true>(a, m, s);
+    case CHR_MIN: return launch_vec_op<DT, CHR_MIN, true>(a, m, s);
     case kMaxSw:
-        if constexpr (DT == CHR_INT32) return launch_vec_op<DT, CHR_MAX>(a, m, s);
-        else return launch_vec_op<DT, kMaxSw>(a, m, s);
+        if constexpr (DT == CHR_INT32) return hipErrorInvalidValue;
+        else return launch_vec_op<DT, kMaxSw, true>(a, m, s);
     case kMinSw:
-        if constexpr (DT == CHR_INT32) return launch_vec_op<DT, CHR_MIN>(a, m, s);
-        else return launch_vec_op<DT, kMinSw>(a, m, s);
+        if constexpr (DT == CHR_INT32) return hipErrorInvalidValue;
+        else return launch_vec_op<DT, kMinSw, true>(a, m, s);
     default: return hipErrorInvalidValue;
     }
 }
 
 template <int DT>
 static hipError_t launch_scalar_dt(const ScalarArgs& a, int op, hipStream_t s) {
-    const size_t trips = (a.n + kBlock - 1) / kBlock;
-    const int grid = (int)(trips < 2048 ? trips : 2048);
     switch (op) {
-    case CHR_SUM: hipLaunchKernelGGL((k_reduce_scalar<DT, CHR_SUM>), dim3(grid), dim3(kBlock), 0, s, a); break;
-    case CHR_PROD: hipLaunchKernelGGL((k_reduce_scalar<DT, CHR_PROD>), dim3(grid), dim3(kBlock), 0, s, a); break;
-    case CHR_MAX: hipLaunchKernelGGL((k_reduce_scalar<DT, CHR_MAX>), dim3(grid), dim3(kBlock), 0, s, a); break;
-    case CHR_MIN: hipLaunchKernelGGL((k_reduce_scalar<DT, CHR_MIN>), dim3(grid), dim3(kBlock), 0, s, a); break;
-    case kMaxSw: hipLaunchKernelGGL((k_reduce_scalar<DT, kMaxSw>), dim3(grid), dim3(kBlock), 0, s, a); break;
-    case kMinSw: hipLaunchKernelGGL((k_reduce_scalar<DT, kMinSw>), dim3(grid), dim3(kBlock), 0, s, a); break;
+    case CHR_SUM: return launch_scalar_op<DT, CHR_SUM>(a, s);
+    case CHR_PROD: return launch_scalar_op<DT, CHR_PROD>(a, s);
+    case CHR_MAX: return launch_scalar_op<DT, CHR_MAX>(a, s);
+    case CHR_MIN: return launch_scalar_op<DT, CHR_MIN>(a, s);
+    case kMaxSw:
+        if constexpr (DT == CHR_INT32) return hipErrorInvalidValue;
+        else return launch_scalar_op<DT, kMaxSw>(a, s);
+    case kMinSw:
+        if constexpr (DT == CHR_INT32) return hipErrorInvalidValue;
+        else return launch_scalar_op<DT, kMinSw>(a, s);
     default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
 }
 
-static hipError_t launch_scalar(void* out, const void* acc, const void* const* ins, int m, size_t n, int dtype,
-                                int op, hipStream_t s) {
+// kdt/kop: the kernel type and op from canon_op
+static hipError_t launch_scalar(void* out, const void* acc, const void* const* ins, int m, size_t n, int kdt,
+                                int kop, hipStream_t s) {
     if (n == 0) return hipSuccess;
     ScalarArgs a{};
     a.out = out;
@@ -230,11 +154,12 @@ static hipError_t launch_scalar(void* out, const void* acc, const void* const* i
     a.m = m;
     a.n = n;
     for (int j = 0; j < m; ++j) a.ins[j] = ins[j];
-    switch (dtype) {
-    case CHR_FLOAT32: return launch_scalar_dt<CHR_FLOAT32>(a, op, s);
-    case CHR_FLOAT64: return launch_scalar_dt<CHR_FLOAT64>(a, op, s);
-    case CHR_INT32: return launch_scalar_dt<CHR_INT32>(a, op, s);
-    case CHR_BFLOAT16: return launch_scalar_dt<CHR_BFLOAT16>(a, op, s);
+    if (!in_core_tu(kdt, kop)) return launch_scalar_int(a, kdt, kop, s);
+    switch (kdt) {
+    case CHR_FLOAT32: return launch_scalar_dt<CHR_FLOAT32>(a, kop, s);
+    case CHR_FLOAT64: return launch_scalar_dt<CHR_FLOAT64>(a, kop, s);
+    case CHR_INT32: return launch_scalar_dt<CHR_INT32>(a, kop, s);
+    case CHR_BFLOAT16: return launch_scalar_dt<CHR_BFLOAT16>(a, kop, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -242,7 +167,7 @@ static hipError_t launch_scalar(void* out, const void* acc, const void* const* i
 // One pass over at most kMaxFanIn inputs.
 static hipError_t launch_group(void* out, const void* acc, const void* const* ins, int m, size_t n, int dtype,
                                int op, hipStream_t s) {
-    const size_t es = dtype_size(dtype);
+    const size_t es = dtype_size(dtype);  // dtype, op: the kernel type and op (canon_op)
     const uintptr_t mis = (uintptr_t)out & 15u;
     bool congruent = ((uintptr_t)acc & 15u) == mis && (mis % es) == 0;
     for (int j = 0; j < m; ++j) congruent = congruent && (((uintptr_t)ins[j] & 15u) == mis);
@@ -260,12 +185,16 @@ static hipError_t launch_group(void* out, const void* acc, const void* const* in
         a.acc = (const u32x4*)((const char*)acc + head * es);
         for (int j = 0; j < m; ++j) a.ins[j] = (const u32x4*)((const char*)ins[j] + head * es);
         a.nvec = nvec;
-        switch (dtype) {
-        case CHR_FLOAT32: err = launch_vec_dt<CHR_FLOAT32>(a, m, op, s); break;
-        case CHR_FLOAT64: err = launch_vec_dt<CHR_FLOAT64>(a, m, op, s); break;
-        case CHR_INT32: err = launch_vec_dt<CHR_INT32>(a, m, op, s); break;
-        case CHR_BFLOAT16: err = launch_vec_dt<CHR_BFLOAT16>(a, m, op, s); break;
-        default: err = hipErrorInvalidValue;
+        if (!in_core_tu(dtype, op)) {
+            err = launch_vec_int(a, dtype, op, m, s);
+        } else {
+            switch (dtype) {
+            case CHR_FLOAT32: err = launch_vec_dt<CHR_FLOAT32>(a, m, op, s); break;
+            case CHR_FLOAT64: err = launch_vec_dt<CHR_FLOAT64>(a, m, op, s); break;
+            case CHR_INT32: err = launch_vec_dt<CHR_INT32>(a, m, op, s); break;
+            case CHR_BFLOAT16: err = launch_vec_dt<CHR_BFLOAT16>(a, m, op, s); break;
+            default: err = hipErrorInvalidValue;
+            }
         }
         if (err != hipSuccess) return err;
     }
@@ -281,9 +210,9 @@ static hipError_t launch_group(void* out, const void* acc, const void* const* in
 hipError_t launch_reduce(void* out, const void* acc, const void* const* ins, int m, size_t n, int dtype, int op,
                          hipStream_t stream, bool running_first) {
     if (n == 0) return hipSuccess;
-    if (op < CHR_SUM || op > CHR_MIN) return hipErrorInvalidValue;
-    if (running_first && (op == CHR_MAX || op == CHR_MIN)) op = op == CHR_MAX ? kMaxSw : kMinSw;
+    if (!valid_dtype_op(dtype, op)) return hipErrorInvalidValue;
     const size_t es = dtype_size(dtype);
+    canon_op(dtype, op, running_first, &dtype, &op);
     if (m == 0) {
         if (out == acc) return hipSuccess;
         return hipMemcpyAsync(out, acc, n * es, hipMemcpyDeviceToDevice, stream);
@@ -308,7 +237,26 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 
 __global__ __launch_bounds__(kBlock) void k_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed,
                                                  uint64_t rank, uint64_t count_for_seq) {
+    const int es = dtype == CHR_INT8 || dtype == CHR_UINT8 ? 1 : dtype == CHR_INT16 || dtype == CHR_UINT16 ? 2
+                   : dtype == CHR_UINT32 || (dtype == CHR_INT32 && pattern == 3) ? 4
+                   : dtype == CHR_INT64 || dtype == CHR_UINT64 ? 8 : 0;
     for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kBlock) {
+        if (es) {  // the integer types beyond int32 (and int32's sparse pattern): seq = rank*count + i,
+                   // ties = {0, 1, -1, 2, 7}, sparse = 1/8 zeros else nonzero random bits, uniform = the
+                   // top 8*es random bits; truncated to the width (orc_fill_at)
+            const uint64_t u = splitmix64(seed ^ (rank << 40) ^ (uint64_t)i);
+            const unsigned sel = (unsigned)(u >> 61);
+            const uint64_t v = pattern == 1   ? rank * count_for_seq + i
+                               : pattern == 2 ? (uint64_t)(int64_t)(sel == 6 ? 2 : sel == 7 ? 7 : sel == 2 ? 1
+                                                                    : sel == 3 ? -1 : 0)
+                               : pattern == 3 ? (sel ? (u >> (64 - 8 * es)) | 1u : 0)
+                                              : u >> (64 - 8 * es);
+            if (es == 1) ((uint8_t*)buf)[i] = (uint8_t)v;
+            else if (es == 2) ((uint16_t*)buf)[i] = (uint16_t)v;
+            else if (es == 4) ((uint32_t*)buf)[i] = (uint32_t)v;
+            else ((uint64_t*)buf)[i] = v;
+            continue;
+        }
         if (pattern == 1) {
             const int32_t v = (int32_t)(uint32_t)(rank * count_for_seq + i);
             switch (dtype) {

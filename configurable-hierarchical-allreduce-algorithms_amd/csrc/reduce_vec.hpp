@@ -1,0 +1,164 @@
+// reduce_vec.hpp -- the fused bucket-reduction kernels (templates), shared by the translation
+// units that instantiate them: reduce_kernels.hip (floating types, int32 arithmetic) and
+// reduce_int.hip (the other MPI integer types, logical and bitwise ops).  See reduce_kernels.hip
+// for the design notes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "reduce_common.hpp"
+
+namespace chr {
+
+constexpr int kMaxFanIn = 8;
+
+struct VecArgs {
+    u32x4* out;
+    const u32x4* acc;
+    const u32x4* ins[kMaxFanIn];
+    size_t nvec;
+};
+
+// U vectors (16 B each) per lane per trip; all M+1 operands of the trip are loaded
+// before the first add so (M+1)*U*16 bytes per lane are in flight.  NT: non-temporal
+// loads and stores (global_load/store_dwordx4 ... nt) for calls that stream far more than
+// the caches hold: +15-40 % on HBM-cold buckets.  ACC0: under NT, the FIRST of the U
+// accumulator vectors keeps the default policy (in place, a quarter of the write-backs then
+// go through the Infinity Cache): per-slot policy sweep
+// (profiles/r01/microbench_focus4_slot_policy.txt) +15 % at 1 GiB m=1, +3-5 % for m>=2 with
+// 256-thread workgroups; with one-wave workgroups it also gains on the 64 MiB m=1 bucket
+// (6 440-6 464 vs 6 041-6 052 GB/s all-nt, profiles/r01/block_ab_bench.txt), so it is used for
+// every nt call; making ALL accumulator slots temporal thrashes the cache (-7 %).  Slot 0 is peeled so that the two policies
+// are separate instructions (a select between a plain and an nt load of one address is
+// merged by LLVM, dropping the nt bit).
+template <int DT, int OP, int M, int U, bool NT, bool ACC0, int BL>
+__global__ __launch_bounds__(BL) void k_reduce_vec(VecArgs a) {
+    const size_t stride = (size_t)gridDim.x * BL * U;
+    for (size_t base = (size_t)blockIdx.x * BL * U + threadIdx.x; base < a.nvec; base += stride) {
+        if (base + (size_t)(U - 1) * BL < a.nvec) {
+            u32x4 acc[U], x[M][U];
+            acc[0] = ld<NT && !ACC0>(&a.acc[base]);
+#pragma unroll
+            for (int u = 1; u < U; ++u) acc[u] = ld<NT>(&a.acc[base + (size_t)u * BL]);
+#pragma unroll
+            for (int j = 0; j < M; ++j)
+#pragma unroll
+                for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&a.ins[j][base + (size_t)u * BL]);
+            // Keep every load of the trip ahead of the first add: without this the
+            // scheduler interleaves the first add (and its vmcnt(0)) between the loads.
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < M; ++j)
+#pragma unroll
+                for (int u = 0; u < U; ++u) acc[u] = apply_vec<DT, OP>(x[j][u], acc[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) st<NT>(&a.out[base + (size_t)u * BL], acc[u]);
+        } else {
+            for (int u = 0; u < U; ++u) {
+                const size_t i = base + (size_t)u * BL;
+                if (i >= a.nvec) break;
+                u32x4 acc = a.acc[i];
+#pragma unroll
+                for (int j = 0; j < M; ++j) acc = apply_vec<DT, OP>(a.ins[j][i], acc);
+                a.out[i] = acc;
+            }
+        }
+    }
+}
+
+struct ScalarArgs {
+    void* out;
+    const void* acc;
+    const void* ins[kMaxFanIn];
+    int m;
+    size_t n;
+};
+
+// Any alignment (odd sizes / offsets): one element per lane per trip.
+template <int DT, int OP>
+__global__ __launch_bounds__(kBlock) void k_reduce_scalar(ScalarArgs a) {
+    using T = typename DTy<DT>::T;
+    T* out = (T*)a.out;
+    const T* acc = (const T*)a.acc;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < a.n; i += (size_t)gridDim.x * kBlock) {
+        T v = acc[i];
+        for (int j = 0; j < a.m; ++j) v = apply<DT, OP>(((const T*)a.ins[j])[i], v);
+        out[i] = v;
+    }
+}
+
+template <int DT, int OP, int M, int BL>
+inline hipError_t launch_vec_mb(const VecArgs& a, bool nt, bool acc0, hipStream_t s) {
+    constexpr int U = M <= 2 ? 4 : 2;
+    const size_t trips = (a.nvec + (size_t)BL * U - 1) / ((size_t)BL * U);
+    const size_t cap = reduce_tuning().max_blocks > 0 ? (size_t)reduce_tuning().max_blocks : trips;
+    const int grid = (int)(trips < cap ? trips : cap);
+    if (!nt)
+        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, false, false, BL>), dim3(grid), dim3(BL), 0, s, a);
+    else if (acc0)
+        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, true, BL>), dim3(grid), dim3(BL), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, false, BL>), dim3(grid), dim3(BL), 0, s, a);
+    return hipGetLastError();
+}
+
+// Policy (profiles/r01/block_ab_*): calls that stream >= 128 MiB run non-temporal with
+// one-wave workgroups and the first accumulator slot temporal (ACC0); smaller, cache-warm
+// calls keep plain accesses and 256-thread workgroups.
+template <int DT, int OP, int M, int BL, bool NT, bool ACC0>
+inline hipError_t launch_vec_mb_one(const VecArgs& a, hipStream_t s) {
+    constexpr int U = M <= 2 ? 4 : 2;
+    const size_t trips = (a.nvec + (size_t)BL * U - 1) / ((size_t)BL * U);
+    const size_t cap = reduce_tuning().max_blocks > 0 ? (size_t)reduce_tuning().max_blocks : trips;
+    const int grid = (int)(trips < cap ? trips : cap);
+    hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, NT, ACC0, BL>), dim3(grid), dim3(BL), 0, s, a);
+    return hipGetLastError();
+}
+
+// FULL: every tuning variant (CHR_REDUCE_BLOCK / CHR_REDUCE_ACC0 overrides) is compiled, for the
+// floating types and int32; the other integer types compile the two policy shapes only (nt: one
+// wave + ACC0; plain: 256 threads) and ignore those two overrides.
+template <int DT, int OP, int M, bool FULL>
+inline hipError_t launch_vec_m(const VecArgs& a, hipStream_t s) {
+    const ReduceTuning& t = reduce_tuning();
+    const size_t call_bytes = (size_t)(M + 2) * a.nvec * 16;
+    const bool nt = t.nt_mode == 1 || (t.nt_mode < 0 && call_bytes >= t.nt_min_bytes);
+    if constexpr (!FULL) {
+        if (nt) return launch_vec_mb_one<DT, OP, M, 64, true, true>(a, s);
+        return launch_vec_mb_one<DT, OP, M, 256, false, false>(a, s);
+    } else {
+        const bool acc0 = t.acc0_mode == 1 || (t.acc0_mode < 0 && (M >= 2 || a.nvec * 16 >= t.acc0_min_bytes));
+        const int bl = t.block ? t.block : nt ? 64 : 256;
+        return bl == 64 ? launch_vec_mb<DT, OP, M, 64>(a, nt, acc0, s) : launch_vec_mb<DT, OP, M, 256>(a, nt, acc0, s);
+    }
+}
+
+template <int DT, int OP, bool FULL>
+inline hipError_t launch_vec_op(const VecArgs& a, int m, hipStream_t s) {
+    switch (m) {
+    case 1: return launch_vec_m<DT, OP, 1, FULL>(a, s);
+    case 2: return launch_vec_m<DT, OP, 2, FULL>(a, s);
+    case 3: return launch_vec_m<DT, OP, 3, FULL>(a, s);
+    case 4: return launch_vec_m<DT, OP, 4, FULL>(a, s);
+    case 5: return launch_vec_m<DT, OP, 5, FULL>(a, s);
+    case 6: return launch_vec_m<DT, OP, 6, FULL>(a, s);
+    case 7: return launch_vec_m<DT, OP, 7, FULL>(a, s);
+    case 8: return launch_vec_m<DT, OP, 8, FULL>(a, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+template <int DT, int OP>
+inline hipError_t launch_scalar_op(const ScalarArgs& a, hipStream_t s) {
+    const size_t trips = (a.n + kBlock - 1) / kBlock;
+    const int grid = (int)(trips < 2048 ? trips : 2048);
+    hipLaunchKernelGGL((k_reduce_scalar<DT, OP>), dim3(grid), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+
+// Launches for the integer kernel types of reduce_int.hip (kdt/kop from canon_op).
+hipError_t launch_vec_int(const VecArgs& a, int kdt, int kop, int m, hipStream_t s);
+hipError_t launch_scalar_int(const ScalarArgs& a, int kdt, int kop, hipStream_t s);
+
+}  // namespace chr

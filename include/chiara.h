@@ -22,16 +22,35 @@
 extern "C" {
 #endif
 
-#define CHR_ABI_VERSION 2
+#define CHR_ABI_VERSION 3
 
+/* Element types.  The reference is generic over MPI_Datatype (all_reduce_radix_batch.cpp:202-204,
+ * sizes from MPI_Type_size at :234-277); these are the MPI predefined types MPICH's
+ * MPI_Reduce_local accepts for the ops below.  Integer arithmetic wraps (two's complement), as
+ * MPICH's C loops do on every supported platform. */
 typedef enum {
     CHR_FLOAT32 = 0,   /* MPI_FLOAT */
     CHR_FLOAT64 = 1,   /* MPI_DOUBLE (testing/main.cpp harness) */
-    CHR_INT32 = 2,     /* MPI_INT (Fugaku_experiments harnesses); wraps on overflow */
-    CHR_BFLOAT16 = 3   /* no MPI equivalent: f32 arithmetic, RNE-rounded after every step */
+    CHR_INT32 = 2,     /* MPI_INT, MPI_INT32_T (Fugaku_experiments harnesses) */
+    CHR_BFLOAT16 = 3,  /* no MPI equivalent: f32 arithmetic, RNE-rounded after every step */
+    CHR_INT8 = 4,      /* MPI_SIGNED_CHAR, MPI_INT8_T, MPI_CHAR */
+    CHR_UINT8 = 5,     /* MPI_UNSIGNED_CHAR, MPI_UINT8_T, MPI_BYTE (bitwise ops), MPI_C_BOOL (logical ops) */
+    CHR_INT16 = 6,     /* MPI_SHORT, MPI_INT16_T */
+    CHR_UINT16 = 7,    /* MPI_UNSIGNED_SHORT, MPI_UINT16_T */
+    CHR_UINT32 = 8,    /* MPI_UNSIGNED, MPI_UINT32_T */
+    CHR_INT64 = 9,     /* MPI_LONG, MPI_LONG_LONG, MPI_INT64_T */
+    CHR_UINT64 = 10    /* MPI_UNSIGNED_LONG, MPI_UNSIGNED_LONG_LONG, MPI_UINT64_T */
 } chr_dtype;
 
-typedef enum { CHR_SUM = 0, CHR_PROD = 1, CHR_MAX = 2, CHR_MIN = 3 } chr_op;
+/* Reduction ops: MPI's predefined ops with MPICH 3.3.2's element semantics
+ * (inout[i] = inout[i] OP in[i]).  SUM/PROD/MAX/MIN on every type; the logical (result 0 or 1)
+ * and bitwise ops on the integer types only.  MPI_MAXLOC/MINLOC and user ops (MPI_Op_create)
+ * are not supported (CHR_ERR_INVALID_ARG; MPI_ERR_OP through the shim). */
+typedef enum {
+    CHR_SUM = 0, CHR_PROD = 1, CHR_MAX = 2, CHR_MIN = 3,
+    CHR_LAND = 4, CHR_LOR = 5, CHR_LXOR = 6,  /* MPI_LAND, MPI_LOR, MPI_LXOR */
+    CHR_BAND = 7, CHR_BOR = 8, CHR_BXOR = 9   /* MPI_BAND, MPI_BOR, MPI_BXOR */
+} chr_op;
 
 typedef enum {
     CHR_SUCCESS = 0,
@@ -294,7 +313,10 @@ int chr_local_allreduce_mpich(chr_local_group* group, const void* const* sends,
 /* ---- utilities -------------------------------------------------------------------------- */
 /* Synthetic inputs on the device with the shared generator (oracle/chiara_oracle.h):
  * pattern 0 = U[-1,1) (random 32-bit ints for INT32), 1 = rank*count_for_seq + i,
- * 2 = ties probe for MAX/MIN ({+0,-0,1,-1,0.5, NaN with per-rank payload}). */
+ * 2 = ties probe for MAX/MIN ({+0,-0,1,-1,0.5, NaN with per-rank payload}; integers {0,1,-1,2,7}),
+ * 3 = sparse (integer types: zero with probability 1/8, else nonzero random bits; floats: as 0).
+ * Integer types beyond int32: 0 = random bits of the full width, 1 = rank*count_for_seq + i
+ * truncated to the width. */
 int chr_fill(void* buf, size_t n, chr_dtype dtype, int pattern, uint64_t seed, int rank,
              uint64_t count_for_seq, hipStream_t stream);
 const char* chr_error_string(int code);

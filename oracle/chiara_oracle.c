@@ -26,17 +26,42 @@ size_t orc_dtype_size(int dtype) {
     case ORC_F64: return 8;
     case ORC_I32: return 4;
     case ORC_BF16: return 2;
+    case ORC_I8: case ORC_U8: return 1;
+    case ORC_I16: case ORC_U16: return 2;
+    case ORC_U32: return 4;
+    case ORC_I64: case ORC_U64: return 8;
     default: return 0;
     }
 }
 
-void orc_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int rank,
-              uint64_t count_for_seq) {
+/* Elements [start, start + n) of rank `rank`'s input, written to buf[0 .. n): the same values as
+ * orc_fill's, so windows of a full-size input can be generated without the whole buffer. */
+void orc_fill_at(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int rank,
+                 uint64_t count_for_seq, uint64_t start) {
     size_t i;
+    const size_t ies = (dtype >= ORC_I8 || (dtype == ORC_I32 && pattern == ORC_PAT_SPARSE)) ? orc_dtype_size(dtype) : 0;
     for (i = 0; i < n; ++i) {
+        const uint64_t g = start + i;
+        if (ies) {
+            /* integer types beyond int32: SEQ = rank*count + i, TIES = {0, 1, -1, 2, 7}, UNIFORM = the
+             * top 8*es random bits; stored truncated to the width (two's complement) */
+            static const int64_t it8[8] = {0, 0, 1, -1, 0, 0, 2, 7};
+            const uint64_t key = orc_key(seed, (uint64_t)rank, g);
+            const uint64_t v = pattern == ORC_PAT_SEQ      ? (uint64_t)rank * count_for_seq + g
+                               : pattern == ORC_PAT_TIES   ? (uint64_t)it8[key >> 61]
+                               : pattern == ORC_PAT_SPARSE ? ((key >> 61) ? (key >> (64 - 8 * ies)) | 1u : 0)
+                                                           : key >> (64 - 8 * ies);
+            switch (ies) {
+            case 1: ((uint8_t*)buf)[i] = (uint8_t)v; break;
+            case 2: ((uint16_t*)buf)[i] = (uint16_t)v; break;
+            case 4: ((uint32_t*)buf)[i] = (uint32_t)v; break;
+            default: ((uint64_t*)buf)[i] = v; break;
+            }
+            continue;
+        }
         if (pattern == ORC_PAT_SEQ) {
             /* Fugaku_experiments/Allreduce/main.cpp:48-49 (int wraps as on the reference). */
-            uint32_t v = (uint32_t)((uint64_t)rank * count_for_seq + i);
+            uint32_t v = (uint32_t)((uint64_t)rank * count_for_seq + g);
             switch (dtype) {
             case ORC_F32: ((float*)buf)[i] = (float)(int32_t)v; break;
             case ORC_F64: ((double*)buf)[i] = (double)(int32_t)v; break;
@@ -44,7 +69,7 @@ void orc_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int ra
             case ORC_BF16: ((uint16_t*)buf)[i] = orc_f32_to_bf16((float)(int32_t)v); break;
             }
         } else if (pattern == ORC_PAT_TIES) {
-            const unsigned sel = (unsigned)(orc_key(seed, (uint64_t)rank, i) >> 61);
+            const unsigned sel = (unsigned)(orc_key(seed, (uint64_t)rank, g) >> 61);
             const uint32_t pay = (uint32_t)(rank + 1) & 0x3Fu;
             static const float ft[7] = {0.0f, -0.0f, 1.0f, -1.0f, 0.0f, -0.0f, 0.5f};
             static const int32_t it[8] = {0, 0, 1, -1, 0, 0, 2, 7};
@@ -74,15 +99,20 @@ void orc_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int ra
             }
         } else {
             switch (dtype) {
-            case ORC_F32: ((float*)buf)[i] = orc_gen_f32(seed, (uint64_t)rank, i); break;
-            case ORC_F64: ((double*)buf)[i] = orc_gen_f64(seed, (uint64_t)rank, i); break;
-            case ORC_I32: ((int32_t*)buf)[i] = (int32_t)(uint32_t)(orc_key(seed, (uint64_t)rank, i) >> 32); break;
+            case ORC_F32: ((float*)buf)[i] = orc_gen_f32(seed, (uint64_t)rank, g); break;
+            case ORC_F64: ((double*)buf)[i] = orc_gen_f64(seed, (uint64_t)rank, g); break;
+            case ORC_I32: ((int32_t*)buf)[i] = (int32_t)(uint32_t)(orc_key(seed, (uint64_t)rank, g) >> 32); break;
             case ORC_BF16:
-                ((uint16_t*)buf)[i] = orc_f32_to_bf16(orc_gen_f32(seed, (uint64_t)rank, i));
+                ((uint16_t*)buf)[i] = orc_f32_to_bf16(orc_gen_f32(seed, (uint64_t)rank, g));
                 break;
             }
         }
     }
+}
+
+void orc_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int rank,
+              uint64_t count_for_seq) {
+    orc_fill_at(buf, n, dtype, pattern, seed, rank, count_for_seq, 0);
 }
 
 /* MPICH 3.3.2 predefined ops (src/mpi/coll/op/opsum.c, opmax.c, ... via
@@ -98,6 +128,23 @@ void orc_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int ra
         for (i = 0; i < n; ++i) { T x = a[i], y = b[i]; b[i] = (EXPR); } \
     } while (0)
 
+/* Integer types: MPICH's C loops on the type (two's complement wrap for SUM/PROD, computed here
+ * in the unsigned type of at least 32 bits so C's promotions cannot overflow), LAND/LOR/LXOR give
+ * 0 or 1 ((a && b), (a || b), (!a != !b)), BAND/BOR/BXOR the bitwise ops. */
+#define ORC_INT_CASE(T, UT, WT)                                                          \
+    switch (op) {                                                                        \
+    case ORC_SUM: ORC_LOOP(T, (T)(UT)((WT)(UT)y + (WT)(UT)x)); break;                    \
+    case ORC_PROD: ORC_LOOP(T, (T)(UT)((WT)(UT)y * (WT)(UT)x)); break;                   \
+    case ORC_MAX: ORC_LOOP(T, y > x ? y : x); break;                                     \
+    case ORC_MIN: ORC_LOOP(T, y < x ? y : x); break;                                     \
+    case ORC_LAND: ORC_LOOP(T, (T)(y && x)); break;                                      \
+    case ORC_LOR: ORC_LOOP(T, (T)(y || x)); break;                                       \
+    case ORC_LXOR: ORC_LOOP(T, (T)(!y != !x)); break;                                    \
+    case ORC_BAND: ORC_LOOP(T, (T)(y & x)); break;                                       \
+    case ORC_BOR: ORC_LOOP(T, (T)(y | x)); break;                                        \
+    case ORC_BXOR: ORC_LOOP(T, (T)(y ^ x)); break;                                       \
+    }
+
 void orc_reduce_local(const void* in, void* inout, size_t n, int dtype, int op) {
     switch (dtype) {
     case ORC_F32:
@@ -112,12 +159,14 @@ void orc_reduce_local(const void* in, void* inout, size_t n, int dtype, int op) 
         else if (op == ORC_MAX) ORC_LOOP(double, y > x ? y : x);
         else ORC_LOOP(double, y < x ? y : x);
         break;
-    case ORC_I32:
-        if (op == ORC_SUM) ORC_LOOP(int32_t, (int32_t)((uint32_t)y + (uint32_t)x));
-        else if (op == ORC_PROD) ORC_LOOP(int32_t, (int32_t)((uint32_t)y * (uint32_t)x));
-        else if (op == ORC_MAX) ORC_LOOP(int32_t, y > x ? y : x);
-        else ORC_LOOP(int32_t, y < x ? y : x);
-        break;
+    case ORC_I32: ORC_INT_CASE(int32_t, uint32_t, uint32_t) break;
+    case ORC_I8: ORC_INT_CASE(int8_t, uint8_t, uint32_t) break;
+    case ORC_U8: ORC_INT_CASE(uint8_t, uint8_t, uint32_t) break;
+    case ORC_I16: ORC_INT_CASE(int16_t, uint16_t, uint32_t) break;
+    case ORC_U16: ORC_INT_CASE(uint16_t, uint16_t, uint32_t) break;
+    case ORC_U32: ORC_INT_CASE(uint32_t, uint32_t, uint32_t) break;
+    case ORC_I64: ORC_INT_CASE(int64_t, uint64_t, uint64_t) break;
+    case ORC_U64: ORC_INT_CASE(uint64_t, uint64_t, uint64_t) break;
     case ORC_BF16:
         /* The reference has no bf16; the golden driver runs it as a user-defined op on
          * MPI_Type_contiguous(2, MPI_BYTE) computing bf16_rne(f32(inout) op f32(in)) with the
@@ -262,7 +311,9 @@ static int orc_phases_0_2(orc_state* s, int nranks, int k_in, int b, size_t recv
     memset(s, 0, sizeof(*s));
     if (b < 1 || nranks < 1 || nranks % b != 0 || k_in < 2) return 1;
     s->es = orc_dtype_size(dtype);
-    if (!s->es || op < ORC_SUM || op > ORC_MIN) return 1;
+    if (!s->es || op < ORC_SUM || op > ORC_BXOR || (op > ORC_MIN && (dtype == ORC_F32 || dtype == ORC_F64 ||
+                                                                      dtype == ORC_BF16)))
+        return 1;
     s->nranks = nranks;
     s->b = b;
     s->recvcount = recvcount;

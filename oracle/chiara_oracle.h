@@ -28,19 +28,28 @@ extern "C" {
 #endif
 
 /* Same numbering as include/chiara.h (chr_dtype / chr_op). */
-enum { ORC_F32 = 0, ORC_F64 = 1, ORC_I32 = 2, ORC_BF16 = 3 };
-enum { ORC_SUM = 0, ORC_PROD = 1, ORC_MAX = 2, ORC_MIN = 3 };
+enum {
+    ORC_F32 = 0, ORC_F64 = 1, ORC_I32 = 2, ORC_BF16 = 3,
+    ORC_I8 = 4, ORC_U8 = 5, ORC_I16 = 6, ORC_U16 = 7, ORC_U32 = 8, ORC_I64 = 9, ORC_U64 = 10
+};
+enum {
+    ORC_SUM = 0, ORC_PROD = 1, ORC_MAX = 2, ORC_MIN = 3,
+    ORC_LAND = 4, ORC_LOR = 5, ORC_LXOR = 6, ORC_BAND = 7, ORC_BOR = 8, ORC_BXOR = 9
+};
 
 /* Input patterns for the generator. */
 enum {
-    ORC_PAT_UNIFORM = 0,  /* f32/f64/bf16: U[-1,1); i32: full-range random 32-bit ints */
+    ORC_PAT_UNIFORM = 0,  /* f32/f64/bf16: U[-1,1); integers: random bits of the full width */
     ORC_PAT_SEQ = 1,      /* the reference harness pattern: rank*count + i
                              (Fugaku_experiments/Allreduce/main.cpp:48-49) */
-    ORC_PAT_TIES = 2      /* MAX/MIN operand-order probe: each element one of {+0, -0, 1, -1,
+    ORC_PAT_TIES = 2,     /* MAX/MIN operand-order probe: each element one of {+0, -0, 1, -1,
                              0.5, NaN with a per-rank payload} (ints: {0, 1, -1, 2, 7}), so
                              ties and unordered compares are frequent and OP(a,b) vs OP(b,a)
-                             differ bitwise.  Used with MAX/MIN only (NaN payloads through
-                             arithmetic are not specified identically on CPU and GPU). */
+                             differ bitwise.  Used with MAX/MIN (and the logical ops) only (NaN
+                             payloads through arithmetic are not specified identically on CPU
+                             and GPU). */
+    ORC_PAT_SPARSE = 3    /* integer types: zero with probability 1/8, else nonzero random bits (the
+                             logical ops: LAND results are a mix of 0 and 1 even at 8 ranks) */
 };
 
 static inline uint64_t orc_splitmix64(uint64_t x) {
@@ -85,6 +94,9 @@ size_t orc_dtype_size(int dtype);
  * count used by the SEQ pattern (value = rank*count_for_seq + i, wrapping int32). */
 void orc_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int rank,
               uint64_t count_for_seq);
+/* Elements [start, start + n) of the same input (window of a full-size buffer). */
+void orc_fill_at(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int rank,
+                 uint64_t count_for_seq, uint64_t start);
 
 /* MPI_Reduce_local restated (MPICH 3.3.2 predefined ops): inout[i] = inout[i] (op) in[i]
  * (MPICH's loop order: MAX/MIN keep inout on ties and NaN compares).

@@ -13,10 +13,13 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
-DTYPES = {"f32": 0, "f64": 1, "i32": 2, "bf16": 3}
-OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3}
-NP_DTYPES = {"f32": np.float32, "f64": np.float64, "i32": np.int32, "bf16": np.uint16}
-PAT_UNIFORM, PAT_SEQ, PAT_TIES = 0, 1, 2
+DTYPES = {"f32": 0, "f64": 1, "i32": 2, "bf16": 3, "i8": 4, "u8": 5, "i16": 6, "u16": 7, "u32": 8, "i64": 9,
+          "u64": 10}
+OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "land": 4, "lor": 5, "lxor": 6, "band": 7, "bor": 8, "bxor": 9}
+NP_DTYPES = {"f32": np.float32, "f64": np.float64, "i32": np.int32, "bf16": np.uint16, "i8": np.int8, "u8": np.uint8,
+             "i16": np.int16, "u16": np.uint16, "u32": np.uint32, "i64": np.int64, "u64": np.uint64}
+INT_DTYPES = ("i32", "i8", "u8", "i16", "u16", "u32", "i64", "u64")
+PAT_UNIFORM, PAT_SEQ, PAT_TIES, PAT_SPARSE = 0, 1, 2, 3
 
 _lib = None
 
@@ -33,6 +36,7 @@ def lib():
         L = ctypes.CDLL(LIB_PATH)
         vp, sz, i, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
         L.orc_fill.argtypes = [vp, sz, i, i, u64, i, u64]
+        L.orc_fill_at.argtypes = [vp, sz, i, i, u64, i, u64, u64]
         L.orc_reduce_local.argtypes = [vp, vp, sz, i, i]
         L.orc_reduce_multi.argtypes = [vp, ctypes.POINTER(vp), i, sz, i, i]
         L.orc_allreduce_radix_batch.argtypes = [i, i, i, sz, i, i, ctypes.POINTER(vp), ctypes.POINTER(vp)]
@@ -52,6 +56,39 @@ def fill(n, dtype, pattern, seed, rank, count_for_seq=None):
     a = np.empty(n, dtype=NP_DTYPES[dtype])
     lib().orc_fill(_ptr(a), n, DTYPES[dtype], pattern, seed, rank, n if count_for_seq is None else count_for_seq)
     return a
+
+
+def fill_at(n, dtype, pattern, seed, rank, start, count_for_seq):
+    """Elements [start, start + n) of the input fill() makes with this count_for_seq."""
+    a = np.empty(n, dtype=NP_DTYPES[dtype])
+    lib().orc_fill_at(_ptr(a), n, DTYPES[dtype], pattern, seed, rank, count_for_seq, start)
+    return a
+
+
+def block_window(nblocks, blocklen, off, width):
+    """Element indices of the window [off, off + width) of every one of `nblocks` blocks of
+    `blocklen` elements, block-major: a (nblocks * width,) index array."""
+    return (np.arange(nblocks, dtype=np.int64)[:, None] * blocklen + off + np.arange(width, dtype=np.int64)).ravel()
+
+
+def window_inputs(nranks, count, off, width, dtype, pattern, seed, nblocks=None):
+    """Every rank's input restricted to the block window [off, off + width) of each of its
+    `nblocks` (default nranks) blocks of count // nblocks elements.
+
+    Block-window property: all_reduce_radix_batch / reduce_scatter_radix_batch address their
+    buffers only in whole blocks of recvcount elements (every offset and count in
+    all_reduce_radix_batch.cpp:239-312, :343-364, :523-530 is a multiple of recvcount, IRC =
+    recvcount * b), and reduce elementwise, so an element's expression depends only on its block.
+    Running the collective on these windows (recvcount' = width) therefore computes, for every
+    element, the same expression as the full-size call: the full-size result restricted to the
+    window.  tests/test_oracle_golden.py::test_block_window_property pins this on the oracle."""
+    nb = nranks if nblocks is None else nblocks
+    blen = count // nb
+    out = []
+    for r in range(nranks):
+        parts = [fill_at(width, dtype, pattern, seed, r, j * blen + off, count) for j in range(nb)]
+        out.append(np.concatenate(parts))
+    return out
 
 
 def reduce_local(inp, inout, dtype, op):

@@ -64,18 +64,32 @@ static void bf16_user_prod(void* in, void* inout, int* len, MPI_Datatype*) {
 }
 
 static int parse_dtype(const std::string& s) {
-    if (s == "f32") return ORC_F32;
-    if (s == "f64") return ORC_F64;
-    if (s == "i32") return ORC_I32;
-    if (s == "bf16") return ORC_BF16;
+    static const char* names[] = {"f32", "f64", "i32", "bf16", "i8", "u8", "i16", "u16", "u32", "i64", "u64"};
+    for (int d = 0; d < (int)(sizeof(names) / sizeof(names[0])); ++d)
+        if (s == names[d]) return d;
     return -1;
 }
 static int parse_op(const std::string& s) {
-    if (s == "sum") return ORC_SUM;
-    if (s == "prod") return ORC_PROD;
-    if (s == "max") return ORC_MAX;
-    if (s == "min") return ORC_MIN;
+    static const char* names[] = {"sum", "prod", "max", "min", "land", "lor", "lxor", "band", "bor", "bxor"};
+    for (int o = 0; o < (int)(sizeof(names) / sizeof(names[0])); ++o)
+        if (s == names[o]) return o;
     return -1;
+}
+// MPI predefined types for the oracle's dtypes (bf16: the user type below)
+static MPI_Datatype mpi_type_of(int dtype) {
+    switch (dtype) {
+    case ORC_F32: return MPI_FLOAT;
+    case ORC_F64: return MPI_DOUBLE;
+    case ORC_I32: return MPI_INT;
+    case ORC_I8: return MPI_SIGNED_CHAR;
+    case ORC_U8: return MPI_UNSIGNED_CHAR;
+    case ORC_I16: return MPI_SHORT;
+    case ORC_U16: return MPI_UNSIGNED_SHORT;
+    case ORC_U32: return MPI_UNSIGNED;
+    case ORC_I64: return MPI_INT64_T;
+    case ORC_U64: return MPI_UINT64_T;
+    default: return MPI_DATATYPE_NULL;
+    }
 }
 
 int main(int argc, char** argv) {
@@ -96,7 +110,8 @@ int main(int argc, char** argv) {
     MPI_Op_create(bf16_user_prod, 1, &bf16_ops[ORC_PROD]);
     MPI_Op_create(bf16_user_max, 1, &bf16_ops[ORC_MAX]);
     MPI_Op_create(bf16_user_min, 1, &bf16_ops[ORC_MIN]);
-    const MPI_Op std_ops[4] = {MPI_SUM, MPI_PROD, MPI_MAX, MPI_MIN};
+    const MPI_Op std_ops[10] = {MPI_SUM, MPI_PROD, MPI_MAX, MPI_MIN, MPI_LAND,
+                                MPI_LOR, MPI_LXOR, MPI_BAND, MPI_BOR, MPI_BXOR};
 
     std::ifstream cases(argv[1]);
     std::string line;
@@ -109,15 +124,12 @@ int main(int argc, char** argv) {
         unsigned long long seed;
         is >> id >> mode >> k >> b >> count >> dts >> ops >> pattern >> seed >> inplace;
         int dtype = parse_dtype(dts), op = parse_op(ops);
-        if (dtype < 0 || op < 0) {
+        if (dtype < 0 || op < 0 || (dtype == ORC_BF16 && op > ORC_MIN)) {
             if (rank == 0) fprintf(stderr, "bad case: %s\n", line.c_str());
             continue;
         }
         size_t es = orc_dtype_size(dtype);
-        MPI_Datatype mdt = dtype == ORC_F32 ? MPI_FLOAT
-                           : dtype == ORC_F64 ? MPI_DOUBLE
-                           : dtype == ORC_I32 ? MPI_INT
-                                              : bf16_t;
+        MPI_Datatype mdt = dtype == ORC_BF16 ? bf16_t : mpi_type_of(dtype);
         MPI_Op mop = dtype == ORC_BF16 ? bf16_ops[op] : std_ops[op];
 
         size_t in_n = (mode == "rs") ? (size_t)count * nprocs : (size_t)count;

@@ -40,3 +40,18 @@ def golden_mpich():
         manifest = json.load(f)
     arrays = np.load(os.path.join(here, "mpich_outputs.npz"), allow_pickle=False)
     return manifest["cases"], arrays
+
+
+@pytest.fixture(scope="session")
+def golden_types():
+    """Golden vectors of the integer types beyond int32 and the logical/bitwise ops, from the
+    reference compiled here against MPICH (gen_golden.py types)."""
+    import json
+
+    import numpy as np
+
+    here = os.path.join(REPO, "tests", "golden")
+    with open(os.path.join(here, "types_manifest.json")) as f:
+        manifest = json.load(f)
+    arrays = np.load(os.path.join(here, "types_outputs.npz"), allow_pickle=False)
+    return manifest["cases"], arrays

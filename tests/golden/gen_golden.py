@@ -151,6 +151,47 @@ def mpich_cases_for(n):
     return out
 
 
+TYPE_OPS = {  # MPI's predefined op/type table: arithmetic on every integer type, logical/bitwise too
+    "i8": ("sum", "prod", "max", "min", "land", "lor", "lxor", "band", "bor", "bxor"),
+    "u8": ("sum", "max", "min", "land", "bxor"),
+    "i16": ("sum", "prod", "max", "min", "lor", "band"),
+    "u16": ("sum", "max", "min", "lxor", "bor"),
+    "i32": ("land", "lor", "lxor", "band", "bor", "bxor"),
+    "u32": ("sum", "prod", "max", "min", "land", "bxor"),
+    "i64": ("sum", "prod", "max", "min", "land", "lor", "lxor", "band", "bor", "bxor"),
+    "u64": ("sum", "max", "min", "lor", "band"),
+}
+
+
+def types_cases_for(n):
+    """The reference is generic over MPI_Datatype x MPI_Op (all_reduce_radix_batch.cpp:202-204,
+    :234-277): the integer types beyond int32 and the logical / bitwise ops, through the radix/batch
+    collectives and a few MPICH baselines.  LOR/LXOR run on the TIES pattern ({0, 1, -1, 2, 7}: zeros
+    are frequent), LAND on SPARSE (1/8 zeros, so its results mix 0 and 1), arithmetic and bitwise
+    ops on full-width random bits (SUM/PROD wrap)."""
+    out = []
+
+    def add(mode, k, b, count, dt, op, pat, inplace):
+        cid = f"{mode}_n{n}_k{k}_b{b}_c{count}_{dt}_{op}_p{pat}_ip{inplace}"
+        out.append(dict(id=cid, mode=mode, n=n, k=k, b=b, count=count, dtype=dt, op=op,
+                        pattern=pat, seed=SEED, inplace=inplace))
+
+    for dt, ops in TYPE_OPS.items():
+        for op in ops:
+            pat = {"land": pyoracle.PAT_SPARSE, "lor": pyoracle.PAT_TIES, "lxor": pyoracle.PAT_TIES}.get(
+                op, pyoracle.PAT_UNIFORM)
+            for i, b in enumerate(divisors(n)):
+                k = (2, 3, 4)[i % 3]
+                add("ar", k, b, n * 24 + (n if i % 2 else 0), dt, op, pat, i % 2)
+                add("rs", k, b, 13 + i, dt, op, pat, 0)
+            if op in ("sum", "max", "band", "land"):
+                add("rx", 3, 0, 40, dt, op, pat, 0)
+                add("ring", 0, 0, 3 * n + 5, dt, op, pat, 0)
+                add("rm", 2, 0, 33, dt, op, pat, 1)
+        add("ag", 2, n if n < 4 else 2, 9, dt, "sum", pyoracle.PAT_UNIFORM, 0)
+    return out
+
+
 def run_n(n, cases, tmp):
     cf = os.path.join(tmp, f"cases_{n}.txt")
     with open(cf, "w") as f:
@@ -172,6 +213,10 @@ def main():
         for n in (1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 16):
             all_cases += mpich_cases_for(n)
         prefix = "mpich_"
+    elif which == "types":
+        for n in (2, 3, 4, 6, 8):
+            all_cases += types_cases_for(n)
+        prefix = "types_"
     else:
         prefix = ""
         for n in (1, 2, 3, 4, 5, 6, 8, 9, 12, 16):
@@ -201,17 +246,25 @@ def main():
             if c["dtype"] == "bf16":
                 af = (a.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
                 lf = (lb.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+            elif c["dtype"] in ("i64", "u64"):  # exact integer difference (doubles lose bits)
+                af, lf = a.view(np.int64).astype(object), lb.view(np.int64).astype(object)
             else:
                 af, lf = a.astype(np.float64), lb.astype(np.float64)
             rec["n_diff_vs_lib"] = int(np.count_nonzero(a != lb))
-            ok = np.isfinite(af) & np.isfinite(lf)
-            rec["max_abs_diff_vs_lib"] = float(np.max(np.abs(af[ok] - lf[ok]))) if ok.any() else 0.0
+            if af.dtype == object:
+                rec["max_abs_diff_vs_lib"] = float(max((abs(int(x) - int(y)) for x, y in zip(af, lf)), default=0))
+            else:
+                ok = np.isfinite(af) & np.isfinite(lf)
+                rec["max_abs_diff_vs_lib"] = float(np.max(np.abs(af[ok] - lf[ok]))) if ok.any() else 0.0
             rec["stored"] = len(out) <= STORE_LIMIT
             if rec["stored"]:
                 arrays[c["id"]] = a.copy()
                 arrays[c["id"] + "__lib"] = lb.copy()
             manifest.append(rec)
-    ref_desc = ("testing/mpich_implementations/all_reduce/{allreduce_ring,allreduce_recursive_doubling,"
+    ref_desc = ("Fugaku_experiments/{Allreduce,Reduce-scatter,Allgather} + testing/mpich_implementations/"
+                "all_reduce/{allreduce_ring,allreduce_recexch,allreduce_recursive_multiplying}.cpp, integer types "
+                "beyond int32 and the logical/bitwise ops" if which == "types" else
+                "testing/mpich_implementations/all_reduce/{allreduce_ring,allreduce_recursive_doubling,"
                 "allreduce_reduce_scatter_allgather,allreduce_recexch,allreduce_k_reduce_scatter_allgather,"
                 "allreduce_recursive_multiplying}.cpp" if which == "mpich" else
                 "Fugaku_experiments/{Allreduce/all_reduce_radix_batch.cpp,Reduce-scatter/reduce_scatter_radix_batch.cpp,"

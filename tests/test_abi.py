@@ -32,7 +32,7 @@ def test_library_is_gfx950_code_object():
 
 
 def test_abi_basics():
-    assert ca.lib().chr_abi_version() == 2
+    assert ca.lib().chr_abi_version() == 3
     assert ca.lib().chr_error_string(2).decode().startswith("count")
     assert ca.lib().chr_error_string(0) == b"success"
 
@@ -58,5 +58,5 @@ def test_reduce_tree_rejects_bad_args_without_device():
     import ctypes
 
     leaves = (ctypes.c_void_p * 2)(0x1000, 0x2000)
-    assert ca.lib().chr_reduce_tree(0x3000, leaves, 2, bytes([0, 1]), None, 0, 9, ca.SUM, None) == 1  # bad dtype
+    assert ca.lib().chr_reduce_tree(0x3000, leaves, 2, bytes([0, 1]), None, 0, 11, ca.SUM, None) == 1  # bad dtype
     assert ca.lib().chr_reduce_tree(0x3000, None, 2, bytes([0, 1]), None, 0, ca.FLOAT32, ca.SUM, None) == 1

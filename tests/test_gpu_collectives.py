@@ -14,8 +14,10 @@ import pyoracle as po
 
 pytestmark = pytest.mark.gpu
 
-DT = {"f32": ca.FLOAT32, "f64": ca.FLOAT64, "i32": ca.INT32, "bf16": ca.BFLOAT16}
-OP = {"sum": ca.SUM, "prod": ca.PROD, "max": ca.MAX, "min": ca.MIN}
+DT = {"f32": ca.FLOAT32, "f64": ca.FLOAT64, "i32": ca.INT32, "bf16": ca.BFLOAT16, "i8": ca.INT8, "u8": ca.UINT8,
+      "i16": ca.INT16, "u16": ca.UINT16, "u32": ca.UINT32, "i64": ca.INT64, "u64": ca.UINT64}
+OP = {"sum": ca.SUM, "prod": ca.PROD, "max": ca.MAX, "min": ca.MIN, "land": ca.LAND, "lor": ca.LOR,
+      "lxor": ca.LXOR, "band": ca.BAND, "bor": ca.BOR, "bxor": ca.BXOR}
 
 
 @pytest.fixture(scope="module")
@@ -99,6 +101,42 @@ def test_local_group_exact_schedule_matches_reference_golden(gu, groups, golden)
             outs = run_local(gu, g, c["mode"], sends, c["k"], c["b"], c["dtype"], c["op"], bool(c["inplace"]))
         finally:
             g.set_schedule(ca.SCHEDULE_FLAT)
+        if hashlib.sha256(b"".join(o.tobytes() for o in outs)).hexdigest() != c["sha256"]:
+            bad.append(c["id"])
+    assert not bad, f"{len(bad)} device/reference mismatches, e.g. {bad[:5]}"
+
+
+@pytest.mark.parametrize("schedule", ["flat", "exact"])
+def test_integer_types_and_logical_bitwise_ops_match_reference_golden(gu, groups, golden_types, schedule):
+    """The reference's generic MPI_Datatype x MPI_Op (all_reduce_radix_batch.cpp:202-204,
+    :234-277): (u)int8/16/64, uint32 and LAND/LOR/LXOR/BAND/BOR/BXOR through the radix/batch
+    collectives and the MPICH baselines, every golden case of the reference run under MPICH 3.3.2
+    bit-exact on the device."""
+    cases, _ = golden_types
+    bad = []
+    for c in cases:
+        if schedule == "exact" and c["mode"] not in ("ar", "rs"):
+            continue
+        n, g = c["n"], groups(c["n"])
+        if c["mode"] in ("ar", "rs", "ag"):
+            in_n = c["count"] * n if c["mode"] == "rs" else c["count"]
+            sends = [po.fill(in_n, c["dtype"], c["pattern"], c["seed"], r) for r in range(n)]
+            g.set_schedule(ca.SCHEDULE_EXACT if schedule == "exact" else ca.SCHEDULE_FLAT)
+            try:
+                outs = run_local(gu, g, c["mode"], sends, c["k"], c["b"], c["dtype"], c["op"], bool(c["inplace"]))
+            finally:
+                g.set_schedule(ca.SCHEDULE_FLAT)
+        else:
+            npdt = po.NP_DTYPES[c["dtype"]]
+            sends = [po.fill(c["count"], c["dtype"], c["pattern"], c["seed"], r) for r in range(n)]
+            d_send = [gu.to_dev(x) for x in sends]
+            if c["inplace"]:
+                d_recv, d_sendp = d_send, [ca.IN_PLACE] * n
+            else:
+                d_recv, d_sendp = [gu.empty_dev(x.nbytes) for x in sends], d_send
+            assert g.allreduce_mpich(MPICH_MODE[c["mode"]], d_sendp, d_recv, c["count"], DT[c["dtype"]], OP[c["op"]],
+                                     c["k"], c["b"]) == 0, c["id"]
+            outs = [gu.from_dev(d, npdt, c["count"]) for d in d_recv]
         if hashlib.sha256(b"".join(o.tobytes() for o in outs)).hexdigest() != c["sha256"]:
             bad.append(c["id"])
     assert not bad, f"{len(bad)} device/reference mismatches, e.g. {bad[:5]}"
@@ -190,6 +228,81 @@ def test_c5_full_size_bf16_properties(gu, groups):
         assert bool(((recvs[0][s0:s0 + step].float() - exact).abs() <= bound).all())
     del sends, recvs
     torch.cuda.empty_cache()
+
+
+SEED = 0xC41A5EED
+
+
+def _window_reader(recvs, n, rc, npdt, tview):
+    def out_window(r, off, w):
+        return recvs[r].view(tview).view(n, rc)[:, off:off + w].contiguous().cpu().numpy().ravel().view(npdt)
+    return out_window
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("dtype,schedule", [("f32", "flat"), ("f32", "exact"), ("bf16", "flat"), ("bf16", "exact")])
+def test_c4_c5_full_size_bit_exact_vs_oracle(gu, groups, dtype, schedule):
+    """C4 (fp32) and C5 (bf16) at their BASELINE size -- 8 ranks, k=4, b=4, 1 GiB per rank,
+    U[-1,1) data -- bit-exact vs the C oracle over every element of every rank.  This is the
+    size that switches on the non-temporal / ACC0 / one-wave kernel instantiations and the
+    automatic 8-slice pipeline; the association order the oracle pins is
+    all_reduce_radix_batch.cpp:343-364 (recexch folds) and :523-530 (lane reduction).  The int32
+    closed form (test_c4_full_size_exact_int) and the bf16 bound stay as fast pre-checks: both
+    are blind to association.  Checked window by window (tests/fullsize_util.py)."""
+    import torch
+
+    import fullsize_util as fs
+
+    n, k, b = 8, 4, 4
+    es = 4 if dtype == "f32" else 2
+    count = (1 << 30) // es
+    rc = count // n
+    cdt = DT[dtype]
+    g = groups(n)
+    sends = [torch.empty(count * es, dtype=torch.uint8, device=gu.DEV) for _ in range(n)]
+    for r, s in enumerate(sends):
+        assert ca.fill(s, count, cdt, po.PAT_UNIFORM, SEED, r, count, gu.stream()) == 0
+    recvs = [torch.empty(count * es, dtype=torch.uint8, device=gu.DEV) for _ in range(n)]
+    gu.sync()
+    g.set_schedule({"flat": ca.SCHEDULE_FLAT, "exact": ca.SCHEDULE_EXACT}[schedule])
+    g.set_slices(0)  # automatic: 8 slices of the 512 MiB chunks
+    try:
+        assert g.all_reduce_radix_batch(sends, recvs, count, cdt, ca.SUM, k, b) == 0
+    finally:
+        g.set_schedule(ca.SCHEDULE_FLAT)
+    gu.sync()
+    del sends
+    torch.cuda.empty_cache()
+    tview = torch.int32 if dtype == "f32" else torch.int16
+    bad = fs.check_allreduce(_window_reader(recvs, n, rc, po.NP_DTYPES[dtype], tview), n, k, b, dtype, count, SEED)
+    assert not bad, f"{len(bad)} (rank, window) mismatches vs the oracle, e.g. {bad[:5]}"
+    del recvs
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("b", [1, 2])
+def test_c3_full_size_windowed_inputs_from_device(gu, groups, b):
+    """C3 (reduce-scatter, n=2, k=2, 256 MiB send buffer) with device-generated inputs, checked
+    window by window like C4/C5: the windowed oracle path on a shape the whole-buffer oracle
+    also covers (test_c3_full_size_bit_exact)."""
+    import torch
+
+    import fullsize_util as fs
+
+    n, k, recvcount = 2, 2, 1 << 25
+    sends = [torch.empty(recvcount * n * 4, dtype=torch.uint8, device=gu.DEV) for _ in range(n)]
+    for r, s in enumerate(sends):
+        assert ca.fill(s, recvcount * n, ca.FLOAT32, po.PAT_UNIFORM, SEED, r, recvcount * n, gu.stream()) == 0
+    recvs = [torch.empty(recvcount * 4, dtype=torch.uint8, device=gu.DEV) for _ in range(n)]
+    gu.sync()
+    assert groups(n).reduce_scatter_radix_batch(sends, recvs, recvcount, ca.FLOAT32, ca.SUM, k, b) == 0
+    gu.sync()
+
+    def out_window(r, off, w):
+        return recvs[r].view(torch.int32)[off:off + w].cpu().numpy().view(np.float32)
+    bad = fs.check_reduce_scatter(out_window, n, k, b, "f32", recvcount, SEED)
+    assert not bad, bad[:5]
 
 
 def test_preconditions_rejected(gu, groups):

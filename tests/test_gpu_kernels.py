@@ -10,8 +10,11 @@ import pyoracle as po
 
 pytestmark = pytest.mark.gpu
 
-DT = {"f32": ca.FLOAT32, "f64": ca.FLOAT64, "i32": ca.INT32, "bf16": ca.BFLOAT16}
-OP = {"sum": ca.SUM, "prod": ca.PROD, "max": ca.MAX, "min": ca.MIN}
+DT = {"f32": ca.FLOAT32, "f64": ca.FLOAT64, "i32": ca.INT32, "bf16": ca.BFLOAT16, "i8": ca.INT8, "u8": ca.UINT8,
+      "i16": ca.INT16, "u16": ca.UINT16, "u32": ca.UINT32, "i64": ca.INT64, "u64": ca.UINT64}
+OP = {"sum": ca.SUM, "prod": ca.PROD, "max": ca.MAX, "min": ca.MIN, "land": ca.LAND, "lor": ca.LOR,
+      "lxor": ca.LXOR, "band": ca.BAND, "bor": ca.BOR, "bxor": ca.BXOR}
+INT_OPS = ("sum", "prod", "max", "min", "land", "lor", "lxor", "band", "bor", "bxor")
 
 
 @pytest.fixture(scope="module")
@@ -22,16 +25,16 @@ def gu():
 
 
 def _bits(a):
-    return a.view({2: np.uint16, 4: np.uint32, 8: np.uint64}[a.itemsize])
+    return a.view({1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[a.itemsize])
 
 
-def _check_multi(gu, dtype, op, m, n, off=0, in_off=None, seed=5):
+def _check_multi(gu, dtype, op, m, n, off=0, in_off=None, seed=5, pattern=0):
     """out = acc op ins[0] ... op ins[m-1] on device, element offsets to test alignment."""
     npdt = po.NP_DTYPES[dtype]
     es = np.dtype(npdt).itemsize
     in_off = off if in_off is None else in_off
-    acc = po.fill(n, dtype, 0, seed, 0)
-    ins = [po.fill(n, dtype, 0, seed, r + 1) for r in range(m)]
+    acc = po.fill(n, dtype, pattern, seed, 0)
+    ins = [po.fill(n, dtype, pattern, seed, r + 1) for r in range(m)]
     if op == "prod" and dtype == "i32":
         ins = [(x % 7).astype(np.int32) for x in ins]
     d_acc = gu.empty_dev((n + off) * es)
@@ -75,6 +78,36 @@ def test_misaligned_buffers(gu, off, in_off):
         _check_multi(gu, dt, "sum", 2, 10007, off, in_off)
 
 
+@pytest.mark.parametrize("dtype", ["i8", "u8", "i16", "u16", "i32", "u32", "i64", "u64"])
+@pytest.mark.parametrize("op", INT_OPS)
+@pytest.mark.parametrize("m", [1, 3, 8, 9])
+def test_integer_types_and_logical_bitwise_ops(gu, dtype, op, m):
+    """MPI integer types beyond int32 and LAND/LOR/LXOR/BAND/BOR/BXOR (the reference's generic
+    MPI_Datatype x MPI_Op, all_reduce_radix_batch.cpp:202-204): vector path, a ragged tail, a
+    misaligned scalar path; the logical ops on the SPARSE / TIES patterns so both results occur."""
+    pat = {"land": po.PAT_SPARSE, "lor": po.PAT_TIES, "lxor": po.PAT_TIES}.get(op, po.PAT_UNIFORM)
+    _check_multi(gu, dtype, op, m, 50021, pattern=pat)
+    _check_multi(gu, dtype, op, m, 999, off=1, in_off=1, pattern=pat)
+    _check_multi(gu, dtype, op, m, 777, off=1, in_off=2, pattern=pat)
+
+
+@pytest.mark.parametrize("dtype", ["u8", "i16", "i64", "u64"])
+def test_integer_types_streaming_path(gu, dtype):
+    """>= 128 MiB calls switch to the non-temporal one-wave instantiation."""
+    n = (48 << 20) // np.dtype(po.NP_DTYPES[dtype]).itemsize
+    _check_multi(gu, dtype, "sum", 1, n)
+    _check_multi(gu, dtype, "max", 3, n // 2 + 7)
+
+
+def test_float_types_reject_logical_and_bitwise_ops(gu):
+    x = gu.empty_dev(64)
+    for dt in (ca.FLOAT32, ca.FLOAT64, ca.BFLOAT16):
+        for op in (ca.LAND, ca.LOR, ca.LXOR, ca.BAND, ca.BOR, ca.BXOR):
+            assert ca.reduce_local(x, x, 4, dt, op, gu.stream()) == 1
+    assert ca.reduce_local(x, x, 4, 11, ca.SUM, gu.stream()) == 1
+    assert ca.reduce_local(x, x, 4, ca.INT8, 10, gu.stream()) == 1
+
+
 def test_reduce_local_mpi_semantics(gu):
     """MPI_Reduce_local (MPICH loop): inout = OP(inout, in); MAX keeps inout only when
     inout > in, so ties (-0/+0) and NaN compares take `in`."""
@@ -104,8 +137,8 @@ def test_int32_wraps(gu):
     assert list(gu.from_dev(db, np.int32)) == [-(2**31), 2**31 - 1, 0]
 
 
-@pytest.mark.parametrize("dtype", ["f32", "f64", "i32", "bf16"])
-@pytest.mark.parametrize("pattern", [0, 1, 2])
+@pytest.mark.parametrize("dtype", ["f32", "f64", "i32", "bf16", "i8", "u8", "i16", "u16", "u32", "i64", "u64"])
+@pytest.mark.parametrize("pattern", [0, 1, 2, 3])
 def test_device_fill_matches_oracle_generator(gu, dtype, pattern):
     n = 300001
     npdt = po.NP_DTYPES[dtype]
@@ -137,8 +170,9 @@ def test_streaming_path_ragged(gu, dtype, op, m, nbytes, off):
 def test_invalid_args(gu):
     assert ca.reduce_local(0, 0, 0, ca.FLOAT32, ca.SUM) == 0  # n == 0 is a no-op
     assert ca.reduce_local(0, 0, 5, ca.FLOAT32, ca.SUM) == 1
-    assert ca.reduce_local(1, 1, 5, 9, ca.SUM) == 1
-    assert ca.reduce_local(1, 1, 5, ca.FLOAT32, 9) == 1
+    assert ca.reduce_local(1, 1, 5, 11, ca.SUM) == 1  # 11: no such dtype
+    assert ca.reduce_local(1, 1, 5, ca.FLOAT32, 10) == 1  # 10: no such op
+    assert ca.reduce_local(1, 1, 5, ca.FLOAT32, ca.BXOR) == 1  # bitwise op on a float type
 
 
 @pytest.mark.parametrize("dtype", ["f32", "f64", "bf16", "i32"])

@@ -304,3 +304,207 @@ def test_rccl_graph_replay_world4():
     res = [q.get() for _ in range(world * 4 * 3)]
     bad = [r for r in res if r[4] != 0 or not r[5]]
     assert not bad, bad
+
+
+def _spawn(target, world, extra=(), timeout=300):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + tuple(extra)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout)
+    alive = [p for p in procs if p.is_alive()]
+    for p in alive:
+        p.kill()
+    assert not alive, "RCCL multi-rank test hung"
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return [q.get() for _ in range(world)]
+
+
+def _setup(rank):
+    """Per-rank environment (distinct RCCL host ids: socket transport on the one GPU) and import
+    paths; must run before the worker imports chiara_amd."""
+    os.environ["NCCL_HOSTID"] = f"chiara-test-host-{rank}"
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    os.environ.setdefault("NCCL_IB_DISABLE", "1")
+    for p in (HERE, os.path.join(REPO, "oracle"), os.path.join(REPO, "configurable-hierarchical-allreduce-algorithms_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
+def _init_worker(rank, world, port):
+    import torch.distributed as dist
+
+    import chiara_amd as ca
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    return ca.Comm.from_torch_distributed(device=0)
+
+
+def _graph_scratch_worker(rank, world, port, q):
+    """a graph captured for small buffers, then calls that grow the scratch
+    through the host-staged and the profiled (eager) paths, then the graph's call again."""
+    _setup(rank)
+    import torch
+    import torch.distributed as dist
+
+    import chiara_amd as ca
+    import pyoracle as po
+
+    comm = _init_worker(rank, world, port)
+    dev = torch.device("cuda:0")
+    ok = True
+    try:
+        comm.set_graphs(True)
+        small, big = 1 << 14, 1 << 21
+        send = torch.empty(small * 4, dtype=torch.uint8, device=dev)
+        out = torch.empty(small * 4, dtype=torch.uint8, device=dev)
+
+        def graph_call(seed):
+            send.copy_(torch.from_numpy(po.fill(small, "f32", 0, seed, rank).view(np.uint8).copy()))
+            rc = ca.all_reduce_radix_batch(send, out, small, ca.FLOAT32, ca.SUM, comm, 4, 4)
+            want = po.allreduce_radix_batch([po.fill(small, "f32", 0, seed, r) for r in range(world)], 4, 4, "f32",
+                                            "sum")[rank]
+            return rc == 0 and np.array_equal(out.cpu().numpy(), want.view(np.uint8))
+
+        ok &= graph_call(1)  # captured
+        ok &= graph_call(2)  # replayed
+        # host-staged, larger: its enqueue grows ACC/STAGE
+        hx = po.fill(big, "f32", 0, 3, rank)
+        hout = np.zeros_like(hx)
+        ok &= ca.all_reduce_radix_batch(hx, hout, big, ca.FLOAT32, ca.SUM, comm, 4, 4) == 0
+        ok &= np.array_equal(hout, po.allreduce_radix_batch([po.fill(big, "f32", 0, 3, r) for r in range(world)],
+                                                            4, 4, "f32", "sum")[rank])
+        ok &= graph_call(4)  # re-captured against the new scratch
+        # profiled device call, larger still: graphs are bypassed while profiling
+        huge = 1 << 23
+        dx = torch.from_numpy(po.fill(huge, "f32", 0, 5, rank).view(np.uint8).copy()).to(dev)
+        dout = torch.empty_like(dx)
+        comm.profile(True)
+        ok &= ca.all_reduce_radix_batch(dx, dout, huge, ca.FLOAT32, ca.SUM, comm, 4, 4) == 0
+        comm.profile_read()
+        comm.profile(False)
+        ok &= graph_call(6)
+        ok &= graph_call(7)
+        dist.barrier()
+    finally:
+        comm.set_graphs(False)
+        comm.destroy()
+        dist.destroy_process_group()
+    q.put((rank, bool(ok)))
+
+
+def test_rccl_graph_cache_survives_scratch_growth_world4():
+    res = _spawn(_graph_scratch_worker, 4)
+    assert all(ok for _, ok in res), res
+
+
+def _timeout_worker(rank, world, port, q):
+    """One rank returns early (never enters the collective); the others must get an error code
+    within their timeout instead of hanging, and their communicators must report aborted."""
+    _setup(rank)
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    import chiara_amd as ca
+
+    comm = _init_worker(rank, world, port)
+    dev = torch.device("cuda:0")
+    res = None
+    try:
+        # warm the connections with one good call
+        x = torch.ones(1 << 16, dtype=torch.float32, device=dev)
+        y = torch.zeros_like(x)
+        assert ca.all_reduce_radix_batch(x, y, x.numel(), ca.FLOAT32, ca.SUM, comm, 4, 4) == 0
+        assert float(y[5].item()) == world
+        comm.set_timeout(5000)
+        if rank == world - 1:
+            dist.barrier()  # waits until the others have given up
+            comm.abort()    # it bailed out: release its side without blocking
+            res = (rank, 0, 0.0, comm.aborted, ca.all_reduce_radix_batch(x, y, x.numel(), ca.FLOAT32, ca.SUM, comm,
+                                                                         4, 4))
+        else:
+            t0 = time.perf_counter()
+            rc = ca.all_reduce_radix_batch(x, y, x.numel(), ca.FLOAT32, ca.SUM, comm, 4, 4)
+            el = time.perf_counter() - t0
+            again = ca.all_reduce_radix_batch(x, y, x.numel(), ca.FLOAT32, ca.SUM, comm, 4, 4)
+            res = (rank, rc, el, comm.aborted, again)
+            dist.barrier()
+    finally:
+        comm.destroy()
+        dist.destroy_process_group()
+    q.put(res)
+
+
+def test_rccl_lost_peer_times_out_world4():
+    import chiara_amd as ca
+
+    res = sorted(_spawn(_timeout_worker, 4, timeout=240))
+    for rank, rc, el, aborted, again in res[:-1]:
+        assert rc in (ca.ERR_TIMEOUT, ca.ERR_RCCL), (rank, rc)
+        assert 4.0 <= el <= 60.0, (rank, el)
+        assert aborted and again == ca.ERR_ABORTED, (rank, aborted, again)
+    assert res[-1][3] and res[-1][4] == ca.ERR_ABORTED
+
+
+def _fullsize_worker(rank, world, port, q, dtype):
+    """C4 (fp32) / C5 (bf16) at full size over RCCL: 8 processes, k=4, b=4, 1 GiB per rank, default
+    (FLAT) schedule, automatic 8-slice pipeline, compute/transfer overlap on two HIP streams."""
+    _setup(rank)
+    import hashlib
+
+    import torch
+    import torch.distributed as dist
+
+    import chiara_amd as ca
+    import fullsize_util as fs
+    import pyoracle as po
+
+    comm = _init_worker(rank, world, port)
+    dev = torch.device("cuda:0")
+    seed = 0xC41A5EED
+    es = 4 if dtype == "f32" else 2
+    cdt = ca.FLOAT32 if dtype == "f32" else ca.BFLOAT16
+    count = (1 << 30) // es
+    out = None
+    try:
+        comm.set_schedule(ca.SCHEDULE_FLAT)
+        comm.set_slices(0)
+        comm.set_overlap(True)
+        send = torch.empty(count * es, dtype=torch.uint8, device=dev)
+        recv = torch.empty(count * es, dtype=torch.uint8, device=dev)
+        assert ca.fill(send, count, cdt, 0, seed, rank, count, torch.cuda.current_stream(dev)) == 0
+        torch.cuda.synchronize()
+        rc = ca.all_reduce_radix_batch(send, recv, count, cdt, ca.SUM, comm, 4, 4)
+        del send
+        host = recv.cpu().numpy()
+        digest = hashlib.sha256(host.tobytes()).hexdigest()
+        hashes = [None] * world
+        dist.all_gather_object(hashes, digest)
+        bad = None
+        if rank == 0:  # every rank holds the same bytes (hashes); rank 0 checks them all vs the oracle
+            npdt = po.NP_DTYPES[dtype]
+            view = host.view(npdt).reshape(world, count // world)
+
+            def out_window(r, off, w):
+                return view[:, off:off + w].ravel()
+            bad = fs.check_allreduce(out_window, world, 4, 4, dtype, count, seed, ranks=[0])
+        dist.barrier()
+        out = (rank, rc, len(set(hashes)) == 1, bad)
+    finally:
+        comm.destroy()
+        dist.destroy_process_group()
+    q.put(out)
+
+
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_rccl_c4_c5_full_size_bit_exact_world8(dtype):
+    res = sorted(_spawn(_fullsize_worker, 8, extra=(dtype,), timeout=900))
+    assert all(rc == 0 for _, rc, _, _ in res), res
+    assert all(same for _, _, same, _ in res), "ranks disagree"
+    assert res[0][3] == [], f"mismatches vs the oracle: {res[0][3][:5]}"

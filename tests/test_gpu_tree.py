@@ -14,8 +14,10 @@ from tree_util import random_program, tree_ref
 
 pytestmark = pytest.mark.gpu
 
-DT = {"f32": ca.FLOAT32, "f64": ca.FLOAT64, "i32": ca.INT32, "bf16": ca.BFLOAT16}
-OP = {"sum": ca.SUM, "prod": ca.PROD, "max": ca.MAX, "min": ca.MIN}
+DT = {"f32": ca.FLOAT32, "f64": ca.FLOAT64, "i32": ca.INT32, "bf16": ca.BFLOAT16, "i8": ca.INT8, "u8": ca.UINT8,
+      "i16": ca.INT16, "u16": ca.UINT16, "u32": ca.UINT32, "i64": ca.INT64, "u64": ca.UINT64}
+OP = {"sum": ca.SUM, "prod": ca.PROD, "max": ca.MAX, "min": ca.MIN, "land": ca.LAND, "lor": ca.LOR,
+      "lxor": ca.LXOR, "band": ca.BAND, "bor": ca.BOR, "bxor": ca.BXOR}
 
 
 @pytest.fixture(scope="module")
@@ -26,7 +28,7 @@ def gu():
 
 
 def _bits(a):
-    return a.view({2: np.uint16, 4: np.uint32, 8: np.uint64}[a.itemsize])
+    return a.view({1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[a.itemsize])
 
 
 def _run(gu, dtype, op, comb, swaps, n, pattern=0, off=0, seed=11, inplace_leaf=None):
@@ -97,3 +99,17 @@ def test_out_aliases_leaf(gu):
 def test_large_nt_path(gu):
     """>= 128 MiB streamed per call takes the non-temporal instantiation."""
     _run(gu, "f32", "sum", *C4_TREE, (16 << 20) + 7)
+
+
+@pytest.mark.parametrize("dtype", ["i8", "u8", "i16", "u16", "i32", "u32", "i64", "u64"])
+@pytest.mark.parametrize("op", ["sum", "prod", "max", "min", "land", "lor", "lxor", "band", "bor", "bxor"])
+def test_integer_types_and_logical_bitwise_ops(gu, dtype, op):
+    """The whole-tree kernel on every MPI integer type and op the reference's generic
+    MPI_Datatype x MPI_Op admits (reduce_tree_int.hip), C4's tree and a depth-4 one, plus a
+    misaligned (scalar) pass."""
+    pat = {"land": po.PAT_SPARSE, "lor": po.PAT_TIES, "lxor": po.PAT_TIES}.get(op, po.PAT_UNIFORM)
+    if op == "prod" and dtype == "i32":
+        return  # int32 arithmetic is the core instantiation, covered above
+    for prog in (C4_TREE, K2B8_TREE):
+        _run(gu, dtype, op, prog[0], prog[1], 30011, pattern=pat)
+    _run(gu, dtype, op, *K4B8_TREE, 1001, pattern=pat, off=1)
