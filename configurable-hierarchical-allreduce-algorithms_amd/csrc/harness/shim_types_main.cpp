@@ -1,0 +1,170 @@
+// shim_types_main.cpp -- the reference-signature binding (csrc/shim/chiara_mpi_shim.cpp) over MPI's
+// predefined datatype x op table.
+//
+//   mpiexec -n 4 bin/chiara_shim_types
+//
+// The reference is generic over MPI_Datatype and MPI_Op (all_reduce_radix_batch.cpp:202-204, sizes
+// from MPI_Type_size at :234-277; reduce_scatter_radix_batch.cpp:200-202; allreduce_ring.cpp:3).
+// For every (type, op) pair this calls the shim's all_reduce_radix_batch, reduce_scatter_radix_batch
+// and MPICH_Allreduce_ring with the reference's own C++ signatures and compares with the MPI
+// library's MPI_Allreduce / MPI_Reduce_scatter_block on the same inputs.  The expectation comes from
+// MPICH itself: a pair MPICH's MPI_Reduce_local accepts must succeed through the shim with the
+// library's result (exact: integer data, and floats holding small integers, so every association
+// rounds the same); a pair it rejects must come back as an MPI error class, as must user ops,
+// MPI_MAXLOC/MINLOC and non-contiguous types.  Prints one JSON line; exit status 0 = all agree.
+#include <mpi.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+int all_reduce_radix_batch(char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
+                           int k, int b);
+int reduce_scatter_radix_batch(const void* sendbuf, void* recvbuf, MPI_Aint recvcount, MPI_Datatype datatype,
+                               MPI_Op op, MPI_Comm comm, int k, int b);
+int MPICH_Allreduce_ring(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+                         MPI_Comm comm);
+int allgather_radix_batch(char* sendbuf, int sendcount, MPI_Datatype datatype, char* recvbuf, MPI_Comm comm, int k,
+                          int b);
+
+namespace {
+
+uint64_t mix(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+struct TypeCase {
+    MPI_Datatype t;
+    const char* name;
+    int kind;  // 0 integer (random bits), 1 float, 2 double, 3 bool (0/1)
+};
+
+void fill(std::vector<char>& buf, int n, const TypeCase& tc, int tsize, int rank, int salt) {
+    buf.assign((size_t)n * tsize, 0);
+    for (int i = 0; i < n; ++i) {
+        const uint64_t u = mix(((uint64_t)rank << 40) ^ ((uint64_t)salt << 20) ^ (uint64_t)i);
+        char* p = buf.data() + (size_t)i * tsize;
+        if (tc.kind == 1) {  // small integers in [-3, 4], zeros included: every sum/product is exact
+            const float f = (float)((int)(u % 8) - 3);
+            std::memcpy(p, &f, 4);
+        } else if (tc.kind == 2) {
+            const double d = (double)((int)(u % 8) - 3);
+            std::memcpy(p, &d, 8);
+        } else if (tc.kind == 3) {
+            p[0] = (char)((u >> 7) & 1);
+        } else if ((u >> 61) == 0) {  // 1/8 zeros so the logical ops see both truth values
+            std::memset(p, 0, tsize);
+        } else {
+            std::memcpy(p, &u, tsize);
+        }
+    }
+}
+
+void user_op(void*, void*, int*, MPI_Datatype*) {}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    MPI_Init(&argc, &argv);
+    MPI_Comm_set_errhandler(MPI_COMM_WORLD, MPI_ERRORS_RETURN);
+    int rank, n;
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    MPI_Comm_size(MPI_COMM_WORLD, &n);
+    const TypeCase types[] = {
+        {MPI_CHAR, "MPI_CHAR", 0}, {MPI_SIGNED_CHAR, "MPI_SIGNED_CHAR", 0},
+        {MPI_UNSIGNED_CHAR, "MPI_UNSIGNED_CHAR", 0}, {MPI_SHORT, "MPI_SHORT", 0},
+        {MPI_UNSIGNED_SHORT, "MPI_UNSIGNED_SHORT", 0}, {MPI_INT, "MPI_INT", 0}, {MPI_UNSIGNED, "MPI_UNSIGNED", 0},
+        {MPI_LONG, "MPI_LONG", 0}, {MPI_UNSIGNED_LONG, "MPI_UNSIGNED_LONG", 0}, {MPI_LONG_LONG, "MPI_LONG_LONG", 0},
+        {MPI_UNSIGNED_LONG_LONG, "MPI_UNSIGNED_LONG_LONG", 0}, {MPI_INT8_T, "MPI_INT8_T", 0},
+        {MPI_UINT8_T, "MPI_UINT8_T", 0}, {MPI_INT16_T, "MPI_INT16_T", 0}, {MPI_UINT16_T, "MPI_UINT16_T", 0},
+        {MPI_INT32_T, "MPI_INT32_T", 0}, {MPI_UINT32_T, "MPI_UINT32_T", 0}, {MPI_INT64_T, "MPI_INT64_T", 0},
+        {MPI_UINT64_T, "MPI_UINT64_T", 0}, {MPI_FLOAT, "MPI_FLOAT", 1}, {MPI_DOUBLE, "MPI_DOUBLE", 2},
+        {MPI_BYTE, "MPI_BYTE", 0}, {MPI_C_BOOL, "MPI_C_BOOL", 3}};
+    const struct {
+        MPI_Op op;
+        const char* name;
+    } ops[] = {{MPI_SUM, "SUM"},   {MPI_PROD, "PROD"}, {MPI_MAX, "MAX"},   {MPI_MIN, "MIN"},  {MPI_LAND, "LAND"},
+               {MPI_LOR, "LOR"},   {MPI_LXOR, "LXOR"}, {MPI_BAND, "BAND"}, {MPI_BOR, "BOR"},  {MPI_BXOR, "BXOR"}};
+    const int per = 37, count = per * n;
+    int pairs = 0, supported = 0, bad = 0;
+    std::string failures;
+    auto fail = [&](const std::string& what) {
+        ++bad;
+        if (failures.size() < 600) failures += (failures.empty() ? "" : "; ") + what;
+    };
+    int salt = 0;
+    for (const TypeCase& tc : types) {
+        int tsize = 0;
+        MPI_Type_size(tc.t, &tsize);
+        for (const auto& o : ops) {
+            ++pairs;
+            ++salt;
+            const std::string id = std::string(tc.name) + "/" + o.name;
+            std::vector<char> probe_in(2 * (size_t)tsize, 0), probe_io(2 * (size_t)tsize, 0);
+            const bool mpich_ok = MPI_Reduce_local(probe_in.data(), probe_io.data(), 1, tc.t, o.op) == MPI_SUCCESS;
+            std::vector<char> send, recv((size_t)count * tsize), lib((size_t)count * tsize);
+            fill(send, count, tc, tsize, rank, salt);
+            // allreduce (k=2, b=2: a two-level geometry at 4 ranks) vs MPI_Allreduce
+            const int rc = all_reduce_radix_batch(send.data(), recv.data(), count, tc.t, o.op, MPI_COMM_WORLD, 2,
+                                                  n % 2 ? 1 : 2);
+            if (!mpich_ok) {
+                if (rc == MPI_SUCCESS) fail(id + " accepted, MPICH rejects it");
+                continue;
+            }
+            ++supported;
+            MPI_Allreduce(send.data(), lib.data(), count, tc.t, o.op, MPI_COMM_WORLD);
+            if (rc != MPI_SUCCESS) fail(id + " allreduce rc=" + std::to_string(rc));
+            else if (recv != lib) fail(id + " allreduce differs from MPI_Allreduce");
+            // reduce-scatter (block) vs MPI_Reduce_scatter_block
+            std::vector<char> rs((size_t)per * tsize), rs_lib((size_t)per * tsize);
+            const int rc2 = reduce_scatter_radix_batch(send.data(), rs.data(), per, tc.t, o.op, MPI_COMM_WORLD, 2, 1);
+            MPI_Reduce_scatter_block(send.data(), rs_lib.data(), per, tc.t, o.op, MPI_COMM_WORLD);
+            if (rc2 != MPI_SUCCESS || rs != rs_lib) fail(id + " reduce_scatter rc=" + std::to_string(rc2));
+            // an MPICH baseline testing/main.cpp drives (ring, reduction at allreduce_ring.cpp:80)
+            std::vector<char> ring((size_t)count * tsize);
+            const int rc3 = MPICH_Allreduce_ring(send.data(), ring.data(), count, tc.t, o.op, MPI_COMM_WORLD);
+            if (rc3 != MPI_SUCCESS || ring != lib) fail(id + " ring rc=" + std::to_string(rc3));
+        }
+    }
+    // what the shim must refuse with an MPI error class
+    {
+        std::vector<char> a(64 * n * 16, 1), r(64 * n * 16, 0);
+        MPI_Op uop;
+        MPI_Op_create(user_op, 1, &uop);
+        if (all_reduce_radix_batch(a.data(), r.data(), 4 * n, MPI_INT, uop, MPI_COMM_WORLD, 2, 1) == MPI_SUCCESS)
+            fail("user op accepted");
+        MPI_Op_free(&uop);
+        if (all_reduce_radix_batch(a.data(), r.data(), 4 * n, MPI_2INT, MPI_MAXLOC, MPI_COMM_WORLD, 2, 1) == MPI_SUCCESS)
+            fail("MPI_MAXLOC accepted");
+        if (all_reduce_radix_batch(a.data(), r.data(), 4 * n, MPI_LONG_DOUBLE, MPI_SUM, MPI_COMM_WORLD, 2, 1) ==
+            MPI_SUCCESS)
+            fail("MPI_LONG_DOUBLE accepted");
+        if (allgather_radix_batch(a.data(), 4, MPI_DOUBLE_INT, r.data(), MPI_COMM_WORLD, 2, 1) == MPI_SUCCESS)
+            fail("non-contiguous allgather type accepted");
+    }
+    // allgather moves any contiguous type as bytes (the reference sizes it with MPI_Type_size)
+    {
+        MPI_Datatype tri;
+        MPI_Type_contiguous(3, MPI_SHORT, &tri);
+        MPI_Type_commit(&tri);
+        const int sc = 11;
+        std::vector<char> s((size_t)sc * 6), g((size_t)sc * 6 * n), lib((size_t)sc * 6 * n);
+        for (size_t i = 0; i < s.size(); ++i) s[i] = (char)mix(((uint64_t)rank << 32) ^ i);
+        const int rc = allgather_radix_batch(s.data(), sc, tri, g.data(), MPI_COMM_WORLD, 2, 1);
+        MPI_Allgather(s.data(), sc, tri, lib.data(), sc, tri, MPI_COMM_WORLD);
+        if (rc != MPI_SUCCESS || g != lib) fail("allgather of a contiguous derived type");
+        MPI_Type_free(&tri);
+    }
+    int all_bad = 0;
+    MPI_Allreduce(&bad, &all_bad, 1, MPI_INT, MPI_SUM, MPI_COMM_WORLD);
+    if (rank == 0)
+        std::printf("{\"pairs\": %d, \"supported_by_mpich\": %d, \"failures\": %d, \"first\": \"%s\"}\n", pairs,
+                    supported, all_bad, failures.c_str());
+    MPI_Finalize();
+    return all_bad ? 1 : 0;
+}

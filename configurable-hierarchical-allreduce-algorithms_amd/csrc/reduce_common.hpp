@@ -83,12 +83,17 @@ __device__ __forceinline__ typename DTy<DT>::T apply(typename DTy<DT>::T x, type
         else if constexpr (OP == CHR_BOR) return (T)(y | x);
         else return (T)(y ^ x);
     } else {
+        using T = typename DTy<DT>::T;
         if constexpr (OP == CHR_SUM) return y + x;
         else if constexpr (OP == CHR_PROD) return y * x;
         else if constexpr (OP == CHR_MAX) return y > x ? y : x;
         else if constexpr (OP == CHR_MIN) return y < x ? y : x;
         else if constexpr (OP == kMaxSw) return x > y ? x : y;
-        else return x < y ? x : y;
+        else if constexpr (OP == kMinSw) return x < y ? x : y;
+        // MPICH also accepts the logical ops on float/double (C truth: NaN true, -0 false)
+        else if constexpr (OP == CHR_LAND) return (T)((y != 0) && (x != 0));
+        else if constexpr (OP == CHR_LOR) return (T)((y != 0) || (x != 0));
+        else return (T)((y != 0) != (x != 0));
     }
 }
 

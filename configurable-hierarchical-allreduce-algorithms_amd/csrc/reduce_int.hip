@@ -1,7 +1,8 @@
 // reduce_int.hip -- the fused bucket reduction for the MPI integer types beyond int32
-// arithmetic: (u)int8/16/64 and uint32, and the logical (LAND/LOR/LXOR) and bitwise
-// (BAND/BOR/BXOR) ops on every integer type.  The reference is generic over MPI_Datatype and
-// MPI_Op (all_reduce_radix_batch.cpp:202-204, MPI_Type_size at :234-277); its arithmetic is
+// arithmetic: (u)int8/16/64 and uint32, the logical (LAND/LOR/LXOR) and bitwise (BAND/BOR/BXOR)
+// ops on every integer type, and the logical ops on float/double (MPICH accepts them).  The
+// reference is generic over MPI_Datatype and MPI_Op (all_reduce_radix_batch.cpp:202-204,
+// MPI_Type_size at :234-277); its arithmetic is
 // MPICH's MPI_Reduce_local loop for the pair.  Same kernels as reduce_kernels.hip (reduce_vec.hpp),
 // compiled here in the two policy shapes only, so this translation unit builds in parallel with
 // the floating-point one.  Kernel types come from canon_op: signedness only matters to MAX/MIN,
@@ -48,8 +49,18 @@ static hipError_t vec_i32_logic(const VecArgs& a, int op, int m, hipStream_t s) 
     }
 }
 
+template <int DT>
+static hipError_t vec_logic(const VecArgs& a, int op, int m, hipStream_t s) {
+    if (op == CHR_LAND) return launch_vec_op<DT, CHR_LAND, false>(a, m, s);
+    if (op == CHR_LOR) return launch_vec_op<DT, CHR_LOR, false>(a, m, s);
+    if (op == CHR_LXOR) return launch_vec_op<DT, CHR_LXOR, false>(a, m, s);
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_vec_int(const VecArgs& a, int kdt, int kop, int m, hipStream_t s) {
     switch (kdt) {
+    case CHR_FLOAT32: return vec_logic<CHR_FLOAT32>(a, kop, m, s);  // MPICH's logical ops on floats
+    case CHR_FLOAT64: return vec_logic<CHR_FLOAT64>(a, kop, m, s);
     case CHR_UINT8: return vec_all_ops<CHR_UINT8>(a, kop, m, s);
     case CHR_UINT16: return vec_all_ops<CHR_UINT16>(a, kop, m, s);
     case CHR_UINT64: return vec_all_ops<CHR_UINT64>(a, kop, m, s);
@@ -86,8 +97,18 @@ static hipError_t scalar_minmax(const ScalarArgs& a, int op, hipStream_t s) {
     return hipErrorInvalidValue;
 }
 
+template <int DT>
+static hipError_t scalar_logic(const ScalarArgs& a, int op, hipStream_t s) {
+    if (op == CHR_LAND) return launch_scalar_op<DT, CHR_LAND>(a, s);
+    if (op == CHR_LOR) return launch_scalar_op<DT, CHR_LOR>(a, s);
+    if (op == CHR_LXOR) return launch_scalar_op<DT, CHR_LXOR>(a, s);
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_scalar_int(const ScalarArgs& a, int kdt, int kop, hipStream_t s) {
     switch (kdt) {
+    case CHR_FLOAT32: return scalar_logic<CHR_FLOAT32>(a, kop, s);
+    case CHR_FLOAT64: return scalar_logic<CHR_FLOAT64>(a, kop, s);
     case CHR_UINT8: return scalar_all_ops<CHR_UINT8>(a, kop, s);
     case CHR_UINT16: return scalar_all_ops<CHR_UINT16>(a, kop, s);
     case CHR_UINT64: return scalar_all_ops<CHR_UINT64>(a, kop, s);

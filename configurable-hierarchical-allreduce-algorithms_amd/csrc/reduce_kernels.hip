@@ -52,12 +52,15 @@ static bool is_float_dtype(int dtype) {
     return dtype == CHR_FLOAT32 || dtype == CHR_FLOAT64 || dtype == CHR_BFLOAT16;
 }
 
-// MPI's predefined-op/type table as MPICH's MPI_Reduce_local applies it: SUM/PROD/MAX/MIN on
-// every type, the logical and bitwise ops on the integer types only.
+// MPI's predefined-op/type table as MPICH 3.3.2's MPI_Reduce_local applies it (probed): SUM/PROD/
+// MAX/MIN on every type, the logical ops on the integer types and on float/double (an MPICH
+// extension of the standard's table), the bitwise ops on the integer types.  bf16 is this
+// library's own type: arithmetic and MAX/MIN only.
 bool valid_dtype_op(int dtype, int op) {
     if (!dtype_size(dtype)) return false;
     if (op >= CHR_SUM && op <= CHR_MIN) return true;
-    return op >= CHR_LAND && op <= CHR_BXOR && !is_float_dtype(dtype);
+    if (op >= CHR_LAND && op <= CHR_LXOR) return dtype != CHR_BFLOAT16;
+    return op >= CHR_BAND && op <= CHR_BXOR && !is_float_dtype(dtype);
 }
 
 // The kernel instantiation that computes (dtype, op).  Signedness only matters to MAX/MIN:
@@ -85,7 +88,7 @@ void canon_op(int dtype, int op, bool running_first, int* kdt, int* kop) {
 
 // kernel types compiled in this translation unit (all tuning variants); the rest: reduce_int.hip
 static bool in_core_tu(int kdt, int kop) {
-    return is_float_dtype(kdt) || (kdt == CHR_INT32 && kop >= CHR_SUM && kop <= CHR_MIN);
+    return (is_float_dtype(kdt) || kdt == CHR_INT32) && ((kop >= CHR_SUM && kop <= CHR_MIN) || kop >= kMaxSw);
 }
 
 ReduceTuning& reduce_tuning() {

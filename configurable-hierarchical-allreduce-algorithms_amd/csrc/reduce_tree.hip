@@ -18,8 +18,8 @@ static hipError_t launch_tree_dt(const TreeArgs& a, const TreeScalarArgs* sa, in
 
 // dtype, op: the kernel type and op (canon_op)
 static hipError_t launch_tree_any(const TreeArgs& a, const TreeScalarArgs* sa, int dtype, int op, hipStream_t s) {
-    const bool core = dtype == CHR_FLOAT32 || dtype == CHR_FLOAT64 || dtype == CHR_BFLOAT16 ||
-                      (dtype == CHR_INT32 && op <= CHR_MIN);
+    const bool core = (dtype == CHR_FLOAT32 || dtype == CHR_FLOAT64 || dtype == CHR_BFLOAT16 || dtype == CHR_INT32) &&
+                      op <= CHR_MIN;
     if (!core) return launch_tree_int(a, sa, dtype, op, s);
     switch (dtype) {
     case CHR_FLOAT32: return launch_tree_dt<CHR_FLOAT32>(a, sa, op, s);

@@ -44,8 +44,18 @@ static hipError_t tree_i32_logic(const TreeArgs& a, const TreeScalarArgs* sa, in
     }
 }
 
+template <int DT>
+static hipError_t tree_logic(const TreeArgs& a, const TreeScalarArgs* sa, int op, hipStream_t s) {
+    if (op == CHR_LAND) return launch_tree_op<DT, CHR_LAND, false>(a, sa, s);
+    if (op == CHR_LOR) return launch_tree_op<DT, CHR_LOR, false>(a, sa, s);
+    if (op == CHR_LXOR) return launch_tree_op<DT, CHR_LXOR, false>(a, sa, s);
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_tree_int(const TreeArgs& a, const TreeScalarArgs* sa, int kdt, int kop, hipStream_t s) {
     switch (kdt) {
+    case CHR_FLOAT32: return tree_logic<CHR_FLOAT32>(a, sa, kop, s);  // MPICH's logical ops on floats
+    case CHR_FLOAT64: return tree_logic<CHR_FLOAT64>(a, sa, kop, s);
     case CHR_UINT8: return tree_all_ops<CHR_UINT8>(a, sa, kop, s);
     case CHR_UINT16: return tree_all_ops<CHR_UINT16>(a, sa, kop, s);
     case CHR_UINT64: return tree_all_ops<CHR_UINT64>(a, sa, kop, s);

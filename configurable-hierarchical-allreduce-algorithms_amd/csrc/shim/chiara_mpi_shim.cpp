@@ -59,28 +59,64 @@ chr_comm* comm_for(MPI_Comm mc) {
     return c;
 }
 
+// MPI predefined types -> element types.  The reference is generic over MPI_Datatype (sizes from
+// MPI_Type_size, all_reduce_radix_batch.cpp:234-277); its arithmetic is MPICH's predefined-op loop
+// for the pair.  C integer types map by size and signedness (MPI_LONG is 64-bit on this LP64
+// platform); MPI_CHAR reduces as a signed char, as in MPICH.  MPI_BYTE takes the bitwise ops and
+// MPI_C_BOOL the logical ones (checked in valid_pair).  Everything else -- MPI_LONG_DOUBLE,
+// complex, pair types for MAXLOC/MINLOC, derived types -- is MPI_ERR_TYPE.
 bool map_type(MPI_Datatype d, chr_dtype* out) {
     if (d == MPI_FLOAT) *out = CHR_FLOAT32;
     else if (d == MPI_DOUBLE) *out = CHR_FLOAT64;
-    else if (d == MPI_INT) *out = CHR_INT32;
+    else if (d == MPI_INT || d == MPI_INT32_T) *out = CHR_INT32;
+    else if (d == MPI_UNSIGNED || d == MPI_UINT32_T) *out = CHR_UINT32;
+    else if (d == MPI_SIGNED_CHAR || d == MPI_INT8_T || d == MPI_CHAR) *out = CHR_INT8;
+    else if (d == MPI_UNSIGNED_CHAR || d == MPI_UINT8_T || d == MPI_BYTE || d == MPI_C_BOOL) *out = CHR_UINT8;
+    else if (d == MPI_SHORT || d == MPI_INT16_T) *out = CHR_INT16;
+    else if (d == MPI_UNSIGNED_SHORT || d == MPI_UINT16_T) *out = CHR_UINT16;
+    else if (d == MPI_LONG || d == MPI_LONG_LONG || d == MPI_LONG_LONG_INT || d == MPI_INT64_T)
+        *out = sizeof(long) == 8 || d != MPI_LONG ? CHR_INT64 : CHR_INT32;
+    else if (d == MPI_UNSIGNED_LONG || d == MPI_UNSIGNED_LONG_LONG || d == MPI_UINT64_T)
+        *out = sizeof(unsigned long) == 8 || d != MPI_UNSIGNED_LONG ? CHR_UINT64 : CHR_UINT32;
     else return false;
     return true;
 }
 
+// MPI predefined ops.  MPI_MAXLOC/MINLOC, MPI_REPLACE/NO_OP and user ops (MPI_Op_create: a host
+// function pointer the device cannot call) are MPI_ERR_OP.
 bool map_op(MPI_Op o, chr_op* out) {
     if (o == MPI_SUM) *out = CHR_SUM;
     else if (o == MPI_PROD) *out = CHR_PROD;
     else if (o == MPI_MAX) *out = CHR_MAX;
     else if (o == MPI_MIN) *out = CHR_MIN;
+    else if (o == MPI_LAND) *out = CHR_LAND;
+    else if (o == MPI_LOR) *out = CHR_LOR;
+    else if (o == MPI_LXOR) *out = CHR_LXOR;
+    else if (o == MPI_BAND) *out = CHR_BAND;
+    else if (o == MPI_BOR) *out = CHR_BOR;
+    else if (o == MPI_BXOR) *out = CHR_BXOR;
     else return false;
     return true;
+}
+
+// MPI's op/type table (MPI-3.1 §5.9.2): MPI_BYTE only with the bitwise ops, MPI_C_BOOL only with
+// the logical ops, floating types not with either; 0 or the MPI error class to return.
+int map_pair(MPI_Datatype d, MPI_Op o, chr_dtype* dt, chr_op* op) {
+    if (!map_type(d, dt)) return MPI_ERR_TYPE;
+    if (!map_op(o, op)) return MPI_ERR_OP;
+    const bool bitwise = *op == CHR_BAND || *op == CHR_BOR || *op == CHR_BXOR;
+    const bool logical = *op == CHR_LAND || *op == CHR_LOR || *op == CHR_LXOR;
+    if (d == MPI_BYTE && !bitwise) return MPI_ERR_OP;
+    if (d == MPI_C_BOOL && !logical) return MPI_ERR_OP;
+    if ((*dt == CHR_FLOAT32 || *dt == CHR_FLOAT64) && (bitwise || logical)) return MPI_ERR_OP;
+    return 0;
 }
 
 int to_mpi(int rc) {
     if (rc == CHR_SUCCESS) return MPI_SUCCESS;
     if (rc == CHR_ERR_COUNT_NOT_DIVISIBLE) return MPI_ERR_COUNT;
     if (rc == CHR_ERR_BATCH_NOT_DIVISOR || rc == CHR_ERR_INVALID_ARG) return MPI_ERR_ARG;
-    return MPI_ERR_OTHER;
+    return MPI_ERR_OTHER;  // HIP / RCCL errors, timeouts and aborted communicators
 }
 
 }  // namespace
@@ -89,8 +125,7 @@ int all_reduce_radix_batch(char* sendbuf, char* recvbuf, int count, MPI_Datatype
                            MPI_Comm comm, int k, int b) {
     chr_dtype dt;
     chr_op o;
-    if (!map_type(datatype, &dt)) return MPI_ERR_TYPE;
-    if (!map_op(op, &o)) return MPI_ERR_OP;
+    if (int err = map_pair(datatype, op, &dt, &o)) return err;
     chr_comm* c = comm_for(comm);
     if (!c) return MPI_ERR_OTHER;
     const void* send = sendbuf == (char*)MPI_IN_PLACE ? CHR_IN_PLACE : (const void*)sendbuf;
@@ -101,8 +136,7 @@ int reduce_scatter_radix_batch(const void* sendbuf, void* recvbuf, MPI_Aint recv
                                MPI_Op op, MPI_Comm comm, int k, int b) {
     chr_dtype dt;
     chr_op o;
-    if (!map_type(datatype, &dt)) return MPI_ERR_TYPE;
-    if (!map_op(op, &o)) return MPI_ERR_OP;
+    if (int err = map_pair(datatype, op, &dt, &o)) return err;
     chr_comm* c = comm_for(comm);
     if (!c) return MPI_ERR_OTHER;
     const void* send = sendbuf == MPI_IN_PLACE ? CHR_IN_PLACE : sendbuf;
@@ -115,8 +149,7 @@ int mpich_call(chr_mode algo, const char* sendbuf, char* recvbuf, int count, MPI
                MPI_Comm comm, int k, int single_phase_recv) {
     chr_dtype dt;
     chr_op o;
-    if (!map_type(datatype, &dt)) return MPI_ERR_TYPE;
-    if (!map_op(op, &o)) return MPI_ERR_OP;
+    if (int err = map_pair(datatype, op, &dt, &o)) return err;
     if (count < 0) return MPI_ERR_COUNT;
     chr_comm* c = comm_for(comm);
     if (!c) return MPI_ERR_OTHER;
@@ -156,13 +189,18 @@ int MPICH_Allreduce_recursive_multiplying(const char* sendbuf, char* recvbuf, in
     return mpich_call(CHR_MODE_MPICH_RMULT, sendbuf, recvbuf, count, datatype, op, comm, k, 0);
 }
 
+// Pure data movement: any datatype the reference accepts (all_gather_radix_batch_1_0.cpp:37 sizes
+// it with MPI_Type_size), moved as bytes; contiguous layouts only (MPI_Type_size == extent).
 int allgather_radix_batch(char* sendbuf, int sendcount, MPI_Datatype datatype, char* recvbuf, MPI_Comm comm, int k,
                           int b) {
-    chr_dtype dt;
-    if (!map_type(datatype, &dt)) return MPI_ERR_TYPE;
     if (sendcount < 0) return MPI_ERR_COUNT;
+    int tsize = 0;
+    MPI_Aint lb = 0, extent = 0;
+    if (MPI_Type_size(datatype, &tsize) != MPI_SUCCESS || MPI_Type_get_extent(datatype, &lb, &extent) != MPI_SUCCESS ||
+        tsize <= 0 || lb != 0 || extent != tsize)
+        return MPI_ERR_TYPE;
     chr_comm* c = comm_for(comm);
     if (!c) return MPI_ERR_OTHER;
     const void* send = sendbuf == (char*)MPI_IN_PLACE ? CHR_IN_PLACE : (const void*)sendbuf;
-    return to_mpi(chr_allgather_radix_batch(send, (size_t)sendcount, dt, recvbuf, c, k, b));
+    return to_mpi(chr_allgather_radix_batch(send, (size_t)sendcount * (size_t)tsize, CHR_UINT8, recvbuf, c, k, b));
 }

@@ -43,8 +43,9 @@ typedef enum {
 } chr_dtype;
 
 /* Reduction ops: MPI's predefined ops with MPICH 3.3.2's element semantics
- * (inout[i] = inout[i] OP in[i]).  SUM/PROD/MAX/MIN on every type; the logical (result 0 or 1)
- * and bitwise ops on the integer types only.  MPI_MAXLOC/MINLOC and user ops (MPI_Op_create)
+ * (inout[i] = inout[i] OP in[i]).  SUM/PROD/MAX/MIN on every type; the logical ops (result 0 or
+ * 1) on the integer types and on float/double (MPICH accepts those; C truth: NaN is true, -0
+ * false); the bitwise ops on the integer types only.  MPI_MAXLOC/MINLOC and user ops (MPI_Op_create)
  * are not supported (CHR_ERR_INVALID_ARG; MPI_ERR_OP through the shim). */
 typedef enum {
     CHR_SUM = 0, CHR_PROD = 1, CHR_MAX = 2, CHR_MIN = 3,

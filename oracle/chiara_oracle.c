@@ -147,17 +147,24 @@ void orc_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int ra
 
 void orc_reduce_local(const void* in, void* inout, size_t n, int dtype, int op) {
     switch (dtype) {
+    /* MPICH 3.3.2 also takes LAND/LOR/LXOR on float and double (probed: rc 0), C truth values. */
     case ORC_F32:
         if (op == ORC_SUM) ORC_LOOP(float, y + x);
         else if (op == ORC_PROD) ORC_LOOP(float, y * x);
         else if (op == ORC_MAX) ORC_LOOP(float, y > x ? y : x);
-        else ORC_LOOP(float, y < x ? y : x);
+        else if (op == ORC_MIN) ORC_LOOP(float, y < x ? y : x);
+        else if (op == ORC_LAND) ORC_LOOP(float, (float)(y && x));
+        else if (op == ORC_LOR) ORC_LOOP(float, (float)(y || x));
+        else if (op == ORC_LXOR) ORC_LOOP(float, (float)(!y != !x));
         break;
     case ORC_F64:
         if (op == ORC_SUM) ORC_LOOP(double, y + x);
         else if (op == ORC_PROD) ORC_LOOP(double, y * x);
         else if (op == ORC_MAX) ORC_LOOP(double, y > x ? y : x);
-        else ORC_LOOP(double, y < x ? y : x);
+        else if (op == ORC_MIN) ORC_LOOP(double, y < x ? y : x);
+        else if (op == ORC_LAND) ORC_LOOP(double, (double)(y && x));
+        else if (op == ORC_LOR) ORC_LOOP(double, (double)(y || x));
+        else if (op == ORC_LXOR) ORC_LOOP(double, (double)(!y != !x));
         break;
     case ORC_I32: ORC_INT_CASE(int32_t, uint32_t, uint32_t) break;
     case ORC_I8: ORC_INT_CASE(int8_t, uint8_t, uint32_t) break;
@@ -311,8 +318,8 @@ static int orc_phases_0_2(orc_state* s, int nranks, int k_in, int b, size_t recv
     memset(s, 0, sizeof(*s));
     if (b < 1 || nranks < 1 || nranks % b != 0 || k_in < 2) return 1;
     s->es = orc_dtype_size(dtype);
-    if (!s->es || op < ORC_SUM || op > ORC_BXOR || (op > ORC_MIN && (dtype == ORC_F32 || dtype == ORC_F64 ||
-                                                                      dtype == ORC_BF16)))
+    if (!s->es || op < ORC_SUM || op > ORC_BXOR || (op > ORC_MIN && dtype == ORC_BF16) ||
+        (op > ORC_LXOR && (dtype == ORC_F32 || dtype == ORC_F64)))
         return 1;
     s->nranks = nranks;
     s->b = b;

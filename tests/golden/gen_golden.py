@@ -160,6 +160,10 @@ TYPE_OPS = {  # MPI's predefined op/type table: arithmetic on every integer type
     "u32": ("sum", "prod", "max", "min", "land", "bxor"),
     "i64": ("sum", "prod", "max", "min", "land", "lor", "lxor", "band", "bor", "bxor"),
     "u64": ("sum", "max", "min", "lor", "band"),
+    # MPICH 3.3.2 accepts the logical ops on float and double too (C truth values; TIES data:
+    # +-0, +-1, 0.5, NaN)
+    "f32": ("land", "lor", "lxor"),
+    "f64": ("land", "lxor"),
 }
 
 
@@ -180,6 +184,8 @@ def types_cases_for(n):
         for op in ops:
             pat = {"land": pyoracle.PAT_SPARSE, "lor": pyoracle.PAT_TIES, "lxor": pyoracle.PAT_TIES}.get(
                 op, pyoracle.PAT_UNIFORM)
+            if dt in ("f32", "f64"):
+                pat = pyoracle.PAT_TIES
             for i, b in enumerate(divisors(n)):
                 k = (2, 3, 4)[i % 3]
                 add("ar", k, b, n * 24 + (n if i % 2 else 0), dt, op, pat, i % 2)

@@ -91,6 +91,16 @@ def test_integer_types_and_logical_bitwise_ops(gu, dtype, op, m):
     _check_multi(gu, dtype, op, m, 777, off=1, in_off=2, pattern=pat)
 
 
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+@pytest.mark.parametrize("op", ["land", "lor", "lxor"])
+@pytest.mark.parametrize("m", [1, 4])
+def test_float_logical_ops(gu, dtype, op, m):
+    """MPICH 3.3.2 accepts LAND/LOR/LXOR on float and double (C truth: NaN true, -0 false): ties
+    data (+-0, +-1, 0.5, NaN payloads)."""
+    _check_multi(gu, dtype, op, m, 30011, pattern=po.PAT_TIES)
+    _check_multi(gu, dtype, op, m, 501, off=1, in_off=1, pattern=po.PAT_TIES)
+
+
 @pytest.mark.parametrize("dtype", ["u8", "i16", "i64", "u64"])
 def test_integer_types_streaming_path(gu, dtype):
     """>= 128 MiB calls switch to the non-temporal one-wave instantiation."""
@@ -99,11 +109,13 @@ def test_integer_types_streaming_path(gu, dtype):
     _check_multi(gu, dtype, "max", 3, n // 2 + 7)
 
 
-def test_float_types_reject_logical_and_bitwise_ops(gu):
+def test_float_types_reject_bitwise_ops(gu):
     x = gu.empty_dev(64)
     for dt in (ca.FLOAT32, ca.FLOAT64, ca.BFLOAT16):
-        for op in (ca.LAND, ca.LOR, ca.LXOR, ca.BAND, ca.BOR, ca.BXOR):
+        for op in (ca.BAND, ca.BOR, ca.BXOR):
             assert ca.reduce_local(x, x, 4, dt, op, gu.stream()) == 1
+    for op in (ca.LAND, ca.LOR, ca.LXOR):  # bf16 is this library's own type: arithmetic and MAX/MIN
+        assert ca.reduce_local(x, x, 4, ca.BFLOAT16, op, gu.stream()) == 1
     assert ca.reduce_local(x, x, 4, 11, ca.SUM, gu.stream()) == 1
     assert ca.reduce_local(x, x, 4, ca.INT8, 10, gu.stream()) == 1
 

@@ -111,3 +111,27 @@ def test_own_harnesses_device_resident(tmp_path, binary, args, n, name, coll):
     assert ours and not bad, bad[:5]
     if "dtype=bf16" not in args or coll == "allgather":  # MPI has no bf16: no baseline rows to plot against
         _plots(tmp_path, coll)
+
+
+def test_shim_over_mpi_datatype_op_table(tmp_path):
+    """The reference-signature binding (csrc/shim) on every MPI predefined datatype x op: pairs MPICH's
+    MPI_Reduce_local accepts give MPI_Allreduce's / MPI_Reduce_scatter_block's result through
+    all_reduce_radix_batch, reduce_scatter_radix_batch and MPICH_Allreduce_ring; pairs it rejects,
+    user ops, MAXLOC and non-contiguous types come back as MPI error classes (shim_types_main.cpp)."""
+    import json
+
+    exe = os.path.join(REPO, *BIN, "chiara_shim_types")
+    if not os.path.exists(exe) or not os.path.exists(MPIEXEC):
+        pytest.skip("shim types binary or MPICH not present")
+    cmd = [MPIEXEC]
+    for r in range(4):
+        if r:
+            cmd.append(":")
+        cmd += ["-n", "1", "-env", "NCCL_HOSTID", f"chiara-shim-types-{r}", "-env", "NCCL_SOCKET_IFNAME", "lo",
+                "-env", "NCCL_IB_DISABLE", "1", exe]
+    out = subprocess.run(cmd, cwd=tmp_path, capture_output=True, text=True, timeout=400)
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert line, out.stdout[-2000:] + out.stderr[-2000:]
+    res = json.loads(line[-1])
+    assert out.returncode == 0 and res["failures"] == 0, res
+    assert res["pairs"] == 230 and res["supported_by_mpich"] >= 150, res

@@ -140,7 +140,7 @@ def test_oracle_matches_reference_on_integer_types_and_logical_bitwise_ops(golde
     the reference equal to MPI's own collective (integer ops are associative)."""
     cases, arrays = golden_types
     assert len(cases) > 1500
-    assert {c["dtype"] for c in cases} == {"i8", "u8", "i16", "u16", "i32", "u32", "i64", "u64"}
+    assert {c["dtype"] for c in cases} == {"i8", "u8", "i16", "u16", "i32", "u32", "i64", "u64", "f32", "f64"}
     assert {c["op"] for c in cases} >= {"sum", "prod", "max", "min", "land", "lor", "lxor", "band", "bor", "bxor"}
     bad = [c["id"] for c in cases
            if hashlib.sha256(b"".join(o.tobytes() for o in _oracle_outputs(c))).hexdigest() != c["sha256"]]
