@@ -353,6 +353,18 @@ def reduce_tree(out, leaves, comb, swaps, count, datatype, op, stream=None):
     return lib().chr_reduce_tree(_addr(out), arr, len(leaves), cb, sb, count, datatype, op, _stream(stream))
 
 
+def reduce_tree_batch(outs, leaves, comb, swaps, count, datatype, op, stream=None):
+    """chr_reduce_tree_batch: len(outs) trees of len(leaves[t]) leaves each (all equal), programs
+    comb[t] / swaps[t] (swaps may be None), batched into as few launches as possible."""
+    nt = len(outs)
+    nl = len(leaves[0]) if nt else 1
+    O = (ctypes.c_void_p * max(1, nt))(*[_addr(x) for x in outs])
+    L = (ctypes.c_void_p * max(1, nt * nl))(*[_addr(x) for lv in leaves for x in lv])
+    cb = bytes(bytearray([c for prog in comb for c in prog]))
+    sb = None if swaps is None else bytes(bytearray([x for prog in swaps for x in prog]))
+    return lib().chr_reduce_tree_batch(O, L, nt, nl, cb, sb, count, datatype, op, _stream(stream))
+
+
 # ---- plan introspection (host only) --------------------------------------------------------------
 
 def describe_plan(mode, nranks, rank, k, b, count, slices=1, schedule=None):

@@ -3,6 +3,7 @@
 
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "chr_internal.hpp"
 #include "schedule.hpp"
@@ -71,6 +72,32 @@ int chr_reduce_tree(void* out, const void* const* leaves, int nleaves, const uns
     for (int j = 0; j < nleaves; ++j)
         if (!leaves[j]) return CHR_ERR_INVALID_ARG;
     return status(chr::launch_reduce_tree(out, leaves, nleaves, comb, swaps, n, dtype, op, stream));
+}
+
+int chr_reduce_tree_batch(void* const* outs, const void* const* leaves, int ntrees, int nleaves,
+                          const unsigned char* comb, const unsigned char* swaps, size_t n, chr_dtype dtype, chr_op op,
+                          hipStream_t stream) {
+    if (!chr::valid_dtype_op(dtype, op) || ntrees < 0 || nleaves < 1 || nleaves > 8) return CHR_ERR_INVALID_ARG;
+    if (ntrees > 0 && (!outs || !leaves || !comb)) return CHR_ERR_INVALID_ARG;
+    std::vector<chr::TreeJob> jobs((size_t)ntrees);
+    for (int t = 0; t < ntrees; ++t) {
+        uint32_t cb = 0, sb = 0;
+        const unsigned char* sw = swaps ? swaps + (size_t)t * (nleaves - 1) : nullptr;
+        if (!chr::tree_program_ok(nleaves, comb + (size_t)t * nleaves, sw, &cb, &sb)) return CHR_ERR_UNSUPPORTED;
+        chr::TreeJob& jb = jobs[t];
+        jb.out = outs[t];
+        jb.nl = nleaves;
+        jb.comb = comb + (size_t)t * nleaves;
+        jb.swaps = sw;
+        jb.n = n;
+        if (n && !jb.out) return CHR_ERR_INVALID_ARG;
+        for (int j = 0; j < nleaves; ++j) {
+            jb.leaves[j] = leaves[(size_t)t * nleaves + j];
+            if (n && !jb.leaves[j]) return CHR_ERR_INVALID_ARG;
+        }
+    }
+    if (n == 0 || ntrees == 0) return CHR_SUCCESS;
+    return status(chr::launch_reduce_tree_multi(jobs.data(), ntrees, dtype, op, stream));
 }
 
 int chr_fill(void* buf, size_t n, chr_dtype dtype, int pattern, uint64_t seed, int rank, uint64_t count_for_seq,

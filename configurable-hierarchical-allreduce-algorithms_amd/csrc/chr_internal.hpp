@@ -29,6 +29,17 @@ hipError_t launch_reduce_tree(void* out, const void* const* leaves, int nl, cons
                               const uint8_t* swaps, size_t n, int dtype, int op, hipStream_t stream);
 bool tree_program_ok(int nl, const uint8_t* comb, const uint8_t* swaps, uint32_t* comb_bits,
                      uint32_t* swap_bits);
+// Several trees, batched: the vector bodies of equal-leaf-count trees share launches (at most 8
+// per launch).  Each job is one chr_reduce_tree call.
+struct TreeJob {
+    void* out;
+    const void* leaves[8];
+    int nl;
+    const uint8_t* comb;
+    const uint8_t* swaps;
+    size_t n;
+};
+hipError_t launch_reduce_tree_multi(const TreeJob* jobs, int njobs, int dtype, int op, hipStream_t stream);
 
 hipError_t launch_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int rank,
                        uint64_t count_for_seq, hipStream_t stream);

@@ -169,6 +169,78 @@ int run_local(const chr::LocalOp& op, const Bufs& B, int dtype, int rop, hipStre
     return rc;
 }
 
+// Consecutive L_TREE ops of one step (the flat schedule's chunks of one pipeline slice) run as ONE
+// batched launch when none writes what another reads or writes (an op's own in-place root over
+// its own leaf is element-wise and fine): fewer grid fills and drains per call
+// (launch_reduce_tree_multi).  Anything else runs op by op.
+bool overlaps(const chr::Ref& x, uint64_t xn, const chr::Ref& y, uint64_t yn) {
+    return x.buf == y.buf && x.off < y.off + yn && y.off < x.off + xn;
+}
+
+bool batchable(const std::vector<chr::LocalOp>& ops, size_t i0, size_t i1) {
+    for (size_t i = i0; i < i1; ++i)
+        for (size_t j = i0; j < i1; ++j) {
+            if (i == j) continue;
+            const chr::LocalOp& w = ops[i];
+            const chr::LocalOp& r = ops[j];
+            if (overlaps(w.dst, w.count, r.dst, r.count) || overlaps(w.dst, w.count, r.acc, r.count)) return false;
+            for (const chr::Ref& x : r.ins)
+                if (overlaps(w.dst, w.count, x, r.count)) return false;
+        }
+    return true;
+}
+
+int run_tree_batch(const std::vector<chr::LocalOp>& ops, size_t i0, size_t i1, const Bufs& B, int dtype, int rop,
+                   hipStream_t s, ReduceProfile* prof) {
+    std::vector<chr::TreeJob> jobs;
+    double bytes = 0;
+    for (size_t i = i0; i < i1; ++i) {
+        const chr::LocalOp& op = ops[i];
+        if (op.count == 0) continue;
+        chr::TreeJob jb{};
+        jb.out = B.ptr(op.dst);
+        jb.leaves[0] = B.ptr(op.acc);
+        for (size_t j = 0; j < op.ins.size(); ++j) jb.leaves[j + 1] = B.ptr(op.ins[j]);
+        jb.nl = (int)op.ins.size() + 1;
+        jb.comb = op.comb.data();
+        jb.swaps = op.swaps.empty() ? nullptr : op.swaps.data();
+        jb.n = op.count;
+        jobs.push_back(jb);
+        bytes += (double)(jb.nl + 1) * op.count * B.es;
+    }
+    if (jobs.empty()) return CHR_SUCCESS;
+    const bool timed = prof && prof->on;
+    std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+    if (timed) {
+        ev = prof->take();
+        (void)hipEventRecord(ev.first, s);
+    }
+    const int rc = hip_code(chr::launch_reduce_tree_multi(jobs.data(), (int)jobs.size(), dtype, rop, s));
+    if (timed) {
+        (void)hipEventRecord(ev.second, s);
+        prof->pending.push_back(ev);
+        prof->bytes += bytes;
+        prof->launches += 1;
+    }
+    return rc;
+}
+
+int run_locals(const std::vector<chr::LocalOp>& ops, const Bufs& B, int dtype, int rop, hipStream_t s,
+               ReduceProfile* prof = nullptr) {
+    for (size_t i = 0; i < ops.size();) {
+        size_t j = i;
+        while (j < ops.size() && ops[j].kind == chr::L_TREE && ops[j].ins.size() + 1 <= 8) ++j;
+        if (j - i >= 2 && batchable(ops, i, j)) {
+            if (int rc = run_tree_batch(ops, i, j, B, dtype, rop, s, prof)) return rc;
+            i = j;
+            continue;
+        }
+        if (int rc = run_local(ops[i], B, dtype, rop, s, prof)) return rc;
+        ++i;
+    }
+    return CHR_SUCCESS;
+}
+
 bool is_device_ptr(const void* p) {
     hipPointerAttribute_t attr;
     std::memset(&attr, 0, sizeof(attr));
@@ -340,8 +412,7 @@ int enqueue_plan(chr_comm* c, const Plan& p, const void* send, void* recv, int d
     if (e != hipSuccess) return hip_code(e);
     Bufs B{(const char*)send, (char*)recv, (char*)c->acc.p, (char*)c->stage.p, es};
     int rc;
-    for (const auto& op_ : p.pre)
-        if ((rc = run_local(op_, B, dtype, op, c->stream, &c->prof))) return rc;
+    if ((rc = run_locals(p.pre, B, dtype, op, c->stream, &c->prof))) return rc;
     // Two streams: transfers on c->stream, local ops on c->cstream.  A step's transfers wait
     // only for the local ops of step comm_wait (schedule.cpp analyze_deps); local ops wait
     // for their own step's transfers.  The call ends with c->stream waiting for the last ops.
@@ -394,16 +465,14 @@ int enqueue_plan(chr_comm* c, const Plan& p, const void* send, void* recv, int d
         }
         if (s.post.empty()) continue;
         if (!two) {
-            for (const auto& op_ : s.post)
-                if ((rc = run_local(op_, B, dtype, op, c->stream, &c->prof))) return rc;
+            if ((rc = run_locals(s.post, B, dtype, op, c->stream, &c->prof))) return rc;
             continue;
         }
         hipEvent_t ec = c->event(2 * t), ed = c->event(2 * t + 1);
         if (!ec || !ed) return CHR_ERR_HIP;
         if ((rc = hip_code(hipEventRecord(ec, c->stream))) || (rc = hip_code(hipStreamWaitEvent(c->cstream, ec, 0))))
             return rc;
-        for (const auto& op_ : s.post)
-            if ((rc = run_local(op_, B, dtype, op, c->cstream, &c->prof))) return rc;
+        if ((rc = run_locals(s.post, B, dtype, op, c->cstream, &c->prof))) return rc;
         if ((rc = hip_code(hipEventRecord(ed, c->cstream)))) return rc;
         last_comp = (int)t;
     }
@@ -705,8 +774,7 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
     }
     int rc;
     for (int r = 0; r < n; ++r)
-        for (const auto& op_ : P[r].pre)
-            if ((rc = run_local(op_, B[r], dtype, op, g->stream))) return rc;
+        if ((rc = run_locals(P[r].pre, B[r], dtype, op, g->stream))) return rc;
     const size_t nsteps = P[0].steps.size();
     for (size_t si = 0; si < nsteps; ++si) {
         // Loopback transport: each receive takes the next unmatched send of its peer to
@@ -747,8 +815,7 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
                         return hip_code(e);
                 }
         for (int r = 0; r < n; ++r)
-            for (const auto& op_ : P[r].steps[si].post)
-                if ((rc = run_local(op_, B[r], dtype, op, g->stream))) return rc;
+            if ((rc = run_locals(P[r].steps[si].post, B[r], dtype, op, g->stream))) return rc;
     }
     return hip_code(hipStreamSynchronize(g->stream));
 }

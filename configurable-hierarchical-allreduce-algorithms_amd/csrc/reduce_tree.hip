@@ -49,50 +49,85 @@ bool tree_program_ok(int nl, const uint8_t* comb, const uint8_t* swaps, uint32_t
     return true;
 }
 
+// Several trees in as few launches as possible: the vector bodies of trees with equal leaf counts
+// share a launch (up to kMaxTreeSegs segments); heads and tails that are not 16-B congruent run
+// on the scalar kernel per tree.  Every tree keeps its own program, so the bits are unchanged.
+hipError_t launch_reduce_tree_multi(const TreeJob* jobs, int njobs, int dtype, int op, hipStream_t stream) {
+    if (!valid_dtype_op(dtype, op)) return hipErrorInvalidValue;
+    const size_t es = dtype_size(dtype);
+    canon_op(dtype, op, false, &dtype, &op);  // the per-combine swap bits carry the operand order
+    const size_t E = 16 / es;
+    TreeArgs pend[kMaxLeaves + 1] = {};  // pending vector segments, by leaf count
+    auto flush = [&](int nl) -> hipError_t {
+        TreeArgs& a = pend[nl];
+        if (!a.nseg) return hipSuccess;
+        a.nl = nl;
+        const hipError_t e = launch_tree_any(a, nullptr, dtype, op, stream);
+        a.nseg = 0;
+        return e;
+    };
+    for (int t = 0; t < njobs; ++t) {
+        const TreeJob& jb = jobs[t];
+        if (jb.n == 0) continue;
+        uint32_t cb = 0, sb = 0;
+        if (!tree_program_ok(jb.nl, jb.comb, jb.swaps, &cb, &sb)) return hipErrorInvalidValue;
+        const int nl = jb.nl;
+        if (nl == 1) {
+            if (jb.out != jb.leaves[0]) {
+                const hipError_t e = hipMemcpyAsync(jb.out, jb.leaves[0], jb.n * es, hipMemcpyDeviceToDevice, stream);
+                if (e != hipSuccess) return e;
+            }
+            continue;
+        }
+        const uintptr_t mis = (uintptr_t)jb.out & 15u;
+        bool congruent = (mis % es) == 0;
+        for (int j = 0; j < nl; ++j) congruent = congruent && (((uintptr_t)jb.leaves[j] & 15u) == mis);
+        auto scalar = [&](size_t off, size_t cnt) -> hipError_t {
+            if (!cnt) return hipSuccess;
+            TreeScalarArgs sa{};
+            sa.out = (char*)jb.out + off * es;
+            for (int j = 0; j < nl; ++j) sa.leaves[j] = (const char*)jb.leaves[j] + off * es;
+            sa.n = cnt;
+            sa.nl = nl;
+            sa.comb = cb;
+            sa.swaps = sb;
+            TreeArgs dummy{};
+            return launch_tree_any(dummy, &sa, dtype, op, stream);
+        };
+        hipError_t err;
+        if (!congruent) {
+            if ((err = scalar(0, jb.n)) != hipSuccess) return err;
+            continue;
+        }
+        size_t head = mis ? (16 - mis) / es : 0;
+        if (head > jb.n) head = jb.n;
+        const size_t nvec = (jb.n - head) / E;
+        const size_t tail = jb.n - head - nvec * E;
+        if ((err = scalar(0, head)) != hipSuccess || (err = scalar(head + nvec * E, tail)) != hipSuccess) return err;
+        if (!nvec) continue;
+        TreeArgs& a = pend[nl];
+        TreeSeg& g = a.seg[a.nseg++];
+        g.out = (u32x4*)((char*)jb.out + head * es);
+        for (int j = 0; j < nl; ++j) g.leaves[j] = (const u32x4*)((const char*)jb.leaves[j] + head * es);
+        g.nvec = nvec;
+        g.comb = cb;
+        g.swaps = sb;
+        if (a.nseg == kMaxTreeSegs && (err = flush(nl)) != hipSuccess) return err;
+    }
+    for (int nl = 2; nl <= kMaxLeaves; ++nl) {
+        const hipError_t e = flush(nl);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 hipError_t launch_reduce_tree(void* out, const void* const* leaves, int nl, const uint8_t* comb, const uint8_t* swaps,
                               size_t n, int dtype, int op, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    if (!valid_dtype_op(dtype, op)) return hipErrorInvalidValue;
-    uint32_t cb = 0, sb = 0;
-    if (!tree_program_ok(nl, comb, swaps, &cb, &sb)) return hipErrorInvalidValue;
-    const size_t es = dtype_size(dtype);
-    canon_op(dtype, op, false, &dtype, &op);  // the per-combine swap bits carry the operand order
-    if (nl == 1) return out == leaves[0] ? hipSuccess
-                                         : hipMemcpyAsync(out, leaves[0], n * es, hipMemcpyDeviceToDevice, stream);
-    const uintptr_t mis = (uintptr_t)out & 15u;
-    bool congruent = (mis % es) == 0;
-    for (int j = 0; j < nl; ++j) congruent = congruent && (((uintptr_t)leaves[j] & 15u) == mis);
-    auto scalar = [&](size_t off, size_t cnt) -> hipError_t {
-        if (!cnt) return hipSuccess;
-        TreeScalarArgs sa{};
-        sa.out = (char*)out + off * es;
-        for (int j = 0; j < nl; ++j) sa.leaves[j] = (const char*)leaves[j] + off * es;
-        sa.n = cnt;
-        sa.nl = nl;
-        sa.comb = cb;
-        sa.swaps = sb;
-        TreeArgs dummy{};
-        return launch_tree_any(dummy, &sa, dtype, op, stream);
-    };
-    if (!congruent) return scalar(0, n);
-    size_t head = mis ? (16 - mis) / es : 0;
-    if (head > n) head = n;
-    const size_t E = 16 / es;
-    const size_t nvec = (n - head) / E;
-    const size_t tail = n - head - nvec * E;
-    hipError_t err = scalar(0, head);
-    if (err != hipSuccess) return err;
-    if (nvec) {
-        TreeArgs a{};
-        a.out = (u32x4*)((char*)out + head * es);
-        for (int j = 0; j < nl; ++j) a.leaves[j] = (const u32x4*)((const char*)leaves[j] + head * es);
-        a.nvec = nvec;
-        a.nl = nl;
-        a.comb = cb;
-        a.swaps = sb;
-        if ((err = launch_tree_any(a, nullptr, dtype, op, stream)) != hipSuccess) return err;
-    }
-    return scalar(head + nvec * E, tail);
+    if (nl < 1 || nl > kMaxLeaves) return hipErrorInvalidValue;
+    TreeJob jb{out, {}, nl, comb, swaps, n};
+    for (int j = 0; j < nl; ++j) jb.leaves[j] = leaves[j];
+    return launch_reduce_tree_multi(&jb, 1, dtype, op, stream);
 }
 
 }  // namespace chr

@@ -28,13 +28,25 @@ namespace chr {
 constexpr int kMaxLeaves = 8;
 constexpr int kTreeDepth = 4;
 
-struct TreeArgs {
+// Segments: one launch may evaluate several trees with the same leaf count (the flat schedule's
+// chunks of one pipeline slice): each has its own leaves, output, length and program, and owns
+// the workgroups [block0, next block0).  At C4 this halves the launches per call and doubles the
+// bytes per launch, so the fixed fill/drain cost of a grid (~4 us) is paid half as often.
+constexpr int kMaxTreeSegs = 8;
+
+struct TreeSeg {
     u32x4* out;
     const u32x4* leaves[kMaxLeaves];
     size_t nvec;
+    uint32_t comb;    // 2 bits per leaf
+    uint32_t swaps;   // 1 bit per combine, in program order
+    uint32_t block0;  // first workgroup of this segment
+};
+
+struct TreeArgs {
+    TreeSeg seg[kMaxTreeSegs];
+    int nseg;
     int nl;
-    uint32_t comb;   // 2 bits per leaf
-    uint32_t swaps;  // 1 bit per combine, in program order
 };
 
 template <int OP>
@@ -94,29 +106,35 @@ struct ScalarOp {
 // the first combine (NL * U <= 16 loads of 16 B in flight per lane).
 template <int DT, int OP, int NL, int U, bool NT, int BL>
 __global__ __launch_bounds__(BL) void k_reduce_tree(TreeArgs a) {
-    const size_t stride = (size_t)gridDim.x * BL * U;
-    for (size_t base = (size_t)blockIdx.x * BL * U + threadIdx.x; base < a.nvec; base += stride) {
-        if (base + (size_t)(U - 1) * BL < a.nvec) {
+    // this workgroup's segment (uniform: scalar loads of the kernel arguments)
+    int s = 0;
+    for (int j = 1; j < a.nseg; ++j)
+        if (blockIdx.x >= a.seg[j].block0) s = j;
+    const TreeSeg& g = a.seg[s];
+    const uint32_t nblk = (s + 1 < a.nseg ? a.seg[s + 1].block0 : gridDim.x) - g.block0;
+    const size_t stride = (size_t)nblk * BL * U;
+    for (size_t base = (size_t)(blockIdx.x - g.block0) * BL * U + threadIdx.x; base < g.nvec; base += stride) {
+        if (base + (size_t)(U - 1) * BL < g.nvec) {
             u32x4 x[NL][U];
 #pragma unroll
             for (int j = 0; j < NL; ++j)
 #pragma unroll
-                for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&a.leaves[j][base + (size_t)u * BL]);
+                for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&g.leaves[j][base + (size_t)u * BL]);
             __builtin_amdgcn_sched_barrier(0);
             u32x4 r[U];
-            tree_eval<u32x4, NL, U, VecOp<DT, OP>>(x, r, a.comb, a.swaps);
+            tree_eval<u32x4, NL, U, VecOp<DT, OP>>(x, r, g.comb, g.swaps);
 #pragma unroll
-            for (int u = 0; u < U; ++u) st<NT>(&a.out[base + (size_t)u * BL], r[u]);
+            for (int u = 0; u < U; ++u) st<NT>(&g.out[base + (size_t)u * BL], r[u]);
         } else {
             for (int u = 0; u < U; ++u) {
                 const size_t i = base + (size_t)u * BL;
-                if (i >= a.nvec) break;
+                if (i >= g.nvec) break;
                 u32x4 x[NL][1];
 #pragma unroll
-                for (int j = 0; j < NL; ++j) x[j][0] = a.leaves[j][i];
+                for (int j = 0; j < NL; ++j) x[j][0] = g.leaves[j][i];
                 u32x4 r[1];
-                tree_eval<u32x4, NL, 1, VecOp<DT, OP>>(x, r, a.comb, a.swaps);
-                a.out[i] = r[0];
+                tree_eval<u32x4, NL, 1, VecOp<DT, OP>>(x, r, g.comb, g.swaps);
+                g.out[i] = r[0];
             }
         }
     }
@@ -144,12 +162,19 @@ __global__ __launch_bounds__(kBlock) void k_reduce_tree_scalar(TreeScalarArgs a)
 }
 
 template <int DT, int OP, int NL, int BL, bool NT>
-inline hipError_t launch_tree_vec(const TreeArgs& a, hipStream_t s) {
+inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
     constexpr int U = NL <= 4 ? 4 : 2;
-    const size_t trips = (a.nvec + (size_t)BL * U - 1) / ((size_t)BL * U);
-    const size_t cap = reduce_tuning().max_blocks > 0 ? (size_t)reduce_tuning().max_blocks : trips;
-    const int grid = (int)(trips < cap ? trips : cap);
-    hipLaunchKernelGGL((k_reduce_tree<DT, OP, NL, U, NT, BL>), dim3(grid), dim3(BL), 0, s, a);
+    TreeArgs a = a_in;
+    // one trip per workgroup; CHR_REDUCE_MAX_BLOCKS caps each segment's share (tuning knob)
+    const size_t cap = reduce_tuning().max_blocks > 0 ? (size_t)reduce_tuning().max_blocks : ~(size_t)0;
+    size_t grid = 0;
+    for (int j = 0; j < a.nseg; ++j) {
+        const size_t trips = (a.seg[j].nvec + (size_t)BL * U - 1) / ((size_t)BL * U);
+        a.seg[j].block0 = (uint32_t)grid;
+        grid += trips < cap ? trips : cap;
+    }
+    if (grid == 0) return hipSuccess;
+    hipLaunchKernelGGL((k_reduce_tree<DT, OP, NL, U, NT, BL>), dim3((unsigned)grid), dim3(BL), 0, s, a);
     return hipGetLastError();
 }
 
@@ -165,7 +190,9 @@ inline hipError_t launch_tree_nl(const TreeArgs& a, const TreeScalarArgs* sa, hi
     }
     // same policy as launch_vec_m: streaming calls (>= 128 MiB) nt with one-wave workgroups
     const ReduceTuning& t = reduce_tuning();
-    const size_t call_bytes = (size_t)(a.nl + 1) * a.nvec * 16;
+    size_t nvec = 0;
+    for (int j = 0; j < a.nseg; ++j) nvec += a.seg[j].nvec;
+    const size_t call_bytes = (size_t)(a.nl + 1) * nvec * 16;
     const bool nt = t.nt_mode == 1 || (t.nt_mode < 0 && call_bytes >= t.nt_min_bytes);
     if constexpr (!FULL) {
         return nt ? launch_tree_vec<DT, OP, NL, 64, true>(a, s) : launch_tree_vec<DT, OP, NL, 256, false>(a, s);

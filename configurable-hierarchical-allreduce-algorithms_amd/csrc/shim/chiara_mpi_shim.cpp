@@ -99,8 +99,9 @@ bool map_op(MPI_Op o, chr_op* out) {
     return true;
 }
 
-// MPI's op/type table (MPI-3.1 §5.9.2): MPI_BYTE only with the bitwise ops, MPI_C_BOOL only with
-// the logical ops, floating types not with either; 0 or the MPI error class to return.
+// MPI's op/type table as MPICH 3.3.2 applies it (probed with MPI_Reduce_local): MPI_BYTE only with
+// the bitwise ops, MPI_C_BOOL only with the logical ops, float/double with the logical ops (an MPICH
+// extension of MPI-3.1 §5.9.2) but not the bitwise ones; 0 or the MPI error class to return.
 int map_pair(MPI_Datatype d, MPI_Op o, chr_dtype* dt, chr_op* op) {
     if (!map_type(d, dt)) return MPI_ERR_TYPE;
     if (!map_op(o, op)) return MPI_ERR_OP;
@@ -108,7 +109,7 @@ int map_pair(MPI_Datatype d, MPI_Op o, chr_dtype* dt, chr_op* op) {
     const bool logical = *op == CHR_LAND || *op == CHR_LOR || *op == CHR_LXOR;
     if (d == MPI_BYTE && !bitwise) return MPI_ERR_OP;
     if (d == MPI_C_BOOL && !logical) return MPI_ERR_OP;
-    if ((*dt == CHR_FLOAT32 || *dt == CHR_FLOAT64) && (bitwise || logical)) return MPI_ERR_OP;
+    if ((*dt == CHR_FLOAT32 || *dt == CHR_FLOAT64) && bitwise) return MPI_ERR_OP;
     return 0;
 }
 

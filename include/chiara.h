@@ -111,6 +111,15 @@ int chr_reduce_tree(void* out, const void* const* leaves, int nleaves, const uns
                     const unsigned char* swaps, size_t n, chr_dtype dtype, chr_op op,
                     hipStream_t stream);
 
+/* Several such trees in as few launches as possible (the flat schedule evaluates one per chunk of
+ * a pipeline slice): tree t writes outs[t] from leaves[t*nleaves .. t*nleaves+nleaves-1] with the
+ * program comb[t*nleaves ..] / swaps[t*(nleaves-1) ..] (swaps may be NULL).  Trees must not write
+ * what another tree of the batch reads or writes (an in-place root over its own leaf is fine).
+ * Bit-identical to ntrees chr_reduce_tree calls. */
+int chr_reduce_tree_batch(void* const* outs, const void* const* leaves, int ntrees, int nleaves,
+                          const unsigned char* comb, const unsigned char* swaps, size_t n,
+                          chr_dtype dtype, chr_op op, hipStream_t stream);
+
 /* ---- communicator (replaces MPI_Comm + MPI p2p: RCCL over xGMI) -------------------- */
 typedef struct chr_comm chr_comm;
 typedef struct { char internal[128]; } chr_unique_id; /* == ncclUniqueId */

@@ -113,3 +113,34 @@ def test_integer_types_and_logical_bitwise_ops(gu, dtype, op):
     for prog in (C4_TREE, K2B8_TREE):
         _run(gu, dtype, op, prog[0], prog[1], 30011, pattern=pat)
     _run(gu, dtype, op, *K4B8_TREE, 1001, pattern=pat, off=1)
+
+
+@pytest.mark.parametrize("ntrees,n,off", [(2, 100003, 0), (3, 4097, 1), (8, 2048 + 5, 0), (9, 1000, 0), (2, 0, 0)])
+def test_batched_trees_bit_identical(gu, ntrees, n, off):
+    """chr_reduce_tree_batch (what the executor does with a slice's chunks): several trees, each with
+    its own program, leaves and output, in shared launches (8 segments at most per launch, 9 trees
+    = two launches), ragged and misaligned heads/tails on the scalar kernel: every tree equal to
+    its own oracle evaluation."""
+    rng = np.random.default_rng(ntrees * 7 + n)
+    npdt = po.NP_DTYPES["f32"]
+    progs = [random_program(rng, 8) for _ in range(ntrees)]
+    leaves = [[po.fill(n, "f32", 0, 3, 8 * t + j) for j in range(8)] for t in range(ntrees)]
+    d_leaves, outs = [], []
+    for t in range(ntrees):
+        row = []
+        for x in leaves[t]:
+            d = gu.empty_dev((n + off) * 4)
+            d[off * 4:(off + n) * 4] = gu.to_dev(x)
+            row.append(d.data_ptr() + off * 4)
+            d_leaves.append(d)
+        outs.append(gu.empty_dev((n + off) * 4))
+        leaves_ptrs = row
+        progs[t] = (progs[t][0], progs[t][1], leaves_ptrs)
+    rc = ca.reduce_tree_batch([o.data_ptr() + off * 4 for o in outs], [p[2] for p in progs], [p[0] for p in progs],
+                              [p[1] for p in progs], n, ca.FLOAT32, ca.SUM, gu.stream())
+    assert rc == 0
+    gu.sync()
+    for t in range(ntrees):
+        got = gu.from_dev(outs[t], npdt)[off:off + n]
+        want = tree_ref(leaves[t], progs[t][0], progs[t][1], "f32", "sum")
+        np.testing.assert_array_equal(_bits(got), _bits(want))

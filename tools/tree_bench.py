@@ -25,7 +25,80 @@ def main():
     out = {}
     for dname, cdt, tdt, es in (("f32", ca.FLOAT32, torch.float32, 4), ("bf16", ca.BFLOAT16, torch.bfloat16, 2)):
         out[dname] = run(dev, s, cdt, tdt, es)
-    print(json.dumps({"tree_vs_folds_c4": out}))
+    batched = {dname: run_batched(dev, s, cdt, tdt, es)
+               for dname, cdt, tdt, es in (("f32", ca.FLOAT32, torch.float32, 4), ("bf16", ca.BFLOAT16, torch.bfloat16, 2))}
+    print(json.dumps({"tree_vs_folds_c4": out, "slice_batched_c4": batched}))
+
+
+def run_batched(dev, s, cdt, tdt, es):
+    """The flat schedule at C4 evaluates, per pipeline slice, the trees of the 2 chunks (8 leaves x
+    piece each).  Two launches (one per chunk) vs one batched launch (chr_reduce_tree_batch), with
+    the leaves cold (cycled over a > 2 GiB working set) and warm (7 of 8 leaves just written by a
+    device copy, as RCCL's receives leave them; only the tree launches are timed)."""
+    out = {}
+    for mib in (8, 16, 32):
+        n = (mib << 20) // es
+        sets = max(2, min(8, (2048 << 20) // (2 * 9 * es * n)))
+        bufs = []
+        for si in range(sets):
+            trees = []
+            for t in range(2):
+                leaves = [torch.empty(n, dtype=tdt, device=dev) for _ in range(8)]
+                for j, x in enumerate(leaves):
+                    ca.fill(x, n, cdt, 0, 7, 16 * si + 8 * t + j, stream=s)
+                trees.append((leaves, torch.empty(n, dtype=tdt, device=dev)))
+            bufs.append(trees)
+        src = torch.empty(n, dtype=tdt, device=dev)
+        ca.fill(src, n, cdt, 0, 9, 0, stream=s)
+        reps = 32
+
+        def separate(i):
+            rc = 0
+            for lv, o in bufs[i % sets]:
+                rc |= ca.reduce_tree(o, lv, COMB, SWAPS, n, cdt, ca.SUM, s)
+            return rc
+
+        def batched(i):
+            tr = bufs[i % sets]
+            return ca.reduce_tree_batch([o for _, o in tr], [lv for lv, _ in tr], [COMB, COMB], [SWAPS, SWAPS], n, cdt,
+                                        ca.SUM, s)
+
+        res = {}
+        for name, fn in (("separate", separate), ("batched", batched)):
+            for warm in (False, True):
+                for i in range(3):
+                    assert fn(i) == 0
+                torch.cuda.synchronize()
+                total = 0.0
+                evs = []
+                for i in range(reps):
+                    if warm:
+                        for lv, _ in bufs[i % sets]:
+                            for x in lv[1:]:
+                                x.copy_(src)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(s)
+                    fn(i)
+                    e1.record(s)
+                    evs.append((e0, e1))
+                torch.cuda.synchronize()
+                total = sum(a.elapsed_time(b) for a, b in evs)
+                us = total / reps * 1e3
+                nbytes = 2 * 9 * es * n
+                res[f"{name}_{'warm' if warm else 'cold'}"] = {
+                    "us": round(us, 2), "GBps": round(nbytes / (us * 1e-6) / 1e9, 1),
+                    "frac": round(nbytes / (us * 1e-6) / 8e12, 4)}
+        tr = bufs[0]
+        separate(0)
+        ref = [o.clone() for _, o in tr]
+        batched(0)
+        torch.cuda.synchronize()
+        res["bit_identical"] = all(bool(torch.equal(a.view(torch.int16), o.view(torch.int16)))
+                                   for a, (_, o) in zip(ref, tr))
+        out[f"piece_{mib}MiB"] = res
+        del bufs
+        torch.cuda.empty_cache()
+    return out
 
 
 def run(dev, s, cdt, tdt, es):
