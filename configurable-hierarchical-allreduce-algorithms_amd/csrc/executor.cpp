@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cctype>
 #include <chrono>
 #include <cstdio>
@@ -299,8 +300,20 @@ int default_schedule() {
     return v;
 }
 
-// Pipeline depth: explicit setting, else CHR_SLICES, else by chunk size (schedule.cpp).
-int pick_slices(int setting, uint64_t count, int mode, int nranks, int b, size_t es) {
+// Pipeline depth: explicit setting, else CHR_SLICES, else by chunk size (schedule.cpp auto_slices).
+// The flat schedules evaluate one piece per (chunk, rank) per slice -- chunk/n elements (allreduce)
+// or the rank's own block (reduce-scatter), divided by the depth -- in batched tree launches whose
+// fixed fill/drain cost dominates small pieces (profiles/r02/tree_bench_batched.json, C4's two
+// 8-leaf trees per slice: 8 MiB pieces 0.58-0.63 of the HBM peak, 16 MiB 0.68-0.77), so their
+// default depth keeps pieces at 16 MiB or more.  CHR_SCHEDULE_AUTO still times every depth from
+// the chunk-size one down.
+constexpr uint64_t kMinFlatPieceBytes = (uint64_t)16 << 20;
+
+bool flat_family(int sched) {
+    return sched == chr::SCHED_FLAT || sched == chr::SCHED_FLAT_AG || sched == chr::SCHED_FLAT_SEQ;
+}
+
+int pick_slices(int setting, uint64_t count, int mode, int nranks, int b, size_t es, int sched) {
     if (chr::is_mpich(mode) || mode == chr::MODE_ALLGATHER) return 1;  // unpipelined schedules
     if (setting > 0) return setting;
     static const int env = [] {
@@ -308,8 +321,16 @@ int pick_slices(int setting, uint64_t count, int mode, int nranks, int b, size_t
         return v ? std::atoi(v) : 0;
     }();
     if (env > 0) return env;
-    const uint64_t recvcount = mode == chr::MODE_ALLREDUCE ? count / (uint64_t)(nranks > 0 ? nranks : 1) : count;
-    return chr::auto_slices(recvcount * (uint64_t)(b > 0 ? b : 1) * es);
+    const uint64_t n = (uint64_t)(nranks > 0 ? nranks : 1);
+    const uint64_t recvcount = mode == chr::MODE_ALLREDUCE ? count / n : count;
+    const uint64_t irc_bytes = recvcount * (uint64_t)(b > 0 ? b : 1) * es;
+    int P = chr::auto_slices(irc_bytes);
+    if (flat_family(sched)) {
+        const uint64_t piece = mode == chr::MODE_ALLREDUCE ? irc_bytes / n : recvcount * es;
+        const int cap = (int)std::max<uint64_t>(1, piece / kMinFlatPieceBytes);
+        P = std::min(P, cap);
+    }
+    return P;
 }
 
 }  // namespace
@@ -372,7 +393,7 @@ struct chr_comm {
     std::map<std::tuple<int, uint64_t, int, int, int, int, int>, std::pair<int, int>> tuned;
 
     const Plan& plan(int mode, int k, int b, uint64_t count, size_t es, int sched_, int slices_) {
-        const int P = pick_slices(slices_, count, mode, nranks, b, es);
+        const int P = pick_slices(slices_, count, mode, nranks, b, es, sched_);
         PlanKey key{mode, rank, k, b, count, (int)es, P, sched_};
         auto it = plans.find(key);
         if (it == plans.end())
@@ -674,7 +695,7 @@ int tune_schedule(chr_comm* c, int mode, const void* send, void* recv, size_t co
     }
     std::vector<std::pair<int, int>> cand;
     std::vector<int> depths;
-    const int pa = pick_slices(c->slices, count, mode, c->nranks, b, es);
+    const int pa = pick_slices(c->slices, count, mode, c->nranks, b, es, chr::SCHED_REFERENCE);  // chunk-size depth
     for (int d = pa; d >= 1; d /= 2) {
         depths.push_back(d);
         if (c->slices > 0) break;  // an explicit depth is kept
@@ -746,7 +767,7 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
                      int dtype, int op, int k, int b) {
     if (!g || !sends || !recvs || !chr::valid_dtype_op(dtype, op)) return CHR_ERR_INVALID_ARG;
     const int n = g->nranks;
-    const int depth = pick_slices(g->slices, count, mode, n, b, chr::dtype_size(dtype));
+    const int depth = pick_slices(g->slices, count, mode, n, b, chr::dtype_size(dtype), g->sched);
     auto key = std::make_tuple(mode, k, b, (uint64_t)count, (int)chr::dtype_size(dtype), depth, g->sched);
     auto it = g->plans.find(key);
     if (it == g->plans.end()) {

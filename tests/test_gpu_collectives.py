@@ -240,12 +240,14 @@ def _window_reader(recvs, n, rc, npdt, tview):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("dtype,schedule", [("f32", "flat"), ("f32", "exact"), ("bf16", "flat"), ("bf16", "exact")])
-def test_c4_c5_full_size_bit_exact_vs_oracle(gu, groups, dtype, schedule):
+@pytest.mark.parametrize("dtype,schedule,slices", [("f32", "flat", 0), ("f32", "flat", 8), ("f32", "exact", 0),
+                                                   ("bf16", "flat", 0), ("bf16", "flat", 8), ("bf16", "exact", 0)])
+def test_c4_c5_full_size_bit_exact_vs_oracle(gu, groups, dtype, schedule, slices):
     """C4 (fp32) and C5 (bf16) at their BASELINE size -- 8 ranks, k=4, b=4, 1 GiB per rank,
     U[-1,1) data -- bit-exact vs the C oracle over every element of every rank.  This is the
-    size that switches on the non-temporal / ACC0 / one-wave kernel instantiations and the
-    automatic 8-slice pipeline; the association order the oracle pins is
+    size that switches on the non-temporal / ACC0 / one-wave kernel instantiations, the batched
+    tree launches and the pipeline (automatic depth: 4 slices for flat, 16 MiB pieces; and 8);
+    the association order the oracle pins is
     all_reduce_radix_batch.cpp:343-364 (recexch folds) and :523-530 (lane reduction).  The int32
     closed form (test_c4_full_size_exact_int) and the bf16 bound stay as fast pre-checks: both
     are blind to association.  Checked window by window (tests/fullsize_util.py)."""
@@ -265,11 +267,12 @@ def test_c4_c5_full_size_bit_exact_vs_oracle(gu, groups, dtype, schedule):
     recvs = [torch.empty(count * es, dtype=torch.uint8, device=gu.DEV) for _ in range(n)]
     gu.sync()
     g.set_schedule({"flat": ca.SCHEDULE_FLAT, "exact": ca.SCHEDULE_EXACT}[schedule])
-    g.set_slices(0)  # automatic: 8 slices of the 512 MiB chunks
+    g.set_slices(slices)
     try:
         assert g.all_reduce_radix_batch(sends, recvs, count, cdt, ca.SUM, k, b) == 0
     finally:
         g.set_schedule(ca.SCHEDULE_FLAT)
+        g.set_slices(0)
     gu.sync()
     del sends
     torch.cuda.empty_cache()

@@ -451,9 +451,9 @@ def test_rccl_lost_peer_times_out_world4():
     assert res[-1][3] and res[-1][4] == ca.ERR_ABORTED
 
 
-def _fullsize_worker(rank, world, port, q, dtype):
+def _fullsize_worker(rank, world, port, q, dtype, slices):
     """C4 (fp32) / C5 (bf16) at full size over RCCL: 8 processes, k=4, b=4, 1 GiB per rank, default
-    (FLAT) schedule, automatic 8-slice pipeline, compute/transfer overlap on two HIP streams."""
+    (FLAT) schedule, pipeline depth automatic (4) or 8, compute/transfer overlap on two HIP streams."""
     _setup(rank)
     import hashlib
 
@@ -473,7 +473,7 @@ def _fullsize_worker(rank, world, port, q, dtype):
     out = None
     try:
         comm.set_schedule(ca.SCHEDULE_FLAT)
-        comm.set_slices(0)
+        comm.set_slices(slices)
         comm.set_overlap(True)
         send = torch.empty(count * es, dtype=torch.uint8, device=dev)
         recv = torch.empty(count * es, dtype=torch.uint8, device=dev)
@@ -502,9 +502,9 @@ def _fullsize_worker(rank, world, port, q, dtype):
 
 
 @pytest.mark.timeout(1200)
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
-def test_rccl_c4_c5_full_size_bit_exact_world8(dtype):
-    res = sorted(_spawn(_fullsize_worker, 8, extra=(dtype,), timeout=900))
+@pytest.mark.parametrize("dtype,slices", [("f32", 0), ("f32", 8), ("bf16", 0)])
+def test_rccl_c4_c5_full_size_bit_exact_world8(dtype, slices):
+    res = sorted(_spawn(_fullsize_worker, 8, extra=(dtype, slices), timeout=900))
     assert all(rc == 0 for _, rc, _, _ in res), res
     assert all(same for _, _, same, _ in res), "ranks disagree"
     assert res[0][3] == [], f"mismatches vs the oracle: {res[0][3][:5]}"

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Why m = 3 / m = 7 buckets drop at >= 512 MiB: the product's fused bucket
+reduction (chr_reduce_multi, in place, fp32 SUM) at m in {1, 3, 7} incoming buckets and bucket
+sizes 256 MiB .. 1 GiB, with the m + 1 operands laid out four ways:
+  sep      one torch allocation per operand (the earlier sweep's layout)
+  slab     one allocation, operands back to back (operand j at j * bucket)
+  slab+d   one allocation, operand j at j * (bucket + d): d = 4 KiB, 64 KiB, 2 MiB + 4 KiB
+HBM-cold: at least 2 GiB of distinct data per rotation (buffer sets cycled).  Prints one JSON line
+per (m, bucket, layout): us per call and algorithmic GB/s ((m + 2) * bucket bytes).
+Usage: mstream_probe.py [--ms 1,3,7] [--mib 256,512,1024] [--layouts sep,slab,...] [--reps N]"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "configurable-hierarchical-allreduce-algorithms_amd")]
+
+import torch  # noqa: E402
+
+import chiara_amd as ca  # noqa: E402
+
+DELTAS = {"slab": 0, "slab+4k": 4 << 10, "slab+64k": 64 << 10, "slab+2m4k": (2 << 20) + (4 << 10)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ms", default="1,3,7")
+    ap.add_argument("--mib", default="256,512,1024")
+    ap.add_argument("--layouts", default="sep,slab,slab+4k,slab+64k,slab+2m4k")
+    ap.add_argument("--reps", type=int, default=12)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream(dev)
+    for m in [int(x) for x in a.ms.split(",")]:
+        for mib in [int(x) for x in a.mib.split(",")]:
+            nbytes = mib << 20
+            n = nbytes // 4
+            sets = max(1, min(4, (2048 << 20) // ((m + 1) * nbytes)))
+            for lay in a.layouts.split(","):
+                bufs, keep = [], []
+                for si in range(sets):
+                    if lay == "sep":
+                        ops = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(m + 1)]
+                        keep.append(ops)
+                        ptrs = [t.data_ptr() for t in ops]
+                    else:
+                        d = DELTAS[lay]
+                        slab = torch.empty((m + 1) * (nbytes + d) + 4096, dtype=torch.uint8, device=dev)
+                        keep.append(slab)
+                        ptrs = [slab.data_ptr() + j * (nbytes + d) for j in range(m + 1)]
+                    for j, p in enumerate(ptrs):
+                        ca.check(ca.fill(p, n, ca.FLOAT32, 0, 3, 16 * si + j, stream=s))
+                    bufs.append(ptrs)
+                torch.cuda.synchronize()
+
+                def go(i):
+                    p = bufs[i % sets]
+                    return ca.reduce_multi(p[0], p[0], p[1:], n, ca.FLOAT32, ca.SUM, s)
+
+                for i in range(2):
+                    ca.check(go(i))
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda.synchronize()
+                e0.record(s)
+                for i in range(a.reps):
+                    go(i)
+                e1.record(s)
+                torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) / a.reps * 1e3
+                gbps = (m + 2) * nbytes / (us * 1e-6) / 1e9
+                print(json.dumps({"m": m, "bucket_MiB": mib, "layout": lay, "sets": sets, "us": round(us, 2),
+                                  "GBps": round(gbps, 1), "frac": round(gbps / 8000, 4)}), flush=True)
+                del bufs, keep
+                torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
