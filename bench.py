@@ -52,6 +52,9 @@ def parse():
                    help="N>1: skip the same-run context lines (RCCL allreduce, MPICH ring on libchiara)")
     p.add_argument("--e2e", action="store_true",
                    help="N=1: host-memory (PCIe-inclusive) staging cost of the reference's host-buffer contract")
+    p.add_argument("--collective-kernels", action="store_true",
+                   help="N=1: the fused reductions of the C4/C5 collectives at full size (8 virtual ranks, "
+                        "loopback transport), HIP-event timed against the HBM roofline")
     return p.parse_args()
 
 
@@ -315,6 +318,51 @@ def bench_e2e(args):
     out["device_resident_ms"] = round((time.perf_counter() - t0) / 3 * 1e3, 3)
     comm.destroy()
     emit({"e2e": out})
+
+
+def bench_collective_kernels(args):
+    """The kernels the 8-rank collective launches, at C4 (fp32) and C5 (bf16) full size: 8 virtual
+    ranks on this GPU (chr_local_group: the real plans, the loopback transport's device copies
+    instead of RCCL), every fused reduction timed with HIP events.  Unlike the one-GPU rehearsal
+    of the N>1 line -- 8 processes time-sharing one GPU, whose event-timed kernels include the
+    other processes' work -- nothing else runs beside these kernels; the leaves are the ones the
+    loopback copies have just written, as RCCL's receives would leave them."""
+    import torch
+
+    import chiara_amd as ca
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    n, k, b = 8, 4, 4
+    g = ca.LocalGroup(n, 0)
+    rows = {}
+    for dname, cdt, es in (("f32", ca.FLOAT32, 4), ("bf16", ca.BFLOAT16, 2)):
+        count = (1 << 30) // es
+        sends = [torch.empty(count * es, dtype=torch.uint8, device=dev) for _ in range(n)]
+        recvs = [torch.empty(count * es, dtype=torch.uint8, device=dev) for _ in range(n)]
+        for r, x in enumerate(sends):
+            ca.check(ca.fill(x, count, cdt, 0, SEED, r, stream=g.stream))
+        for slices in (0, 8):
+            g.set_slices(slices)
+            ca.check(g.all_reduce_radix_batch(sends, recvs, count, cdt, ca.SUM, k, b))  # warm: plans, scratch
+            g.profile(True)
+            g.profile_read()
+            reps = 3
+            for _ in range(reps):
+                ca.check(g.all_reduce_radix_batch(sends, recvs, count, cdt, ca.SUM, k, b))
+            ms, by, launches = g.profile_read()
+            g.profile(False)
+            ach = by / (ms * 1e-3) / 1e9
+            rows[f"{'c4' if dname == 'f32' else 'c5'}_{dname}_slices_{slices or 'auto'}"] = {
+                "launches_per_call_all_ranks": launches // reps, "kernel_ms_per_call_all_ranks": round(ms / reps, 4),
+                "algorithmic_bytes_per_call_all_ranks": int(by / reps), "achieved_GBps": round(ach, 1),
+                "frac": round(ach / HBM_PEAK_GBPS, 4)}
+        g.set_slices(0)
+        del sends, recvs
+        torch.cuda.empty_cache()
+    g.destroy()
+    emit({"collective_kernels": {"workload": "all_reduce_radix_batch fused reductions, 8 virtual ranks, k=4, b=4, "
+                                             "1 GiB per rank, flat schedule (batched trees)", "rows": rows}})
 
 
 # ---- N > 1: hierarchical allreduce over RCCL ---------------------------------------------------
@@ -654,6 +702,9 @@ def _main():
         return
     if args.e2e:
         bench_e2e(args)
+        return
+    if args.collective_kernels:
+        bench_collective_kernels(args)
         return
     cpu = None if args.no_cpu_baseline else cpu_baseline(args.cpu_seconds)
     bench_bucket(args, cpu)

@@ -84,6 +84,12 @@ def _load():
         "chr_comm_synchronize": ([vp], i),
         "chr_comm_is_aborted": ([vp], i),
         "chr_reduce_tree_batch": ([pp, pp, i, i, ctypes.c_char_p, ctypes.c_char_p, sz, i, i, vp], i),
+        "chr_reduce_scatter_mpich": ([vp, vp, sz, i, i, vp, i, i], i),
+        "chr_reduce_scatter_mpich_async": ([vp, vp, sz, i, i, vp, i, i], i),
+        "chr_local_reduce_scatter_mpich": ([vp, pp, pp, sz, i, i, i, i], i),
+        "chr_local_group_profile": ([vp, i], i),
+        "chr_local_group_profile_read": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                          ctypes.POINTER(ctypes.c_long), i], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -113,5 +119,7 @@ EXPORTED = [
     "chr_allgather_radix_batch_async", "chr_local_allgather_radix_batch", "chr_comm_set_schedule", "chr_comm_set_overlap",
     "chr_local_group_set_schedule", "chr_plan_describe_ex", "chr_reduce_tree", "chr_comm_profile_phases",
     "chr_comm_tuned_schedule", "chr_comm_set_graphs", "chr_comm_set_timeout", "chr_comm_abort",
-    "chr_comm_synchronize", "chr_comm_is_aborted", "chr_reduce_tree_batch",
+    "chr_comm_synchronize", "chr_comm_is_aborted", "chr_reduce_tree_batch", "chr_local_group_profile",
+    "chr_local_group_profile_read", "chr_reduce_scatter_mpich", "chr_reduce_scatter_mpich_async",
+    "chr_local_reduce_scatter_mpich",
 ]

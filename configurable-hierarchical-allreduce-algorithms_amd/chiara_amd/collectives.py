@@ -44,6 +44,9 @@ MODE_ALLREDUCE, MODE_REDUCE_SCATTER = 0, 1
 MODE_MPICH_RING, MODE_MPICH_RD, MODE_MPICH_RSAG, MODE_MPICH_RECEXCH = 2, 3, 4, 5
 MODE_MPICH_KRSAG, MODE_MPICH_RMULT = 6, 7
 MODE_ALLGATHER = 8
+# MPICH baseline reduce-scatters (testing/mpich_implementations/reduce_scatter/)
+MODE_MPICH_RS_RADIX, MODE_MPICH_RS_HALVING, MODE_MPICH_RS_DOUBLING, MODE_MPICH_RS_PAIRWISE = 9, 10, 11, 12
+RS_MODES = (1, 9, 10, 11, 12)  # count = recvcount, send = nranks * recvcount
 SCHEDULE_REFERENCE, SCHEDULE_BALANCED, SCHEDULE_FLAT, SCHEDULE_EXACT, SCHEDULE_FLAT_AG, SCHEDULE_FLAT_SEQ = 0, 1, 2, 3, 4, 5
 SCHEDULE_AUTO = 6  # measured choice among FLAT / FLAT_SEQ / FLAT_AG and the pipeline depth (Comm only)
 REDUCE_RUNNING_FIRST = 1  # chr_reduce_multi_ex flag (MPICH_do_reduce operand order)
@@ -246,6 +249,17 @@ class LocalGroup:
     def set_schedule(self, schedule):
         check(lib().chr_local_group_set_schedule(self._h, int(schedule)))
 
+    def profile(self, enable=True):
+        """Time every virtual rank's fused reduction launches (HIP events)."""
+        check(lib().chr_local_group_profile(self._h, 1 if enable else 0))
+
+    def profile_read(self, reset=True):
+        """(kernel_ms, algorithmic_bytes, launches) of the reductions since the last reset."""
+        ms, by, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_long()
+        check(lib().chr_local_group_profile_read(self._h, ctypes.byref(ms), ctypes.byref(by), ctypes.byref(n),
+                                                 1 if reset else 0))
+        return ms.value, by.value, n.value
+
     def all_reduce_radix_batch(self, sendbufs, recvbufs, count, datatype, op, k, b):
         S = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in sendbufs])
         R = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in recvbufs])
@@ -260,6 +274,12 @@ class LocalGroup:
         S = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in sendbufs])
         R = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in recvbufs])
         return lib().chr_local_allgather_radix_batch(self._h, S, R, sendcount, datatype, k, b)
+
+    def reduce_scatter_mpich(self, algo, sendbufs, recvbufs, recvcount, datatype, op, k=2):
+        """algo: MODE_MPICH_RS_RADIX / _HALVING / _DOUBLING / _PAIRWISE."""
+        S = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in sendbufs])
+        R = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in recvbufs])
+        return lib().chr_local_reduce_scatter_mpich(self._h, S, R, recvcount, datatype, op, algo, k)
 
     def allreduce_mpich(self, algo, sendbufs, recvbufs, count, datatype, op, k=2, single_phase_recv=0):
         """algo: MODE_MPICH_RING / _RD / _RSAG / _RECEXCH."""
@@ -336,6 +356,33 @@ def MPICH_Allreduce_k_reduce_scatter_allgather(sendbuf, recvbuf, count, datatype
 def MPICH_Allreduce_recursive_multiplying(sendbuf, recvbuf, count, datatype, op, comm, k, async_op=False):
     """allreduce_recursive_multiplying.cpp:3 -- k-ary recursive doubling."""
     return _mpich(MODE_MPICH_RMULT, sendbuf, recvbuf, count, datatype, op, comm, k, async_op=async_op)
+
+
+# ---- MPICH baseline reduce-scatters driven by testing/mpich_implementations/reduce_scatter/main.cpp ----
+
+def _mpich_rs(algo, sendbuf, recvbuf, recvcount, datatype, op, comm, k=0, async_op=False):
+    fn = lib().chr_reduce_scatter_mpich_async if async_op else lib().chr_reduce_scatter_mpich
+    return fn(_addr(sendbuf), _addr(recvbuf), recvcount, datatype, op, comm.handle, algo, k)
+
+
+def MPICH_reduce_scatter_radix(sendbuf, recvbuf, recvcount, datatype, op, comm, k, async_op=False):
+    """reduce_scatter_radix.cpp:204 -- recexch reduce-scatter, the single-level ancestor of CHiArA's phase 1."""
+    return _mpich_rs(MODE_MPICH_RS_RADIX, sendbuf, recvbuf, recvcount, datatype, op, comm, k, async_op)
+
+
+def MPICH_reduce_scatter_rec_halving(sendbuf, recvbuf, count, datatype, op, comm, async_op=False):
+    """reduce_scatter_recursive_halving.cpp:7."""
+    return _mpich_rs(MODE_MPICH_RS_HALVING, sendbuf, recvbuf, count, datatype, op, comm, 0, async_op)
+
+
+def MPICH_reduce_scatter_rec_doubling(sendbuf, recvbuf, recvcount, datatype, op, comm, async_op=False):
+    """reduce_scatter_recursive_doubling.cpp:10."""
+    return _mpich_rs(MODE_MPICH_RS_DOUBLING, sendbuf, recvbuf, recvcount, datatype, op, comm, 0, async_op)
+
+
+def MPICH_reduce_scatter_pairwise(sendbuf, recvbuf, recvcount, datatype, op, comm, async_op=False):
+    """reduce_scatter_pairwise.cpp:4."""
+    return _mpich_rs(MODE_MPICH_RS_PAIRWISE, sendbuf, recvbuf, recvcount, datatype, op, comm, 0, async_op)
 
 
 def reduce_multi_ex(out, acc, ins, count, datatype, op, flags, stream=None):

@@ -406,6 +406,7 @@ struct chr_comm {
 
 struct chr_local_group {
     int nranks = 0, device = 0;
+    ReduceProfile prof;  // chr_local_group_profile: every rank's fused reductions, HIP events
     int slices = 0;  // 0 = auto
     int sched = default_schedule() == CHR_SCHEDULE_AUTO ? (int)chr::SCHED_FLAT : default_schedule();  // no tuning
     hipStream_t stream = nullptr;
@@ -795,7 +796,7 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
     }
     int rc;
     for (int r = 0; r < n; ++r)
-        if ((rc = run_locals(P[r].pre, B[r], dtype, op, g->stream))) return rc;
+        if ((rc = run_locals(P[r].pre, B[r], dtype, op, g->stream, &g->prof))) return rc;
     const size_t nsteps = P[0].steps.size();
     for (size_t si = 0; si < nsteps; ++si) {
         // Loopback transport: each receive takes the next unmatched send of its peer to
@@ -836,7 +837,7 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
                         return hip_code(e);
                 }
         for (int r = 0; r < n; ++r)
-            if ((rc = run_locals(P[r].steps[si].post, B[r], dtype, op, g->stream))) return rc;
+            if ((rc = run_locals(P[r].steps[si].post, B[r], dtype, op, g->stream, &g->prof))) return rc;
     }
     return hip_code(hipStreamSynchronize(g->stream));
 }
@@ -1068,10 +1069,33 @@ int chr_local_group_create(chr_local_group** out, int nranks, int device) {
     return CHR_SUCCESS;
 }
 
+int chr_local_group_profile(chr_local_group* g, int enable) {
+    if (!g) return CHR_ERR_INVALID_ARG;
+    g->prof.on = enable != 0;
+    return CHR_SUCCESS;
+}
+
+int chr_local_group_profile_read(chr_local_group* g, double* reduce_ms, double* reduce_bytes, long* launches,
+                                 int reset) {
+    if (!g) return CHR_ERR_INVALID_ARG;
+    (void)hipSetDevice(g->device);
+    g->prof.drain();
+    if (reduce_ms) *reduce_ms = g->prof.ms;
+    if (reduce_bytes) *reduce_bytes = g->prof.bytes;
+    if (launches) *launches = g->prof.launches;
+    if (reset) {
+        g->prof.ms = 0;
+        g->prof.bytes = 0;
+        g->prof.launches = 0;
+    }
+    return CHR_SUCCESS;
+}
+
 int chr_local_group_destroy(chr_local_group* g) {
     if (!g) return CHR_SUCCESS;
     (void)hipSetDevice(g->device);
     if (g->stream) (void)hipStreamSynchronize(g->stream);
+    g->prof.release();
     for (auto& d : g->acc) d.release();
     for (auto& d : g->stage) d.release();
     if (g->stream) (void)hipStreamDestroy(g->stream);
@@ -1099,6 +1123,10 @@ static bool valid_mpich_mode(chr_mode m) {
     return m >= CHR_MODE_MPICH_RING && m <= CHR_MODE_MPICH_RMULT;
 }
 
+static bool valid_mpich_rs_mode(chr_mode m) {
+    return m >= CHR_MODE_MPICH_RS_RADIX && m <= CHR_MODE_MPICH_RS_PAIRWISE;
+}
+
 int chr_allreduce_mpich(const void* send, void* recv, size_t count, chr_dtype dtype, chr_op op, chr_comm* comm,
                         chr_mode algo, int k, int single_phase_recv) {
     if (!valid_mpich_mode(algo)) return CHR_ERR_INVALID_ARG;
@@ -1115,6 +1143,24 @@ int chr_local_allreduce_mpich(chr_local_group* g, const void* const* sends, void
                               chr_dtype dtype, chr_op op, chr_mode algo, int k, int single_phase_recv) {
     if (!valid_mpich_mode(algo)) return CHR_ERR_INVALID_ARG;
     return local_collective(g, algo, sends, recvs, count, dtype, op, k, single_phase_recv);
+}
+
+int chr_reduce_scatter_mpich(const void* send, void* recv, size_t recvcount, chr_dtype dtype, chr_op op,
+                             chr_comm* comm, chr_mode algo, int k) {
+    if (!valid_mpich_rs_mode(algo)) return CHR_ERR_INVALID_ARG;
+    return collective(comm, algo, send, recv, recvcount, dtype, op, k, 0, true);
+}
+
+int chr_reduce_scatter_mpich_async(const void* send, void* recv, size_t recvcount, chr_dtype dtype, chr_op op,
+                                   chr_comm* comm, chr_mode algo, int k) {
+    if (!valid_mpich_rs_mode(algo)) return CHR_ERR_INVALID_ARG;
+    return collective(comm, algo, send, recv, recvcount, dtype, op, k, 0, false);
+}
+
+int chr_local_reduce_scatter_mpich(chr_local_group* g, const void* const* sends, void* const* recvs, size_t recvcount,
+                                   chr_dtype dtype, chr_op op, chr_mode algo, int k) {
+    if (!valid_mpich_rs_mode(algo)) return CHR_ERR_INVALID_ARG;
+    return local_collective(g, algo, sends, recvs, recvcount, dtype, op, k, 0);
 }
 
 int chr_allgather_radix_batch(const void* send, size_t sendcount, chr_dtype dtype, void* recv, chr_comm* comm, int k,

@@ -1354,6 +1354,243 @@ void build_krsag(MB& b, int k_in) {
     }
 }
 
+// ---- MPICH baseline reduce-scatters (block) ------------------------------------------------
+// testing/mpich_implementations/reduce_scatter/*.cpp, driven by that directory's main.cpp
+// (MPI_Reduce_scatter_block semantics: rank r gets block r of the reduced n*rc buffer).  SEND holds
+// the n*rc input (RECV under MPI_IN_PLACE), RECV the rc-element result, ACC the reference's
+// tmp_results, STAGE its tmp_recvbuf.
+struct RB {
+    Plan& p;
+    int n, me;
+    uint64_t rc, total;
+    Step& add(const char* label) {
+        p.steps.emplace_back();
+        p.steps.back().label = label;
+        return p.steps.back();
+    }
+    void need(uint64_t e) { p.stage_elems = std::max(p.stage_elems, e); }
+};
+
+// reduce_scatter_pairwise.cpp:4-74: n-1 Sendrecv rounds, round i sends block (me+i) to me+i and
+// receives my block from me-i, each folded into the result in round order (:54 / :56).  The
+// blocks sent are never written, so all rounds share one group and one fused reduction.
+void build_rs_pairwise(RB& b) {
+    const uint64_t rc = b.rc;
+    if (b.n == 1) {
+        b.p.pre.push_back(make_copy({BUF_RECV, 0}, {BUF_SEND, 0}, rc, 32));
+        return;
+    }
+    Step& s = b.add("pw");
+    std::vector<Ref> ins;
+    for (int i = 1; i < b.n; ++i) {
+        const int src = (b.me - i + b.n) % b.n, dst = (b.me + i) % b.n;
+        s.sends.push_back({dst, {BUF_SEND, (uint64_t)dst * rc}, rc});
+        s.recvs.push_back({src, {BUF_STAGE, (uint64_t)(i - 1) * rc}, rc});
+        ins.push_back({BUF_STAGE, (uint64_t)(i - 1) * rc});
+    }
+    b.need((uint64_t)(b.n - 1) * rc);
+    // in place the result lands in block 0 of recvbuf (:64-66); its input is sent in this step
+    s.post.push_back(make_reduce({BUF_RECV, 0}, {BUF_SEND, (uint64_t)b.me * rc}, ins, rc, 54));
+}
+
+// reduce_scatter_recursive_halving.cpp:7-153: the 2*rem lowest ranks fold pairwise (even -> odd,
+// whole buffer, :50-66), the pof2 survivors halve the live range log2(pof2) times (:88-128) over
+// blocks of 1 or 2 ranks (newcnts), then odd fold ranks return their partner's block (:137-143).
+void build_rs_halving(RB& b) {
+    const int n = b.n, me = b.me;
+    const uint64_t rc = b.rc, total = b.total;
+    int pof2 = 1;
+    while (pof2 <= n) pof2 *= 2;
+    pof2 = pof2 == n ? pof2 : pof2 / 2;  // :40-46
+    const int rem = n - pof2;
+    const int newrank = me < 2 * rem ? (me % 2 ? me / 2 : -1) : me - rem;
+    if (newrank >= 0) {
+        b.p.pre.push_back(make_copy({BUF_ACC, 0}, {BUF_SEND, 0}, total, 35));
+        b.p.acc_elems = total;
+    }
+    {
+        Step& s = b.add("rh-fold");
+        if (me < 2 * rem) {
+            if (me % 2 == 0) {
+                s.sends.push_back({me + 1, {BUF_SEND, 0}, total});
+            } else {
+                s.recvs.push_back({me - 1, {BUF_STAGE, 0}, total});
+                b.need(total);
+                s.post.push_back(make_reduce({BUF_ACC, 0}, {BUF_ACC, 0}, {{BUF_STAGE, 0}}, total, 59));
+            }
+        }
+    }
+    std::vector<uint64_t> cnts(pof2), disps(pof2, 0);
+    for (int i = 0; i < pof2; ++i) {  // :74-86
+        const int old_i = i < rem ? i * 2 + 1 : i + rem;
+        cnts[i] = old_i < 2 * rem ? 2 * rc : rc;
+    }
+    for (int i = 1; i < pof2; ++i) disps[i] = disps[i - 1] + cnts[i - 1];
+    auto sum = [&](int a, int e) {
+        uint64_t t = 0;
+        for (int i = a; i < e; ++i) t += cnts[i];
+        return t;
+    };
+    int send_idx = 0, recv_idx = 0, last_idx = pof2;
+    for (int mask = pof2 >> 1; mask > 0; mask >>= 1) {  // :91-128
+        Step& s = b.add("rh");
+        if (newrank < 0) continue;
+        const int newdst = newrank ^ mask, dst = newdst < rem ? newdst * 2 + 1 : newdst + rem;
+        uint64_t send_cnt, recv_cnt;
+        if (newrank < newdst) {
+            send_idx = recv_idx + mask;
+            send_cnt = sum(send_idx, last_idx);
+            recv_cnt = sum(recv_idx, send_idx);
+        } else {
+            recv_idx = send_idx + mask;
+            send_cnt = sum(send_idx, recv_idx);
+            recv_cnt = sum(recv_idx, last_idx);
+        }
+        if (send_cnt) s.sends.push_back({dst, {BUF_ACC, disps[send_idx]}, send_cnt});
+        if (recv_cnt) {
+            s.recvs.push_back({dst, {BUF_STAGE, disps[recv_idx]}, recv_cnt});
+            b.need(total);
+            s.post.push_back(make_reduce({BUF_ACC, disps[recv_idx]}, {BUF_ACC, disps[recv_idx]},
+                                         {{BUF_STAGE, disps[recv_idx]}}, recv_cnt, 121));
+        }
+        send_idx = recv_idx;
+        last_idx = recv_idx + mask;
+    }
+    Step& s = b.add("rh-unfold");
+    if (me < 2 * rem) {
+        if (me % 2) s.sends.push_back({me - 1, {BUF_ACC, (uint64_t)(me - 1) * rc}, rc});
+        else s.recvs.push_back({me + 1, {BUF_RECV, 0}, rc});
+    }
+    if (newrank >= 0) s.post.push_back(make_copy({BUF_RECV, 0}, {BUF_ACC, (uint64_t)me * rc}, rc, 130));
+}
+
+// reduce_scatter_recursive_doubling.cpp:10-177 (commutative path: every predefined op, and the
+// bf16 user op, is commutative): at distance `mask` each rank exchanges every block outside its
+// own and its partner's subtree of `mask` ranks (two hindexed blocks each way, :58-104); for a
+// non-power-of-two size the ranks without a partner get the data relayed down the subtree
+// (:106-130); the received blocks are folded into tmp_results (:132-155).
+void build_rs_doubling(RB& b) {
+    const int P = b.n, me = b.me;
+    const uint64_t rc = b.rc, total = b.total;
+    b.p.pre.push_back(make_copy({BUF_ACC, 0}, {BUF_SEND, 0}, total, 39));
+    b.p.acc_elems = total;
+    b.need(total);
+    const bool pof2 = (P & (P - 1)) == 0;
+    int stage = 0;
+    for (int mask = 1; mask < P; mask <<= 1, ++stage) {
+        const int dst = me ^ mask;
+        const int dtr = (dst >> stage) << stage, mtr = (me >> stage) << stage;
+        // (offset, length) in elements of the two send and receive blocks
+        const uint64_t s0 = (uint64_t)mtr * rc;
+        const uint64_t s1 = P - (mtr + mask) > 0 ? (uint64_t)(P - (mtr + mask)) * rc : 0;
+        const uint64_t s1off = s0 + rc * (uint64_t)(std::min(mtr + mask, P) - mtr);
+        const uint64_t r0 = rc * (uint64_t)std::min(dtr, P);
+        const uint64_t r1 = P - (dtr + mask) > 0 ? (uint64_t)(P - (dtr + mask)) * rc : 0;
+        const uint64_t r1off = r0 + rc * (uint64_t)(std::min(dtr + mask, P) - dtr);
+        bool received = false;
+        Step* last = &b.add("rd");
+        if (dst < P) {
+            if (s0) last->sends.push_back({dst, {BUF_ACC, 0}, s0});
+            if (s1) last->sends.push_back({dst, {BUF_ACC, s1off}, s1});
+            if (r0) last->recvs.push_back({dst, {BUF_STAGE, 0}, r0});
+            if (r1) last->recvs.push_back({dst, {BUF_STAGE, r1off}, r1});
+            received = true;
+        }
+        if (!pof2) {  // relays: one step per level for every rank, so the steps line up
+            const bool tail = dtr + mask > P;
+            const int npc = P - mtr - mask;
+            int k = 0;
+            for (int j = mask; j >>= 1;) ++k;  // log2(mask)
+            for (int tmp_mask = mask >> 1; tmp_mask; tmp_mask >>= 1, --k) {
+                Step& s = b.add("rd-relay");
+                last = &s;
+                if (!tail) continue;
+                const int sd = me ^ tmp_mask, tree_root = (me >> k) << k;
+                if (sd > me && me < tree_root + npc && sd >= tree_root + npc) {
+                    if (r0) s.sends.push_back({sd, {BUF_STAGE, 0}, r0});
+                    if (r1) s.sends.push_back({sd, {BUF_STAGE, r1off}, r1});
+                } else if (sd < me && sd < tree_root + npc && me >= tree_root + npc) {
+                    if (r0) s.recvs.push_back({sd, {BUF_STAGE, 0}, r0});
+                    if (r1) s.recvs.push_back({sd, {BUF_STAGE, r1off}, r1});
+                    received = true;
+                }
+            }
+        }
+        if (received) {
+            if (r0) last->post.push_back(make_reduce({BUF_ACC, 0}, {BUF_ACC, 0}, {{BUF_STAGE, 0}}, r0, 141));
+            if (r1)
+                last->post.push_back(make_reduce({BUF_ACC, r1off}, {BUF_ACC, r1off}, {{BUF_STAGE, r1off}}, r1, 151));
+        }
+    }
+    Step& s = b.add("rd-out");  // :171-174
+    s.post.push_back(make_copy({BUF_RECV, 0}, {BUF_ACC, (uint64_t)me * rc}, rc, 173));
+}
+
+// reduce_scatter_radix.cpp:204-377: the single-level ancestor of CHiArA's phase 1.  Recexch
+// step 1 folds the non-participants' whole buffers (:247-273), step 2 exchanges, per phase from
+// the highest digit down, with the k-1 neighbours the regions count/offset name in units of
+// recvcount blocks, folding each into the own region in neighbour order (:279-318), step 3 returns
+// the non-participants' blocks (:321-347).  The k-1 exchanges of a phase touch disjoint regions,
+// so they share one group and one fused reduction.
+void build_rs_radix(RB& b, int k_in) {
+    const int n = b.n, me = b.me;
+    const uint64_t rc = b.rc, total = b.total;
+    Recexch x;
+    if (recexch_neighbors(me, n, k_in, &x)) {
+        b.p.error = 1;
+        return;
+    }
+    const int k = x.k, nph = x.step2_nphases;
+    const bool part = x.step1_sendto == -1;
+    std::vector<int> cnt, off;
+    recexch_count_offset(n, std::max(nph, 1), k, &cnt, &off);
+    if (part) {
+        b.p.pre.push_back(make_copy({BUF_ACC, 0}, {BUF_SEND, 0}, total, 240));
+        b.p.acc_elems = total;
+    }
+    {
+        Step& s = b.add("rr-step1");
+        if (!part) {
+            s.sends.push_back({x.step1_sendto, {BUF_SEND, 0}, total});
+        } else if (x.step1_nrecvs) {
+            std::vector<Ref> ins;
+            for (int i = 0; i < x.step1_nrecvs; ++i) {
+                s.recvs.push_back({x.step1_recvfrom[i], {BUF_STAGE, (uint64_t)i * total}, total});
+                ins.push_back({BUF_STAGE, (uint64_t)i * total});
+            }
+            b.need((uint64_t)x.step1_nrecvs * total);
+            s.post.push_back(make_reduce({BUF_ACC, 0}, {BUF_ACC, 0}, ins, total, 266));
+        }
+    }
+    for (int ph = nph - 1; ph >= 0; --ph) {
+        Step& s = b.add("rr-phase");
+        if (!part) continue;
+        const uint64_t moff = (uint64_t)off[ph * n + me] * rc, mlen = (uint64_t)cnt[ph * n + me] * rc;
+        std::vector<Ref> ins;
+        for (int i = 0; i < k - 1; ++i) {
+            const int dst = x.step2_nbrs[ph][i];
+            const uint64_t soff = (uint64_t)off[ph * n + dst] * rc, slen = (uint64_t)cnt[ph * n + dst] * rc;
+            if (slen) s.sends.push_back({dst, {BUF_ACC, soff}, slen});
+            if (mlen) {
+                s.recvs.push_back({dst, {BUF_STAGE, (uint64_t)i * total}, mlen});
+                ins.push_back({BUF_STAGE, (uint64_t)i * total});
+            }
+        }
+        if (mlen) {
+            b.need((uint64_t)(k - 1) * total);
+            s.post.push_back(make_reduce({BUF_ACC, moff}, {BUF_ACC, moff}, ins, mlen, 310));
+        }
+    }
+    Step& s = b.add("rr-step3");
+    if (!part) {
+        s.recvs.push_back({x.step1_sendto, {BUF_RECV, 0}, rc});
+    } else {
+        for (int i = 0; i < x.step1_nrecvs; ++i)
+            s.sends.push_back({x.step1_recvfrom[i], {BUF_ACC, (uint64_t)x.step1_recvfrom[i] * rc}, rc});
+        s.post.push_back(make_copy({BUF_RECV, 0}, {BUF_ACC, (uint64_t)me * rc}, rc, 322));
+    }
+}
+
 }  // namespace
 
 Plan build_plan_mpich(Mode mode, int n, int me, int k, int aux, uint64_t count) {
@@ -1367,6 +1604,25 @@ Plan build_plan_mpich(Mode mode, int n, int me, int k, int aux, uint64_t count) 
     }
     p.g.nranks = n;
     p.g.k = k;
+    if (is_mpich_rs(mode)) {
+        if (mode == MODE_MPICH_RS_RADIX && k < 2) {
+            p.error = 1;
+            return p;
+        }
+        p.g.recvcount = count;
+        p.g.total = count * (uint64_t)n;
+        p.send_elems = p.g.total;
+        p.recv_elems = count;
+        if (count == 0) return p;
+        RB rb{p, n, me, count, p.g.total};
+        switch (mode) {
+        case MODE_MPICH_RS_RADIX: build_rs_radix(rb, k); break;
+        case MODE_MPICH_RS_HALVING: build_rs_halving(rb); break;
+        case MODE_MPICH_RS_DOUBLING: build_rs_doubling(rb); break;
+        default: build_rs_pairwise(rb); break;
+        }
+        return p;
+    }
     p.g.total = count;
     p.send_elems = p.recv_elems = count;
     if (count == 0) return p;

@@ -84,9 +84,16 @@ enum Mode : int {
     MODE_MPICH_RECEXCH = 5,    // .../allreduce_recexch.cpp (k, single_phase_recv)
     MODE_MPICH_KRSAG = 6,      // .../allreduce_k_reduce_scatter_allgather.cpp (k, single_phase_recv)
     MODE_MPICH_RMULT = 7,      // .../allreduce_recursive_multiplying.cpp (k)
-    MODE_ALLGATHER = 8         // allgather_radix_batch (count = sendcount)
+    MODE_ALLGATHER = 8,        // allgather_radix_batch (count = sendcount)
+    // MPICH baseline reduce-scatters (block) of testing/mpich_implementations/reduce_scatter/
+    // (count = recvcount; driven by that directory's main.cpp)
+    MODE_MPICH_RS_RADIX = 9,     // reduce_scatter_radix.cpp:204 (k)
+    MODE_MPICH_RS_HALVING = 10,  // reduce_scatter_recursive_halving.cpp:7
+    MODE_MPICH_RS_DOUBLING = 11, // reduce_scatter_recursive_doubling.cpp:10
+    MODE_MPICH_RS_PAIRWISE = 12  // reduce_scatter_pairwise.cpp:4
 };
-inline bool is_mpich(int mode) { return mode >= MODE_MPICH_RING && mode <= MODE_MPICH_RMULT; }
+inline bool is_mpich_rs(int mode) { return mode >= MODE_MPICH_RS_RADIX && mode <= MODE_MPICH_RS_PAIRWISE; }
+inline bool is_mpich(int mode) { return (mode >= MODE_MPICH_RING && mode <= MODE_MPICH_RMULT) || is_mpich_rs(mode); }
 
 struct Geometry {
     int nranks = 0, b = 0, k = 0, nnodes = 0, nstages = 0, nu = 0, nph = 0;
@@ -140,7 +147,8 @@ enum Sched : int {
 Plan build_plan(Mode mode, int nranks, int rank, int k, int b, uint64_t count, int slices = 1,
                 int sched = SCHED_FLAT);
 int auto_slices(uint64_t irc_bytes);
-// MPICH baseline allreduces (count = elements per rank; aux = recexch single_phase_recv).
+// MPICH baseline allreduces (count = elements per rank; aux = recexch single_phase_recv) and
+// reduce-scatters (count = recvcount).
 Plan build_plan_mpich(Mode mode, int nranks, int rank, int k, int aux, uint64_t count);
 Plan build_plan_allgather(int nranks, int rank, int k, int b, uint64_t sendcount);
 std::string describe(const Plan& p);

@@ -16,6 +16,10 @@
 //       recursive_doubling.cpp:4, reduce_scatter_allgather.cpp:3, recexch.cpp:188,
 //       k_reduce_scatter_allgather.cpp:257, recursive_multiplying.cpp:3}: all six baselines
 //       testing/main.cpp times, so that harness links against libchiara unchanged
+//   MPICH_reduce_scatter_{radix, rec_halving, rec_doubling, pairwise}
+//       replace testing/mpich_implementations/reduce_scatter/reduce_scatter_{radix.cpp:204,
+//       recursive_halving.cpp:7, recursive_doubling.cpp:10, pairwise.cpp:4}: the baselines that
+//       directory's main.cpp times
 //
 // One chr_comm per MPI communicator, created on first use (RCCL unique id broadcast with
 // MPI_Bcast, device = node-local rank mod visible GPUs) and cached as an MPI attribute.
@@ -204,4 +208,40 @@ int allgather_radix_batch(char* sendbuf, int sendcount, MPI_Datatype datatype, c
     if (!c) return MPI_ERR_OTHER;
     const void* send = sendbuf == (char*)MPI_IN_PLACE ? CHR_IN_PLACE : (const void*)sendbuf;
     return to_mpi(chr_allgather_radix_batch(send, (size_t)sendcount * (size_t)tsize, CHR_UINT8, recvbuf, c, k, b));
+}
+
+namespace {
+
+int mpich_rs_call(chr_mode algo, const void* sendbuf, void* recvbuf, long long recvcount, MPI_Datatype datatype,
+                  MPI_Op op, MPI_Comm comm, int k) {
+    chr_dtype dt;
+    chr_op o;
+    if (int err = map_pair(datatype, op, &dt, &o)) return err;
+    if (recvcount < 0) return MPI_ERR_COUNT;
+    chr_comm* c = comm_for(comm);
+    if (!c) return MPI_ERR_OTHER;
+    const void* send = sendbuf == MPI_IN_PLACE ? CHR_IN_PLACE : sendbuf;
+    return to_mpi(chr_reduce_scatter_mpich(send, recvbuf, (size_t)recvcount, dt, o, c, algo, k));
+}
+
+}  // namespace
+
+int MPICH_reduce_scatter_radix(const void* sendbuf, void* recvbuf, MPI_Aint recvcount, MPI_Datatype datatype,
+                               MPI_Op op, MPI_Comm comm, int k) {
+    return mpich_rs_call(CHR_MODE_MPICH_RS_RADIX, sendbuf, recvbuf, recvcount, datatype, op, comm, k);
+}
+
+int MPICH_reduce_scatter_rec_halving(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+                                     MPI_Comm comm) {
+    return mpich_rs_call(CHR_MODE_MPICH_RS_HALVING, sendbuf, recvbuf, count, datatype, op, comm, 0);
+}
+
+int MPICH_reduce_scatter_rec_doubling(const void* sendbuf, void* recvbuf, MPI_Aint recvcount, MPI_Datatype datatype,
+                                      MPI_Op op, MPI_Comm comm) {
+    return mpich_rs_call(CHR_MODE_MPICH_RS_DOUBLING, sendbuf, recvbuf, recvcount, datatype, op, comm, 0);
+}
+
+int MPICH_reduce_scatter_pairwise(const void* sendbuf, void* recvbuf, MPI_Aint recvcount, MPI_Datatype datatype,
+                                  MPI_Op op, MPI_Comm comm) {
+    return mpich_rs_call(CHR_MODE_MPICH_RS_PAIRWISE, sendbuf, recvbuf, recvcount, datatype, op, comm, 0);
 }

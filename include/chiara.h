@@ -264,6 +264,12 @@ int chr_local_group_destroy(chr_local_group* group);
 int chr_local_group_stream(const chr_local_group* group, hipStream_t* stream);
 int chr_local_group_set_slices(chr_local_group* group, int slices);
 int chr_local_group_set_schedule(chr_local_group* group, int schedule);
+/* Timing of every virtual rank's fused reductions (HIP events on the group's stream), as
+ * chr_comm_profile / chr_comm_profile_read: the collective's own kernels at full size with the
+ * leaves just written by the loopback copies, one rank at a time. */
+int chr_local_group_profile(chr_local_group* group, int enable);
+int chr_local_group_profile_read(chr_local_group* group, double* reduce_ms, double* reduce_bytes,
+                                 long* launches, int reset);
 int chr_local_allreduce_radix_batch(chr_local_group* group, const void* const* sends,
                                     void* const* recvs, size_t count, chr_dtype dtype, chr_op op,
                                     int k, int b);
@@ -288,7 +294,13 @@ typedef enum {
     CHR_MODE_MPICH_RECEXCH = 5,    /* .../allreduce_recexch.cpp:188 (k, b = single_phase_recv) */
     CHR_MODE_MPICH_KRSAG = 6,      /* .../allreduce_k_reduce_scatter_allgather.cpp:257 (k, b = spr) */
     CHR_MODE_MPICH_RMULT = 7,      /* .../allreduce_recursive_multiplying.cpp:3 (k) */
-    CHR_MODE_ALLGATHER = 8         /* allgather_radix_batch (count = sendcount) */
+    CHR_MODE_ALLGATHER = 8,        /* allgather_radix_batch (count = sendcount) */
+    /* MPICH baseline reduce-scatters (block), testing/mpich_implementations/reduce_scatter/
+     * (count = recvcount) */
+    CHR_MODE_MPICH_RS_RADIX = 9,    /* reduce_scatter_radix.cpp:204 (k) */
+    CHR_MODE_MPICH_RS_HALVING = 10, /* reduce_scatter_recursive_halving.cpp:7 */
+    CHR_MODE_MPICH_RS_DOUBLING = 11,/* reduce_scatter_recursive_doubling.cpp:10 */
+    CHR_MODE_MPICH_RS_PAIRWISE = 12 /* reduce_scatter_pairwise.cpp:4 */
 } chr_mode;
 long chr_plan_describe(chr_mode mode, int nranks, int rank, int k, int b, size_t count,
                        int slices, char* buf, size_t len);
@@ -319,6 +331,28 @@ int chr_allreduce_mpich_async(const void* send, void* recv, size_t count, chr_dt
 int chr_local_allreduce_mpich(chr_local_group* group, const void* const* sends,
                               void* const* recvs, size_t count, chr_dtype dtype, chr_op op,
                               chr_mode algo, int k, int single_phase_recv);
+
+/* ---- MPICH baseline reduce-scatters (the ones testing/mpich_implementations/reduce_scatter/
+ * main.cpp benchmarks) ------------------------------------------------------------------------
+ * Replace  int MPICH_reduce_scatter_radix(const void* sendbuf, void* recvbuf, MPI_Aint recvcount,
+ *            MPI_Datatype, MPI_Op, MPI_Comm, int k)                (reduce_scatter_radix.cpp:204)
+ *          MPICH_reduce_scatter_rec_halving(const char*, char*, int count, ...)
+ *                                                   (reduce_scatter_recursive_halving.cpp:7)
+ *          MPICH_reduce_scatter_rec_doubling(const void*, void*, MPI_Aint recvcount, ...)
+ *                                                   (reduce_scatter_recursive_doubling.cpp:10)
+ *          MPICH_reduce_scatter_pairwise(const void*, void*, MPI_Aint recvcount, ...)
+ *                                                   (reduce_scatter_pairwise.cpp:4)
+ * algo is one of CHR_MODE_MPICH_RS_*; k is used by RS_RADIX.  MPI_Reduce_scatter_block semantics:
+ * send holds nranks*recvcount elements (recv does, under CHR_IN_PLACE), recv gets block `rank`.
+ * Results bit-identical to the reference's code on the same inputs; every reduction on the fused
+ * HIP kernel. */
+int chr_reduce_scatter_mpich(const void* send, void* recv, size_t recvcount, chr_dtype dtype, chr_op op,
+                             chr_comm* comm, chr_mode algo, int k);
+int chr_reduce_scatter_mpich_async(const void* send, void* recv, size_t recvcount, chr_dtype dtype,
+                                   chr_op op, chr_comm* comm, chr_mode algo, int k);
+int chr_local_reduce_scatter_mpich(chr_local_group* group, const void* const* sends,
+                                   void* const* recvs, size_t recvcount, chr_dtype dtype, chr_op op,
+                                   chr_mode algo, int k);
 
 /* ---- utilities -------------------------------------------------------------------------- */
 /* Synthetic inputs on the device with the shared generator (oracle/chiara_oracle.h):

@@ -862,3 +862,250 @@ int orc_allgather_radix_batch(int n, int k, int b, size_t count, int dtype, cons
     }
     return 0;
 }
+
+/* ---- MPICH baseline reduce-scatters (block): testing/mpich_implementations/reduce_scatter/ ---- */
+/* Every rank's input is send[r] (n*rc elements) or, under MPI_IN_PLACE (send[r] == NULL), recv[r];
+ * every rank's result (rc elements) goes to recv[r][0 .. rc).  Results are written only after
+ * every rank's computation, so in place the inputs stay intact while they are read. */
+
+static const char* orc_rs_input(const void* const* send, void* const* recv, int r) {
+    return send && send[r] ? (const char*)send[r] : (const char*)recv[r];
+}
+
+static void orc_rs_store(int n, size_t rc, size_t es, char** res, void* const* recv) {
+    int r;
+    for (r = 0; r < n; r++) {
+        memcpy(recv[r], res[r], rc * es);
+        free(res[r]);
+    }
+    free(res);
+}
+
+/* reduce_scatter_pairwise.cpp:4-74: own block, then the block from rank (r - i) for i = 1..n-1,
+ * each MPI_Reduce_local(tmp, result) (:54 / :56). */
+int orc_reduce_scatter_pairwise(int n, size_t rc, int dtype, int op, const void* const* send, void* const* recv) {
+    size_t es = orc_dtype_size(dtype);
+    char** res;
+    int r, i;
+    if (n < 1 || !es) return 1;
+    res = (char**)calloc((size_t)n, sizeof(char*));
+    for (r = 0; r < n; r++) {
+        res[r] = (char*)malloc(rc * es + 1);
+        memcpy(res[r], orc_rs_input(send, recv, r) + (size_t)r * rc * es, rc * es);
+        for (i = 1; i < n; i++) {
+            int src = (r - i + n) % n;
+            orc_reduce_local(orc_rs_input(send, recv, src) + (size_t)r * rc * es, res[r], rc, dtype, op);
+        }
+    }
+    orc_rs_store(n, rc, es, res, recv);
+    return 0;
+}
+
+/* reduce_scatter_recursive_halving.cpp:7-153. */
+int orc_reduce_scatter_rec_halving(int n, size_t rc, int dtype, int op, const void* const* send,
+                                   void* const* recv) {
+    size_t es = orc_dtype_size(dtype), total = rc * (size_t)n, *cnts, *disps;
+    int pof2 = 1, rem, r, i, mask;
+    char **tmp, **snap, **res;
+    int *newrank, *send_idx, *recv_idx, *last_idx;
+    if (n < 1 || !es) return 1;
+    while (pof2 <= n) pof2 *= 2; /* :40-46 */
+    pof2 = pof2 == n ? pof2 : pof2 / 2;
+    rem = n - pof2;
+    tmp = (char**)calloc((size_t)n, sizeof(char*));
+    snap = (char**)calloc((size_t)n, sizeof(char*));
+    res = (char**)calloc((size_t)n, sizeof(char*));
+    newrank = (int*)calloc((size_t)n, sizeof(int));
+    send_idx = (int*)calloc((size_t)n, sizeof(int));
+    recv_idx = (int*)calloc((size_t)n, sizeof(int));
+    last_idx = (int*)calloc((size_t)n, sizeof(int));
+    for (r = 0; r < n; r++) {
+        tmp[r] = (char*)malloc(total * es + 1);
+        snap[r] = (char*)malloc(total * es + 1);
+        res[r] = (char*)malloc(rc * es + 1);
+        memcpy(tmp[r], orc_rs_input(send, recv, r), total * es); /* :34-38 */
+    }
+    for (r = 0; r < n; r++) { /* :50-66: odd r < 2*rem folds its even partner's whole buffer */
+        if (r < 2 * rem) {
+            newrank[r] = r % 2 ? r / 2 : -1;
+            if (r % 2) orc_reduce_local(tmp[r - 1], tmp[r], total, dtype, op);
+        } else {
+            newrank[r] = r - rem;
+        }
+        send_idx[r] = recv_idx[r] = 0;
+        last_idx[r] = pof2;
+    }
+    cnts = (size_t*)calloc((size_t)pof2, sizeof(size_t));
+    disps = (size_t*)calloc((size_t)pof2, sizeof(size_t));
+    for (i = 0; i < pof2; i++) { /* :74-86 */
+        int old_i = i < rem ? i * 2 + 1 : i + rem;
+        cnts[i] = old_i < 2 * rem ? 2 * rc : rc;
+        if (i) disps[i] = disps[i - 1] + cnts[i - 1];
+    }
+    for (mask = pof2 >> 1; mask > 0; mask >>= 1) { /* :91-128, every rank from the pre-step state */
+        for (r = 0; r < n; r++) memcpy(snap[r], tmp[r], total * es);
+        for (r = 0; r < n; r++) {
+            int nr = newrank[r], newdst, dst, j;
+            size_t recv_cnt = 0;
+            if (nr < 0) continue;
+            newdst = nr ^ mask;
+            dst = newdst < rem ? newdst * 2 + 1 : newdst + rem;
+            if (nr < newdst) {
+                send_idx[r] = recv_idx[r] + mask;
+                for (j = recv_idx[r]; j < send_idx[r]; j++) recv_cnt += cnts[j];
+            } else {
+                recv_idx[r] = send_idx[r] + mask;
+                for (j = recv_idx[r]; j < last_idx[r]; j++) recv_cnt += cnts[j];
+            }
+            /* the partner sends exactly this range of its tmp_results (:112-117) */
+            if (recv_cnt)
+                orc_reduce_local(snap[dst] + disps[recv_idx[r]] * es, tmp[r] + disps[recv_idx[r]] * es, recv_cnt,
+                                 dtype, op);
+            send_idx[r] = recv_idx[r];
+            last_idx[r] = recv_idx[r] + mask;
+        }
+    }
+    for (r = 0; r < n; r++) { /* :130, :137-143 */
+        if (newrank[r] >= 0) memcpy(res[r], tmp[r] + (size_t)r * rc * es, rc * es);
+        else memcpy(res[r], tmp[r + 1] + (size_t)r * rc * es, rc * es);
+    }
+    for (r = 0; r < n; r++) {
+        free(tmp[r]);
+        free(snap[r]);
+    }
+    free(tmp);
+    free(snap);
+    free(cnts);
+    free(disps);
+    free(newrank);
+    free(send_idx);
+    free(recv_idx);
+    free(last_idx);
+    orc_rs_store(n, rc, es, res, recv);
+    return 0;
+}
+
+/* reduce_scatter_recursive_doubling.cpp:10-177, commutative path. */
+int orc_reduce_scatter_rec_doubling(int n, size_t rc, int dtype, int op, const void* const* send,
+                                    void* const* recv) {
+    const int P = n;
+    size_t es = orc_dtype_size(dtype), total = rc * (size_t)n;
+    char **tmp, **trecv, **res;
+    int *received, r, mask, stage;
+    if (n < 1 || !es) return 1;
+    tmp = (char**)calloc((size_t)n, sizeof(char*));
+    trecv = (char**)calloc((size_t)n, sizeof(char*));
+    res = (char**)calloc((size_t)n, sizeof(char*));
+    received = (int*)calloc((size_t)n, sizeof(int));
+    for (r = 0; r < n; r++) {
+        tmp[r] = (char*)malloc(total * es + 1);
+        trecv[r] = (char*)calloc(total * es + 1, 1);
+        res[r] = (char*)malloc(rc * es + 1);
+        memcpy(tmp[r], orc_rs_input(send, recv, r), total * es); /* :31-40 */
+    }
+    for (mask = 1, stage = 0; mask < P; mask <<= 1, stage++) { /* :52-168 */
+        /* receive blocks (:71-81): everything outside the partner's subtree */
+        for (r = 0; r < n; r++) {
+            int dst = r ^ mask, dtr = (dst >> stage) << stage;
+            size_t r0 = rc * (size_t)(dtr < P ? dtr : P);
+            size_t r1 = P - (dtr + mask) > 0 ? (size_t)(P - (dtr + mask)) * rc : 0;
+            size_t r1off = r0 + rc * (size_t)(((dtr + mask) < P ? (dtr + mask) : P) - dtr);
+            received[r] = 0;
+            if (dst < P) { /* :98-104: the partner's tmp_results at these blocks (not yet reduced) */
+                memcpy(trecv[r], tmp[dst], r0 * es);
+                memcpy(trecv[r] + r1off * es, tmp[dst] + r1off * es, r1 * es);
+                received[r] = 1;
+            }
+        }
+        if ((P & (P - 1)) != 0) { /* :106-130, level by level (tmp_mask decreasing) */
+            int level_mask, kk = 0, j;
+            for (j = mask; j >>= 1;) kk++;
+            for (level_mask = mask >> 1; level_mask; level_mask >>= 1, kk--) {
+                for (r = 0; r < n; r++) {
+                    int dst = r ^ mask, dtr = (dst >> stage) << stage, mtr = (r >> stage) << stage;
+                    int npc = P - mtr - mask, sd = r ^ level_mask, tree_root = (r >> kk) << kk;
+                    if (!(dtr + mask > P)) continue;
+                    if (sd < r && sd < tree_root + npc && r >= tree_root + npc) {
+                        size_t r0 = rc * (size_t)(dtr < P ? dtr : P);
+                        size_t r1 = P - (dtr + mask) > 0 ? (size_t)(P - (dtr + mask)) * rc : 0;
+                        size_t r1off = r0 + rc * (size_t)(((dtr + mask) < P ? (dtr + mask) : P) - dtr);
+                        memcpy(trecv[r], trecv[sd], r0 * es); /* the relaying rank's recvtype blocks */
+                        memcpy(trecv[r] + r1off * es, trecv[sd] + r1off * es, r1 * es);
+                        received[r] = 1;
+                    }
+                }
+            }
+        }
+        for (r = 0; r < n; r++) { /* :132-155: tmp_results op= received blocks */
+            int dst = r ^ mask, dtr = (dst >> stage) << stage;
+            size_t r0 = rc * (size_t)(dtr < P ? dtr : P);
+            size_t r1 = P - (dtr + mask) > 0 ? (size_t)(P - (dtr + mask)) * rc : 0;
+            size_t r1off = r0 + rc * (size_t)(((dtr + mask) < P ? (dtr + mask) : P) - dtr);
+            if (!received[r]) continue;
+            if (r0) orc_reduce_local(trecv[r], tmp[r], r0, dtype, op);
+            if (r1) orc_reduce_local(trecv[r] + r1off * es, tmp[r] + r1off * es, r1, dtype, op);
+        }
+    }
+    for (r = 0; r < n; r++) memcpy(res[r], tmp[r] + (size_t)r * rc * es, rc * es); /* :171-174 */
+    for (r = 0; r < n; r++) {
+        free(tmp[r]);
+        free(trecv[r]);
+    }
+    free(tmp);
+    free(trecv);
+    free(received);
+    orc_rs_store(n, rc, es, res, recv);
+    return 0;
+}
+
+/* reduce_scatter_radix.cpp:204-377. */
+int orc_reduce_scatter_radix(int n, int k_in, size_t rc, int dtype, int op, const void* const* send,
+                             void* const* recv) {
+    size_t es = orc_dtype_size(dtype), total = rc * (size_t)n;
+    orc_recexch_t* rx;
+    char **tmp, **res;
+    int *cnt, *off, r, i, ph, nph, k;
+    if (n < 1 || !es || k_in < 2) return 1;
+    rx = (orc_recexch_t*)calloc((size_t)n, sizeof(orc_recexch_t));
+    for (r = 0; r < n; r++)
+        if (orc_recexch_neighbors(r, n, k_in, &rx[r])) { /* :230 */
+            free(rx);
+            return 1;
+        }
+    k = rx[0].k;
+    nph = rx[0].step2_nphases;
+    cnt = (int*)calloc((size_t)(nph > 0 ? nph : 1) * (size_t)n, sizeof(int));
+    off = (int*)calloc((size_t)(nph > 0 ? nph : 1) * (size_t)n, sizeof(int));
+    orc_recexch_count_offset(n, nph > 0 ? nph : 1, k, cnt, off);
+    tmp = (char**)calloc((size_t)n, sizeof(char*));
+    res = (char**)calloc((size_t)n, sizeof(char*));
+    for (r = 0; r < n; r++) {
+        tmp[r] = (char*)malloc(total * es + 1);
+        res[r] = (char*)malloc(rc * es + 1);
+        memcpy(tmp[r], orc_rs_input(send, recv, r), total * es); /* :238-244 */
+    }
+    for (r = 0; r < n; r++) /* step 1 (:255-272): the non-participants' whole inputs, recvfrom order */
+        if (rx[r].step1_sendto == -1)
+            for (i = 0; i < rx[r].step1_nrecvs; i++)
+                orc_reduce_local(orc_rs_input(send, recv, rx[r].step1_recvfrom[i]), tmp[r], total, dtype, op);
+    for (ph = nph - 1; ph >= 0; ph--) /* step 2 (:279-318): regions of a phase are disjoint */
+        for (r = 0; r < n; r++) {
+            size_t moff = (size_t)off[ph * n + r] * rc, mlen = (size_t)cnt[ph * n + r] * rc;
+            if (rx[r].step1_sendto != -1) continue;
+            for (i = 0; i < k - 1; i++) {
+                int dst = rx[r].step2_nbrs[ph][i];
+                orc_reduce_local(tmp[dst] + moff * es, tmp[r] + moff * es, mlen, dtype, op);
+            }
+        }
+    for (r = 0; r < n; r++) { /* :321-343 */
+        const int owner = rx[r].step1_sendto == -1 ? r : rx[r].step1_sendto;
+        memcpy(res[r], tmp[owner] + (size_t)r * rc * es, rc * es);
+    }
+    for (r = 0; r < n; r++) free(tmp[r]);
+    free(tmp);
+    free(cnt);
+    free(off);
+    free(rx);
+    orc_rs_store(n, rc, es, res, recv);
+    return 0;
+}

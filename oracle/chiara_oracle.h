@@ -145,6 +145,17 @@ int orc_allreduce_recursive_multiplying(int nranks, int k, size_t count, int dty
 int orc_allreduce_k_reduce_scatter_allgather(int nranks, int k, size_t count, int dtype, int op,
                                              const void* const* send, void* const* recv);
 
+/* MPICH baseline reduce-scatters (block) of testing/mpich_implementations/reduce_scatter/: every
+ * rank's result (rc elements) into recv[r]; send[r] holds n*rc elements (send[r] == NULL: in place,
+ * the input is in recv[r]). */
+int orc_reduce_scatter_pairwise(int n, size_t rc, int dtype, int op, const void* const* send, void* const* recv);
+int orc_reduce_scatter_rec_halving(int n, size_t rc, int dtype, int op, const void* const* send,
+                                   void* const* recv);
+int orc_reduce_scatter_rec_doubling(int n, size_t rc, int dtype, int op, const void* const* send,
+                                    void* const* recv);
+int orc_reduce_scatter_radix(int n, int k, size_t rc, int dtype, int op, const void* const* send,
+                             void* const* recv);
+
 #ifdef __cplusplus
 }
 #endif

@@ -205,3 +205,41 @@ def mpich_allreduce(algo, sends, dtype, op, k=2, inplace=False):
     if rc:
         raise ValueError(f"oracle {algo} rejected (rc={rc})")
     return recvs
+
+
+MPICH_RS_ALGOS = ("rs_radix", "rs_halving", "rs_doubling", "rs_pairwise")
+
+
+def mpich_reduce_scatter(algo, sends, dtype, op, k=2, inplace=False):
+    """All ranks' outputs (recvcount each) of the MPICH baseline reduce-scatter `algo`
+    (testing/mpich_implementations/reduce_scatter/).  sends: n*recvcount elements per rank."""
+    L = lib()
+    vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    if not getattr(L, "_rs_ready", False):
+        for name in ("orc_reduce_scatter_pairwise", "orc_reduce_scatter_rec_halving",
+                     "orc_reduce_scatter_rec_doubling"):
+            fn = getattr(L, name)
+            fn.argtypes = [i, sz, i, i, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+            fn.restype = i
+        L.orc_reduce_scatter_radix.argtypes = [i, i, sz, i, i, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+        L.orc_reduce_scatter_radix.restype = i
+        L._rs_ready = True
+    n = len(sends)
+    rc = sends[0].size // n
+    recvs = [s.copy() for s in sends] if inplace else [np.zeros(rc, dtype=s.dtype) for s in sends]
+    sp = _ptr_array([None] * n) if inplace else _ptr_array(sends)
+    rp = _ptr_array(recvs)
+    d, o = DTYPES[dtype], OPS[op]
+    if algo == "rs_radix":
+        rc_ = L.orc_reduce_scatter_radix(n, k, rc, d, o, sp, rp)
+    elif algo == "rs_halving":
+        rc_ = L.orc_reduce_scatter_rec_halving(n, rc, d, o, sp, rp)
+    elif algo == "rs_doubling":
+        rc_ = L.orc_reduce_scatter_rec_doubling(n, rc, d, o, sp, rp)
+    elif algo == "rs_pairwise":
+        rc_ = L.orc_reduce_scatter_pairwise(n, rc, d, o, sp, rp)
+    else:
+        raise ValueError(algo)
+    if rc_:
+        raise ValueError(f"oracle {algo} rejected (rc={rc_})")
+    return [r[:rc] for r in recvs]

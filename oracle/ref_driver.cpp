@@ -11,8 +11,9 @@
 //
 // Usage: mpiexec -n N ref_driver <cases.txt> <outdir>
 //   one case per line: id mode k b count dtype op pattern seed inplace
-//   mode: ar | rs | ag (radix_batch), ring | rd | rsag | rx | krsag | rm (MPICH baselines; rx and
-//   krsag use b as single_phase_recv)
+//   mode: ar | rs | ag (radix_batch), ring | rd | rsag | rx | krsag | rm (MPICH baseline allreduces;
+//   rx and krsag use b as single_phase_recv), rs_radix | rs_halving | rs_doubling | rs_pairwise
+//   (MPICH baseline reduce-scatters, count = recvcount; rs_radix uses k)
 // For each case rank 0 writes <outdir>/<id>.out (all ranks' outputs, rank-major) and
 // <outdir>/<id>.lib (the MPI library collective's result on the same inputs).
 #include <mpi.h>
@@ -48,6 +49,15 @@ int allgather_radix_batch(char* sendbuf, int sendcount, MPI_Datatype datatype, c
                           int b);
 int MPICH_Allreduce_recursive_multiplying(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype,
                                           MPI_Op op, MPI_Comm comm, int k);
+// testing/mpich_implementations/reduce_scatter/ (the baselines that directory's main.cpp drives)
+int MPICH_reduce_scatter_rec_halving(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+                                     MPI_Comm comm);
+int MPICH_reduce_scatter_rec_doubling(const void* sendbuf, void* recvbuf, MPI_Aint recvcount, MPI_Datatype datatype,
+                                      MPI_Op op, MPI_Comm comm);
+int MPICH_reduce_scatter_radix(const void* sendbuf, void* recvbuf, MPI_Aint recvcount, MPI_Datatype datatype,
+                               MPI_Op op, MPI_Comm comm, int k);
+int MPICH_reduce_scatter_pairwise(const void* sendbuf, void* recvbuf, MPI_Aint recvcount, MPI_Datatype datatype,
+                                  MPI_Op op, MPI_Comm comm);
 
 // orc_reduce_local is the single definition of the bf16 op semantics.
 static void bf16_user_op(void* in, void* inout, int* len, MPI_Datatype*) {
@@ -132,7 +142,8 @@ int main(int argc, char** argv) {
         MPI_Datatype mdt = dtype == ORC_BF16 ? bf16_t : mpi_type_of(dtype);
         MPI_Op mop = dtype == ORC_BF16 ? bf16_ops[op] : std_ops[op];
 
-        size_t in_n = (mode == "rs") ? (size_t)count * nprocs : (size_t)count;
+        const bool rs_mode = mode == "rs" || mode.rfind("rs_", 0) == 0;
+        size_t in_n = rs_mode ? (size_t)count * nprocs : (size_t)count;
         size_t out_n = (mode == "ag") ? (size_t)count * nprocs : (size_t)count;
         std::vector<char> send(in_n * es), recv(in_n * es, 0), lib(out_n * es, 0);
         orc_fill(send.data(), in_n, dtype, pattern, seed, rank, in_n);
@@ -163,6 +174,19 @@ int main(int argc, char** argv) {
             else if (mode == "krsag")
                 MPICH_Allreduce_k_reduce_scatter_allgather(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD, k, b);
             else MPICH_Allreduce_recursive_multiplying(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD, k);
+        } else if (mode.rfind("rs_", 0) == 0) {
+            MPI_Reduce_scatter_block(send.data(), lib.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
+            if (inplace) memcpy(recv.data(), send.data(), in_n * es);
+            MPI_Barrier(MPI_COMM_WORLD);
+            const void* sb = inplace ? MPI_IN_PLACE : (const void*)send.data();
+            if (mode == "rs_radix")
+                MPICH_reduce_scatter_radix(sb, recv.data(), (MPI_Aint)count, mdt, mop, MPI_COMM_WORLD, k);
+            else if (mode == "rs_halving")
+                MPICH_reduce_scatter_rec_halving((const char*)sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
+            else if (mode == "rs_doubling")
+                MPICH_reduce_scatter_rec_doubling(sb, recv.data(), (MPI_Aint)count, mdt, mop, MPI_COMM_WORLD);
+            else
+                MPICH_reduce_scatter_pairwise(sb, recv.data(), (MPI_Aint)count, mdt, mop, MPI_COMM_WORLD);
         } else {
             MPI_Reduce_scatter_block(send.data(), lib.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
             if (inplace) memcpy(recv.data(), send.data(), in_n * es);

@@ -55,3 +55,18 @@ def golden_types():
         manifest = json.load(f)
     arrays = np.load(os.path.join(here, "types_outputs.npz"), allow_pickle=False)
     return manifest["cases"], arrays
+
+
+@pytest.fixture(scope="session")
+def golden_rsmpich():
+    """Golden vectors of the MPICH baseline reduce-scatters that
+    testing/mpich_implementations/reduce_scatter/main.cpp drives (gen_golden.py rsmpich)."""
+    import json
+
+    import numpy as np
+
+    here = os.path.join(REPO, "tests", "golden")
+    with open(os.path.join(here, "rsmpich_manifest.json")) as f:
+        manifest = json.load(f)
+    arrays = np.load(os.path.join(here, "rsmpich_outputs.npz"), allow_pickle=False)
+    return manifest["cases"], arrays

@@ -198,6 +198,39 @@ def types_cases_for(n):
     return out
 
 
+def rsmpich_cases_for(n):
+    """testing/mpich_implementations/reduce_scatter/: radix (k), recursive halving, recursive
+    doubling (relays for non-powers of two) and pairwise, driven by that directory's main.cpp
+    (MPI_DOUBLE, MPI_SUM, MPI_Reduce_scatter_block semantics; count = recvcount)."""
+    out = []
+
+    def add(mode, k, count, dt, op, pat, inplace):
+        cid = f"{mode}_n{n}_k{k}_c{count}_{dt}_{op}_p{pat}_ip{inplace}"
+        out.append(dict(id=cid, mode=mode, n=n, k=k, b=0, count=count, dtype=dt, op=op,
+                        pattern=pat, seed=SEED, inplace=inplace))
+
+    for mode in ("rs_halving", "rs_doubling", "rs_pairwise"):
+        for count in (1, 7, 33):
+            add(mode, 0, count, "f64", "sum", pyoracle.PAT_UNIFORM, 0)  # the harness's datatype
+            add(mode, 0, count, "f32", "sum", pyoracle.PAT_UNIFORM, count % 2)
+        add(mode, 0, 16, "i32", "sum", pyoracle.PAT_SEQ, 0)
+        add(mode, 0, 16, "bf16", "sum", pyoracle.PAT_UNIFORM, 0)
+        add(mode, 0, 16, "f32", "max", pyoracle.PAT_TIES, 0)
+        add(mode, 0, 16, "f64", "min", pyoracle.PAT_TIES, 1)
+        add(mode, 0, 16, "bf16", "max", pyoracle.PAT_TIES, 1)
+        add(mode, 0, 16, "i64", "bxor", pyoracle.PAT_UNIFORM, 0)
+    for k in (2, 3, 4, 5, 8):
+        for count in (1, 13):
+            add("rs_radix", k, count, "f64", "sum", pyoracle.PAT_UNIFORM, 0)
+            add("rs_radix", k, count, "f32", "sum", pyoracle.PAT_UNIFORM, 1)
+        add("rs_radix", k, 16, "i32", "sum", pyoracle.PAT_SEQ, 0)
+        add("rs_radix", k, 16, "bf16", "sum", pyoracle.PAT_UNIFORM, 0)
+        add("rs_radix", k, 16, "f32", "max", pyoracle.PAT_TIES, 0)
+        add("rs_radix", k, 16, "f64", "min", pyoracle.PAT_TIES, 1)
+        add("rs_radix", k, 16, "u16", "land", pyoracle.PAT_SPARSE, 0)
+    return out
+
+
 def run_n(n, cases, tmp):
     cf = os.path.join(tmp, f"cases_{n}.txt")
     with open(cf, "w") as f:
@@ -219,6 +252,10 @@ def main():
         for n in (1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 16):
             all_cases += mpich_cases_for(n)
         prefix = "mpich_"
+    elif which == "rsmpich":
+        for n in (1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 16):
+            all_cases += rsmpich_cases_for(n)
+        prefix = "rsmpich_"
     elif which == "types":
         for n in (2, 3, 4, 6, 8):
             all_cases += types_cases_for(n)
@@ -267,7 +304,10 @@ def main():
                 arrays[c["id"]] = a.copy()
                 arrays[c["id"] + "__lib"] = lb.copy()
             manifest.append(rec)
-    ref_desc = ("Fugaku_experiments/{Allreduce,Reduce-scatter,Allgather} + testing/mpich_implementations/"
+    ref_desc = ("testing/mpich_implementations/reduce_scatter/{reduce_scatter_radix,"
+                "reduce_scatter_recursive_halving,reduce_scatter_recursive_doubling,reduce_scatter_pairwise}.cpp"
+                if which == "rsmpich" else
+                "Fugaku_experiments/{Allreduce,Reduce-scatter,Allgather} + testing/mpich_implementations/"
                 "all_reduce/{allreduce_ring,allreduce_recexch,allreduce_recursive_multiplying}.cpp, integer types "
                 "beyond int32 and the logical/bitwise ops" if which == "types" else
                 "testing/mpich_implementations/all_reduce/{allreduce_ring,allreduce_recursive_doubling,"

@@ -119,11 +119,12 @@ def execute(plans, sends, dtype, rop, inplace=False):
 
 def simulate(mode, sends, k, b, dtype, op, inplace=False, slices=1, schedule=None):
     n = len(sends)
-    count = sends[0].size // n if mode == ca.MODE_REDUCE_SCATTER else sends[0].size
+    rs = mode in ca.RS_MODES
+    count = sends[0].size // n if rs else sends[0].size
     plans = load_plans(mode, n, k, b, count, slices, schedule)
     if plans[0]["header"]["error"]:
         raise ValueError(f"plan error {plans[0]['header']['error']}")
     outs = execute(plans, sends, dtype, op, inplace)
-    if mode == ca.MODE_REDUCE_SCATTER:
+    if rs:
         outs = [o[:count] for o in outs]
     return outs

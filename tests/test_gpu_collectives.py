@@ -461,3 +461,44 @@ def test_tiny_ragged_and_empty_every_schedule(gu, groups, schedule):
     finally:
         for g in (g8, g6):
             g.set_schedule(ca.SCHEDULE_FLAT)
+
+
+RS_MODE = {"rs_radix": ca.MODE_MPICH_RS_RADIX, "rs_halving": ca.MODE_MPICH_RS_HALVING,
+           "rs_doubling": ca.MODE_MPICH_RS_DOUBLING, "rs_pairwise": ca.MODE_MPICH_RS_PAIRWISE}
+
+
+def test_mpich_reduce_scatter_baselines_match_reference_golden(gu, groups, golden_rsmpich):
+    """The four baselines testing/mpich_implementations/reduce_scatter/main.cpp times (radix,
+    recursive halving, recursive doubling with relays, pairwise): every golden case of the
+    reference's own code bit-exact on the device, in place and not."""
+    cases, _ = golden_rsmpich
+    bad = []
+    for c in cases:
+        n = c["n"]
+        npdt = po.NP_DTYPES[c["dtype"]]
+        sends = [po.fill(c["count"] * n, c["dtype"], c["pattern"], c["seed"], r) for r in range(n)]
+        d_send = [gu.to_dev(x) for x in sends]
+        if c["inplace"]:
+            d_recv, d_sendp = d_send, [ca.IN_PLACE] * n
+        else:
+            d_recv, d_sendp = [gu.empty_dev(c["count"] * x.itemsize) for x in sends], d_send
+        rc = groups(n).reduce_scatter_mpich(RS_MODE[c["mode"]], d_sendp, d_recv, c["count"], DT[c["dtype"]],
+                                           OP[c["op"]], c["k"])
+        assert rc == 0, (c["id"], rc)
+        outs = [gu.from_dev(d, npdt, c["count"]) for d in d_recv]
+        if hashlib.sha256(b"".join(o.tobytes() for o in outs)).hexdigest() != c["sha256"]:
+            bad.append(c["id"])
+    assert not bad, f"{len(bad)} device/reference mismatches, e.g. {bad[:5]}"
+
+
+@pytest.mark.parametrize("algo", sorted(RS_MODE))
+def test_mpich_reduce_scatter_baselines_large(gu, groups, algo):
+    """6 ranks (non-power of two: folds and relays), 4 MiB fp32 blocks: bit-exact vs the oracle."""
+    n, rc = 6, (1 << 20) + 3
+    sends = [po.fill(rc * n, "f32", po.PAT_UNIFORM, 77, r) for r in range(n)]
+    want = po.mpich_reduce_scatter(algo, sends, "f32", "sum", k=3)
+    d_send = [gu.to_dev(x) for x in sends]
+    d_recv = [gu.empty_dev(rc * 4) for _ in range(n)]
+    assert groups(n).reduce_scatter_mpich(RS_MODE[algo], d_send, d_recv, rc, ca.FLOAT32, ca.SUM, 3) == 0
+    for r in range(n):
+        np.testing.assert_array_equal(gu.from_dev(d_recv[r], np.float32, rc).view(np.uint32), want[r].view(np.uint32))

@@ -50,7 +50,7 @@ def _worker(rank, world, port, cases, q):
             inplace = len(extra) > 2 and extra[2]
             npdt = po.NP_DTYPES[dtype]
             cdt = {"f32": ca.FLOAT32, "bf16": ca.BFLOAT16, "i32": ca.INT32}[dtype]
-            in_n = count * world if mode == "rs" else count
+            in_n = count * world if (mode == "rs" or mode.startswith("rs_")) else count
             out_n = count * world if mode == "ag" else count
             pat = po.PAT_TIES if mode == "rx" else 0  # recexch: operand-order sensitive data, MAX
             x = po.fill(in_n, dtype, pat, 4242, rank)
@@ -72,6 +72,13 @@ def _worker(rank, world, port, cases, q):
                 rc = fn(send, dst, count, cdt, ca.SUM, comm, k, b)
                 f = po.allreduce_radix_batch if mode == "ar" else po.reduce_scatter_radix_batch
                 ref = f(allx, k, b, dtype, "sum")[rank]
+            elif mode.startswith("rs_"):
+                rc = {"rs_radix": lambda: ca.MPICH_reduce_scatter_radix(send, dst, count, cdt, ca.SUM, comm, k),
+                      "rs_halving": lambda: ca.MPICH_reduce_scatter_rec_halving(send, dst, count, cdt, ca.SUM, comm),
+                      "rs_doubling": lambda: ca.MPICH_reduce_scatter_rec_doubling(send, dst, count, cdt, ca.SUM, comm),
+                      "rs_pairwise": lambda: ca.MPICH_reduce_scatter_pairwise(send, dst, count, cdt, ca.SUM, comm)
+                      }[mode]()
+                ref = po.mpich_reduce_scatter(mode, allx, dtype, "sum", k=k)[rank]
             elif mode == "rx":
                 rc = ca.MPICH_Allreduce_recursive_exchange(send, dst, count, cdt, ca.MAX, comm, k, b)
                 ref = po.mpich_allreduce("rx", allx, dtype, "max", k=k)[rank]
@@ -141,6 +148,18 @@ def test_rccl_mpich_baselines_world5_and_8():
     _run(5, cases)
     _run(8, cases[:1] + [("rx", 4, 0, 1 << 16, "f32", False, 0), ("rsag", 0, 0, 1 << 16, "bf16", False, 0),
                          ("krsag", 2, 1, 1 << 16, "f32", False, 0), ("rm", 3, 0, 12345, "bf16", False, 0)],
+         timeout=600)
+
+
+def test_rccl_mpich_reduce_scatter_baselines_world5_and_8():
+    """testing/mpich_implementations/reduce_scatter/'s four baselines over RCCL: 5 ranks (folds,
+    recursive doubling's relays) and 8, host-staged and device buffers: bit-exact vs the oracle."""
+    cases = [("rs_radix", 3, 0, 4099, "f32", False, 0), ("rs_halving", 0, 0, 1001, "f32", False, 0),
+             ("rs_doubling", 0, 0, 777, "bf16", False, 0), ("rs_pairwise", 0, 0, 3000, "f32", True, 0),
+             ("rs_radix", 2, 0, 64, "i32", True, 0)]
+    _run(5, cases)
+    _run(8, [("rs_radix", 4, 0, 1 << 14, "f32", False, 0), ("rs_doubling", 0, 0, 5000, "f32", False, 0),
+             ("rs_halving", 0, 0, 4096, "bf16", True, 0), ("rs_pairwise", 0, 0, 1 << 14, "f32", False, 0)],
          timeout=600)
 
 
@@ -263,7 +282,7 @@ def _graph_worker(rank, world, port, q):
             comm.set_schedule(sched)
             comm.set_overlap(ov)
             cdt = {"f32": ca.FLOAT32, "bf16": ca.BFLOAT16}[dtype]
-            in_n = count * world if mode == "rs" else count
+            in_n = count * world if (mode == "rs" or mode.startswith("rs_")) else count
             es = 4 if dtype == "f32" else 2
             send = torch.empty(in_n * es, dtype=torch.uint8, device=dev)
             out_t = torch.empty(count * es, dtype=torch.uint8, device=dev)

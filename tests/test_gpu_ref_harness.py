@@ -18,7 +18,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MPIEXEC = "/opt/conda/bin/mpiexec"
 
 
-def _run(binary, args, n, tmp_path, where=("oracle", "_ref")):
+def _run(binary, args, n, tmp_path, where=("oracle", "_ref"), prefix="results"):
     exe = os.path.join(REPO, *where, binary)
     if not os.path.exists(exe) or not os.path.exists(MPIEXEC):
         pytest.skip("reference harness binary or MPICH not present")
@@ -30,7 +30,7 @@ def _run(binary, args, n, tmp_path, where=("oracle", "_ref")):
                 "-env", "NCCL_IB_DISABLE", "1", exe] + args
     out = subprocess.run(cmd, cwd=tmp_path, capture_output=True, text=True, timeout=400)
     assert out.returncode == 0, out.stderr[-3000:]
-    files = [f for f in os.listdir(tmp_path) if f.startswith("results") and f.endswith(".csv")]
+    files = [f for f in os.listdir(tmp_path) if f.startswith(prefix) and f.endswith(".csv")]
     assert len(files) == 1, files
     with open(os.path.join(tmp_path, files[0])) as f:
         return list(csv.DictReader(f))
@@ -71,6 +71,18 @@ def test_reference_mpich_baseline_harness_on_mi355x(tmp_path):
                      "reduce_scatter_allgather", "ring", "recursive_doubling"}
     assert len(rows) == 3 * (3 * 3 + 3) * 50  # sizes x (k in 2..4 x 3 + 3 without k) x reps
     assert {r["send_count"] for r in rows} == {"8", "16", "32"}
+    assert all(r["is_correct"] == "1" for r in rows)
+
+
+def test_reference_mpich_reduce_scatter_harness_on_mi355x(tmp_path):
+    """testing/mpich_implementations/reduce_scatter/main.cpp unchanged: MPICH_reduce_scatter_radix at
+    k = 2, 4, .., 30 (clamped to the 4 ranks), recursive halving, recursive doubling, pairwise and
+    MPI_Reduce_scatter_block, 50 reps per size, check_correctness on doubles (eps 1e-9)."""
+    rows = _run("ref_harness_rs_testing", ["2", "--overwrite"], 4, tmp_path, prefix="reduce_scatter_results")
+    names = {r["algorithm_name"] for r in rows}
+    assert names == {"MPICH_reduce_scatter_radix", "MPICH_reduce_scatter_rec_halving",
+                     "MPICH_reduce_scatter_rec_doubling", "MPICH_reduce_scatter_pairwise", "MPI_Reduce_scatter_block"}
+    assert len(rows) == 2 * (15 + 4) * 50  # sizes x (k = 2..30 step 2, four without k) x reps
     assert all(r["is_correct"] == "1" for r in rows)
 
 

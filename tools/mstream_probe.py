@@ -4,7 +4,8 @@ reduction (chr_reduce_multi, in place, fp32 SUM) at m in {1, 3, 7} incoming buck
 sizes 256 MiB .. 1 GiB, with the m + 1 operands laid out four ways:
   sep      one torch allocation per operand (the earlier sweep's layout)
   slab     one allocation, operands back to back (operand j at j * bucket)
-  slab+d   one allocation, operand j at j * (bucket + d): d = 4 KiB, 64 KiB, 2 MiB + 4 KiB
+  slab+d   one allocation, operand j at j * (bucket + d): d = 4 KiB, 64 KiB, 2 MiB + 4 KiB, and
+           64 / 96 / 192 / 320 MiB (moving the operands' high address bits apart)
 HBM-cold: at least 2 GiB of distinct data per rotation (buffer sets cycled).  Prints one JSON line
 per (m, bucket, layout): us per call and algorithmic GB/s ((m + 2) * bucket bytes).
 Usage: mstream_probe.py [--ms 1,3,7] [--mib 256,512,1024] [--layouts sep,slab,...] [--reps N]"""
@@ -20,7 +21,8 @@ import torch  # noqa: E402
 
 import chiara_amd as ca  # noqa: E402
 
-DELTAS = {"slab": 0, "slab+4k": 4 << 10, "slab+64k": 64 << 10, "slab+2m4k": (2 << 20) + (4 << 10)}
+DELTAS = {"slab": 0, "slab+4k": 4 << 10, "slab+64k": 64 << 10, "slab+2m4k": (2 << 20) + (4 << 10),
+          "slab+64m": 64 << 20, "slab+192m": 192 << 20, "slab+320m": 320 << 20, "slab+96m4k": (96 << 20) + (4 << 10)}
 
 
 def main():

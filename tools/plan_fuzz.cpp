@@ -52,8 +52,10 @@ int main(int argc, char** argv) {
             ++g_bad;
         }
     long plans = 0;
-    const int modes[] = {MODE_ALLREDUCE, MODE_REDUCE_SCATTER, MODE_ALLGATHER, MODE_MPICH_RING, MODE_MPICH_RD,
-                         MODE_MPICH_RSAG, MODE_MPICH_RECEXCH, MODE_MPICH_KRSAG, MODE_MPICH_RMULT};
+    const int modes[] = {MODE_ALLREDUCE,         MODE_REDUCE_SCATTER,    MODE_ALLGATHER,        MODE_MPICH_RING,
+                         MODE_MPICH_RD,          MODE_MPICH_RSAG,        MODE_MPICH_RECEXCH,    MODE_MPICH_KRSAG,
+                         MODE_MPICH_RMULT,       MODE_MPICH_RS_RADIX,    MODE_MPICH_RS_HALVING, MODE_MPICH_RS_DOUBLING,
+                         MODE_MPICH_RS_PAIRWISE};
     for (int mode : modes)
         for (int n = 1; n <= max_n; ++n)
             for (int b = 1; b <= n; ++b) {
