@@ -1,0 +1,61 @@
+#!/bin/bash
+# One script for every GPU-box session (replaces the per-call tools/gpu_*.sh of rounds 1-2).
+#
+#   gpurun --timeout 1200 -- bash tools/gpu.sh STEP [STEP ...]
+#
+# Steps run in the order given; each GPU step has its own time limit and the first failure
+# (test failure, fault, abort, time limit) ends the script, so nothing more touches the GPU.
+#   suite      the whole -m gpu suite, as the driver runs it    -> pytest_suite.txt
+#   tests      the pytest node ids in $TESTS                     -> pytest_${TAG:-tests}.txt
+#   smoke      __graft_entry__.smoke()                           -> smoke.txt
+#   bench      bench.py at the driver's settings (20 / 5)        -> bench.json
+#   bench200   bench.py --steps 200 --warmup 20                  -> bench200.json
+#   prof       rocprofv3 kernel trace + stats of the bench (csv) -> prof/
+#   pmc        FETCH_SIZE and WRITE_SIZE passes of the bench     -> pmc_FETCH_SIZE/, pmc_WRITE_SIZE/
+#   kernels    bench.py --collective-kernels (C4/C5 in-collective kernel rows) -> collective_kernels.json
+#   probe      tools/mstream_probe.py $PROBE_ARGS               -> mstream_probe.jsonl
+#   tree       tools/tree_bench.py $TREE_ARGS                   -> tree_bench.json
+#   rehearse   the N>1 bench line with ${N:-4} ranks sharing the one GPU (socket transport;
+#              exercises the code path, its GB/s mean nothing)  -> bench_n${N}_rehearsal.json
+# Everything lands under gpurun_out/.
+set -u -o pipefail
+cd "$(dirname "$0")/.."
+OUT=gpurun_out
+mkdir -p $OUT
+export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
+PYT="python -u -m pytest -x -q --timeout-method thread"
+
+run() {  # run <seconds> <log> cmd...: the step's own limit; stop the script on failure
+  local secs=$1 log=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "$OUT/$log" 2> "$OUT/$log.err"
+  local rc=$?
+  echo "[$(date +%T)] $log rc=$rc"
+  if [ $rc -ne 0 ]; then tail -20 "$OUT/$log" "$OUT/$log.err"; exit $rc; fi
+}
+
+for step in "$@"; do
+  case "$step" in
+  suite) run 1100 pytest_suite.txt $PYT --timeout 900 -m gpu tests/ ;;
+  tests) run "${TEST_LIMIT:-900}" "pytest_${TAG:-tests}.txt" $PYT -v --timeout 600 -m gpu ${TESTS:?set TESTS} ;;
+  smoke) run 300 smoke.txt python -c "import __graft_entry__ as g; g.smoke()" ;;
+  bench) run 300 bench.json python bench.py --steps 20 --warmup 5 ;;
+  bench200) run 300 bench200.json python bench.py --steps 200 --warmup 20 --no-cpu-baseline ;;
+  prof) run 300 prof_bench.json rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof" -o run \
+          -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline ;;
+  pmc)
+    for ctr in FETCH_SIZE WRITE_SIZE; do
+      run 300 "pmc_$ctr.json" rocprofv3 --pmc $ctr --output-format csv -d "$PWD/$OUT/pmc_$ctr" -o run \
+        -- python3 bench.py --steps 40 --warmup 5 --no-cpu-baseline
+    done ;;
+  kernels) run 400 collective_kernels.json python bench.py --collective-kernels ;;
+  probe) run 400 mstream_probe.jsonl python tools/mstream_probe.py ${PROBE_ARGS:-} ;;
+  tree) run 400 tree_bench.json python tools/tree_bench.py ${TREE_ARGS:-} ;;
+  rehearse)
+    n=${N:-4}
+    CHR_BENCH_VIRTUAL_HOSTS=1 run 600 "bench_n${n}_rehearsal.json" python -m torch.distributed.run --nnodes=1 \
+      --nproc-per-node "$n" --master-addr 127.0.0.1 --master-port 29731 bench.py --gpus "$n" --steps 3 --warmup 1 \
+      --count $((1 << 21)) ;;
+  *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo ALL_DONE

@@ -6,6 +6,8 @@ sizes 256 MiB .. 1 GiB, with the m + 1 operands laid out four ways:
   slab     one allocation, operands back to back (operand j at j * bucket)
   slab+d   one allocation, operand j at j * (bucket + d): d = 4 KiB, 64 KiB, 2 MiB + 4 KiB, and
            64 / 96 / 192 / 320 MiB (moving the operands' high address bits apart)
+  sep/sN   as sep, but each call issued as N back-to-back launches over consecutive 1/N pieces
+           (bounds how far the in-flight workgroups of one launch can drift apart)
 HBM-cold: at least 2 GiB of distinct data per rotation (buffer sets cycled).  Prints one JSON line
 per (m, bucket, layout): us per call and algorithmic GB/s ((m + 2) * bucket bytes).
 Usage: mstream_probe.py [--ms 1,3,7] [--mib 256,512,1024] [--layouts sep,slab,...] [--reps N]"""
@@ -42,7 +44,7 @@ def main():
             for lay in a.layouts.split(","):
                 bufs, keep = [], []
                 for si in range(sets):
-                    if lay == "sep":
+                    if lay.split("/")[0] == "sep":
                         ops = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(m + 1)]
                         keep.append(ops)
                         ptrs = [t.data_ptr() for t in ops]
@@ -56,9 +58,17 @@ def main():
                     bufs.append(ptrs)
                 torch.cuda.synchronize()
 
+                split = int(lay.split("/s")[1]) if "/s" in lay else 1
+                piece = ((n + split - 1) // split + 255) // 256 * 256
+
                 def go(i):
                     p = bufs[i % sets]
-                    return ca.reduce_multi(p[0], p[0], p[1:], n, ca.FLOAT32, ca.SUM, s)
+                    rc = 0
+                    for o in range(0, n, piece):
+                        c = min(piece, n - o)
+                        rc = rc or ca.reduce_multi(p[0] + 4 * o, p[0] + 4 * o, [q + 4 * o for q in p[1:]], c,
+                                                   ca.FLOAT32, ca.SUM, s)
+                    return rc
 
                 for i in range(2):
                     ca.check(go(i))
