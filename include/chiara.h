@@ -152,7 +152,8 @@ int chr_comm_size(const chr_comm* comm, int* nranks);
 int chr_comm_stream(const chr_comm* comm, hipStream_t* stream);
 /* Pipeline depth of the schedules: every chunk is cut into `slices` element slices and
  * consecutive phases of different slices share one RCCL group (different xGMI links
- * busy at once).  0 = automatic (~64 MiB per slice message, up to 8; env CHR_SLICES).
+ * busy at once).  0 = automatic (~64 MiB per slice message, up to 8; the flat schedules stop
+ * where an evaluated piece would drop below 16 MiB, e.g. 4 at C4/C5; env CHR_SLICES).
  * Results are bit-identical for every depth. */
 int chr_comm_set_slices(chr_comm* comm, int slices);
 /* Where the radix/batch reductions are evaluated.  The result bits never depend on it: every

@@ -6,11 +6,13 @@ sizes 256 MiB .. 1 GiB, with the m + 1 operands laid out four ways:
   slab     one allocation, operands back to back (operand j at j * bucket)
   slab+d   one allocation, operand j at j * (bucket + d): d = 4 KiB, 64 KiB, 2 MiB + 4 KiB, and
            64 / 96 / 192 / 320 MiB (moving the operands' high address bits apart)
+  contig   one hipExtMallocWithFlags(hipDeviceMallocContiguous) per operand (physically contiguous:
+           can the page tables map it with larger fragments?)
   sep/sN   as sep, but each call issued as N back-to-back launches over consecutive 1/N pieces
            (bounds how far the in-flight workgroups of one launch can drift apart)
 HBM-cold: at least 2 GiB of distinct data per rotation (buffer sets cycled).  Prints one JSON line
 per (m, bucket, layout): us per call and algorithmic GB/s ((m + 2) * bucket bytes).
-Usage: mstream_probe.py [--ms 1,3,7] [--mib 256,512,1024] [--layouts sep,slab,...] [--reps N]"""
+Usage: mstream_probe.py [--ms 1,3,7] [--mib 256,512,1024] [--layouts sep,slab,...] [--reps N] [--sets 1,2,4]"""
 import argparse
 import json
 import os
@@ -18,6 +20,8 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "configurable-hierarchical-allreduce-algorithms_amd")]
+
+import ctypes  # noqa: E402
 
 import torch  # noqa: E402
 
@@ -27,12 +31,35 @@ DELTAS = {"slab": 0, "slab+4k": 4 << 10, "slab+64k": 64 << 10, "slab+2m4k": (2 <
           "slab+64m": 64 << 20, "slab+192m": 192 << 20, "slab+320m": 320 << 20, "slab+96m4k": (96 << 20) + (4 << 10)}
 
 
+def _hip():
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+    lib.hipExtMallocWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+    lib.hipFree.argtypes = [ctypes.c_void_p]
+    return lib
+
+
+class Contig:
+    """hipExtMallocWithFlags(..., hipDeviceMallocContiguous = 0x4)."""
+
+    def __init__(self, nbytes):
+        self.lib = _hip()
+        p = ctypes.c_void_p()
+        rc = self.lib.hipExtMallocWithFlags(ctypes.byref(p), nbytes, 0x4)
+        if rc != 0:
+            raise RuntimeError(f"hipExtMallocWithFlags contiguous rc={rc}")
+        self.ptr = p.value
+
+    def __del__(self):
+        self.lib.hipFree(self.ptr)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ms", default="1,3,7")
     ap.add_argument("--mib", default="256,512,1024")
     ap.add_argument("--layouts", default="sep,slab,slab+4k,slab+64k,slab+2m4k")
     ap.add_argument("--reps", type=int, default=12)
+    ap.add_argument("--sets", default="", help="buffer sets to rotate over (comma list; default: >= 2 GiB)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     s = torch.cuda.current_stream(dev)
@@ -40,11 +67,15 @@ def main():
         for mib in [int(x) for x in a.mib.split(",")]:
             nbytes = mib << 20
             n = nbytes // 4
-            sets = max(1, min(4, (2048 << 20) // ((m + 1) * nbytes)))
-            for lay in a.layouts.split(","):
+            auto = max(1, min(4, (2048 << 20) // ((m + 1) * nbytes)))
+            for lay, sets in [(x, int(y)) for x in a.layouts.split(",") for y in (a.sets.split(",") if a.sets else [auto])]:
                 bufs, keep = [], []
                 for si in range(sets):
-                    if lay.split("/")[0] == "sep":
+                    if lay.split("/")[0] == "contig":
+                        ops = [Contig(nbytes) for _ in range(m + 1)]
+                        keep.append(ops)
+                        ptrs = [o.ptr for o in ops]
+                    elif lay.split("/")[0] == "sep":
                         ops = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(m + 1)]
                         keep.append(ops)
                         ptrs = [t.data_ptr() for t in ops]
@@ -84,6 +115,7 @@ def main():
                 print(json.dumps({"m": m, "bucket_MiB": mib, "layout": lay, "sets": sets, "us": round(us, 2),
                                   "GBps": round(gbps, 1), "frac": round(gbps / 8000, 4)}), flush=True)
                 del bufs, keep
+                torch.cuda.synchronize()
                 torch.cuda.empty_cache()
 
 
