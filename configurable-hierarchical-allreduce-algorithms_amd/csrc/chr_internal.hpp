@@ -45,7 +45,9 @@ hipError_t launch_fill(void* buf, size_t n, int dtype, int pattern, uint64_t see
                        uint64_t count_for_seq, hipStream_t stream);
 
 // Tunables (read once from the environment):
-//   CHR_REDUCE_MAX_BLOCKS    cap on the grid (default 0 = one trip per workgroup)
+//   CHR_XCD_RUN_KIB          streaming (NT) calls: KiB of consecutive trips each XCD takes before
+//                            the next XCD's run (0 = plain round-robin); unset = policy
+//                            (xcd_run_shift in reduce_common.hpp)
 //   CHR_REDUCE_NT            0 / 1 forces plain / non-temporal loads+stores; unset = by size
 //   CHR_REDUCE_NT_MIN_BYTES  bytes streamed by one call from which NT is used (128 MiB)
 //   CHR_REDUCE_ACC0          0 / 1 forces the first accumulator slot nt / default policy
@@ -54,7 +56,7 @@ hipError_t launch_fill(void* buf, size_t n, int dtype, int pattern, uint64_t see
 //   CHR_REDUCE_BLOCK         threads per workgroup of the vector kernels: 64 or 256;
 //                            unset = 64 for NT calls, 256 otherwise
 struct ReduceTuning {
-    int max_blocks;
+    int xcd_run_kib;  // -1: policy
     int block;
     int nt_mode;
     size_t nt_min_bytes;

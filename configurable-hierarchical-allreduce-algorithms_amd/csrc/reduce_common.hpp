@@ -126,6 +126,33 @@ __device__ __forceinline__ u32x4 apply_vec(u32x4 in, u32x4 acc) {
     return r;
 }
 
+// ---- XCD-aware workgroup -> trip map -----------------------------------------------------
+// Workgroups are dispatched round-robin over the 8 XCDs (block b runs on XCD b % 8).  Every
+// kernel here does one trip (BL x U vectors per operand) per workgroup.  With the identity map
+// the 8 XCDs interleave at trip granularity (1-4 KiB); xcd_trip gives each XCD runs of C = 2^cs
+// consecutive trips instead: block b's (b / 8)-th trip goes to run (b / 8) / C of XCD b % 8, and
+// XCD x owns runs x, x + 8, x + 16, ...  Blocks past the last whole 8·C group keep the identity,
+// so the map is a bijection on [0, n).  Runs of 256-512 KiB measured +2-4 % on HBM-cold
+// streams (tools/reduce_microbench focus8/focus9, profiles/r02/microbench_focus9_xcd_runs.txt):
+// each XCD's translation caches and DRAM pages see fewer distinct pages per unit time, while
+// the 8 XCDs still stream within a few MiB of each other.
+__device__ __forceinline__ size_t xcd_trip(uint32_t b, uint32_t n, uint32_t cs) {
+    const uint32_t full = n & ~((8u << cs) - 1u);
+    if (b >= full) return b;
+    const uint32_t x = b & 7u, i = b >> 3;
+    return ((((size_t)(i >> cs)) * 8u + x) << cs) | (i & ((1u << cs) - 1u));
+}
+
+// log2 of the trips in one XCD run for a launch of `trip_bytes` per operand per workgroup:
+// CHR_XCD_RUN_KIB if set, else `policy_kib` (0 = identity map).
+inline uint32_t xcd_run_shift(size_t policy_kib, size_t trip_bytes) {
+    const int env = reduce_tuning().xcd_run_kib;
+    const size_t kib = env >= 0 ? (size_t)env : policy_kib;
+    uint32_t cs = 0;
+    while (((size_t)2 << cs) * trip_bytes <= kib * 1024 && cs < 16) ++cs;
+    return cs;
+}
+
 template <bool NT>
 __device__ __forceinline__ u32x4 ld(const u32x4* p) {
     if constexpr (NT) return __builtin_nontemporal_load(p);

@@ -94,8 +94,8 @@ static bool in_core_tu(int kdt, int kop) {
 ReduceTuning& reduce_tuning() {
     static ReduceTuning t = [] {
         ReduceTuning r;
-        const char* s = std::getenv("CHR_REDUCE_MAX_BLOCKS");
-        r.max_blocks = s ? std::atoi(s) : 0;  // 0: one trip per workgroup (full grid)
+        const char* s = std::getenv("CHR_XCD_RUN_KIB");
+        r.xcd_run_kib = s ? std::atoi(s) : -1;  // -1: policy (vec_xcd_run_kib / tree_xcd_run_kib)
         s = std::getenv("CHR_REDUCE_NT");     // 0 / 1 / unset = by size
         r.nt_mode = s ? std::atoi(s) : -1;
         s = std::getenv("CHR_REDUCE_NT_MIN_BYTES");

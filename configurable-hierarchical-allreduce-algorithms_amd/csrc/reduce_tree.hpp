@@ -47,7 +47,12 @@ struct TreeArgs {
     TreeSeg seg[kMaxTreeSegs];
     int nseg;
     int nl;
+    uint32_t xrun;  // log2 of the trips per XCD run within a segment (xcd_trip); set by the launcher
 };
+
+// A segment's vector body is at most this many 16-B vectors (1 GiB per operand); longer trees are
+// cut into several segments, so a grid stays far below 2^31 threads.
+constexpr size_t kMaxSegVec = (size_t)1 << 26;
 
 template <int OP>
 constexpr int swapped_op() {
@@ -103,7 +108,9 @@ struct ScalarOp {
 };
 
 // U vectors per lane per trip for NL leaves: every leaf load of the trip is issued before
-// the first combine (NL * U <= 16 loads of 16 B in flight per lane).
+// the first combine (NL * U <= 16 loads of 16 B in flight per lane).  One trip per workgroup;
+// within its segment a workgroup's trip is placed by xcd_trip (the segment's first block may sit
+// anywhere in the 8-XCD rotation: blocks of one local residue class still share one XCD).
 template <int DT, int OP, int NL, int U, bool NT, int BL>
 __global__ __launch_bounds__(BL) void k_reduce_tree(TreeArgs a) {
     // this workgroup's segment (uniform: scalar loads of the kernel arguments)
@@ -112,30 +119,28 @@ __global__ __launch_bounds__(BL) void k_reduce_tree(TreeArgs a) {
         if (blockIdx.x >= a.seg[j].block0) s = j;
     const TreeSeg& g = a.seg[s];
     const uint32_t nblk = (s + 1 < a.nseg ? a.seg[s + 1].block0 : gridDim.x) - g.block0;
-    const size_t stride = (size_t)nblk * BL * U;
-    for (size_t base = (size_t)(blockIdx.x - g.block0) * BL * U + threadIdx.x; base < g.nvec; base += stride) {
-        if (base + (size_t)(U - 1) * BL < g.nvec) {
-            u32x4 x[NL][U];
+    const size_t base = xcd_trip(blockIdx.x - g.block0, nblk, a.xrun) * BL * U + threadIdx.x;
+    if (base + (size_t)(U - 1) * BL < g.nvec) {
+        u32x4 x[NL][U];
 #pragma unroll
-            for (int j = 0; j < NL; ++j)
+        for (int j = 0; j < NL; ++j)
 #pragma unroll
-                for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&g.leaves[j][base + (size_t)u * BL]);
-            __builtin_amdgcn_sched_barrier(0);
-            u32x4 r[U];
-            tree_eval<u32x4, NL, U, VecOp<DT, OP>>(x, r, g.comb, g.swaps);
+            for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&g.leaves[j][base + (size_t)u * BL]);
+        __builtin_amdgcn_sched_barrier(0);
+        u32x4 r[U];
+        tree_eval<u32x4, NL, U, VecOp<DT, OP>>(x, r, g.comb, g.swaps);
 #pragma unroll
-            for (int u = 0; u < U; ++u) st<NT>(&g.out[base + (size_t)u * BL], r[u]);
-        } else {
-            for (int u = 0; u < U; ++u) {
-                const size_t i = base + (size_t)u * BL;
-                if (i >= g.nvec) break;
-                u32x4 x[NL][1];
+        for (int u = 0; u < U; ++u) st<NT>(&g.out[base + (size_t)u * BL], r[u]);
+    } else {
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + (size_t)u * BL;
+            if (i >= g.nvec) break;
+            u32x4 x[NL][1];
 #pragma unroll
-                for (int j = 0; j < NL; ++j) x[j][0] = g.leaves[j][i];
-                u32x4 r[1];
-                tree_eval<u32x4, NL, 1, VecOp<DT, OP>>(x, r, g.comb, g.swaps);
-                g.out[i] = r[0];
-            }
+            for (int j = 0; j < NL; ++j) x[j][0] = g.leaves[j][i];
+            u32x4 r[1];
+            tree_eval<u32x4, NL, 1, VecOp<DT, OP>>(x, r, g.comb, g.swaps);
+            g.out[i] = r[0];
         }
     }
 }
@@ -161,19 +166,27 @@ __global__ __launch_bounds__(kBlock) void k_reduce_tree_scalar(TreeScalarArgs a)
     }
 }
 
+// XCD runs for streaming (nt) tree launches (profiles/r02/xcd_runs/ab_tree_*.json, C4 slice of 2
+// batched 8-leaf trees, HBM-cold, identity -> 512 KiB): 8 MiB pieces 0.571 -> 0.634, 16 MiB
+// 0.668 -> 0.700, 32 MiB 0.719 -> 0.750; fused reductions of a whole C4 call 0.676 -> 0.719.
+template <int NL>
+constexpr size_t tree_xcd_run_kib() {
+    return 512;
+}
+
 template <int DT, int OP, int NL, int BL, bool NT>
 inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
     constexpr int U = NL <= 4 ? 4 : 2;
     TreeArgs a = a_in;
-    // one trip per workgroup; CHR_REDUCE_MAX_BLOCKS caps each segment's share (tuning knob)
-    const size_t cap = reduce_tuning().max_blocks > 0 ? (size_t)reduce_tuning().max_blocks : ~(size_t)0;
     size_t grid = 0;
     for (int j = 0; j < a.nseg; ++j) {
+        if (a.seg[j].nvec > kMaxSegVec) return hipErrorInvalidValue;  // launch_reduce_tree_multi cuts them
         const size_t trips = (a.seg[j].nvec + (size_t)BL * U - 1) / ((size_t)BL * U);
         a.seg[j].block0 = (uint32_t)grid;
-        grid += trips < cap ? trips : cap;
+        grid += trips;
     }
     if (grid == 0) return hipSuccess;
+    a.xrun = NT ? xcd_run_shift(tree_xcd_run_kib<NL>(), (size_t)BL * U * 16) : 0;
     hipLaunchKernelGGL((k_reduce_tree<DT, OP, NL, U, NT, BL>), dim3((unsigned)grid), dim3(BL), 0, s, a);
     return hipGetLastError();
 }

@@ -17,7 +17,9 @@ struct VecArgs {
     const u32x4* acc;
     const u32x4* ins[kMaxFanIn];
     size_t nvec;
+    uint32_t xrun;  // log2 of the trips per XCD run (xcd_trip); set by the launcher
 };
+
 
 // U vectors (16 B each) per lane per trip; all M+1 operands of the trip are loaded
 // before the first add so (M+1)*U*16 bytes per lane are in flight.  NT: non-temporal
@@ -31,37 +33,38 @@ struct VecArgs {
 // every nt call; making ALL accumulator slots temporal thrashes the cache (-7 %).  Slot 0 is peeled so that the two policies
 // are separate instructions (a select between a plain and an nt load of one address is
 // merged by LLVM, dropping the nt bit).
+//
+// One trip per workgroup (grid = trips, no grid-stride loop: the loop form measured 2-3 % slower
+// at m = 1, microbench focus9 "product direct" vs "xmap C=1"), trips placed by xcd_trip.
 template <int DT, int OP, int M, int U, bool NT, bool ACC0, int BL>
 __global__ __launch_bounds__(BL) void k_reduce_vec(VecArgs a) {
-    const size_t stride = (size_t)gridDim.x * BL * U;
-    for (size_t base = (size_t)blockIdx.x * BL * U + threadIdx.x; base < a.nvec; base += stride) {
-        if (base + (size_t)(U - 1) * BL < a.nvec) {
-            u32x4 acc[U], x[M][U];
-            acc[0] = ld<NT && !ACC0>(&a.acc[base]);
+    const size_t base = xcd_trip(blockIdx.x, gridDim.x, a.xrun) * BL * U + threadIdx.x;
+    if (base + (size_t)(U - 1) * BL < a.nvec) {
+        u32x4 acc[U], x[M][U];
+        acc[0] = ld<NT && !ACC0>(&a.acc[base]);
 #pragma unroll
-            for (int u = 1; u < U; ++u) acc[u] = ld<NT>(&a.acc[base + (size_t)u * BL]);
+        for (int u = 1; u < U; ++u) acc[u] = ld<NT>(&a.acc[base + (size_t)u * BL]);
 #pragma unroll
-            for (int j = 0; j < M; ++j)
+        for (int j = 0; j < M; ++j)
 #pragma unroll
-                for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&a.ins[j][base + (size_t)u * BL]);
-            // Keep every load of the trip ahead of the first add: without this the
-            // scheduler interleaves the first add (and its vmcnt(0)) between the loads.
-            __builtin_amdgcn_sched_barrier(0);
+            for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&a.ins[j][base + (size_t)u * BL]);
+        // Keep every load of the trip ahead of the first add: without this the
+        // scheduler interleaves the first add (and its vmcnt(0)) between the loads.
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int j = 0; j < M; ++j)
+        for (int j = 0; j < M; ++j)
 #pragma unroll
-                for (int u = 0; u < U; ++u) acc[u] = apply_vec<DT, OP>(x[j][u], acc[u]);
+            for (int u = 0; u < U; ++u) acc[u] = apply_vec<DT, OP>(x[j][u], acc[u]);
 #pragma unroll
-            for (int u = 0; u < U; ++u) st<NT>(&a.out[base + (size_t)u * BL], acc[u]);
-        } else {
-            for (int u = 0; u < U; ++u) {
-                const size_t i = base + (size_t)u * BL;
-                if (i >= a.nvec) break;
-                u32x4 acc = a.acc[i];
+        for (int u = 0; u < U; ++u) st<NT>(&a.out[base + (size_t)u * BL], acc[u]);
+    } else {
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + (size_t)u * BL;
+            if (i >= a.nvec) break;
+            u32x4 acc = a.acc[i];
 #pragma unroll
-                for (int j = 0; j < M; ++j) acc = apply_vec<DT, OP>(a.ins[j][i], acc);
-                a.out[i] = acc;
-            }
+            for (int j = 0; j < M; ++j) acc = apply_vec<DT, OP>(a.ins[j][i], acc);
+            a.out[i] = acc;
         }
     }
 }
@@ -87,32 +90,58 @@ __global__ __launch_bounds__(kBlock) void k_reduce_scalar(ScalarArgs a) {
     }
 }
 
+// XCD runs for streaming calls, measured through the product API (profiles/r02/xcd_runs/,
+// fraction of 8 TB/s, identity -> 512 KiB runs): m = 3 at 256 MiB 0.854 -> 0.896 (1.25 GiB working
+// set) and 0.784 -> 0.795 (10 GiB); m = 7 0.811 -> 0.833 / 0.747 -> 0.751.  m <= 2 keeps the
+// identity: the C2 bucket measured 0.806 identity, 0.803 at 256 KiB, 0.792 at 512 KiB.  Cache-warm
+// (plain) calls keep the identity map too.
+template <int M>
+constexpr size_t vec_xcd_run_kib() {
+    return M <= 2 ? 0 : 512;
+}
+
+// A grid holds at most 2^31 threads here; larger calls (> 32 GiB per operand at BL = 64, U = 2)
+// run as consecutive launches over consecutive pieces.
+template <int BL, int U, typename L>
+inline hipError_t for_each_launch_piece(VecArgs a, L launch) {
+    const size_t max_vec = ((size_t)1 << 31) / BL * BL * U;
+    for (size_t off = 0; off < a.nvec; off += max_vec) {
+        VecArgs p = a;
+        p.out = a.out + off;
+        p.acc = a.acc + off;
+        for (int j = 0; j < kMaxFanIn; ++j) p.ins[j] = a.ins[j] ? a.ins[j] + off : nullptr;
+        p.nvec = a.nvec - off < max_vec ? a.nvec - off : max_vec;
+        launch(p, (unsigned)((p.nvec + (size_t)BL * U - 1) / ((size_t)BL * U)));
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 template <int DT, int OP, int M, int BL>
-inline hipError_t launch_vec_mb(const VecArgs& a, bool nt, bool acc0, hipStream_t s) {
+inline hipError_t launch_vec_mb(VecArgs a, bool nt, bool acc0, hipStream_t s) {
     constexpr int U = M <= 2 ? 4 : 2;
-    const size_t trips = (a.nvec + (size_t)BL * U - 1) / ((size_t)BL * U);
-    const size_t cap = reduce_tuning().max_blocks > 0 ? (size_t)reduce_tuning().max_blocks : trips;
-    const int grid = (int)(trips < cap ? trips : cap);
-    if (!nt)
-        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, false, false, BL>), dim3(grid), dim3(BL), 0, s, a);
-    else if (acc0)
-        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, true, BL>), dim3(grid), dim3(BL), 0, s, a);
-    else
-        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, false, BL>), dim3(grid), dim3(BL), 0, s, a);
-    return hipGetLastError();
+    a.xrun = nt ? xcd_run_shift(vec_xcd_run_kib<M>(), (size_t)BL * U * 16) : 0;
+    return for_each_launch_piece<BL, U>(a, [&](const VecArgs& p, unsigned grid) {
+        if (!nt)
+            hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, false, false, BL>), dim3(grid), dim3(BL), 0, s, p);
+        else if (acc0)
+            hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, true, BL>), dim3(grid), dim3(BL), 0, s, p);
+        else
+            hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, false, BL>), dim3(grid), dim3(BL), 0, s, p);
+    });
 }
 
 // Policy (profiles/r01/block_ab_*): calls that stream >= 128 MiB run non-temporal with
 // one-wave workgroups and the first accumulator slot temporal (ACC0); smaller, cache-warm
 // calls keep plain accesses and 256-thread workgroups.
 template <int DT, int OP, int M, int BL, bool NT, bool ACC0>
-inline hipError_t launch_vec_mb_one(const VecArgs& a, hipStream_t s) {
+inline hipError_t launch_vec_mb_one(VecArgs a, hipStream_t s) {
     constexpr int U = M <= 2 ? 4 : 2;
-    const size_t trips = (a.nvec + (size_t)BL * U - 1) / ((size_t)BL * U);
-    const size_t cap = reduce_tuning().max_blocks > 0 ? (size_t)reduce_tuning().max_blocks : trips;
-    const int grid = (int)(trips < cap ? trips : cap);
-    hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, NT, ACC0, BL>), dim3(grid), dim3(BL), 0, s, a);
-    return hipGetLastError();
+    a.xrun = NT ? xcd_run_shift(vec_xcd_run_kib<M>(), (size_t)BL * U * 16) : 0;
+    return for_each_launch_piece<BL, U>(a, [&](const VecArgs& p, unsigned grid) {
+        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, NT, ACC0, BL>), dim3(grid), dim3(BL), 0, s, p);
+    });
 }
 
 // FULL: every tuning variant (CHR_REDUCE_BLOCK / CHR_REDUCE_ACC0 overrides) is compiled, for the

@@ -10,6 +10,7 @@
 #include <cstdio>
 
 #include "chiara.h"
+#include "../configurable-hierarchical-allreduce-algorithms_amd/csrc/reduce_vec.hpp"
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -987,10 +988,110 @@ static void layout_mode() {
     release();
 }
 
+// ---- focus8: XCD-chunked workgroup -> address maps under a warm vs a cold translation state ---
+// The product (one trip per one-wave workgroup, ACC0 nt policy) with blockIdx remapped so each XCD
+// streams runs of C consecutive trips: workgroups dispatch round-robin over the 8 XCDs, so block b
+// runs on XCD b % 8; its (b / 8)-th trip goes to chunk (b / 8) / C of that XCD, and XCD x owns
+// chunks x, x + 8, x + 16, ...  C = 1 is the identity map.  A large C lets each XCD's translation
+// caches see fewer distinct pages per unit time; a small C keeps all XCDs in the same DRAM rows.
+template <int M, int U>
+__global__ __launch_bounds__(64) void k_xmap(Args a, unsigned C) {
+    const unsigned b = blockIdx.x, x = b % 8, i = b / 8;
+    const size_t trip = ((size_t)(i / C) * 8 + x) * C + i % C;
+    const size_t base = trip * 64 * U + threadIdx.x;
+    f32x4 acc[U], v[M][U];
+    acc[0] = a.acc[base];
+#pragma unroll
+    for (int u = 1; u < U; ++u) acc[u] = __builtin_nontemporal_load(&a.acc[base + (size_t)u * 64]);
+#pragma unroll
+    for (int j = 0; j < M; ++j)
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[j][u] = __builtin_nontemporal_load(&a.ins[j][base + (size_t)u * 64]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < M; ++j)
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] = v[j][u] + acc[u];
+#pragma unroll
+    for (int u = 0; u < U; ++u) __builtin_nontemporal_store(acc[u], &a.out[base + (size_t)u * 64]);
+}
+
+template <int M, int U>
+static void focus8_m(size_t bytes, int sets, int rounds, std::vector<unsigned> Cs = {1u, 4u, 16u, 64u, 256u, 1024u}) {
+    const size_t nvec = bytes / 16;
+    const unsigned G = (unsigned)(nvec / (64 * U));
+    if ((size_t)G * 64 * U != nvec || G % 8) {
+        std::fprintf(stderr, "focus8: bucket must be a whole number of 8-trip groups\n");
+        std::exit(1);
+    }
+    Sets S = make_sets(M, nvec, sets);
+    const int reps = 64;
+    auto args_for = [&](int i) {
+        Args a{};
+        auto& b = S.bufs[i % sets];
+        a.out = b[0];
+        a.acc = b[0];
+        for (int j = 0; j < M; ++j) a.ins[j] = b[j + 1];
+        a.nvec = nvec;
+        return a;
+    };
+    char tag[64];
+    std::snprintf(tag, sizeof tag, " sets=%d ws=%zuMiB", sets, (size_t)sets * (M + 1) * (bytes >> 20));
+    for (int r = 0; r < rounds; ++r) {
+        double us = time_launches([&](int i) {
+            Args a = args_for(i);
+            const void* ins[8];
+            for (int j = 0; j < M; ++j) ins[j] = a.ins[j];
+            chr_reduce_multi(a.out, a.acc, ins, M, a.nvec * 4, CHR_FLOAT32, CHR_SUM, 0);
+        }, reps);
+        report((std::string("libchiara chr_reduce_multi") + tag).c_str(), M, bytes, us);
+        {  // the product's kernel template, launched directly (isolates the host path)
+            double t = time_launches([&](int i) {
+                Args a = args_for(i);
+                chr::VecArgs v{};
+                v.out = (chr::u32x4*)a.out;
+                v.acc = (const chr::u32x4*)a.acc;
+                for (int j = 0; j < M; ++j) v.ins[j] = (const chr::u32x4*)a.ins[j];
+                v.nvec = a.nvec;
+                hipLaunchKernelGGL((chr::k_reduce_vec<CHR_FLOAT32, CHR_SUM, M, U, true, true, 64>), dim3(G), dim3(64), 0, 0, v);
+            }, reps);
+            report((std::string("product k_reduce_vec direct") + tag).c_str(), M, bytes, t);
+        }
+        for (unsigned C : Cs) {
+            if ((G / 8) % C) continue;
+            double t = time_launches([&](int i) { hipLaunchKernelGGL((k_xmap<M, U>), dim3(G), dim3(64), 0, 0, args_for(i), C); },
+                                     reps);
+            char name[96];
+            std::snprintf(name, sizeof name, "xmap C=%u (%zu KiB/XCD run)%s", C, (size_t)C * 64 * U * 16 >> 10, tag);
+            report(name, M, bytes, t);
+        }
+        std::printf("--\n");
+    }
+    free_sets(S);
+}
+
 int main(int argc, char** argv) {
     check();
     if (argc > 1 && std::string(argv[1]) == "layout") {
         layout_mode();
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus9") {  // finer runs: 128 KiB .. 1 MiB per XCD
+        const std::vector<unsigned> c4 = {1u, 32u, 64u, 128u, 256u}, c2 = {1u, 64u, 128u, 256u, 512u};
+        focus8_m<1, 4>(64 << 20, 16, 3, c4);
+        focus8_m<1, 4>(64 << 20, 64, 3, c4);
+        focus8_m<3, 2>(256 << 20, 1, 3, c2);
+        focus8_m<3, 2>(256 << 20, 8, 3, c2);
+        focus8_m<7, 2>(64 << 20, 4, 3, c2);
+        focus8_m<7, 2>(64 << 20, 16, 3, c2);
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus8") {
+        focus8_m<1, 4>(64 << 20, 16, 2);   // C2: 2 GiB rotation (warm translations)
+        focus8_m<1, 4>(64 << 20, 64, 2);   // C2 shape, 8 GiB rotation (cold)
+        focus8_m<3, 2>(256 << 20, 1, 2);   // m = 3, 1.25 GiB (warm)
+        focus8_m<3, 2>(256 << 20, 8, 2);   // m = 3, 10 GiB (cold)
+        focus8_m<7, 2>(64 << 20, 16, 1);   // the tree-like 9-stream shape, 8 GiB (cold)
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus7") {
