@@ -131,13 +131,15 @@ __device__ __forceinline__ u32x4 apply_vec(u32x4 in, u32x4 acc) {
 // kernel here does one trip (BL x U vectors per operand) per workgroup.  With the identity map
 // the 8 XCDs interleave at trip granularity (1-4 KiB); xcd_trip gives each XCD runs of C = 2^cs
 // consecutive trips instead: block b's (b / 8)-th trip goes to run (b / 8) / C of XCD b % 8, and
-// XCD x owns runs x, x + 8, x + 16, ...  Blocks past the last whole 8·C group keep the identity,
-// so the map is a bijection on [0, n).  Runs of 256-512 KiB measured +2-4 % on HBM-cold
+// XCD x owns runs x, x + 8, x + 16, ...  Blocks from `full` on (past the last whole 8·C group of
+// the grid, xcd_full) keep the identity, so the map is a bijection on [0, n).  Runs of 256-512 KiB measured +2-4 % on HBM-cold
 // streams (tools/reduce_microbench focus8/focus9, profiles/r02/microbench_focus9_xcd_runs.txt):
 // each XCD's translation caches and DRAM pages see fewer distinct pages per unit time, while
 // the 8 XCDs still stream within a few MiB of each other.
-__device__ __forceinline__ size_t xcd_trip(uint32_t b, uint32_t n, uint32_t cs) {
-    const uint32_t full = n & ~((8u << cs) - 1u);
+__host__ __device__ __forceinline__ uint32_t xcd_full(uint32_t n, uint32_t cs) {
+    return n & ~((8u << cs) - 1u);
+}
+__host__ __device__ __forceinline__ size_t xcd_trip(uint32_t b, uint32_t full, uint32_t cs) {
     if (b >= full) return b;
     const uint32_t x = b & 7u, i = b >> 3;
     return ((((size_t)(i >> cs)) * 8u + x) << cs) | (i & ((1u << cs) - 1u));
@@ -151,6 +153,18 @@ inline uint32_t xcd_run_shift(size_t policy_kib, size_t trip_bytes) {
     uint32_t cs = 0;
     while (((size_t)2 << cs) * trip_bytes <= kib * 1024 && cs < 16) ++cs;
     return cs;
+}
+
+// Materialise a wave-uniform pointer (a kernel argument) in SGPRs at this point: an empty asm
+// with an SGPR operand, so every such pointer is loaded by the scalar loads at the kernel's top
+// and waited for once, instead of being fetched lazily between vector loads.
+template <typename P>
+__device__ __forceinline__ void pin_sgpr(P* p) {
+    asm volatile("" ::"s"(p));
+}
+template <typename P, typename Q>
+__device__ __forceinline__ void pin_sgpr(P* p, Q* q, size_t n, uint32_t k, uint32_t f) {
+    asm volatile("" ::"s"(p), "s"(q), "s"(n), "s"(k), "s"(f));
 }
 
 template <bool NT>

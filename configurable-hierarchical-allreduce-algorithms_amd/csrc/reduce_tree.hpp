@@ -119,7 +119,7 @@ __global__ __launch_bounds__(BL) void k_reduce_tree(TreeArgs a) {
         if (blockIdx.x >= a.seg[j].block0) s = j;
     const TreeSeg& g = a.seg[s];
     const uint32_t nblk = (s + 1 < a.nseg ? a.seg[s + 1].block0 : gridDim.x) - g.block0;
-    const size_t base = xcd_trip(blockIdx.x - g.block0, nblk, a.xrun) * BL * U + threadIdx.x;
+    const size_t base = xcd_trip(blockIdx.x - g.block0, xcd_full(nblk, a.xrun), a.xrun) * BL * U + threadIdx.x;
     if (base + (size_t)(U - 1) * BL < g.nvec) {
         u32x4 x[NL][U];
 #pragma unroll

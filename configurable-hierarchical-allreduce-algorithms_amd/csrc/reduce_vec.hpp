@@ -17,7 +17,8 @@ struct VecArgs {
     const u32x4* acc;
     const u32x4* ins[kMaxFanIn];
     size_t nvec;
-    uint32_t xrun;  // log2 of the trips per XCD run (xcd_trip); set by the launcher
+    uint32_t xrun;   // log2 of the trips per XCD run (xcd_trip); set by the launcher
+    uint32_t xfull;  // blocks [0, xfull) are remapped (xcd_full of the grid); set per launch
 };
 
 
@@ -34,20 +35,38 @@ struct VecArgs {
 // are separate instructions (a select between a plain and an nt load of one address is
 // merged by LLVM, dropping the nt bit).
 //
-// One trip per workgroup (grid = trips, no grid-stride loop: the loop form measured 2-3 % slower
-// at m = 1, microbench focus9 "product direct" vs "xmap C=1"), trips placed by xcd_trip.
+// One trip per workgroup (grid = trips, no grid-stride loop), trips placed by xcd_trip.  With the
+// pinned arguments below this kernel runs within 0.3-1 % of a bare one-trip kernel without any
+// bounds check (microbench focus9: C2 shape 0.813-0.821 vs 0.822-0.824); the earlier grid-stride
+// form with lazily loaded pointers ran at 0.798-0.802.
+//
+// Every operand pointer is pinned into SGPRs before the trip's first load (kernarg_pointers): left
+// to itself the compiler loads the input pointers from the kernel arguments between the
+// accumulator and input loads, which puts a second scalar-load round trip (s_waitcnt lgkmcnt)
+// in front of half of the trip's loads.  The full/partial decision is per trip (scalar).
 template <int DT, int OP, int M, int U, bool NT, bool ACC0, int BL>
 __global__ __launch_bounds__(BL) void k_reduce_vec(VecArgs a) {
-    const size_t base = xcd_trip(blockIdx.x, gridDim.x, a.xrun) * BL * U + threadIdx.x;
-    if (base + (size_t)(U - 1) * BL < a.nvec) {
-        u32x4 acc[U], x[M][U];
-        acc[0] = ld<NT && !ACC0>(&a.acc[base]);
+    u32x4* const out = a.out;
+    const u32x4* const accp = a.acc;
+    const u32x4* ins[M];
 #pragma unroll
-        for (int u = 1; u < U; ++u) acc[u] = ld<NT>(&a.acc[base + (size_t)u * BL]);
+    for (int j = 0; j < M; ++j) ins[j] = a.ins[j];
+    const size_t nvec = a.nvec;
+    const uint32_t xrun = a.xrun, xfull = a.xfull;
+    pin_sgpr(out, accp, nvec, xrun, xfull);
+#pragma unroll
+    for (int j = 0; j < M; ++j) pin_sgpr(ins[j]);
+    const size_t trip = xcd_trip(blockIdx.x, xfull, xrun);
+    const size_t base = trip * BL * U + threadIdx.x;
+    if ((trip + 1) * BL * U <= nvec) {
+        u32x4 acc[U], x[M][U];
+        acc[0] = ld<NT && !ACC0>(&accp[base]);
+#pragma unroll
+        for (int u = 1; u < U; ++u) acc[u] = ld<NT>(&accp[base + (size_t)u * BL]);
 #pragma unroll
         for (int j = 0; j < M; ++j)
 #pragma unroll
-            for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&a.ins[j][base + (size_t)u * BL]);
+            for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&ins[j][base + (size_t)u * BL]);
         // Keep every load of the trip ahead of the first add: without this the
         // scheduler interleaves the first add (and its vmcnt(0)) between the loads.
         __builtin_amdgcn_sched_barrier(0);
@@ -56,15 +75,15 @@ __global__ __launch_bounds__(BL) void k_reduce_vec(VecArgs a) {
 #pragma unroll
             for (int u = 0; u < U; ++u) acc[u] = apply_vec<DT, OP>(x[j][u], acc[u]);
 #pragma unroll
-        for (int u = 0; u < U; ++u) st<NT>(&a.out[base + (size_t)u * BL], acc[u]);
+        for (int u = 0; u < U; ++u) st<NT>(&out[base + (size_t)u * BL], acc[u]);
     } else {
         for (int u = 0; u < U; ++u) {
             const size_t i = base + (size_t)u * BL;
-            if (i >= a.nvec) break;
-            u32x4 acc = a.acc[i];
+            if (i >= nvec) break;
+            u32x4 acc = accp[i];
 #pragma unroll
-            for (int j = 0; j < M; ++j) acc = apply_vec<DT, OP>(a.ins[j][i], acc);
-            a.out[i] = acc;
+            for (int j = 0; j < M; ++j) acc = apply_vec<DT, OP>(ins[j][i], acc);
+            out[i] = acc;
         }
     }
 }
@@ -111,7 +130,9 @@ inline hipError_t for_each_launch_piece(VecArgs a, L launch) {
         p.acc = a.acc + off;
         for (int j = 0; j < kMaxFanIn; ++j) p.ins[j] = a.ins[j] ? a.ins[j] + off : nullptr;
         p.nvec = a.nvec - off < max_vec ? a.nvec - off : max_vec;
-        launch(p, (unsigned)((p.nvec + (size_t)BL * U - 1) / ((size_t)BL * U)));
+        const unsigned grid = (unsigned)((p.nvec + (size_t)BL * U - 1) / ((size_t)BL * U));
+        p.xfull = xcd_full(grid, p.xrun);
+        launch(p, grid);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
