@@ -166,6 +166,13 @@ template <typename P, typename Q>
 __device__ __forceinline__ void pin_sgpr(P* p, Q* q, size_t n, uint32_t k, uint32_t f) {
     asm volatile("" ::"s"(p), "s"(q), "s"(n), "s"(k), "s"(f));
 }
+__device__ __forceinline__ void pin_sgpr_u32(uint32_t x, uint32_t y) {
+    asm volatile("" ::"s"(x), "s"(y));
+}
+template <typename P, typename Q>
+__device__ __forceinline__ void pin_sgpr(P* p, Q* q, size_t n, uint32_t k) {
+    asm volatile("" ::"s"(p), "s"(q), "s"(n), "s"(k));
+}
 
 template <bool NT>
 __device__ __forceinline__ u32x4 ld(const u32x4* p) {

@@ -40,10 +40,13 @@ struct TreeSeg {
     size_t nvec;
     uint32_t comb;    // 2 bits per leaf
     uint32_t swaps;   // 1 bit per combine, in program order
-    uint32_t block0;  // first workgroup of this segment
 };
 
+// The per-segment workgroup table comes first, so a workgroup finds its segment from one scalar
+// load of 64 bytes (set by launch_tree_vec): block0 ascending, ~0u past the last segment.
 struct TreeArgs {
+    uint32_t block0[kMaxTreeSegs];  // first workgroup of each segment
+    uint32_t xfull[kMaxTreeSegs];   // each segment's blocks [0, xfull) take the XCD map (xcd_full)
     TreeSeg seg[kMaxTreeSegs];
     int nseg;
     int nl;
@@ -113,34 +116,59 @@ struct ScalarOp {
 // anywhere in the 8-XCD rotation: blocks of one local residue class still share one XCD).
 template <int DT, int OP, int NL, int U, bool NT, int BL>
 __global__ __launch_bounds__(BL) void k_reduce_tree(TreeArgs a) {
-    // this workgroup's segment (uniform: scalar loads of the kernel arguments)
+    // this workgroup's segment: one pass over the block0 table (scalar compares, no loop-carried
+    // loads), then the segment's pointers pinned into SGPRs before the first vector load
+    const uint32_t b = blockIdx.x, xrun = a.xrun;
+    uint32_t b0s[kMaxTreeSegs], xfs[kMaxTreeSegs];
+#pragma unroll
+    for (int j = 0; j < kMaxTreeSegs; ++j) {
+        b0s[j] = a.block0[j];
+        xfs[j] = a.xfull[j];
+        pin_sgpr_u32(b0s[j], xfs[j]);
+    }
+    pin_sgpr_u32(xrun, xrun);
     int s = 0;
-    for (int j = 1; j < a.nseg; ++j)
-        if (blockIdx.x >= a.seg[j].block0) s = j;
+    uint32_t b0 = 0, xfull = xfs[0];
+#pragma unroll
+    for (int j = 1; j < kMaxTreeSegs; ++j)
+        if (b >= b0s[j]) {
+            s = j;
+            b0 = b0s[j];
+            xfull = xfs[j];
+        }
     const TreeSeg& g = a.seg[s];
-    const uint32_t nblk = (s + 1 < a.nseg ? a.seg[s + 1].block0 : gridDim.x) - g.block0;
-    const size_t base = xcd_trip(blockIdx.x - g.block0, xcd_full(nblk, a.xrun), a.xrun) * BL * U + threadIdx.x;
-    if (base + (size_t)(U - 1) * BL < g.nvec) {
+    u32x4* const out = g.out;
+    const u32x4* leaves[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) leaves[j] = g.leaves[j];
+    const size_t nvec = g.nvec;
+    const uint32_t comb = g.comb, swaps = g.swaps;
+    pin_sgpr(out, leaves[0], nvec, comb, swaps);
+#pragma unroll
+    for (int j = 1; j < NL; ++j) pin_sgpr(leaves[j]);
+    const size_t trip = xcd_trip(b - b0, xfull, xrun);
+    const size_t base = trip * BL * U + threadIdx.x;
+    if ((trip + 1) * BL * U <= nvec) {
         u32x4 x[NL][U];
 #pragma unroll
         for (int j = 0; j < NL; ++j)
 #pragma unroll
-            for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&g.leaves[j][base + (size_t)u * BL]);
+            for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&leaves[j][base + (size_t)u * BL]);
         __builtin_amdgcn_sched_barrier(0);
         u32x4 r[U];
-        tree_eval<u32x4, NL, U, VecOp<DT, OP>>(x, r, g.comb, g.swaps);
+        tree_eval<u32x4, NL, U, VecOp<DT, OP>>(x, r, comb, swaps);
 #pragma unroll
-        for (int u = 0; u < U; ++u) st<NT>(&g.out[base + (size_t)u * BL], r[u]);
+        for (int u = 0; u < U; ++u) st<NT>(&out[base + (size_t)u * BL], r[u]);
     } else {
         for (int u = 0; u < U; ++u) {
             const size_t i = base + (size_t)u * BL;
-            if (i >= g.nvec) break;
+            if (i >= nvec) break;
             u32x4 x[NL][1];
 #pragma unroll
-            for (int j = 0; j < NL; ++j) x[j][0] = g.leaves[j][i];
+            for (int j = 0; j < NL; ++j) x[j][0] = leaves[j][i];
             u32x4 r[1];
-            tree_eval<u32x4, NL, 1, VecOp<DT, OP>>(x, r, g.comb, g.swaps);
-            g.out[i] = r[0];
+            tree_eval<u32x4, NL, 1, VecOp<DT, OP>>(x, r, comb, swaps);
+            out[i] = r[0];
         }
     }
 }
@@ -178,15 +206,21 @@ template <int DT, int OP, int NL, int BL, bool NT>
 inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
     constexpr int U = NL <= 4 ? 4 : 2;
     TreeArgs a = a_in;
+    a.xrun = NT ? xcd_run_shift(tree_xcd_run_kib<NL>(), (size_t)BL * U * 16) : 0;
     size_t grid = 0;
-    for (int j = 0; j < a.nseg; ++j) {
+    for (int j = 0; j < kMaxTreeSegs; ++j) {
+        if (j >= a.nseg) {
+            a.block0[j] = ~0u;
+            a.xfull[j] = 0;
+            continue;
+        }
         if (a.seg[j].nvec > kMaxSegVec) return hipErrorInvalidValue;  // launch_reduce_tree_multi cuts them
         const size_t trips = (a.seg[j].nvec + (size_t)BL * U - 1) / ((size_t)BL * U);
-        a.seg[j].block0 = (uint32_t)grid;
+        a.block0[j] = (uint32_t)grid;
+        a.xfull[j] = xcd_full((uint32_t)trips, a.xrun);
         grid += trips;
     }
     if (grid == 0) return hipSuccess;
-    a.xrun = NT ? xcd_run_shift(tree_xcd_run_kib<NL>(), (size_t)BL * U * 16) : 0;
     hipLaunchKernelGGL((k_reduce_tree<DT, OP, NL, U, NT, BL>), dim3((unsigned)grid), dim3(BL), 0, s, a);
     return hipGetLastError();
 }
