@@ -380,10 +380,16 @@ def bench_allreduce(args):
         # use its socket transport between ranks that share a device (numbers meaningless)
         os.environ["NCCL_HOSTID"] = f"chiara-bench-vhost-{rank}"
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import datetime
+
+    # a rank that dies must not leave the others in a gloo barrier for gloo's default 30 minutes
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=900))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     comm = ca.Comm.from_torch_distributed(device=local)
+    # every blocking call (tuning included) and every comm.synchronize() gives up after this long:
+    # a collective that never completes becomes ERR_TIMEOUT (communicator aborted), not a hang
+    comm.set_timeout(int(os.environ.get("CHR_BENCH_TIMEOUT_MS", "300000")))
     b = 4 if world % 4 == 0 else world
     k = min(4, b) if b > 1 else 2
     dt = ca.FLOAT32 if args.dtype == "f32" else ca.BFLOAT16
@@ -408,6 +414,7 @@ def bench_allreduce(args):
     sched_names = {0: "reference", 1: "balanced", 2: "flat", 3: "exact", 4: "flat_ag", 5: "flat_seq"}
     for _ in range(args.warmup):
         ca.check(ca.all_reduce_radix_batch(send, recv, count, dt, ca.SUM, comm, k, b, async_op=True))
+    ca.check(comm.synchronize())
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
@@ -415,6 +422,7 @@ def bench_allreduce(args):
     for _ in range(args.steps):
         ca.check(ca.all_reduce_radix_batch(send, recv, count, dt, ca.SUM, comm, k, b, async_op=True))
     t_enq = time.perf_counter() - t0  # host time to enqueue every call (RCCL groups, launches, events)
+    ca.check(comm.synchronize())  # under the timeout; the torch sync below then returns at once
     torch.cuda.synchronize()
     dist.barrier()
     el = time.perf_counter() - t0
@@ -506,17 +514,25 @@ def bench_allreduce(args):
     dist.destroy_process_group()
 
 
-def _timed_max(torch, dist, fn, steps, warmup):
-    """Seconds for `steps` calls of fn after `warmup`, barrier + sync on both sides, max over ranks."""
+def _timed_max(torch, dist, fn, steps, warmup, comm=None):
+    """Seconds for `steps` calls of fn after `warmup`, barrier + sync on both sides, max over ranks.
+    With `comm`, the waits go through comm.synchronize() first (bounded by its timeout)."""
+    def sync():
+        if comm is not None:
+            rc = comm.synchronize()
+            if rc:
+                raise RuntimeError(f"chr_comm_synchronize: {rc}")
+        torch.cuda.synchronize()
+
     for _ in range(warmup):
         fn()
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         fn()
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -529,7 +545,7 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
     (testing/mpich_implementations/all_reduce/allreduce_ring.cpp) run on libchiara's executor and
     (3) the metric's own schedule with the reductions on the transfer stream (no overlap),
     (4) its arithmetic under the balanced, reference-route and exact (the reference's messages
-    end to end) schedules, (5) the flat schedule at pipeline depths 1, 2 and 4 and (6) the other
+    end to end) schedules, (5) the flat schedule at pipeline depths 1, 2 and 8 and (6) the other
     multi-GPU BASELINE configs, C3 and C5 (baseline_configs)."""
     steps, warm = max(1, min(args.steps, 20)), 2
     S = count * (4 if dt == ca.FLOAT32 else 2)
@@ -549,9 +565,21 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
     except Exception as e:  # context only: never fail the metric line for it
         out["rccl_allreduce"] = {"error": str(e)[:200]}
 
+    def timed(name, fn):
+        """One context entry on libchiara; a failure (e.g. a timeout that aborted the communicator)
+        is recorded in the line instead of failing the metric, and skips the entries after it."""
+        if out.get("aborted"):
+            return
+        try:
+            out[name] = entry(_timed_max(torch, dist, fn, steps, warm, comm))
+        except Exception as e:
+            out[name] = {"error": str(e)[:200]}
+            if comm.aborted:
+                out["aborted"] = name
+
     def ring():
         ca.check(ca.MPICH_Allreduce_ring(send, recv, count, dt, ca.SUM, comm, async_op=True))
-    out["mpich_ring_on_libchiara"] = entry(_timed_max(torch, dist, ring, steps, warm))
+    timed("mpich_ring_on_libchiara", ring)
 
     # the same radix/batch arithmetic under the other schedules (same bits, other routes)
     restore = ca.SCHEDULE_FLAT if metric_sched is None else metric_sched
@@ -560,7 +588,7 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
         ca.check(ca.all_reduce_radix_batch(send, recv, count, dt, ca.SUM, comm, k, b, async_op=True))
     comm.set_overlap(False)
     try:
-        out["radix_batch_no_overlap"] = entry(_timed_max(torch, dist, radix, steps, warm))
+        timed("radix_batch_no_overlap", radix)
     finally:
         comm.set_overlap(True)
     for name, sch in (("radix_batch_flat", ca.SCHEDULE_FLAT),
@@ -571,20 +599,22 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
                       ("radix_batch_flat_separate_groups", ca.SCHEDULE_FLAT_SEQ)):
         comm.set_schedule(sch)
         try:
-            out[name] = entry(_timed_max(torch, dist, radix, steps, warm))
+            timed(name, radix)
         finally:
             comm.set_schedule(restore)
-    # pipeline depth of the flat schedule: automatic is 8 slices at 1 GiB
+    # pipeline depth of the flat schedule (automatic: 4 slices at 1 GiB, 16 MiB pieces)
     comm.set_schedule(ca.SCHEDULE_FLAT)
     try:
-        for P in (1, 2, 4):
+        for P in (1, 2, 8):
             comm.set_slices(P)
             try:
-                out[f"radix_batch_flat_slices{P}"] = entry(_timed_max(torch, dist, radix, steps, warm))
+                timed(f"radix_batch_flat_slices{P}", radix)
             finally:
                 comm.set_slices(0)
     finally:
         comm.set_schedule(restore)
+    if out.get("aborted"):
+        return out
     out["small_messages"] = small_messages(ca, torch, dist, comm, dt, k, b, world, dev)
     out.update(baseline_configs(args, ca, torch, dist, comm, world, dev, steps, warm))
     return out
@@ -630,7 +660,7 @@ def baseline_configs(args, ca, torch, dist, comm, world, dev, steps, warm):
         for b in sorted({1, 2} & {d for d in range(1, world + 1) if world % d == 0}):
             def rs():
                 ca.check(ca.reduce_scatter_radix_batch(s_rs, r_rs, rc, ca.FLOAT32, ca.SUM, comm, 2, b, async_op=True))
-            el = _timed_max(torch, dist, rs, steps, warm)
+            el = _timed_max(torch, dist, rs, steps, warm, comm)
             algbw = rc * world * 4 * steps / el / 1e9  # nccl-tests: send-buffer bytes / time
             out[f"c3_reduce_scatter_fp32_k2_b{b}_256MiB"] = {
                 "algbw_GBps": round(algbw, 2), "busbw_GBps": round(algbw * (world - 1) / world, 2),
@@ -644,7 +674,7 @@ def baseline_configs(args, ca, torch, dist, comm, world, dev, steps, warm):
 
             def c5():
                 ca.check(ca.all_reduce_radix_batch(s5, r5, cnt, ca.BFLOAT16, ca.SUM, comm, 4, 4, async_op=True))
-            el = _timed_max(torch, dist, c5, steps, warm)
+            el = _timed_max(torch, dist, c5, steps, warm, comm)
             algbw = cnt * 2 * steps / el / 1e9
             out["c5_allreduce_bf16_k4_b4_1GiB"] = {
                 "algbw_GBps": round(algbw, 2), "busbw_GBps": round(algbw * 2 * (world - 1) / world, 2),
