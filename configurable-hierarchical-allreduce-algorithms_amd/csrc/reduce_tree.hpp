@@ -197,9 +197,11 @@ __global__ __launch_bounds__(kBlock) void k_reduce_tree_scalar(TreeScalarArgs a)
 // XCD runs for streaming (nt) tree launches (profiles/r02/xcd_runs/ab_tree_*.json, C4 slice of 2
 // batched 8-leaf trees, HBM-cold, identity -> 512 KiB): 8 MiB pieces 0.571 -> 0.634, 16 MiB
 // 0.668 -> 0.700, 32 MiB 0.719 -> 0.750; fused reductions of a whole C4 call 0.676 -> 0.719.
+// Two leaves move the m = 1 bucket's traffic (2 reads + 1 write), which runs best unmapped
+// (vec_xcd_run_kib), so they keep the identity.
 template <int NL>
 constexpr size_t tree_xcd_run_kib() {
-    return 512;
+    return NL <= 2 ? 0 : 512;
 }
 
 template <int DT, int OP, int NL, int BL, bool NT>
