@@ -45,6 +45,9 @@ hipError_t launch_fill(void* buf, size_t n, int dtype, int pattern, uint64_t see
                        uint64_t count_for_seq, hipStream_t stream);
 
 // Tunables (read once from the environment):
+//   CHR_REDUCE_MAX_LAUNCH_VEC  cap on the 16-B vectors one bucket launch or one tree segment
+//                            covers (default: 2^31 threads / 1 GiB); tests set it small to run the
+//                            splitting paths at oracle sizes
 //   CHR_XCD_RUN_KIB          streaming (NT) calls: KiB of consecutive trips each XCD takes before
 //                            the next XCD's run (0 = plain round-robin); unset = policy
 //                            (xcd_run_shift in reduce_common.hpp)
@@ -56,7 +59,8 @@ hipError_t launch_fill(void* buf, size_t n, int dtype, int pattern, uint64_t see
 //   CHR_REDUCE_BLOCK         threads per workgroup of the vector kernels: 64 or 256;
 //                            unset = 64 for NT calls, 256 otherwise
 struct ReduceTuning {
-    int xcd_run_kib;  // -1: policy
+    int xcd_run_kib;        // -1: policy
+    size_t max_launch_vec;  // 0: the grid limit; else cap on 16-B vectors per launch / tree segment
     int block;
     int nt_mode;
     size_t nt_min_bytes;

@@ -94,7 +94,9 @@ static bool in_core_tu(int kdt, int kop) {
 ReduceTuning& reduce_tuning() {
     static ReduceTuning t = [] {
         ReduceTuning r;
-        const char* s = std::getenv("CHR_XCD_RUN_KIB");
+        const char* s = std::getenv("CHR_REDUCE_MAX_LAUNCH_VEC");
+        r.max_launch_vec = s ? (size_t)std::atoll(s) : 0;
+        s = std::getenv("CHR_XCD_RUN_KIB");
         r.xcd_run_kib = s ? std::atoi(s) : -1;  // -1: policy (vec_xcd_run_kib / tree_xcd_run_kib)
         s = std::getenv("CHR_REDUCE_NT");     // 0 / 1 / unset = by size
         r.nt_mode = s ? std::atoi(s) : -1;

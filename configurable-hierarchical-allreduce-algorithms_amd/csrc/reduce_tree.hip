@@ -104,12 +104,14 @@ hipError_t launch_reduce_tree_multi(const TreeJob* jobs, int njobs, int dtype, i
         const size_t nvec = (jb.n - head) / E;
         const size_t tail = jb.n - head - nvec * E;
         if ((err = scalar(0, head)) != hipSuccess || (err = scalar(head + nvec * E, tail)) != hipSuccess) return err;
-        for (size_t off = 0; off < nvec; off += kMaxSegVec) {  // pieces of at most 1 GiB per operand
+        const size_t cap = reduce_tuning().max_launch_vec;
+        const size_t seg_cap = cap && cap < kMaxSegVec ? cap : kMaxSegVec;
+        for (size_t off = 0; off < nvec; off += seg_cap) {  // pieces of at most 1 GiB per operand
             TreeArgs& a = pend[nl];
             TreeSeg& g = a.seg[a.nseg++];
             g.out = (u32x4*)((char*)jb.out + head * es) + off;
             for (int j = 0; j < nl; ++j) g.leaves[j] = (const u32x4*)((const char*)jb.leaves[j] + head * es) + off;
-            g.nvec = nvec - off < kMaxSegVec ? nvec - off : kMaxSegVec;
+            g.nvec = nvec - off < seg_cap ? nvec - off : seg_cap;
             g.comb = cb;
             g.swaps = sb;
             if (a.nseg == kMaxTreeSegs && (err = flush(nl)) != hipSuccess) return err;

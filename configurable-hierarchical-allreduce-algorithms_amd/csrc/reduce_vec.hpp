@@ -123,7 +123,8 @@ constexpr size_t vec_xcd_run_kib() {
 // run as consecutive launches over consecutive pieces.
 template <int BL, int U, typename L>
 inline hipError_t for_each_launch_piece(VecArgs a, L launch) {
-    const size_t max_vec = ((size_t)1 << 31) / BL * BL * U;
+    const size_t cap = reduce_tuning().max_launch_vec;
+    const size_t max_vec = cap ? cap : ((size_t)1 << 31) / BL * BL * U;
     for (size_t off = 0; off < a.nvec; off += max_vec) {
         VecArgs p = a;
         p.out = a.out + off;

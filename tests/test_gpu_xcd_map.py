@@ -64,11 +64,14 @@ print(json.dumps({{"bad": [str(b) for b in bad]}}))
 """
 
 
-@pytest.mark.parametrize("run_kib", [4, 8, 64])
-def test_xcd_run_map_covers_every_trip(run_kib):
+@pytest.mark.parametrize("run_kib,max_vec", [(4, 0), (8, 0), (64, 0), (8, 3000)])
+def test_xcd_run_map_covers_every_trip(run_kib, max_vec):
+    """max_vec > 0 also caps the vectors per launch / tree segment (CHR_REDUCE_MAX_LAUNCH_VEC), so the
+    paths that split > 32 GiB buckets into several launches and > 1 GiB trees into several segments
+    (and several flushes of 8 segments) run at these sizes, with partial trips inside a call."""
     code = CHILD.format(here=HERE, oracle=os.path.join(REPO, "oracle"),
                         pkg=os.path.join(REPO, "configurable-hierarchical-allreduce-algorithms_amd"))
-    env = dict(os.environ, CHR_REDUCE_NT="1", CHR_XCD_RUN_KIB=str(run_kib))
+    env = dict(os.environ, CHR_REDUCE_NT="1", CHR_XCD_RUN_KIB=str(run_kib), CHR_REDUCE_MAX_LAUNCH_VEC=str(max_vec))
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     res = json.loads(out.stdout.strip().splitlines()[-1])
