@@ -13,6 +13,7 @@
 #   prof       rocprofv3 kernel trace + stats of the bench (csv) -> prof/
 #   pmc        FETCH_SIZE and WRITE_SIZE passes of the bench     -> pmc_FETCH_SIZE/, pmc_WRITE_SIZE/
 #   kernels    bench.py --collective-kernels (C4/C5 in-collective kernel rows) -> collective_kernels.json
+#   e2e        bench.py --e2e: host-buffer (PCIe-inclusive) cost of the reference's contract -> e2e.json
 #   sweep      bench.py --sweep: 1 KiB .. 1 GiB buckets, m = 1/3/7, fp32 + bf16 (table in sweep.json.err)
 #   probe      tools/mstream_probe.py $PROBE_ARGS               -> mstream_probe.jsonl
 #   tree       tools/tree_bench.py $TREE_ARGS                   -> tree_bench.json
@@ -50,6 +51,7 @@ for step in "$@"; do
     done ;;
   kernels) run 400 collective_kernels.json python bench.py --collective-kernels ;;
   sweep) run 600 sweep.json python bench.py --sweep --no-cpu-baseline ;;
+  e2e) run 300 e2e.json python bench.py --e2e --no-cpu-baseline ;;
   probe) run 400 mstream_probe.jsonl python tools/mstream_probe.py ${PROBE_ARGS:-} ;;
   tree) run 400 tree_bench.json python tools/tree_bench.py ${TREE_ARGS:-} ;;
   rehearse)
