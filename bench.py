@@ -648,8 +648,9 @@ def small_messages(ca, torch, dist, comm, dt, k, b, world, dev):
 
 def baseline_configs(args, ca, torch, dist, comm, world, dev, steps, warm):
     """The other multi-GPU BASELINE configs at this world size, default schedule, same run:
-    C3 (fp32 reduce-scatter, radix 2, 256 MiB send buffer; b = 1 and 2) and C5 (bf16 allreduce,
-    b = 4 ("4x2": 4 ranks per group x 2 groups), k = 4, 1 GiB, compute/xGMI overlap) at 8 ranks."""
+    C3 (fp32 reduce-scatter, radix 2, 256 MiB send buffer; b = 1 and 2; next to it the four MPICH
+    reduce-scatter baselines on the same buffers) and C5 (bf16 allreduce, b = 4 ("4x2": 4 ranks per
+    group x 2 groups), k = 4, 1 GiB, compute/xGMI overlap) at 8 ranks."""
     out = {}
     try:
         rs_send = (256 << 20) // 4  # elements in the send buffer
@@ -663,6 +664,21 @@ def baseline_configs(args, ca, torch, dist, comm, world, dev, steps, warm):
             el = _timed_max(torch, dist, rs, steps, warm, comm)
             algbw = rc * world * 4 * steps / el / 1e9  # nccl-tests: send-buffer bytes / time
             out[f"c3_reduce_scatter_fp32_k2_b{b}_256MiB"] = {
+                "algbw_GBps": round(algbw, 2), "busbw_GBps": round(algbw * (world - 1) / world, 2),
+                "ms_per_call": round(el / steps * 1e3, 4)}
+        # the MPICH reduce-scatters testing/mpich_implementations/reduce_scatter/main.cpp times
+        # against, on the same buffers and executor (radix at k = 2)
+        for name, fn in (("radix_k2", lambda: ca.MPICH_reduce_scatter_radix(s_rs, r_rs, rc, ca.FLOAT32, ca.SUM, comm, 2,
+                                                                             async_op=True)),
+                         ("rec_halving", lambda: ca.MPICH_reduce_scatter_rec_halving(s_rs, r_rs, rc, ca.FLOAT32, ca.SUM,
+                                                                                     comm, async_op=True)),
+                         ("rec_doubling", lambda: ca.MPICH_reduce_scatter_rec_doubling(s_rs, r_rs, rc, ca.FLOAT32,
+                                                                                       ca.SUM, comm, async_op=True)),
+                         ("pairwise", lambda: ca.MPICH_reduce_scatter_pairwise(s_rs, r_rs, rc, ca.FLOAT32, ca.SUM, comm,
+                                                                               async_op=True))):
+            el = _timed_max(torch, dist, lambda: ca.check(fn()), steps, warm, comm)
+            algbw = rc * world * 4 * steps / el / 1e9
+            out[f"c3_mpich_reduce_scatter_{name}_256MiB"] = {
                 "algbw_GBps": round(algbw, 2), "busbw_GBps": round(algbw * (world - 1) / world, 2),
                 "ms_per_call": round(el / steps * 1e3, 4)}
         del s_rs, r_rs

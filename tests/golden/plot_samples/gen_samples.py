@@ -15,3 +15,11 @@ for name, rel in (("allreduce", "all_reduce/results_custom_polaris.csv"),
     df = df[df["send_count"].isin(sizes)]
     df.to_csv(os.path.join(HERE, f"{name}.csv"), index=False)
     print(name, len(df), "rows", sorted(df["algorithm_name"].unique()))
+
+# the MPICH reduce-scatter baselines' own results (testing/mpich_implementations/reduce_scatter/,
+# the CSV make_median_algo_plot.py reads): two sizes of the 8-rank file
+df = pd.read_csv("/root/reference/testing/mpich_implementations/reduce_scatter/reduce_scatter_results8.csv")
+sizes = sorted(df["send_count"].unique())[:2]
+df = df[df["send_count"].isin(sizes)]
+df.to_csv(os.path.join(HERE, "reduce_scatter_mpich.csv"), index=False)
+print("reduce_scatter_mpich", len(df), "rows", sorted(df["algorithm_name"].unique()))

@@ -8,6 +8,10 @@ pivot to one column per algorithm (:36), require the baseline column (:39-41: MP
 reduce_scatter_standard, allgather_standard), pick the per-cell winner (:45) and the speedup of the
 best non-baseline algorithm over the baseline (:49-56).  matplotlib is absent here, so only this
 stage runs; it is what decides whether a CSV is consumable by the plotters unchanged.
+
+testing/plots/reduce_scatter/make_median_algo_plot.py (the per-algorithm view used for the MPICH
+reduce-scatter baselines' CSVs, testing/mpich_implementations/reduce_scatter/) has a data stage of
+its own, restated in per_algo_medians.
 """
 import pandas as pd
 
@@ -37,3 +41,22 @@ def plotter_frame(csv_path, collective, agg="median"):
         raise RuntimeError("No non-baseline algorithms found to compare against the baseline.")
     speedup = (wide[base] / wide[mine].min(axis=1)).unstack(level=-1)
     return wide, best_algo, speedup
+
+
+def per_algo_medians(csv_path):
+    """make_median_algo_plot.py's data stage: refuse incorrect rows (:25-32) and missing columns
+    (:34-37), label variants by k when k is set and nonzero (:40-44), x = send_count / nprocs
+    (:47), median time per (nprocs, x, algorithm) (:50-55).  Returns that frame."""
+    df = pd.read_csv(csv_path)
+    if "is_correct" in df.columns and not df["is_correct"].eq(1).all():
+        raise RuntimeError("Found incorrect measurement(s)")
+    need = {"nprocs", "send_count", "algorithm_name", "k", "time"}
+    miss = need - set(df.columns)
+    if miss:
+        raise RuntimeError(f"Missing columns: {sorted(miss)}")
+    df["algorithm"] = df.apply(
+        lambda r: f"{r['algorithm_name']} (k={int(r['k'])})" if pd.notna(r["k"]) and int(r["k"]) != 0
+        else str(r["algorithm_name"]), axis=1)
+    df["send_count_norm"] = df["send_count"] / df["nprocs"]
+    return (df.groupby(["nprocs", "send_count_norm", "algorithm"], as_index=False)["time"].median()
+            .rename(columns={"time": "median_time"}))

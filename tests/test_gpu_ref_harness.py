@@ -11,7 +11,7 @@ import shutil
 import subprocess
 
 import pytest
-from plot_pipeline import COLUMNS, plotter_frame
+from plot_pipeline import COLUMNS, per_algo_medians, plotter_frame
 
 pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -84,6 +84,10 @@ def test_reference_mpich_reduce_scatter_harness_on_mi355x(tmp_path):
                      "MPICH_reduce_scatter_rec_doubling", "MPICH_reduce_scatter_pairwise", "MPI_Reduce_scatter_block"}
     assert len(rows) == 2 * (15 + 4) * 50  # sizes x (k = 2..30 step 2, four without k) x reps
     assert all(r["is_correct"] == "1" for r in rows)
+    # the reference's per-algorithm plotter (make_median_algo_plot.py) accepts the CSV unchanged
+    csvs = [f for f in os.listdir(tmp_path) if f.startswith("reduce_scatter_results")]
+    med = per_algo_medians(os.path.join(tmp_path, csvs[0]))
+    assert med["algorithm"].nunique() == 4 + 15 and (med["median_time"] > 0).all()
 
 
 def test_reference_allgather_harness_on_mi355x(tmp_path):

@@ -7,7 +7,7 @@ import os
 import pandas as pd
 import pytest
 
-from plot_pipeline import BASELINES, COLUMNS, plotter_frame
+from plot_pipeline import BASELINES, COLUMNS, per_algo_medians, plotter_frame
 
 SAMPLES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "plot_samples")
 
@@ -53,3 +53,20 @@ def test_k_labels_and_speedup(tmp_path):
     assert set(wide.columns) == {"MPICH_allreduce", "all_reduce_radix_batch (k=2)", "all_reduce_radix_batch (k=4)"}
     assert best.loc[8, 128] == "all_reduce_radix_batch (k=2)"  # k=4: median 2.25e-4
     assert speedup.loc[8, 128] == pytest.approx(2.0)
+
+
+def test_reference_mpich_reduce_scatter_sample_per_algo_medians():
+    """make_median_algo_plot.py on the reference's own MPICH reduce-scatter baseline results: every
+    radix k is its own line, the k-less baselines keep their names."""
+    med = per_algo_medians(os.path.join(SAMPLES, "reduce_scatter_mpich.csv"))
+    algos = set(med["algorithm"])
+    assert {"MPICH_reduce_scatter_pairwise", "MPICH_reduce_scatter_rec_doubling", "MPICH_reduce_scatter_rec_halving",
+            "MPI_Reduce_scatter_block"} <= algos
+    assert {f"MPICH_reduce_scatter_radix (k={k})" for k in range(2, 32, 2)} <= algos
+    assert (med["median_time"] > 0).all() and med["send_count_norm"].nunique() == 2
+
+
+def test_per_algo_medians_refuses_incorrect_rows(tmp_path):
+    p = _write(tmp_path, [["MPICH_reduce_scatter_pairwise", 0, 0, 4, 32, 1e-4, 0]])
+    with pytest.raises(RuntimeError, match="incorrect"):
+        per_algo_medians(p)
