@@ -527,3 +527,71 @@ def test_rccl_c4_c5_full_size_bit_exact_world8(dtype, slices):
     assert all(rc == 0 for _, rc, _, _ in res), res
     assert all(same for _, _, same, _ in res), "ranks disagree"
     assert res[0][3] == [], f"mismatches vs the oracle: {res[0][3][:5]}"
+
+
+def _graph_baselines_worker(rank, world, port, q):
+    """Graph replay of the other plan families: the MPICH reduce-scatter and allreduce baselines and
+    allgather_radix_batch, three rounds of new data in the same buffers each (round 0 captures,
+    rounds 1-2 replay), bit-exact vs the oracle."""
+    _setup(rank)
+    import torch
+    import torch.distributed as dist
+
+    import chiara_amd as ca
+    import pyoracle as po
+
+    comm = _init_worker(rank, world, port)
+    dev = torch.device("cuda:0")
+    bad = []
+    try:
+        comm.set_graphs(True)
+        rc_ = 3001
+        s_rs = torch.empty(rc_ * world * 4, dtype=torch.uint8, device=dev)
+        r_rs = torch.empty(rc_ * 4, dtype=torch.uint8, device=dev)
+        n_ar = 4096 * world
+        s_ar = torch.empty(n_ar * 4, dtype=torch.uint8, device=dev)
+        r_ar = torch.empty(n_ar * 4, dtype=torch.uint8, device=dev)
+        n_ag = 777
+        s_ag = torch.empty(n_ag * 4, dtype=torch.uint8, device=dev)
+        r_ag = torch.empty(n_ag * world * 4, dtype=torch.uint8, device=dev)
+        cases = (
+            ("rs_radix", lambda: ca.MPICH_reduce_scatter_radix(s_rs, r_rs, rc_, ca.FLOAT32, ca.SUM, comm, 3)),
+            ("rs_halving", lambda: ca.MPICH_reduce_scatter_rec_halving(s_rs, r_rs, rc_, ca.FLOAT32, ca.SUM, comm)),
+            ("rs_doubling", lambda: ca.MPICH_reduce_scatter_rec_doubling(s_rs, r_rs, rc_, ca.FLOAT32, ca.SUM, comm)),
+            ("rs_pairwise", lambda: ca.MPICH_reduce_scatter_pairwise(s_rs, r_rs, rc_, ca.FLOAT32, ca.SUM, comm)),
+            ("ring", lambda: ca.MPICH_Allreduce_ring(s_ar, r_ar, n_ar, ca.FLOAT32, ca.SUM, comm)),
+            ("rx", lambda: ca.MPICH_Allreduce_recursive_exchange(s_ar, r_ar, n_ar, ca.FLOAT32, ca.SUM, comm, 3, 0)),
+            ("ag", lambda: ca.allgather_radix_batch(s_ag, n_ag, ca.FLOAT32, r_ag, comm, 2, 2)))
+        for name, call in cases:
+            for rnd in range(3):
+                seed = 100 + 10 * rnd
+                if name.startswith("rs_"):
+                    allx = [po.fill(rc_ * world, "f32", 0, seed, r) for r in range(world)]
+                    s_rs.copy_(torch.from_numpy(allx[rank].view(np.uint8).copy()))
+                    want = po.mpich_reduce_scatter(name, allx, "f32", "sum", k=3)[rank]
+                    out = r_rs
+                elif name == "ag":
+                    allx = [po.fill(n_ag, "f32", 0, seed, r) for r in range(world)]
+                    s_ag.copy_(torch.from_numpy(allx[rank].view(np.uint8).copy()))
+                    want = np.concatenate(allx)
+                    out = r_ag
+                else:
+                    allx = [po.fill(n_ar, "f32", 0, seed, r) for r in range(world)]
+                    s_ar.copy_(torch.from_numpy(allx[rank].view(np.uint8).copy()))
+                    want = po.mpich_allreduce(name, allx, "f32", "sum", k=3)[rank]
+                    out = r_ar
+                torch.cuda.synchronize()
+                rc = call()
+                got = out.cpu().numpy().view(np.float32)[:want.size]
+                if rc != 0 or not np.array_equal(got.view(np.uint32), want.view(np.uint32)):
+                    bad.append((name, rnd, rc))
+    finally:
+        comm.destroy()
+        dist.destroy_process_group()
+    q.put((rank, bad))
+
+
+def test_rccl_graph_replay_baselines_world4():
+    res = _spawn(_graph_baselines_worker, 4)
+    bad = [r for r in res if r[1]]
+    assert not bad, bad

@@ -1,0 +1,26 @@
+"""CPU check of the XCD-run workgroup map (reduce_common.hpp xcd_trip): the kernels' own
+__host__ __device__ functions, host-compiled with hipcc, must form a bijection on every grid size
+and send every remapped block into a run of its own XCD.  The GPU side
+(tests/test_gpu_xcd_map.py) checks the kernels element by element."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not present")
+def test_xcd_trip_is_a_bijection_with_xcd_owned_runs(tmp_path):
+    exe = os.path.join(tmp_path, "xcd_map_check")
+    subprocess.run([HIPCC, "-x", "hip", "--offload-host-only", "-O1", "-std=c++17",
+                    "-I" + os.path.join(REPO, "include"),
+                    "-I" + os.path.join(REPO, "configurable-hierarchical-allreduce-algorithms_amd", "csrc"),
+                    "-o", exe, os.path.join(HERE, "host", "xcd_map_check.cpp")],
+                   check=True, capture_output=True, timeout=300)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0 and out.stdout.strip() == "0", out.stdout + out.stderr
+    shutil.rmtree(tmp_path, ignore_errors=True)
