@@ -11,6 +11,7 @@
 
 #include "chiara.h"
 #include "../configurable-hierarchical-allreduce-algorithms_amd/csrc/reduce_vec.hpp"
+#include "../configurable-hierarchical-allreduce-algorithms_amd/csrc/reduce_tree.hpp"
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -1070,10 +1071,74 @@ static void focus8_m(size_t bytes, int sets, int rounds, std::vector<unsigned> C
     free_sets(S);
 }
 
+// ---- focus10: the product tree kernel's U and XCD runs at the C4 slice shape -------------------
+// Two 8-leaf trees (C4's ((l0 l1 l2 l3)(l4 l5 l6 l7)) program) of `piece` bytes per leaf in one
+// launch, as the flat schedule's batched evaluation issues them; leaves rotated over `sets`.
+template <int U>
+static double tree_launches(const std::vector<std::vector<f32x4*>>& bufs, size_t nvec, int sets, uint32_t cs, int reps) {
+    auto args_for = [&](int i) {
+        chr::TreeArgs a{};
+        const auto& b = bufs[i % sets];  // 18 buffers: tree t leaves b[9t .. 9t+7], out b[9t+8]
+        a.nseg = 2;
+        a.nl = 8;
+        a.xrun = cs;
+        const uint32_t trips = (uint32_t)((nvec + 64 * U - 1) / (64 * U));
+        for (int j = 0; j < chr::kMaxTreeSegs; ++j) {
+            a.block0[j] = j < 2 ? j * trips : ~0u;
+            a.xfull[j] = j < 2 ? chr::xcd_full(trips, cs) : 0;
+        }
+        for (int t = 0; t < 2; ++t) {
+            chr::TreeSeg& g = a.seg[t];
+            for (int l = 0; l < 8; ++l) g.leaves[l] = (const chr::u32x4*)b[9 * t + l];
+            g.out = (chr::u32x4*)b[9 * t + 8];
+            g.nvec = nvec;
+            g.comb = 0;
+            const int comb[8] = {0, 1, 1, 1, 0, 1, 1, 2};
+            for (int l = 0; l < 8; ++l) g.comb |= (uint32_t)comb[l] << (2 * l);
+            g.swaps = 0;
+        }
+        return std::make_pair(a, 2 * trips);
+    };
+    return time_launches([&](int i) {
+        auto [a, grid] = args_for(i);
+        hipLaunchKernelGGL((chr::k_reduce_tree<CHR_FLOAT32, CHR_SUM, 8, U, true, 64>), dim3(grid), dim3(64), 0, 0, a);
+    }, reps);
+}
+
+static void focus10(size_t piece, int sets, int rounds) {
+    const size_t nvec = piece / 16;
+    Sets S = make_sets(17, nvec, sets);  // 18 operands per set
+    const double bytes = 2.0 * 9 * piece;
+    char tag[96];
+    std::snprintf(tag, sizeof tag, " piece=%zuMiB sets=%d ws=%zuMiB", piece >> 20, sets, (size_t)sets * 18 * (piece >> 20));
+    for (int r = 0; r < rounds; ++r) {
+        for (int u : {1, 2, 4})
+            for (uint32_t run_kib : {0u, 256u, 512u, 1024u}) {
+                const size_t trip = (size_t)64 * u * 16;
+                uint32_t cs = 0;
+                while (((size_t)2 << cs) * trip <= (size_t)run_kib * 1024 && cs < 16) ++cs;
+                const double us = u == 1 ? tree_launches<1>(S.bufs, nvec, sets, cs, 40)
+                                : u == 2 ? tree_launches<2>(S.bufs, nvec, sets, cs, 40)
+                                         : tree_launches<4>(S.bufs, nvec, sets, cs, 40);
+                char name[160];
+                std::snprintf(name, sizeof name, "tree8x2 U=%d run=%uKiB%s", u, run_kib, tag);
+                report_moved(name, bytes, us);
+            }
+        std::printf("--\n");
+    }
+    free_sets(S);
+}
+
 int main(int argc, char** argv) {
     check();
     if (argc > 1 && std::string(argv[1]) == "layout") {
         layout_mode();
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus10") {
+        focus10(16 << 20, 16, 2);  // C4 slice at the automatic depth, 4.5 GiB rotation (cold)
+        focus10(16 << 20, 4, 2);   // 1.1 GiB rotation (warm translations)
+        focus10(32 << 20, 8, 1);
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus9") {  // finer runs: 128 KiB .. 1 MiB per XCD
