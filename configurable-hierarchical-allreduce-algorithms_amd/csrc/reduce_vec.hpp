@@ -21,7 +21,6 @@ struct VecArgs {
     uint32_t xfull;  // blocks [0, xfull) are remapped (xcd_full of the grid); set per launch
 };
 
-
 // U vectors (16 B each) per lane per trip; all M+1 operands of the trip are loaded
 // before the first add so (M+1)*U*16 bytes per lane are in flight.  NT: non-temporal
 // loads and stores (global_load/store_dwordx4 ... nt) for calls that stream far more than
@@ -31,16 +30,16 @@ struct VecArgs {
 // (profiles/r01/microbench_focus4_slot_policy.txt) +15 % at 1 GiB m=1, +3-5 % for m>=2 with
 // 256-thread workgroups; with one-wave workgroups it also gains on the 64 MiB m=1 bucket
 // (6 440-6 464 vs 6 041-6 052 GB/s all-nt, profiles/r01/block_ab_bench.txt), so it is used for
-// every nt call; making ALL accumulator slots temporal thrashes the cache (-7 %).  Slot 0 is peeled so that the two policies
-// are separate instructions (a select between a plain and an nt load of one address is
-// merged by LLVM, dropping the nt bit).
+// every nt call; making ALL accumulator slots temporal thrashes the cache (-7 %).  Slot 0 is
+// peeled so that the two policies are separate instructions (a select between a plain and an nt
+// load of one address is merged by LLVM, dropping the nt bit).
 //
 // One trip per workgroup (grid = trips, no grid-stride loop), trips placed by xcd_trip.  With the
 // pinned arguments below this kernel runs within 0.3-1 % of a bare one-trip kernel without any
 // bounds check (microbench focus9: C2 shape 0.813-0.821 vs 0.822-0.824); the earlier grid-stride
 // form with lazily loaded pointers ran at 0.798-0.802.
 //
-// Every operand pointer is pinned into SGPRs before the trip's first load (kernarg_pointers): left
+// Every operand pointer is pinned into SGPRs before the trip's first load (pin_sgpr): left
 // to itself the compiler loads the input pointers from the kernel arguments between the
 // accumulator and input loads, which puts a second scalar-load round trip (s_waitcnt lgkmcnt)
 // in front of half of the trip's loads.  The full/partial decision is per trip (scalar).
