@@ -295,20 +295,27 @@ def bench_e2e(args):
     comm = ca.Comm(1, ca.get_unique_id(), 0, 0)
     n = 1 << 28  # 1 GiB fp32 per rank, the C4 buffer
     out = {"workload": "host-buffer staging, 1 GiB fp32, nranks=1 (H2D + schedule + D2H)"}
+    # window 0: one H2D, the collective, one D2H; else chr_comm_set_host_pipeline windows of that
+    # many MiB per rank, with H2D / collective / D2H of consecutive windows on three streams
     for kind in ("pageable", "pinned"):
         if kind == "pageable":
             h_send, h_recv = np.ones(n, dtype=np.float32), np.zeros(n, dtype=np.float32)
         else:
             h_send = torch.ones(n, dtype=torch.float32).pin_memory()
             h_recv = torch.zeros(n, dtype=torch.float32).pin_memory()
-        ca.check(ca.all_reduce_radix_batch(h_send, h_recv, n, ca.FLOAT32, ca.SUM, comm, 2, 1))
-        reps = 3
-        t0 = time.perf_counter()
-        for _ in range(reps):
+        for window in (0, 32, 128):
+            comm.set_host_pipeline(window)
+            h_recv[12345] = 0.0
             ca.check(ca.all_reduce_radix_batch(h_send, h_recv, n, ca.FLOAT32, ca.SUM, comm, 2, 1))
-        dt = (time.perf_counter() - t0) / reps
-        out[kind] = {"ms": round(dt * 1e3, 2), "GBps_per_direction": round(4 * n / (dt / 2) / 1e9, 2)}
-        assert float(h_recv[12345]) == 1.0
+            reps = 3
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ca.check(ca.all_reduce_radix_batch(h_send, h_recv, n, ca.FLOAT32, ca.SUM, comm, 2, 1))
+            dt = (time.perf_counter() - t0) / reps
+            key = kind if window == 0 else f"{kind}_pipelined_{window}MiB_windows"
+            out[key] = {"ms": round(dt * 1e3, 2), "GBps_per_direction": round(4 * n / (dt / 2) / 1e9, 2)}
+            assert float(h_recv[12345]) == 1.0
+    comm.set_host_pipeline(0)
     d_send = torch.ones(n, dtype=torch.float32, device="cuda:0")
     d_recv = torch.zeros(n, dtype=torch.float32, device="cuda:0")
     ca.check(ca.all_reduce_radix_batch(d_send, d_recv, n, ca.FLOAT32, ca.SUM, comm, 2, 1))

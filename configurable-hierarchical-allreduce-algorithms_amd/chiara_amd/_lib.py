@@ -79,6 +79,7 @@ def _load():
         "chr_comm_profile_phases": ([vp, ctypes.c_char_p, sz, i], ctypes.c_long),
         "chr_comm_tuned_schedule": ([vp, i, sz, i, i, i, ctypes.POINTER(i), ctypes.POINTER(i)], i),
         "chr_comm_set_graphs": ([vp, i], i),
+        "chr_comm_set_host_pipeline": ([vp, i], i),
         "chr_comm_set_timeout": ([vp, i], i),
         "chr_comm_abort": ([vp], i),
         "chr_comm_synchronize": ([vp], i),
@@ -118,7 +119,7 @@ EXPORTED = [
     "chr_allreduce_mpich_async", "chr_local_allreduce_mpich", "chr_allgather_radix_batch",
     "chr_allgather_radix_batch_async", "chr_local_allgather_radix_batch", "chr_comm_set_schedule", "chr_comm_set_overlap",
     "chr_local_group_set_schedule", "chr_plan_describe_ex", "chr_reduce_tree", "chr_comm_profile_phases",
-    "chr_comm_tuned_schedule", "chr_comm_set_graphs", "chr_comm_set_timeout", "chr_comm_abort",
+    "chr_comm_tuned_schedule", "chr_comm_set_graphs", "chr_comm_set_host_pipeline", "chr_comm_set_timeout", "chr_comm_abort",
     "chr_comm_synchronize", "chr_comm_is_aborted", "chr_reduce_tree_batch", "chr_local_group_profile",
     "chr_local_group_profile_read", "chr_reduce_scatter_mpich", "chr_reduce_scatter_mpich_async",
     "chr_local_reduce_scatter_mpich",

@@ -162,6 +162,12 @@ class Comm:
         """Replay device-resident collectives from captured HIP graphs (one per plan and buffers)."""
         check(lib().chr_comm_set_graphs(self._h, int(bool(enable))))
 
+    def set_host_pipeline(self, window_mib):
+        """Host-buffer allreduce / reduce-scatter calls larger than one window run as pipelined
+        windows (H2D, collective and D2H on three streams); 0 = off.  Every rank must then pass host
+        buffers for the same calls.  Same bits (block-window property)."""
+        check(lib().chr_comm_set_host_pipeline(self._h, int(window_mib)))
+
     def set_timeout(self, timeout_ms):
         """Blocking calls give up after timeout_ms (0 = never): the communicator is aborted and
         ERR_TIMEOUT returned, so a lost peer is an error code instead of a hang."""

@@ -276,6 +276,14 @@ int default_graphs() {
 
 // CHR_TIMEOUT_MS: blocking calls give up after this many milliseconds (0 = wait forever, the
 // default); see chr_comm_set_timeout
+int default_host_window_mib() {
+    static const int v = [] {
+        const char* e = std::getenv("CHR_HOST_WINDOW_MIB");
+        return e ? std::max(0, std::atoi(e)) : 0;
+    }();
+    return v;
+}
+
 int default_timeout_ms() {
     static const int v = [] {
         const char* e = std::getenv("CHR_TIMEOUT_MS");
@@ -355,6 +363,37 @@ struct chr_comm {
     DevBuf acc, stage, hsend, hrecv;
     ReduceProfile prof;
     std::map<PlanKey, std::unique_ptr<Plan>> plans;
+
+    // Pipelined host staging (chr_comm_set_host_pipeline): copy-in and copy-out streams, two
+    // device window buffers per direction, and the events that order them against the collective.
+    int host_window_mib = default_host_window_mib();
+    hipStream_t hin = nullptr, hout = nullptr;
+    DevBuf wsend[2], wrecv[2];
+    hipEvent_t ev_in[2] = {}, ev_coll[2] = {}, ev_out[2] = {};
+    hipError_t host_pipeline_init() {
+        if (hin) return hipSuccess;
+        hipError_t e = hipStreamCreateWithFlags(&hin, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&hout, hipStreamNonBlocking);
+        for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+            e = hipEventCreateWithFlags(&ev_in[i], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&ev_coll[i], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&ev_out[i], hipEventDisableTiming);
+        }
+        return e;
+    }
+    void host_pipeline_release() {
+        if (hin) (void)hipStreamSynchronize(hin);
+        if (hout) (void)hipStreamSynchronize(hout);
+        for (int i = 0; i < 2; ++i) {
+            wsend[i].release();
+            wrecv[i].release();
+            for (hipEvent_t* e : {&ev_in[i], &ev_coll[i], &ev_out[i]})
+                if (*e) (void)hipEventDestroy(*e);
+        }
+        if (hin) (void)hipStreamDestroy(hin);
+        if (hout) (void)hipStreamDestroy(hout);
+        hin = hout = nullptr;
+    }
 
     // Failure handling.  A call that fails after it has posted RCCL operations, or that times
     // out, aborts the RCCL communicator (ncclCommAbort: its kernels exit, peers see the closed
@@ -578,6 +617,61 @@ int wait_call(chr_comm* c) {
     }
 }
 
+// Pipelined host staging (chr_comm_set_host_pipeline).  An allreduce/reduce-scatter output element
+// depends only on the elements at the same offset of every recvcount block (every reduction is
+// element-wise, every message block-granular; pinned by test_block_window_property), so a host
+// call splits into collectives over windows [off, off + w) of every block, each with the plan for
+// n*w (allreduce) or w (reduce-scatter) elements -- the bits of the whole call.  Window j's H2D
+// (2-D copy, one row per block) runs on `hin`, its collective on the communicator's streams, its
+// D2H on `hout`; two device buffers per direction let window j+1 come in and j-1 go out while j
+// is reduced.  Returns -1 when the call is not split (one window would cover it).
+int run_host_windows(chr_comm* c, int sched, int slices, int mode, const void* input, void* recv, size_t count,
+                     int dtype, int op, int k, int b) {
+    if (c->host_window_mib <= 0 || (mode != chr::MODE_ALLREDUCE && mode != chr::MODE_REDUCE_SCATTER)) return -1;
+    const size_t es = chr::dtype_size(dtype), n = (size_t)c->nranks;
+    const size_t block = mode == chr::MODE_ALLREDUCE ? count / n : count;  // recvcount
+    if (mode == chr::MODE_ALLREDUCE && block * n != count) return -1;      // the plan reports the error
+    size_t w = ((size_t)c->host_window_mib << 20) / (n * es);
+    w -= w % 64;  // windows start 256 B-aligned within each block when the block is
+    if (w == 0 || w >= block) return -1;
+    hipError_t e = c->host_pipeline_init();
+    if (e != hipSuccess) return hip_code(e);
+    const size_t out_rows = mode == chr::MODE_ALLREDUCE ? n : 1;
+    for (int i = 0; i < 2; ++i) {
+        if ((e = c->wsend[i].reserve(n * w * es, c->stream)) != hipSuccess) return hip_code(e);
+        if ((e = c->wrecv[i].reserve(out_rows * w * es, c->stream)) != hipSuccess) return hip_code(e);
+    }
+    const char* hsrc = (const char*)input;
+    char* hdst = (char*)recv;
+    size_t j = 0;
+    for (size_t off = 0; off < block; off += w, ++j) {
+        const int i = (int)(j & 1);
+        const size_t wj = std::min(w, block - off);
+        // window j reuses window j-2's buffers: its copy-in waits for j-2's collective, and the
+        // collective for j-2's copy-out (events recorded before first use are complete)
+        if (j >= 2 && (e = hipStreamWaitEvent(c->hin, c->ev_coll[i], 0)) != hipSuccess) return hip_code(e);
+        if ((e = hipMemcpy2DAsync(c->wsend[i].p, wj * es, hsrc + off * es, block * es, wj * es, n,
+                                  hipMemcpyHostToDevice, c->hin)) != hipSuccess)
+            return hip_code(e);
+        if ((e = hipEventRecord(c->ev_in[i], c->hin)) != hipSuccess) return hip_code(e);
+        if ((e = hipStreamWaitEvent(c->stream, c->ev_in[i], 0)) != hipSuccess) return hip_code(e);
+        if (j >= 2 && (e = hipStreamWaitEvent(c->stream, c->ev_out[i], 0)) != hipSuccess) return hip_code(e);
+        const Plan& p = c->plan(mode, k, b, mode == chr::MODE_ALLREDUCE ? n * wj : wj, es, sched, slices);
+        if (p.error) return p.error;
+        int rc = enqueue_rccl(c, p, c->wsend[i].p, c->wrecv[i].p, dtype, op);
+        if (rc) return rc;
+        if ((e = hipEventRecord(c->ev_coll[i], c->stream)) != hipSuccess) return hip_code(e);
+        if ((e = hipStreamWaitEvent(c->hout, c->ev_coll[i], 0)) != hipSuccess) return hip_code(e);
+        if ((e = hipMemcpy2DAsync(hdst + off * es, block * es, c->wrecv[i].p, wj * es, wj * es, out_rows,
+                                  hipMemcpyDeviceToHost, c->hout)) != hipSuccess)
+            return hip_code(e);
+        if ((e = hipEventRecord(c->ev_out[i], c->hout)) != hipSuccess) return hip_code(e);
+    }
+    int rc = wait_call(c);  // the last collective, under the communicator's timeout
+    if (rc) return rc;
+    return hip_code(hipStreamSynchronize(c->hout));
+}
+
 int run_collective(chr_comm* c, int sched, int slices, int mode, const void* send, void* recv, size_t count, int dtype,
                    int op, int k, int b, bool sync) {
     const Plan& p = c->plan(mode, k, b, count, chr::dtype_size(dtype), sched, slices);
@@ -600,6 +694,10 @@ int run_collective(chr_comm* c, int sched, int slices, int mode, const void* sen
         return wait_call(c);
     }
     if (!sync) return CHR_ERR_UNSUPPORTED;  // async needs device-resident buffers
+    if (!dev_in && !dev_out) {
+        const int rc = run_host_windows(c, sched, slices, mode, input, recv, count, dtype, op, k, b);
+        if (rc >= 0) return rc;
+    }
     // Host-memory contract of the reference: stage through HBM (PCIe H2D / D2H).
     const void* dsend = input;
     void* drecv = recv;
@@ -891,6 +989,7 @@ int chr_comm_destroy(chr_comm* c) {
     c->stage.release();
     c->hsend.release();
     c->hrecv.release();
+    c->host_pipeline_release();
     if (c->cstream) (void)hipStreamSynchronize(c->cstream);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
@@ -990,6 +1089,12 @@ int chr_comm_set_overlap(chr_comm* c, int enable) {
 int chr_comm_set_schedule(chr_comm* c, int schedule) {
     if (!c || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_AUTO) return CHR_ERR_INVALID_ARG;
     c->sched = schedule;
+    return CHR_SUCCESS;
+}
+
+int chr_comm_set_host_pipeline(chr_comm* c, int window_mib) {
+    if (!c || window_mib < 0) return CHR_ERR_INVALID_ARG;
+    c->host_window_mib = window_mib;
     return CHR_SUCCESS;
 }
 

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define CHR_ABI_VERSION 3
+#define CHR_ABI_VERSION 4
 
 /* Element types.  The reference is generic over MPI_Datatype (all_reduce_radix_batch.cpp:202-204,
  * sizes from MPI_Type_size at :234-277); these are the MPI predefined types MPICH's
@@ -207,6 +207,16 @@ int chr_comm_set_overlap(chr_comm* comm, int enable);
  * cost per call to one launch (small messages are bound by it).  Buffers must stay allocated
  * while graphs that name them may be replayed; disabling drops every cached graph.  Same bits. */
 int chr_comm_set_graphs(chr_comm* comm, int enable);
+/* Pipelined host staging (default off; env CHR_HOST_WINDOW_MIB).  The reference's contract starts
+ * and ends in host memory; with window_mib > 0 a host-buffer allreduce_radix_batch or
+ * reduce_scatter_radix_batch whose per-rank buffer exceeds one window runs as a sequence of
+ * collectives over windows of every recvcount block (about window_mib MiB per rank each): the
+ * H2D copy of window j+1, the collective of window j and the D2H copy of window j-1 run on three
+ * streams at once.  The bits are those of the whole call (an output window depends only on the
+ * same window of every block: tests/test_oracle_golden.py::test_block_window_property).  Every
+ * rank of the communicator must then pass host buffers for the same calls (the number of RCCL
+ * collectives a call issues depends on it).  0 restores one H2D, one collective, one D2H. */
+int chr_comm_set_host_pipeline(chr_comm* comm, int window_mib);
 /* Opt-in timing of the fused bucket-reduction launches of this communicator (HIP events
  * on its stream).  _read synchronises on the recorded launches and returns the summed
  * kernel milliseconds, the algorithmic bytes ((m+2)*n*sizeof(T) per launch) and the

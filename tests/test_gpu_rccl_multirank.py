@@ -595,3 +595,50 @@ def test_rccl_graph_replay_baselines_world4():
     res = _spawn(_graph_baselines_worker, 4)
     bad = [r for r in res if r[1]]
     assert not bad, bad
+
+
+def _host_pipeline_worker(rank, world, port, q):
+    """chr_comm_set_host_pipeline: host-buffer calls split into block windows (H2D / collective /
+    D2H on three streams), ragged last window, in place and not: bit-exact vs the oracle."""
+    _setup(rank)
+    import torch.distributed as dist
+
+    import chiara_amd as ca
+    import pyoracle as po
+
+    comm = _init_worker(rank, world, port)
+    bad = []
+    try:
+        comm.set_host_pipeline(1)  # 1 MiB windows per rank: several windows at these sizes
+        for mode, dtype, rc_, inplace, sched in (("ar", "f32", 300001, False, ca.SCHEDULE_FLAT),
+                                                  ("ar", "bf16", 200003, True, ca.SCHEDULE_REFERENCE),
+                                                  ("rs", "f32", 250001, False, ca.SCHEDULE_FLAT),
+                                                  ("rs", "f32", 70000, True, ca.SCHEDULE_EXACT),
+                                                  ("ar", "i32", 65536 * 3, False, ca.SCHEDULE_FLAT_SEQ)):
+            comm.set_schedule(sched)
+            cdt = {"f32": ca.FLOAT32, "bf16": ca.BFLOAT16, "i32": ca.INT32}[dtype]
+            npdt = po.NP_DTYPES[dtype]
+            n_in = rc_ * world
+            allx = [po.fill(n_in, dtype, 0, 555, r) for r in range(world)]
+            x = allx[rank].copy()
+            if mode == "ar":
+                out = x if inplace else np.zeros(n_in, dtype=npdt)
+                rc = ca.all_reduce_radix_batch(ca.IN_PLACE if inplace else x, out, n_in, cdt, ca.SUM, comm, 2, 2)
+                want = po.allreduce_radix_batch(allx, 2, 2, dtype, "sum")[rank]
+            else:
+                out = x if inplace else np.zeros(rc_, dtype=npdt)
+                rc = ca.reduce_scatter_radix_batch(ca.IN_PLACE if inplace else x, out, rc_, cdt, ca.SUM, comm, 2, 2)
+                want = po.reduce_scatter_radix_batch(allx, 2, 2, dtype, "sum")[rank]
+            got = out[:want.size]
+            if rc != 0 or got.tobytes() != want.tobytes():
+                bad.append((mode, dtype, rc_, inplace, rc))
+    finally:
+        comm.destroy()
+        dist.destroy_process_group()
+    q.put((rank, bad))
+
+
+def test_rccl_host_pipeline_windows_world4():
+    res = _spawn(_host_pipeline_worker, 4)
+    bad = [r for r in res if r[1]]
+    assert not bad, bad
