@@ -368,8 +368,78 @@ def bench_collective_kernels(args):
         del sends, recvs
         torch.cuda.empty_cache()
     g.destroy()
+    for dname, cdt, es in (("f32", ca.FLOAT32, 4), ("bf16", ca.BFLOAT16, 2)):
+        for slices in (4, 8):
+            for recv_copies in (False, True):
+                key = f"{'c4' if dname == 'f32' else 'c5'}_{dname}_rank0_alone_slices_{slices}" + \
+                      ("_after_recv_copies" if recv_copies else "")
+                rows[key] = replay_rank_trees(ca, torch, dev, cdt, es, (1 << 30) // es, n, k, b, slices, recv_copies)
+                torch.cuda.empty_cache()
     emit({"collective_kernels": {"workload": "all_reduce_radix_batch fused reductions, 8 virtual ranks, k=4, b=4, "
-                                             "1 GiB per rank, flat schedule (batched trees)", "rows": rows}})
+                                             "1 GiB per rank, flat schedule (batched trees); *_rank0_alone rows: "
+                                             "rank 0's own trees on its own send/recv/STAGE only", "rows": rows}})
+
+
+def replay_rank_trees(ca, torch, dev, cdt, es, count, n, k, b, slices, recv_copies, reps=5):
+    """Rank 0's fused reductions of one C4/C5 call, alone, on rank 0's own buffers: send, recv and
+    STAGE (~3 GiB), the working set one GPU of an 8-GPU node holds.  The 8-virtual-rank rows above
+    hold all eight ranks' buffers (~25 GiB, past the translation cliff of DESIGN §4.1) and so
+    under-state the per-GPU case.  The plan is the flat schedule's own (describe_plan), its tree
+    ops batched per step as the executor batches them (chr_reduce_tree_batch); leaf data are
+    synthetic (timing only, SUM is data-independent).  With recv_copies, every step's receives are
+    first written into STAGE by device copies from SEND (as RCCL's receives would leave them) and
+    only the tree launches are timed."""
+    plan = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, n, 0, k, b, count, slices, ca.SCHEDULE_FLAT))
+    h = plan["header"]
+    bufs = {name: torch.empty(max(1, h[name.lower()]) * es, dtype=torch.uint8, device=dev)
+            for name in ("SEND", "RECV", "STAGE", "ACC")}
+    s = torch.cuda.current_stream(dev)
+    for i, (name, t) in enumerate(bufs.items()):
+        ca.check(ca.fill(t, t.numel() // es, cdt, 0, SEED, i, stream=s))
+    ptr = lambda ref: bufs[ref[0]].data_ptr() + ref[1] * es  # noqa: E731
+    steps = []
+    for st in plan["steps"]:
+        trees = [op for op in st["post"] if op[0] == "tree"]
+        if trees:
+            assert len({len(op[4]) for op in trees}) == 1 and len({op[3] for op in trees}) == 1
+        copies = [(bufs[dst[0]].narrow(0, dst[1] * es, cnt * es), bufs["SEND"].narrow(0, 0, cnt * es))
+                  for (_, dst, cnt) in st["recvs"]]
+        steps.append((trees, copies))
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in steps]
+    ms = by = launches = 0
+
+    def call(timed):
+        nonlocal ms, by, launches
+        for (trees, copies), (e0, e1) in zip(steps, evs):
+            if recv_copies:
+                for d, src in copies:
+                    d.copy_(src)  # D2D on s
+            if not trees:
+                continue
+            e0.record(s)
+            ca.check(ca.reduce_tree_batch([ptr(op[1]) for op in trees],
+                                          [[ptr(op[2])] + [ptr(x) for x in op[4]] for op in trees],
+                                          [op[5][0] for op in trees], [op[5][1] for op in trees],
+                                          trees[0][3], cdt, ca.SUM, s))
+            e1.record(s)
+        if timed:
+            torch.cuda.synchronize()
+            for (trees, _), (e0, e1) in zip(steps, evs):
+                if trees:
+                    ms += e0.elapsed_time(e1)
+                    by += sum((len(op[4]) + 2) * op[3] * es for op in trees)
+                    launches += 1
+
+    for _ in range(2):
+        call(False)
+    for _ in range(reps):
+        call(True)
+    del bufs
+    ach = by / (ms * 1e-3) / 1e9
+    return {"launches_per_call": launches // reps, "kernel_ms_per_call": round(ms / reps, 4),
+            "algorithmic_bytes_per_call": int(by / reps), "working_set_GiB": round(
+                (h["send"] + h["recv"] + h["stage"] + h["acc"]) * es / 2**30, 2),
+            "achieved_GBps": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4)}
 
 
 # ---- N > 1: hierarchical allreduce over RCCL ---------------------------------------------------
