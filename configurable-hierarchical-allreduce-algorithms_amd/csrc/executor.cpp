@@ -16,11 +16,13 @@
 #include <algorithm>
 #include <cctype>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <tuple>
@@ -624,7 +626,17 @@ int wait_call(chr_comm* c) {
 // n*w (allreduce) or w (reduce-scatter) elements -- the bits of the whole call.  Window j's H2D
 // (2-D copy, one row per block) runs on `hin`, its collective on the communicator's streams, its
 // D2H on `hout`; two device buffers per direction let window j+1 come in and j-1 go out while j
-// is reduced.  Returns -1 when the call is not split (one window would cover it).
+// is reduced.
+//
+// The D2H side is issued from a second host thread.  A copy from or to pageable memory (the
+// reference harness mallocs its buffers) returns only when HIP has staged it through its own
+// pinned bounce buffers, so from one thread the two directions strictly alternate; from two
+// threads they overlap (tools/host_stage_probe: 1 GiB each way, 38.2 ms one after the other,
+// 22.5 ms from two threads, the same as pinned memory).  The threads hand windows over through
+// two counters: the issuing thread publishes "window j's collective is enqueued" (the D2H may then
+// wait on ev_coll), the copy-out thread "window j's D2H is enqueued" (a later collective may then
+// wait on ev_out before overwriting that window's device buffer).  Returns -1 when the call is
+// not split (one window would cover it).
 int run_host_windows(chr_comm* c, int sched, int slices, int mode, const void* input, void* recv, size_t count,
                      int dtype, int op, int k, int b) {
     if (c->host_window_mib <= 0 || (mode != chr::MODE_ALLREDUCE && mode != chr::MODE_REDUCE_SCATTER)) return -1;
@@ -643,33 +655,83 @@ int run_host_windows(chr_comm* c, int sched, int slices, int mode, const void* i
     }
     const char* hsrc = (const char*)input;
     char* hdst = (char*)recv;
-    size_t j = 0;
-    for (size_t off = 0; off < block; off += w, ++j) {
-        const int i = (int)(j & 1);
-        const size_t wj = std::min(w, block - off);
-        // window j reuses window j-2's buffers: its copy-in waits for j-2's collective, and the
-        // collective for j-2's copy-out (events recorded before first use are complete)
-        if (j >= 2 && (e = hipStreamWaitEvent(c->hin, c->ev_coll[i], 0)) != hipSuccess) return hip_code(e);
-        if ((e = hipMemcpy2DAsync(c->wsend[i].p, wj * es, hsrc + off * es, block * es, wj * es, n,
-                                  hipMemcpyHostToDevice, c->hin)) != hipSuccess)
-            return hip_code(e);
-        if ((e = hipEventRecord(c->ev_in[i], c->hin)) != hipSuccess) return hip_code(e);
-        if ((e = hipStreamWaitEvent(c->stream, c->ev_in[i], 0)) != hipSuccess) return hip_code(e);
-        if (j >= 2 && (e = hipStreamWaitEvent(c->stream, c->ev_out[i], 0)) != hipSuccess) return hip_code(e);
-        const Plan& p = c->plan(mode, k, b, mode == chr::MODE_ALLREDUCE ? n * wj : wj, es, sched, slices);
-        if (p.error) return p.error;
-        int rc = enqueue_rccl(c, p, c->wsend[i].p, c->wrecv[i].p, dtype, op);
-        if (rc) return rc;
-        if ((e = hipEventRecord(c->ev_coll[i], c->stream)) != hipSuccess) return hip_code(e);
-        if ((e = hipStreamWaitEvent(c->hout, c->ev_coll[i], 0)) != hipSuccess) return hip_code(e);
-        if ((e = hipMemcpy2DAsync(hdst + off * es, block * es, c->wrecv[i].p, wj * es, wj * es, out_rows,
-                                  hipMemcpyDeviceToHost, c->hout)) != hipSuccess)
-            return hip_code(e);
-        if ((e = hipEventRecord(c->ev_out[i], c->hout)) != hipSuccess) return hip_code(e);
+    const size_t nwin = (block + w - 1) / w;
+
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t coll_enqueued = 0, out_enqueued = 0;  // windows handed over, under mu
+    bool stop = false;                           // the issuing thread failed: copy-out ends
+    int out_rc = CHR_SUCCESS;                    // the copy-out thread's first error
+    std::thread copy_out([&] {
+        if (hipSetDevice(c->device) != hipSuccess) {
+            std::lock_guard<std::mutex> g(mu);
+            out_rc = CHR_ERR_HIP;
+            cv.notify_all();
+            return;
+        }
+        for (size_t j = 0; j < nwin; ++j) {
+            {
+                std::unique_lock<std::mutex> g(mu);
+                cv.wait(g, [&] { return stop || coll_enqueued > j; });
+                if (stop) return;
+            }
+            const int i = (int)(j & 1);
+            const size_t off = j * w, wj = std::min(w, block - off);
+            hipError_t ee = hipStreamWaitEvent(c->hout, c->ev_coll[i], 0);
+            if (ee == hipSuccess)
+                ee = hipMemcpy2DAsync(hdst + off * es, block * es, c->wrecv[i].p, wj * es, wj * es, out_rows,
+                                      hipMemcpyDeviceToHost, c->hout);
+            if (ee == hipSuccess) ee = hipEventRecord(c->ev_out[i], c->hout);
+            std::lock_guard<std::mutex> g(mu);
+            if (ee != hipSuccess) {
+                out_rc = hip_code(ee);
+                cv.notify_all();
+                return;
+            }
+            out_enqueued = j + 1;
+            cv.notify_all();
+        }
+    });
+    auto issue = [&]() -> int {
+        for (size_t j = 0; j < nwin; ++j) {
+            const int i = (int)(j & 1);
+            const size_t off = j * w, wj = std::min(w, block - off);
+            // window j reuses window j-2's buffers: its copy-in waits for j-2's collective, and
+            // the collective for j-2's copy-out, once the copy-out thread has enqueued it
+            if (j >= 2 && (e = hipStreamWaitEvent(c->hin, c->ev_coll[i], 0)) != hipSuccess) return hip_code(e);
+            if ((e = hipMemcpy2DAsync(c->wsend[i].p, wj * es, hsrc + off * es, block * es, wj * es, n,
+                                      hipMemcpyHostToDevice, c->hin)) != hipSuccess)
+                return hip_code(e);
+            if ((e = hipEventRecord(c->ev_in[i], c->hin)) != hipSuccess) return hip_code(e);
+            if ((e = hipStreamWaitEvent(c->stream, c->ev_in[i], 0)) != hipSuccess) return hip_code(e);
+            if (j >= 2) {
+                std::unique_lock<std::mutex> g(mu);
+                cv.wait(g, [&] { return out_rc != CHR_SUCCESS || out_enqueued >= j - 1; });
+                if (out_rc != CHR_SUCCESS) return out_rc;
+                if ((e = hipStreamWaitEvent(c->stream, c->ev_out[i], 0)) != hipSuccess) return hip_code(e);
+            }
+            const Plan& p = c->plan(mode, k, b, mode == chr::MODE_ALLREDUCE ? n * wj : wj, es, sched, slices);
+            if (p.error) return p.error;
+            int rc = enqueue_rccl(c, p, c->wsend[i].p, c->wrecv[i].p, dtype, op);
+            if (rc) return rc;
+            if ((e = hipEventRecord(c->ev_coll[i], c->stream)) != hipSuccess) return hip_code(e);
+            std::lock_guard<std::mutex> g(mu);
+            coll_enqueued = j + 1;
+            cv.notify_all();
+        }
+        return CHR_SUCCESS;
+    };
+    int rc = issue();
+    if (rc) {
+        std::lock_guard<std::mutex> g(mu);
+        stop = true;
+        cv.notify_all();
     }
-    int rc = wait_call(c);  // the last collective, under the communicator's timeout
+    if (!rc) rc = wait_call(c);  // the last collective, under the communicator's timeout
+    copy_out.join();
+    const int rc_out = hip_code(hipStreamSynchronize(c->hout));
     if (rc) return rc;
-    return hip_code(hipStreamSynchronize(c->hout));
+    return out_rc ? out_rc : rc_out;
 }
 
 int run_collective(chr_comm* c, int sched, int slices, int mode, const void* send, void* recv, size_t count, int dtype,

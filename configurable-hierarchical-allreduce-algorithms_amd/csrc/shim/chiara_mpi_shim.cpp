@@ -28,6 +28,8 @@
 
 #include <cstdio>
 
+#include <cstdlib>
+
 #include "chiara.h"
 
 namespace {
@@ -59,6 +61,10 @@ chr_comm* comm_for(MPI_Comm mc) {
     MPI_Bcast(&id, sizeof(id), MPI_BYTE, 0, mc);
     chr_comm* c = nullptr;
     if (chr_comm_init_rank(&c, n, &id, rank, lrank % ndev) != CHR_SUCCESS) return nullptr;
+    // The MPI signatures' contract is host memory on every rank (the reference harness mallocs
+    // its buffers), which is what pipelined host staging needs: on by default here, 32 MiB windows
+    // per rank, unless CHR_HOST_WINDOW_MIB says otherwise.
+    if (!std::getenv("CHR_HOST_WINDOW_MIB")) chr_comm_set_host_pipeline(c, 32);
     MPI_Comm_set_attr(mc, g_keyval, c);
     return c;
 }

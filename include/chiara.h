@@ -215,7 +215,9 @@ int chr_comm_set_graphs(chr_comm* comm, int enable);
  * streams at once.  The bits are those of the whole call (an output window depends only on the
  * same window of every block: tests/test_oracle_golden.py::test_block_window_property).  Every
  * rank of the communicator must then pass host buffers for the same calls (the number of RCCL
- * collectives a call issues depends on it).  0 restores one H2D, one collective, one D2H. */
+ * collectives a call issues depends on it).  0 restores one H2D, one collective, one D2H.  The
+ * D2H copies are issued from a second host thread, so copies from and to pageable memory overlap
+ * in both directions too.  The MPI-signature shim turns this on (32 MiB) for its communicators. */
 int chr_comm_set_host_pipeline(chr_comm* comm, int window_mib);
 /* Opt-in timing of the fused bucket-reduction launches of this communicator (HIP events
  * on its stream).  _read synchronises on the recorded launches and returns the summed

@@ -599,8 +599,10 @@ def test_rccl_graph_replay_baselines_world4():
 
 def _host_pipeline_worker(rank, world, port, q):
     """chr_comm_set_host_pipeline: host-buffer calls split into block windows (H2D / collective /
-    D2H on three streams), ragged last window, in place and not: bit-exact vs the oracle."""
+    D2H on three streams, D2H issued from a second host thread), ragged last window, pageable and
+    page-locked buffers, in place and not: bit-exact vs the oracle."""
     _setup(rank)
+    import torch
     import torch.distributed as dist
 
     import chiara_amd as ca
@@ -614,19 +616,27 @@ def _host_pipeline_worker(rank, world, port, q):
                                                   ("ar", "bf16", 200003, True, ca.SCHEDULE_REFERENCE),
                                                   ("rs", "f32", 250001, False, ca.SCHEDULE_FLAT),
                                                   ("rs", "f32", 70000, True, ca.SCHEDULE_EXACT),
-                                                  ("ar", "i32", 65536 * 3, False, ca.SCHEDULE_FLAT_SEQ)):
+                                                  ("ar", "i32", 65536 * 3, False, ca.SCHEDULE_FLAT_SEQ),
+                                                  ("ar", "f32", 131075 * 2, "pinned", ca.SCHEDULE_FLAT),
+                                                  ("rs", "f32", 300007, "pinned", ca.SCHEDULE_FLAT)):
             comm.set_schedule(sched)
             cdt = {"f32": ca.FLOAT32, "bf16": ca.BFLOAT16, "i32": ca.INT32}[dtype]
             npdt = po.NP_DTYPES[dtype]
             n_in = rc_ * world
             allx = [po.fill(n_in, dtype, 0, 555, r) for r in range(world)]
             x = allx[rank].copy()
+            if inplace == "pinned":  # page-locked buffers (the D2H thread then overlaps async copies)
+                inplace = False
+                x = torch.from_numpy(x).pin_memory().numpy()
+                pinned_out = torch.zeros(n_in if mode == "ar" else rc_, dtype=torch.float32).pin_memory()
+            else:
+                pinned_out = None
             if mode == "ar":
-                out = x if inplace else np.zeros(n_in, dtype=npdt)
+                out = x if inplace else (pinned_out.numpy() if pinned_out is not None else np.zeros(n_in, dtype=npdt))
                 rc = ca.all_reduce_radix_batch(ca.IN_PLACE if inplace else x, out, n_in, cdt, ca.SUM, comm, 2, 2)
                 want = po.allreduce_radix_batch(allx, 2, 2, dtype, "sum")[rank]
             else:
-                out = x if inplace else np.zeros(rc_, dtype=npdt)
+                out = x if inplace else (pinned_out.numpy() if pinned_out is not None else np.zeros(rc_, dtype=npdt))
                 rc = ca.reduce_scatter_radix_batch(ca.IN_PLACE if inplace else x, out, rc_, cdt, ca.SUM, comm, 2, 2)
                 want = po.reduce_scatter_radix_batch(allx, 2, 2, dtype, "sum")[rank]
             got = out[:want.size]

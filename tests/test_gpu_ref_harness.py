@@ -18,7 +18,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MPIEXEC = "/opt/conda/bin/mpiexec"
 
 
-def _run(binary, args, n, tmp_path, where=("oracle", "_ref"), prefix="results"):
+def _run(binary, args, n, tmp_path, where=("oracle", "_ref"), prefix="results", env=()):
     exe = os.path.join(REPO, *where, binary)
     if not os.path.exists(exe) or not os.path.exists(MPIEXEC):
         pytest.skip("reference harness binary or MPICH not present")
@@ -27,7 +27,10 @@ def _run(binary, args, n, tmp_path, where=("oracle", "_ref"), prefix="results"):
         if r:
             cmd.append(":")
         cmd += ["-n", "1", "-env", "NCCL_HOSTID", f"chiara-ref-harness-{r}", "-env", "NCCL_SOCKET_IFNAME", "lo",
-                "-env", "NCCL_IB_DISABLE", "1", exe] + args
+                "-env", "NCCL_IB_DISABLE", "1"]
+        for kv in env:
+            cmd += ["-env", *kv]
+        cmd += [exe] + args
     out = subprocess.run(cmd, cwd=tmp_path, capture_output=True, text=True, timeout=400)
     assert out.returncode == 0, out.stderr[-3000:]
     files = [f for f in os.listdir(tmp_path) if f.startswith(prefix) and f.endswith(".csv")]
@@ -53,6 +56,22 @@ def test_reference_allreduce_harness_on_mi355x(tmp_path):
     assert {r["k"] for r in ours} == {"2", "3"}
     assert all(r["is_correct"] == "1" for r in rows)
     _plots(tmp_path, "allreduce")
+
+
+def test_reference_harnesses_with_host_windows(tmp_path):
+    """The shim turns pipelined host staging on: with 1 MiB windows (CHR_HOST_WINDOW_MIB) a 4 Mi-int
+    call per rank runs as 4 window collectives, H2D / collective / D2H overlapped, the D2H from a
+    second host thread.  The reference's own is_correct must still be 1 on every row."""
+    (tmp_path / "ar").mkdir()
+    rows = _run("ref_harness_allreduce", ["1", "--overwrite", "b=4", "base=1048576"], 4, tmp_path / "ar",
+                env=[("CHR_HOST_WINDOW_MIB", "1")])
+    assert {r["k"] for r in rows if r["algorithm_name"] == "all_reduce_radix_batch"} == {"2", "3"}
+    assert all(r["is_correct"] == "1" for r in rows)
+    (tmp_path / "rs").mkdir()
+    rows = _run("ref_harness_reduce_scatter", ["1", "--overwrite", "b=4", "base=1048576"], 4, tmp_path / "rs",
+                env=[("CHR_HOST_WINDOW_MIB", "1")])
+    assert any(r["algorithm_name"] == "reduce_scatter_radix_batch" for r in rows)
+    assert all(r["is_correct"] == "1" for r in rows)
 
 
 def test_reference_reduce_scatter_harness_on_mi355x(tmp_path):
