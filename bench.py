@@ -303,7 +303,7 @@ def bench_e2e(args):
         else:
             h_send = torch.ones(n, dtype=torch.float32).pin_memory()
             h_recv = torch.zeros(n, dtype=torch.float32).pin_memory()
-        for window in (0, 32, 128):
+        for window in (0, 8, 16, 32, 128):
             comm.set_host_pipeline(window)
             h_recv[12345] = 0.0
             ca.check(ca.all_reduce_radix_batch(h_send, h_recv, n, ca.FLOAT32, ca.SUM, comm, 2, 1))

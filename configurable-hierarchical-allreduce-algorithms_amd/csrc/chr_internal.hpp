@@ -58,6 +58,9 @@ hipError_t launch_fill(void* buf, size_t n, int dtype, int pattern, uint64_t see
 //   CHR_REDUCE_ACC0_MIN_BYTES  bucket size from which m = 1 uses it too (0: always)
 //   CHR_REDUCE_BLOCK         threads per workgroup of the vector kernels: 64 or 256;
 //                            unset = 64 for NT calls, 256 otherwise
+//   CHR_WG_PER_CU_VEC        streaming (NT) bucket launches: at most this many workgroups resident
+//   CHR_WG_PER_CU_TREE       per CU, capped through dynamic LDS (0 = uncapped); unset = policy
+//                            (nt_lds_bytes in reduce_common.hpp); likewise for the tree kernel
 struct ReduceTuning {
     int xcd_run_kib;        // -1: policy
     size_t max_launch_vec;  // 0: the grid limit; else cap on 16-B vectors per launch / tree segment
@@ -66,6 +69,9 @@ struct ReduceTuning {
     size_t nt_min_bytes;
     int acc0_mode;
     size_t acc0_min_bytes;
+    int wg_per_cu_vec;   // -1: policy
+    int wg_per_cu_tree;  // -1: policy
+    unsigned lds_per_cu; // bytes of LDS per CU (device attribute; 160 KiB on gfx950)
 };
 ReduceTuning& reduce_tuning();
 

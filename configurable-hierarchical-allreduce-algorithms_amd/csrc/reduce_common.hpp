@@ -155,6 +155,15 @@ inline uint32_t xcd_run_shift(size_t policy_kib, size_t trip_bytes) {
     return cs;
 }
 
+// Dynamic LDS per workgroup that leaves at most `cap` workgroups resident per CU (the kernels use
+// no LDS; the allocation only caps occupancy).  env >= 0 overrides the policy; 0 = uncapped.
+inline unsigned nt_lds_bytes(int env, int policy) {
+    const unsigned lds = reduce_tuning().lds_per_cu;
+    const int cap = env >= 0 ? env : policy;
+    if (cap <= 0 || lds == 0) return 0;
+    return (lds / (unsigned)cap) & ~255u;
+}
+
 // Materialise a wave-uniform pointer (a kernel argument) in SGPRs at this point: an empty asm
 // with an SGPR operand, so every such pointer is loaded by the scalar loads at the kernel's top
 // and waited for once, instead of being fetched lazily between vector loads.

@@ -28,6 +28,8 @@
 //    (v_cvt_pk_bf16_f32, reduce_common.hpp).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <cstdlib>
 
 #include "reduce_vec.hpp"
@@ -108,6 +110,16 @@ ReduceTuning& reduce_tuning() {
         r.acc0_min_bytes = s ? (size_t)std::atoll(s) : 0;
         s = std::getenv("CHR_REDUCE_BLOCK");  // 64 / 256 / unset = by policy (launch_vec_m)
         r.block = s ? (std::atoi(s) == 64 ? 64 : 256) : 0;
+        s = std::getenv("CHR_WG_PER_CU_VEC");
+        r.wg_per_cu_vec = s ? std::max(0, std::atoi(s)) : -1;
+        s = std::getenv("CHR_WG_PER_CU_TREE");
+        r.wg_per_cu_tree = s ? std::max(0, std::atoi(s)) : -1;
+        int dev = 0, lds = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess ||
+            lds <= 0)
+            lds = 0;  // unknown: no cap
+        r.lds_per_cu = (unsigned)lds;
         return r;
     }();
     return t;

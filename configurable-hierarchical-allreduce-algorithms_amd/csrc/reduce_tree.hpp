@@ -204,6 +204,14 @@ constexpr size_t tree_xcd_run_kib() {
     return NL <= 2 ? 0 : 512;
 }
 
+// Resident workgroups per CU for streaming tree launches (nt_lds_bytes); 0 = uncapped: 8, 10 and
+// 12 per CU moved the C4/C5 collective rows by -2..+1 % (profiles/r02/occupancy_cap/), so the knob
+// (CHR_WG_PER_CU_TREE) is there for machines where it pays.
+template <int NL>
+constexpr int tree_wg_per_cu() {
+    return 0;
+}
+
 template <int DT, int OP, int NL, int BL, bool NT>
 inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
     constexpr int U = NL <= 4 ? 4 : 2;
@@ -223,7 +231,8 @@ inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
         grid += trips;
     }
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((k_reduce_tree<DT, OP, NL, U, NT, BL>), dim3((unsigned)grid), dim3(BL), 0, s, a);
+    const unsigned lds = NT ? nt_lds_bytes(reduce_tuning().wg_per_cu_tree, tree_wg_per_cu<NL>()) : 0;
+    hipLaunchKernelGGL((k_reduce_tree<DT, OP, NL, U, NT, BL>), dim3((unsigned)grid), dim3(BL), lds, s, a);
     return hipGetLastError();
 }
 

@@ -118,6 +118,18 @@ constexpr size_t vec_xcd_run_kib() {
     return M <= 2 ? 0 : 512;
 }
 
+// Resident workgroups per CU for streaming launches (nt_lds_bytes); 0 = uncapped.  Uncapped, a
+// CU holds ~20-32 one-wave workgroups, each with (m+1)*U*1 KiB of loads in flight the moment it
+// starts; 12 per CU measured best for m <= 3 through the product API (profiles/r02/occupancy_cap/,
+// 2 rounds, bench.py C2: 0.815 -> 0.823-0.826; m = 3 at 256 MiB 0.893 -> 0.924 with a 1.25 GiB
+// rotation, 0.814 -> 0.830 with 10 GiB; 16 and 10 per CU lose or tie).  m = 7 ties at 12 (0.814 /
+// 0.774 either way), and the tree kernel gains nothing at 8-12 (collective rows within noise), so
+// both stay uncapped.
+template <int M>
+constexpr int vec_wg_per_cu() {
+    return M <= 3 ? 12 : 0;
+}
+
 // A grid holds at most 2^31 threads here; larger calls (> 32 GiB per operand at BL = 64, U = 2)
 // run as consecutive launches over consecutive pieces.
 template <int BL, int U, typename L>
@@ -143,13 +155,14 @@ template <int DT, int OP, int M, int BL>
 inline hipError_t launch_vec_mb(VecArgs a, bool nt, bool acc0, hipStream_t s) {
     constexpr int U = M <= 2 ? 4 : 2;
     a.xrun = nt ? xcd_run_shift(vec_xcd_run_kib<M>(), (size_t)BL * U * 16) : 0;
+    const unsigned lds = nt ? nt_lds_bytes(reduce_tuning().wg_per_cu_vec, vec_wg_per_cu<M>()) : 0;
     return for_each_launch_piece<BL, U>(a, [&](const VecArgs& p, unsigned grid) {
         if (!nt)
             hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, false, false, BL>), dim3(grid), dim3(BL), 0, s, p);
         else if (acc0)
-            hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, true, BL>), dim3(grid), dim3(BL), 0, s, p);
+            hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, true, BL>), dim3(grid), dim3(BL), lds, s, p);
         else
-            hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, false, BL>), dim3(grid), dim3(BL), 0, s, p);
+            hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, false, BL>), dim3(grid), dim3(BL), lds, s, p);
     });
 }
 
@@ -160,8 +173,9 @@ template <int DT, int OP, int M, int BL, bool NT, bool ACC0>
 inline hipError_t launch_vec_mb_one(VecArgs a, hipStream_t s) {
     constexpr int U = M <= 2 ? 4 : 2;
     a.xrun = NT ? xcd_run_shift(vec_xcd_run_kib<M>(), (size_t)BL * U * 16) : 0;
+    const unsigned lds = NT ? nt_lds_bytes(reduce_tuning().wg_per_cu_vec, vec_wg_per_cu<M>()) : 0;
     return for_each_launch_piece<BL, U>(a, [&](const VecArgs& p, unsigned grid) {
-        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, NT, ACC0, BL>), dim3(grid), dim3(BL), 0, s, p);
+        hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, NT, ACC0, BL>), dim3(grid), dim3(BL), lds, s, p);
     });
 }
 

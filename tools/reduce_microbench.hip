@@ -1129,10 +1129,97 @@ static void focus10(size_t piece, int sets, int rounds) {
     free_sets(S);
 }
 
+// ---- focus11: occupancy caps on the product kernels --------------------------------------------
+// One-wave workgroups of the nt kernels reach ~20 waves per CU (82 VGPRs for the tree, fewer for
+// the bucket kernel), i.e. every CU has 16-20 workgroups' loads queued at once at the start of a
+// launch.  Dynamic LDS caps the resident workgroups per CU (160 KiB / shmem) without touching the
+// kernel: does fewer, earlier-finishing waves shorten the ramp/drain of a ~30-55 us launch?
+static unsigned lds_for_cap(int cap) { return cap <= 0 ? 0u : (unsigned)((160u << 10) / (unsigned)cap) & ~255u; }
+
+static void focus11_vec(size_t bytes, int sets, int rounds) {
+    const size_t nvec = bytes / 16;
+    constexpr int U = 4;
+    const unsigned G = (unsigned)(nvec / (64 * U));
+    Sets S = make_sets(1, nvec, sets);
+    char tag[64];
+    std::snprintf(tag, sizeof tag, " sets=%d ws=%zuMiB", sets, (size_t)sets * 2 * (bytes >> 20));
+    for (int r = 0; r < rounds; ++r) {
+        for (int cap : {0, 16, 12, 8, 6, 4}) {
+            const unsigned lds = lds_for_cap(cap);
+            double t = time_launches([&](int i) {
+                auto& b = S.bufs[i % sets];
+                chr::VecArgs v{};
+                v.out = (chr::u32x4*)b[0];
+                v.acc = (const chr::u32x4*)b[0];
+                v.ins[0] = (const chr::u32x4*)b[1];
+                v.nvec = nvec;
+                hipLaunchKernelGGL((chr::k_reduce_vec<CHR_FLOAT32, CHR_SUM, 1, U, true, true, 64>), dim3(G), dim3(64), lds, 0,
+                                   v);
+            }, 200);
+            char name[96];
+            std::snprintf(name, sizeof name, "vec m=1 cap=%d/CU (lds %u)%s", cap, lds, tag);
+            report(name, 1, bytes, t);
+        }
+        std::printf("--\n");
+    }
+    free_sets(S);
+}
+
+static void focus11_tree(size_t piece, int sets, int rounds) {
+    const size_t nvec = piece / 16;
+    Sets S = make_sets(17, nvec, sets);
+    const double bytes = 2.0 * 9 * piece;
+    constexpr int U = 2;
+    uint32_t cs = 0;
+    while (((size_t)2 << cs) * (64 * U * 16) <= (size_t)512 * 1024 && cs < 16) ++cs;  // the shipped 512 KiB runs
+    char tag[96];
+    std::snprintf(tag, sizeof tag, " piece=%zuMiB sets=%d ws=%zuMiB", piece >> 20, sets, (size_t)sets * 18 * (piece >> 20));
+    for (int r = 0; r < rounds; ++r) {
+        for (int cap : {0, 16, 12, 8, 6, 4}) {
+            const unsigned lds = lds_for_cap(cap);
+            double t = time_launches([&](int i) {
+                chr::TreeArgs a{};
+                const auto& b = S.bufs[i % sets];
+                a.nseg = 2;
+                a.nl = 8;
+                a.xrun = cs;
+                const uint32_t trips = (uint32_t)((nvec + 64 * U - 1) / (64 * U));
+                for (int j = 0; j < chr::kMaxTreeSegs; ++j) {
+                    a.block0[j] = j < 2 ? j * trips : ~0u;
+                    a.xfull[j] = j < 2 ? chr::xcd_full(trips, cs) : 0;
+                }
+                const int comb[8] = {0, 1, 1, 1, 0, 1, 1, 2};
+                for (int t2 = 0; t2 < 2; ++t2) {
+                    chr::TreeSeg& g = a.seg[t2];
+                    for (int l = 0; l < 8; ++l) g.leaves[l] = (const chr::u32x4*)b[9 * t2 + l];
+                    g.out = (chr::u32x4*)b[9 * t2 + 8];
+                    g.nvec = nvec;
+                    g.comb = 0;
+                    for (int l = 0; l < 8; ++l) g.comb |= (uint32_t)comb[l] << (2 * l);
+                    g.swaps = 0;
+                }
+                hipLaunchKernelGGL((chr::k_reduce_tree<CHR_FLOAT32, CHR_SUM, 8, U, true, 64>), dim3(2 * trips), dim3(64), lds,
+                                   0, a);
+            }, 40);
+            char name[160];
+            std::snprintf(name, sizeof name, "tree8x2 cap=%d/CU (lds %u)%s", cap, lds, tag);
+            report_moved(name, bytes, t);
+        }
+        std::printf("--\n");
+    }
+    free_sets(S);
+}
+
 int main(int argc, char** argv) {
     check();
     if (argc > 1 && std::string(argv[1]) == "layout") {
         layout_mode();
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus11") {
+        focus11_vec(64 << 20, 16, 2);    // C2
+        focus11_tree(16 << 20, 16, 2);   // C4 slice, cold rotation
+        focus11_tree(16 << 20, 4, 2);    // warm translations
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus10") {
