@@ -1210,10 +1210,54 @@ static void focus11_tree(size_t piece, int sets, int rounds) {
     free_sets(S);
 }
 
+// ---- focus12: U x occupancy cap for the product bucket kernel -----------------------------------
+template <int M, int U>
+static void focus12_mu(size_t bytes, int sets, std::initializer_list<int> caps) {
+    const size_t nvec = bytes / 16;
+    const unsigned G = (unsigned)(nvec / (64 * U));
+    Sets S = make_sets(M, nvec, sets);
+    uint32_t cs = 0;  // the shipped XCD runs: identity for m <= 2, 512 KiB above
+    if (M > 2)
+        while (((size_t)2 << cs) * (64 * U * 16) <= (size_t)512 * 1024 && cs < 16) ++cs;
+    char tag[64];
+    std::snprintf(tag, sizeof tag, " sets=%d ws=%zuMiB", sets, (size_t)sets * (M + 1) * (bytes >> 20));
+    for (int cap : caps) {
+        const unsigned lds = lds_for_cap(cap);
+        double t = time_launches([&](int i) {
+            auto& b = S.bufs[i % sets];
+            chr::VecArgs v{};
+            v.out = (chr::u32x4*)b[0];
+            v.acc = (const chr::u32x4*)b[0];
+            for (int j = 0; j < M; ++j) v.ins[j] = (const chr::u32x4*)b[j + 1];
+            v.nvec = nvec;
+            v.xrun = cs;
+            v.xfull = chr::xcd_full(G, cs);
+            hipLaunchKernelGGL((chr::k_reduce_vec<CHR_FLOAT32, CHR_SUM, M, U, true, true, 64>), dim3(G), dim3(64), lds, 0, v);
+        }, M == 1 ? 200 : 40);
+        char name[96];
+        std::snprintf(name, sizeof name, "vec U=%d cap=%d/CU%s", U, cap, tag);
+        report(name, M, bytes, t);
+    }
+    free_sets(S);
+}
+
 int main(int argc, char** argv) {
     check();
     if (argc > 1 && std::string(argv[1]) == "layout") {
         layout_mode();
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus12") {
+        for (int r = 0; r < 2; ++r) {
+            focus12_mu<1, 2>(64 << 20, 16, {0, 12, 16, 20, 24});
+            focus12_mu<1, 4>(64 << 20, 16, {0, 10, 11, 12, 13, 14});
+            focus12_mu<1, 8>(64 << 20, 16, {0, 6, 8, 10, 12});
+            focus12_mu<3, 2>(256 << 20, 1, {0, 10, 12, 14, 16});
+            focus12_mu<3, 4>(256 << 20, 1, {0, 6, 8, 10, 12});
+            focus12_mu<7, 2>(64 << 20, 4, {0, 8, 10, 12, 16});
+            focus12_mu<7, 1>(64 << 20, 4, {0, 12, 16, 20, 24});
+            std::printf("--\n");
+        }
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus11") {
