@@ -110,12 +110,14 @@ __global__ __launch_bounds__(kBlock) void k_reduce_scalar(ScalarArgs a) {
 
 // XCD runs for streaming calls, measured through the product API (profiles/r02/xcd_runs/,
 // fraction of 8 TB/s, identity -> 512 KiB runs): m = 3 at 256 MiB 0.854 -> 0.896 (1.25 GiB working
-// set) and 0.784 -> 0.795 (10 GiB); m = 7 0.811 -> 0.833 / 0.747 -> 0.751.  m <= 2 keeps the
-// identity: the C2 bucket measured 0.806 identity, 0.803 at 256 KiB, 0.792 at 512 KiB.  Cache-warm
-// (plain) calls keep the identity map too.
+// set) and 0.784 -> 0.795 (10 GiB); m = 7 0.811 -> 0.833 / 0.747 -> 0.751.  m = 1: uncapped, the C2
+// bucket measured 0.806 identity, 0.803 at 256 KiB, 0.792 at 512 KiB; under the 12-per-CU cap
+// (vec_wg_per_cu) 256 KiB runs win instead, 0.829-0.831 -> 0.833 over three alternating rounds
+// (profiles/r02/ab_runs/; microbench focus13: 0.814-0.822 -> 0.828).  m = 2 keeps the identity
+// (not measured under the cap).  Cache-warm (plain) calls keep the identity map too.
 template <int M>
 constexpr size_t vec_xcd_run_kib() {
-    return M <= 2 ? 0 : 512;
+    return M == 1 ? 256 : M == 2 ? 0 : 512;
 }
 
 // Resident workgroups per CU for streaming launches (nt_lds_bytes); 0 = uncapped.  Uncapped, a

@@ -1241,10 +1241,64 @@ static void focus12_mu(size_t bytes, int sets, std::initializer_list<int> caps) 
     free_sets(S);
 }
 
+// ---- focus13: the C2 shape under the occupancy cap: XCD runs, ACC0 and workgroup size ----------
+template <bool ACC0, int BL>
+static double c2_variant(Sets& S, size_t nvec, int sets, unsigned lds, uint32_t cs) {
+    constexpr int U = 4;
+    const unsigned G = (unsigned)(nvec / (BL * U));
+    return time_launches([&](int i) {
+        auto& b = S.bufs[i % sets];
+        chr::VecArgs v{};
+        v.out = (chr::u32x4*)b[0];
+        v.acc = (const chr::u32x4*)b[0];
+        v.ins[0] = (const chr::u32x4*)b[1];
+        v.nvec = nvec;
+        v.xrun = cs;
+        v.xfull = chr::xcd_full(G, cs);
+        hipLaunchKernelGGL((chr::k_reduce_vec<CHR_FLOAT32, CHR_SUM, 1, U, true, ACC0, BL>), dim3(G), dim3(BL), lds, 0, v);
+    }, 200);
+}
+
+static void focus13(int rounds) {
+    const size_t bytes = 64 << 20, nvec = bytes / 16;
+    const int sets = 16;
+    Sets S = make_sets(1, nvec, sets);
+    for (int r = 0; r < rounds; ++r) {
+        for (int cap : {12, 13}) {
+            for (unsigned run_kib : {0u, 64u, 256u, 1024u}) {
+                uint32_t cs = 0;
+                while (((size_t)2 << cs) * (64 * 4 * 16) <= (size_t)run_kib * 1024 && cs < 16) ++cs;
+                char name[96];
+                std::snprintf(name, sizeof name, "c2 cap=%d run=%uKiB acc0", cap, run_kib);
+                report(name, 1, bytes, c2_variant<true, 64>(S, nvec, sets, lds_for_cap(cap), cs));
+            }
+            char name[96];
+            std::snprintf(name, sizeof name, "c2 cap=%d all-nt", cap);
+            report(name, 1, bytes, c2_variant<false, 64>(S, nvec, sets, lds_for_cap(cap), 0));
+        }
+        for (int cap : {0, 5, 6, 7, 8}) {  // two-wave workgroups: cap counts workgroups
+            char name[96];
+            std::snprintf(name, sizeof name, "c2 BL=128 cap=%d acc0", cap);
+            report(name, 1, bytes, c2_variant<true, 128>(S, nvec, sets, lds_for_cap(cap), 0));
+        }
+        for (int cap : {0, 3, 4}) {
+            char name[96];
+            std::snprintf(name, sizeof name, "c2 BL=256 cap=%d acc0", cap);
+            report(name, 1, bytes, c2_variant<true, 256>(S, nvec, sets, lds_for_cap(cap), 0));
+        }
+        std::printf("--\n");
+    }
+    free_sets(S);
+}
+
 int main(int argc, char** argv) {
     check();
     if (argc > 1 && std::string(argv[1]) == "layout") {
         layout_mode();
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus13") {
+        focus13(3);
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus12") {
