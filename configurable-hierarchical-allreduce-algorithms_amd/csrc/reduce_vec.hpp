@@ -124,12 +124,33 @@ constexpr size_t vec_xcd_run_kib() {
 // CU holds ~20-32 one-wave workgroups, each with (m+1)*U*1 KiB of loads in flight the moment it
 // starts; 12 per CU measured best for m <= 3 through the product API (profiles/r02/occupancy_cap/,
 // 2 rounds, bench.py C2: 0.815 -> 0.823-0.826; m = 3 at 256 MiB 0.893 -> 0.924 with a 1.25 GiB
-// rotation, 0.814 -> 0.830 with 10 GiB; 16 and 10 per CU lose or tie).  m = 7 ties at 12 (0.814 /
-// 0.774 either way), and the tree kernel gains nothing at 8-12 (collective rows within noise), so
-// both stay uncapped.
+// rotation, 0.814 -> 0.830 with 10 GiB; 16 and 10 per CU lose or tie).  Wider fan-in takes 16 per CU
+// with U = 1 (vec_u_nt below); the tree kernel gains nothing at 8-12 (collective rows within
+// noise) and stays uncapped.
 template <int M>
 constexpr int vec_wg_per_cu() {
-    return M <= 3 ? 12 : 0;
+    return M == 2 ? 16 : 12;
+}
+
+// Vectors per lane per trip of streaming launches.  U x cap over m = 1..8 with the product template
+// (tools/reduce_microbench focus12/14/15, profiles/r02/occupancy_cap/, 2 rounds each): m = 1 U = 4
+// (U = 2 / 8 lose 3-9 %); m = 2 U = 2 with 16 per CU, 0.817-0.830 against U = 4's 0.80-0.817; m = 3
+// U = 2 with 12 per CU (U = 1 loses 10 %); m >= 4 U = 1 with 12 per CU.  Within the translation
+// reach (rotations <= 2 GiB) U = 1 gains 2-4 % over U = 2 at every measured shape (m = 4 at 128 MiB
+// 0.846-0.851 -> 0.859-0.896, m = 5 at 64 MiB 0.812-0.815 -> 0.827-0.852, m = 7 at 256 MiB
+// 0.803-0.820 -> 0.843-0.867, m = 8 at 128 MiB 0.807-0.812 -> 0.831-0.840); past it (focus16, 4-16
+// GiB rotations) twice the workgroups each touch m + 1 pages for 1 KiB, and U = 1 ties at m = 7 /
+// 256 MiB (0.769-0.772 vs 0.762-0.774), wins at m = 4 (0.790-0.798 vs 0.760-0.772) and loses ~4 %
+// at m = 7 / 64 MiB (uncapped and at 16 per CU; 12 not measured there).  With U = 1 the ACC0 slot
+// is the whole accumulator stream: that is the measured shape.  Cache-warm (plain) launches keep
+// U = 4 / 2.
+template <int M>
+constexpr int vec_u_nt() {
+    return M == 1 ? 4 : M <= 3 ? 2 : 1;
+}
+template <int M, bool NT>
+constexpr int vec_u() {
+    return NT ? vec_u_nt<M>() : M <= 2 ? 4 : 2;
 }
 
 // A grid holds at most 2^31 threads here; larger calls (> 32 GiB per operand at BL = 64, U = 2)
@@ -153,27 +174,12 @@ inline hipError_t for_each_launch_piece(VecArgs a, L launch) {
     return hipSuccess;
 }
 
-template <int DT, int OP, int M, int BL>
-inline hipError_t launch_vec_mb(VecArgs a, bool nt, bool acc0, hipStream_t s) {
-    constexpr int U = M <= 2 ? 4 : 2;
-    a.xrun = nt ? xcd_run_shift(vec_xcd_run_kib<M>(), (size_t)BL * U * 16) : 0;
-    const unsigned lds = nt ? nt_lds_bytes(reduce_tuning().wg_per_cu_vec, vec_wg_per_cu<M>()) : 0;
-    return for_each_launch_piece<BL, U>(a, [&](const VecArgs& p, unsigned grid) {
-        if (!nt)
-            hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, false, false, BL>), dim3(grid), dim3(BL), 0, s, p);
-        else if (acc0)
-            hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, true, BL>), dim3(grid), dim3(BL), lds, s, p);
-        else
-            hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, true, false, BL>), dim3(grid), dim3(BL), lds, s, p);
-    });
-}
-
 // Policy (profiles/r01/block_ab_*): calls that stream >= 128 MiB run non-temporal with
 // one-wave workgroups and the first accumulator slot temporal (ACC0); smaller, cache-warm
 // calls keep plain accesses and 256-thread workgroups.
 template <int DT, int OP, int M, int BL, bool NT, bool ACC0>
 inline hipError_t launch_vec_mb_one(VecArgs a, hipStream_t s) {
-    constexpr int U = M <= 2 ? 4 : 2;
+    constexpr int U = vec_u<M, NT>();
     a.xrun = NT ? xcd_run_shift(vec_xcd_run_kib<M>(), (size_t)BL * U * 16) : 0;
     const unsigned lds = NT ? nt_lds_bytes(reduce_tuning().wg_per_cu_vec, vec_wg_per_cu<M>()) : 0;
     return for_each_launch_piece<BL, U>(a, [&](const VecArgs& p, unsigned grid) {
@@ -184,6 +190,12 @@ inline hipError_t launch_vec_mb_one(VecArgs a, hipStream_t s) {
 // FULL: every tuning variant (CHR_REDUCE_BLOCK / CHR_REDUCE_ACC0 overrides) is compiled, for the
 // floating types and int32; the other integer types compile the two policy shapes only (nt: one
 // wave + ACC0; plain: 256 threads) and ignore those two overrides.
+template <int DT, int OP, int M, int BL>
+inline hipError_t launch_vec_mb(const VecArgs& a, bool nt, bool acc0, hipStream_t s) {
+    if (!nt) return launch_vec_mb_one<DT, OP, M, BL, false, false>(a, s);
+    return acc0 ? launch_vec_mb_one<DT, OP, M, BL, true, true>(a, s) : launch_vec_mb_one<DT, OP, M, BL, true, false>(a, s);
+}
+
 template <int DT, int OP, int M, bool FULL>
 inline hipError_t launch_vec_m(const VecArgs& a, hipStream_t s) {
     const ReduceTuning& t = reduce_tuning();

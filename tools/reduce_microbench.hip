@@ -1297,6 +1297,49 @@ int main(int argc, char** argv) {
         layout_mode();
         return 0;
     }
+    if (argc > 1 && std::string(argv[1]) == "focus16") {  // the cold (large rotation) side of U = 1
+        for (int r = 0; r < 2; ++r) {
+            focus12_mu<7, 2>(256 << 20, 8, {0, 16});
+            focus12_mu<7, 1>(256 << 20, 8, {0, 12, 16});
+            focus12_mu<4, 2>(256 << 20, 8, {0, 16});
+            focus12_mu<4, 1>(256 << 20, 8, {0, 12, 16});
+            focus12_mu<7, 2>(64 << 20, 8, {0, 16});
+            focus12_mu<7, 1>(64 << 20, 8, {0, 16});
+            std::printf("--\n");
+        }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus15") {  // m = 2 and 3: U x cap
+        for (int r = 0; r < 2; ++r) {
+            focus12_mu<2, 4>(64 << 20, 8, {0, 12, 16});
+            focus12_mu<2, 2>(64 << 20, 8, {0, 12, 16});
+            focus12_mu<2, 1>(64 << 20, 8, {0, 12, 16});
+            focus12_mu<3, 2>(64 << 20, 8, {0, 12, 16});
+            focus12_mu<3, 1>(64 << 20, 8, {0, 12, 16});
+            focus12_mu<3, 2>(256 << 20, 2, {0, 12, 16});
+            focus12_mu<3, 1>(256 << 20, 2, {0, 12, 16});
+            focus12_mu<6, 2>(64 << 20, 4, {0, 12, 16});
+            focus12_mu<6, 1>(64 << 20, 4, {0, 12, 16});
+            std::printf("--\n");
+        }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus14") {  // U = 1 vs 2 for wide fan-in, with and without the cap
+        for (int r = 0; r < 2; ++r) {
+            focus12_mu<5, 2>(64 << 20, 4, {0, 12});
+            focus12_mu<5, 1>(64 << 20, 4, {0, 12, 16});
+            focus12_mu<7, 2>(64 << 20, 4, {0, 12});
+            focus12_mu<7, 1>(64 << 20, 4, {0, 12, 16});
+            focus12_mu<7, 2>(256 << 20, 1, {0, 12});
+            focus12_mu<7, 1>(256 << 20, 1, {0, 12, 16});
+            focus12_mu<8, 2>(128 << 20, 2, {0, 12});
+            focus12_mu<8, 1>(128 << 20, 2, {0, 12, 16});
+            focus12_mu<4, 2>(128 << 20, 2, {0, 12});
+            focus12_mu<4, 1>(128 << 20, 2, {0, 12, 16});
+            std::printf("--\n");
+        }
+        return 0;
+    }
     if (argc > 1 && std::string(argv[1]) == "focus13") {
         focus13(3);
         return 0;
