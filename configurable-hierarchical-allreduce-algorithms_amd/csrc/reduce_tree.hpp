@@ -204,17 +204,23 @@ constexpr size_t tree_xcd_run_kib() {
     return NL <= 2 ? 0 : 512;
 }
 
-// Resident workgroups per CU for streaming tree launches (nt_lds_bytes); 0 = uncapped: 8, 10 and
-// 12 per CU moved the C4/C5 collective rows by -2..+1 % (profiles/r02/occupancy_cap/), so the knob
-// (CHR_WG_PER_CU_TREE) is there for machines where it pays.
+// Vectors per lane per trip and resident workgroups per CU (nt_lds_bytes; 0 = uncapped) of
+// streaming tree launches.  At U = 2, 8-12 per CU moved the C4/C5 collective rows by -2..+1 %
+// (profiles/r02/occupancy_cap/); U = 1 with 16 per CU measured 0.751-0.763 against U = 2
+// uncapped's 0.739-0.750 on the C4 slice (2 x 8 leaves x 16 MiB, 4.5 and 1.1 GiB rotations, 2
+// rounds: microbench_focus17_tree_u_cap.txt), so trees of 5+ leaves take that shape.
+template <int NL>
+constexpr int tree_u() {
+    return NL <= 4 ? 4 : 1;
+}
 template <int NL>
 constexpr int tree_wg_per_cu() {
-    return 0;
+    return NL <= 4 ? 0 : 16;
 }
 
 template <int DT, int OP, int NL, int BL, bool NT>
 inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
-    constexpr int U = NL <= 4 ? 4 : 2;
+    constexpr int U = tree_u<NL>();
     TreeArgs a = a_in;
     a.xrun = NT ? xcd_run_shift(tree_xcd_run_kib<NL>(), (size_t)BL * U * 16) : 0;
     size_t grid = 0;

@@ -1165,17 +1165,17 @@ static void focus11_vec(size_t bytes, int sets, int rounds) {
     free_sets(S);
 }
 
-static void focus11_tree(size_t piece, int sets, int rounds) {
+template <int U = 2>
+static void focus11_tree(size_t piece, int sets, int rounds, std::initializer_list<int> caps = {0, 16, 12, 8, 6, 4}) {
     const size_t nvec = piece / 16;
     Sets S = make_sets(17, nvec, sets);
     const double bytes = 2.0 * 9 * piece;
-    constexpr int U = 2;
     uint32_t cs = 0;
     while (((size_t)2 << cs) * (64 * U * 16) <= (size_t)512 * 1024 && cs < 16) ++cs;  // the shipped 512 KiB runs
     char tag[96];
     std::snprintf(tag, sizeof tag, " piece=%zuMiB sets=%d ws=%zuMiB", piece >> 20, sets, (size_t)sets * 18 * (piece >> 20));
     for (int r = 0; r < rounds; ++r) {
-        for (int cap : {0, 16, 12, 8, 6, 4}) {
+        for (int cap : caps) {
             const unsigned lds = lds_for_cap(cap);
             double t = time_launches([&](int i) {
                 chr::TreeArgs a{};
@@ -1202,7 +1202,7 @@ static void focus11_tree(size_t piece, int sets, int rounds) {
                                    0, a);
             }, 40);
             char name[160];
-            std::snprintf(name, sizeof name, "tree8x2 cap=%d/CU (lds %u)%s", cap, lds, tag);
+            std::snprintf(name, sizeof name, "tree8x2 U=%d cap=%d/CU (lds %u)%s", U, cap, lds, tag);
             report_moved(name, bytes, t);
         }
         std::printf("--\n");
@@ -1295,6 +1295,15 @@ int main(int argc, char** argv) {
     check();
     if (argc > 1 && std::string(argv[1]) == "layout") {
         layout_mode();
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus17") {  // tree: U = 1 vs 2 under caps
+        for (int r = 0; r < 2; ++r) {
+            focus11_tree<2>(16 << 20, 16, 1, {0, 12, 16});
+            focus11_tree<1>(16 << 20, 16, 1, {0, 12, 16, 20});
+            focus11_tree<2>(16 << 20, 4, 1, {0, 12, 16});
+            focus11_tree<1>(16 << 20, 4, 1, {0, 12, 16, 20});
+        }
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus16") {  // the cold (large rotation) side of U = 1
