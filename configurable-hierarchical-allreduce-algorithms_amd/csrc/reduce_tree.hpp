@@ -197,25 +197,30 @@ __global__ __launch_bounds__(kBlock) void k_reduce_tree_scalar(TreeScalarArgs a)
 // XCD runs for streaming (nt) tree launches (profiles/r02/xcd_runs/ab_tree_*.json, C4 slice of 2
 // batched 8-leaf trees, HBM-cold, identity -> 512 KiB): 8 MiB pieces 0.571 -> 0.634, 16 MiB
 // 0.668 -> 0.700, 32 MiB 0.719 -> 0.750; fused reductions of a whole C4 call 0.676 -> 0.719.
-// Two leaves move the m = 1 bucket's traffic (2 reads + 1 write), which runs best unmapped
-// (vec_xcd_run_kib), so they keep the identity.
+// Two leaves move the m = 1 bucket's traffic (2 reads + 1 write) and, like it under the 12-per-CU
+// cap, take 256 KiB runs (focus18 below).
 template <int NL>
 constexpr size_t tree_xcd_run_kib() {
-    return NL <= 2 ? 0 : 512;
+    return NL <= 2 ? 256 : 512;
 }
 
 // Vectors per lane per trip and resident workgroups per CU (nt_lds_bytes; 0 = uncapped) of
 // streaming tree launches.  At U = 2, 8-12 per CU moved the C4/C5 collective rows by -2..+1 %
 // (profiles/r02/occupancy_cap/); U = 1 with 16 per CU measured 0.751-0.763 against U = 2
 // uncapped's 0.739-0.750 on the C4 slice (2 x 8 leaves x 16 MiB, 4.5 and 1.1 GiB rotations, 2
-// rounds: microbench_focus17_tree_u_cap.txt), so trees of 5+ leaves take that shape.
+// rounds: microbench_focus17_tree_u_cap.txt), so trees of 5+ leaves take that shape.  The small
+// trees of the N = 2 / N = 4 flat schedules (focus18, microbench_focus18_small_trees.txt, 2 rounds,
+// 6 HBM-cold sets): 2 leaves at 128 MiB U = 4 uncapped 0.774-0.783 -> 0.801-0.804 with 12 per CU and
+// 256 KiB runs (U = 2 at 16 per CU ties, 0.800-0.817); 4 leaves at 64 MiB U = 4 uncapped 0.741-0.750
+// -> U = 2 at 12 per CU 0.774-0.781.  3 leaves (not measured) follow the 3-input bucket (m = 2):
+// U = 2 at 16 per CU.
 template <int NL>
 constexpr int tree_u() {
-    return NL <= 4 ? 4 : 1;
+    return NL == 2 ? 4 : NL <= 4 ? 2 : 1;
 }
 template <int NL>
 constexpr int tree_wg_per_cu() {
-    return NL <= 4 ? 0 : 16;
+    return NL == 2 || NL == 4 ? 12 : 16;
 }
 
 template <int DT, int OP, int NL, int BL, bool NT>

@@ -1291,10 +1291,61 @@ static void focus13(int rounds) {
     free_sets(S);
 }
 
+// ---- focus18: small trees (the N = 2 / N = 4 flat schedules: 2 and 4 leaves) -------------------
+// One segment of NL leaves (a left fold, MPI_Reduce_local order) of `piece` bytes per leaf.
+template <int NL, int U>
+static void focus18_tree(size_t piece, int sets, std::initializer_list<int> caps, uint32_t run_kib) {
+    const size_t nvec = piece / 16;
+    Sets S = make_sets(NL, nvec, sets);  // NL + 1 operands: leaves b[0..NL-1], out b[NL]
+    const double bytes = (NL + 1.0) * piece;
+    uint32_t cs = 0;
+    while (run_kib && ((size_t)2 << cs) * (64 * U * 16) <= (size_t)run_kib * 1024 && cs < 16) ++cs;
+    for (int cap : caps) {
+        const unsigned lds = lds_for_cap(cap);
+        double t = time_launches([&](int i) {
+            chr::TreeArgs a{};
+            const auto& b = S.bufs[i % sets];
+            a.nseg = 1;
+            a.nl = NL;
+            a.xrun = cs;
+            const uint32_t trips = (uint32_t)((nvec + 64 * U - 1) / (64 * U));
+            for (int j = 0; j < chr::kMaxTreeSegs; ++j) {
+                a.block0[j] = j == 0 ? 0 : ~0u;
+                a.xfull[j] = j == 0 ? chr::xcd_full(trips, cs) : 0;
+            }
+            chr::TreeSeg& g = a.seg[0];
+            for (int l = 0; l < NL; ++l) g.leaves[l] = (const chr::u32x4*)b[l];
+            g.out = (chr::u32x4*)b[NL];
+            g.nvec = nvec;
+            g.comb = 0;
+            for (int l = 1; l < NL; ++l) g.comb |= 1u << (2 * l);  // left fold
+            g.swaps = 0;
+            hipLaunchKernelGGL((chr::k_reduce_tree<CHR_FLOAT32, CHR_SUM, NL, U, true, 64>), dim3(trips), dim3(64), lds, 0, a);
+        }, 40);
+        char name[160];
+        std::snprintf(name, sizeof name, "tree NL=%d U=%d cap=%d run=%uKiB piece=%zuMiB sets=%d", NL, U, cap, run_kib,
+                      piece >> 20, sets);
+        report_moved(name, bytes, t);
+    }
+    free_sets(S);
+}
+
 int main(int argc, char** argv) {
     check();
     if (argc > 1 && std::string(argv[1]) == "layout") {
         layout_mode();
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus18") {
+        for (int r = 0; r < 2; ++r) {
+            focus18_tree<2, 4>(128 << 20, 6, {0, 12, 16}, 0);
+            focus18_tree<2, 4>(128 << 20, 6, {0, 12}, 256);
+            focus18_tree<2, 2>(128 << 20, 6, {0, 12, 16}, 0);
+            focus18_tree<4, 4>(64 << 20, 6, {0, 12, 16}, 512);
+            focus18_tree<4, 2>(64 << 20, 6, {0, 12, 16}, 512);
+            focus18_tree<4, 1>(64 << 20, 6, {0, 12, 16}, 512);
+            std::printf("--\n");
+        }
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus17") {  // tree: U = 1 vs 2 under caps
