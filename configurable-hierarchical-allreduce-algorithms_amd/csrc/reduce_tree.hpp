@@ -214,8 +214,9 @@ constexpr size_t tree_xcd_run_kib() {
 // 256 KiB runs (U = 2 at 16 per CU ties, 0.800-0.817); 4 leaves at 64 MiB U = 4 uncapped 0.741-0.750
 // -> U = 2 at 12 per CU 0.774-0.781.  3 leaves (not measured) follow the 3-input bucket (m = 2):
 // U = 2 at 16 per CU.
-template <int NL>
+template <int NL, bool NT>
 constexpr int tree_u() {
+    if constexpr (!NT) return NL <= 4 ? 4 : 2;  // cache-warm (plain) launches: the round-1 shapes
     return NL == 2 ? 4 : NL <= 4 ? 2 : 1;
 }
 template <int NL>
@@ -225,7 +226,7 @@ constexpr int tree_wg_per_cu() {
 
 template <int DT, int OP, int NL, int BL, bool NT>
 inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
-    constexpr int U = tree_u<NL>();
+    constexpr int U = tree_u<NL, NT>();
     TreeArgs a = a_in;
     a.xrun = NT ? xcd_run_shift(tree_xcd_run_kib<NL>(), (size_t)BL * U * 16) : 0;
     size_t grid = 0;
