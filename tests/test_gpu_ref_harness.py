@@ -111,7 +111,7 @@ def test_reference_mpich_reduce_scatter_harness_on_mi355x(tmp_path):
 
 def test_reference_allgather_harness_on_mi355x(tmp_path):
     """Fugaku_experiments/Allgather/main.cpp unchanged: k = 2..b-1, check_correctness vs MPI_Allgather."""
-    rows = _run("ref_harness_allgather", ["3", "--overwrite", "b=4", "base=16"], 8, tmp_path)
+    rows = _run("ref_harness_allgather", ["2", "--overwrite", "b=4", "base=16"], 8, tmp_path)
     ours = [r for r in rows if r["algorithm_name"] == "allgather_radix_batch"]
     assert ours and {r["k"] for r in ours} == {"2", "3"}
     assert all(r["is_correct"] == "1" for r in rows)
@@ -122,11 +122,11 @@ BIN = ("configurable-hierarchical-allreduce-algorithms_amd", "bin")
 
 
 @pytest.mark.parametrize("binary,args,n,name,coll", [
-    ("chiara_allreduce", ["2", "--overwrite", "b=4", "base=4096", "mem=device", "dtype=f32", "reps=5"], 8,
+    ("chiara_allreduce", ["2", "--overwrite", "b=4", "base=4096", "mem=device", "dtype=f32", "reps=3"], 8,
      "all_reduce_radix_batch", "allreduce"),
     ("chiara_reduce_scatter", ["2", "--overwrite", "b=4", "base=1000", "mem=device", "reps=5"], 4,
      "reduce_scatter_radix_batch", "reduce_scatter"),
-    ("chiara_allgather", ["3", "--overwrite", "b=4", "base=100", "mem=device", "dtype=bf16", "reps=5"], 8,
+    ("chiara_allgather", ["2", "--overwrite", "b=4", "base=100", "mem=device", "dtype=bf16", "reps=3"], 8,
      "allgather_radix_batch", "allgather"),
     # cancelling inputs (pattern=cancel): the reduced value is tiny next to sum|x_i|, so the
     # association difference from MPI's own collective exceeds ulp(|result|); is_correct holds
