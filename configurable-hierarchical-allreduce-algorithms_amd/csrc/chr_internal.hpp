@@ -52,7 +52,8 @@ hipError_t launch_fill(void* buf, size_t n, int dtype, int pattern, uint64_t see
 //                            the next XCD's run (0 = plain round-robin); unset = policy
 //                            (xcd_run_shift in reduce_common.hpp)
 //   CHR_REDUCE_NT            0 / 1 forces plain / non-temporal loads+stores; unset = by size
-//   CHR_REDUCE_NT_MIN_BYTES  bytes streamed by one call from which NT is used (128 MiB)
+//   CHR_REDUCE_NT_MIN_BYTES  bytes streamed by one call from which NT is used (128 MiB for
+//                            bucket launches, 64 MiB for tree launches; the variable sets both)
 //   CHR_REDUCE_ACC0          0 / 1 forces the first accumulator slot nt / default policy
 //                            under NT; unset = default policy for m >= 2 or large buckets
 //   CHR_REDUCE_ACC0_MIN_BYTES  bucket size from which m = 1 uses it too (0: always)
@@ -66,7 +67,8 @@ struct ReduceTuning {
     size_t max_launch_vec;  // 0: the grid limit; else cap on 16-B vectors per launch / tree segment
     int block;
     int nt_mode;
-    size_t nt_min_bytes;
+    size_t nt_min_bytes;       // bucket launches
+    size_t tree_nt_min_bytes;  // tree launches
     int acc0_mode;
     size_t acc0_min_bytes;
     int wg_per_cu_vec;   // -1: policy

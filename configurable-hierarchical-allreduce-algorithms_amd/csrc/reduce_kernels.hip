@@ -104,6 +104,11 @@ ReduceTuning& reduce_tuning() {
         r.nt_mode = s ? std::atoi(s) : -1;
         s = std::getenv("CHR_REDUCE_NT_MIN_BYTES");
         r.nt_min_bytes = s ? (size_t)std::atoll(s) : (size_t)128 << 20;
+        // trees stream 3-9 operands at once: from 64 MiB per launch the nt shapes win on HBM-cold
+        // leaves and tie on cache-warm ones (C4 slice, 4 MiB pieces = 72 MiB: nt 0.591-0.602 vs
+        // plain 0.572-0.577 cold, 0.651-0.657 vs 0.599-0.666 warm; 2 MiB pieces tie;
+        // profiles/r02/occupancy_cap/microbench_focus19_nt_threshold.txt)
+        r.tree_nt_min_bytes = s ? r.nt_min_bytes : (size_t)64 << 20;
         s = std::getenv("CHR_REDUCE_ACC0");   // 0 / 1 / unset = by fan-in and size
         r.acc0_mode = s ? std::atoi(s) : -1;
         s = std::getenv("CHR_REDUCE_ACC0_MIN_BYTES");

@@ -258,12 +258,12 @@ inline hipError_t launch_tree_nl(const TreeArgs& a, const TreeScalarArgs* sa, hi
         hipLaunchKernelGGL((k_reduce_tree_scalar<DT, OP, NL>), dim3(grid), dim3(kBlock), 0, s, *sa);
         return hipGetLastError();
     }
-    // same policy as launch_vec_m: streaming calls (>= 128 MiB) nt with one-wave workgroups
+    // as launch_vec_m: streaming calls (>= 64 MiB for trees) nt with one-wave workgroups
     const ReduceTuning& t = reduce_tuning();
     size_t nvec = 0;
     for (int j = 0; j < a.nseg; ++j) nvec += a.seg[j].nvec;
     const size_t call_bytes = (size_t)(a.nl + 1) * nvec * 16;
-    const bool nt = t.nt_mode == 1 || (t.nt_mode < 0 && call_bytes >= t.nt_min_bytes);
+    const bool nt = t.nt_mode == 1 || (t.nt_mode < 0 && call_bytes >= t.tree_nt_min_bytes);
     if constexpr (!FULL) {
         return nt ? launch_tree_vec<DT, OP, NL, 64, true>(a, s) : launch_tree_vec<DT, OP, NL, 256, false>(a, s);
     } else {

@@ -1330,10 +1330,97 @@ static void focus18_tree(size_t piece, int sets, std::initializer_list<int> caps
     free_sets(S);
 }
 
+// ---- focus19: the NT threshold under the new shapes (mid sizes: plain 256-thread vs nt one-wave) ---
+template <int U, bool NT, int BL>
+static double tree8x2_time(Sets& S, size_t nvec, int sets, unsigned lds, uint32_t cs) {
+    return time_launches([&](int i) {
+        chr::TreeArgs a{};
+        const auto& b = S.bufs[i % sets];
+        a.nseg = 2;
+        a.nl = 8;
+        a.xrun = cs;
+        const uint32_t trips = (uint32_t)((nvec + BL * U - 1) / (BL * U));
+        for (int j = 0; j < chr::kMaxTreeSegs; ++j) {
+            a.block0[j] = j < 2 ? j * trips : ~0u;
+            a.xfull[j] = j < 2 ? chr::xcd_full(trips, cs) : 0;
+        }
+        const int comb[8] = {0, 1, 1, 1, 0, 1, 1, 2};
+        for (int t2 = 0; t2 < 2; ++t2) {
+            chr::TreeSeg& g = a.seg[t2];
+            for (int l = 0; l < 8; ++l) g.leaves[l] = (const chr::u32x4*)b[9 * t2 + l];
+            g.out = (chr::u32x4*)b[9 * t2 + 8];
+            g.nvec = nvec;
+            g.comb = 0;
+            for (int l = 0; l < 8; ++l) g.comb |= (uint32_t)comb[l] << (2 * l);
+            g.swaps = 0;
+        }
+        hipLaunchKernelGGL((chr::k_reduce_tree<CHR_FLOAT32, CHR_SUM, 8, U, NT, BL>), dim3(2 * trips), dim3(BL), lds, 0, a);
+    }, 100);
+}
+
+static void focus19(size_t piece, int sets) {
+    const size_t nvec = piece / 16;
+    Sets S = make_sets(17, nvec, sets);
+    const double bytes = 2.0 * 9 * piece;
+    uint32_t cs = 0;
+    while (((size_t)2 << cs) * (64 * 1 * 16) <= (size_t)512 * 1024 && cs < 16) ++cs;
+    char name[128];
+    std::snprintf(name, sizeof name, "tree8x2 plain U=2 BL=256 piece=%zuMiB sets=%d", piece >> 20, sets);
+    report_moved(name, bytes, tree8x2_time<2, false, 256>(S, nvec, sets, 0, 0));
+    std::snprintf(name, sizeof name, "tree8x2 nt U=1 cap16 runs piece=%zuMiB sets=%d", piece >> 20, sets);
+    report_moved(name, bytes, tree8x2_time<1, true, 64>(S, nvec, sets, lds_for_cap(16), cs));
+    std::snprintf(name, sizeof name, "tree8x2 nt U=2 uncapped piece=%zuMiB sets=%d", piece >> 20, sets);
+    report_moved(name, bytes, tree8x2_time<2, true, 64>(S, nvec, sets, 0, 0));
+    free_sets(S);
+}
+
+template <bool NT, int BL, int U>
+static double vec1_time(Sets& S, size_t nvec, int sets, unsigned lds, uint32_t cs) {
+    const unsigned G = (unsigned)(nvec / (BL * U));
+    return time_launches([&](int i) {
+        auto& b = S.bufs[i % sets];
+        chr::VecArgs v{};
+        v.out = (chr::u32x4*)b[0];
+        v.acc = (const chr::u32x4*)b[0];
+        v.ins[0] = (const chr::u32x4*)b[1];
+        v.nvec = nvec;
+        v.xrun = cs;
+        v.xfull = chr::xcd_full(G, cs);
+        hipLaunchKernelGGL((chr::k_reduce_vec<CHR_FLOAT32, CHR_SUM, 1, U, NT, NT, BL>), dim3(G), dim3(BL), lds, 0, v);
+    }, 200);
+}
+
+static void focus19_vec(size_t bytes, int sets) {
+    const size_t nvec = bytes / 16;
+    Sets S = make_sets(1, nvec, sets);
+    uint32_t cs = 0;
+    while (((size_t)2 << cs) * (64 * 4 * 16) <= (size_t)256 * 1024 && cs < 16) ++cs;
+    char name[128];
+    std::snprintf(name, sizeof name, "vec m=1 plain BL=256 sets=%d", sets);
+    report(name, 1, bytes, vec1_time<false, 256, 4>(S, nvec, sets, 0, 0));
+    std::snprintf(name, sizeof name, "vec m=1 nt cap12 runs256 sets=%d", sets);
+    report(name, 1, bytes, vec1_time<true, 64, 4>(S, nvec, sets, lds_for_cap(12), cs));
+    free_sets(S);
+}
+
 int main(int argc, char** argv) {
     check();
     if (argc > 1 && std::string(argv[1]) == "layout") {
         layout_mode();
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus19") {
+        for (int r = 0; r < 2; ++r) {
+            for (size_t mib : {2, 4, 8}) {
+                focus19(mib << 20, 32);  // cold
+                focus19(mib << 20, 2);   // warm (Infinity Cache)
+            }
+            for (size_t mib : {8, 16, 32}) {
+                focus19_vec(mib << 20, 64);
+                focus19_vec(mib << 20, 2);
+            }
+            std::printf("--\n");
+        }
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus18") {
