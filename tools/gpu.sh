@@ -13,6 +13,7 @@
 #   prof       rocprofv3 kernel trace + stats of the bench (csv) -> prof/
 #   pmc        FETCH_SIZE and WRITE_SIZE passes of the bench     -> pmc_FETCH_SIZE/, pmc_WRITE_SIZE/
 #   kernels    bench.py --collective-kernels (C4/C5 in-collective kernel rows) -> collective_kernels.json
+#   treepmc    rocprofv3 stats + FETCH_SIZE / WRITE_SIZE passes of the tree kernel alone (tools/tree_pmc.py)
 #   e2e        bench.py --e2e: host-buffer (PCIe-inclusive) cost of the reference's contract -> e2e.json
 #   sweep      bench.py --sweep: 1 KiB .. 1 GiB buckets, m = 1/3/7, fp32 + bf16 (table in sweep.json.err)
 #   probe      tools/mstream_probe.py $PROBE_ARGS               -> mstream_probe.jsonl
@@ -50,6 +51,13 @@ for step in "$@"; do
         -- python3 bench.py --steps 40 --warmup 5 --no-cpu-baseline
     done ;;
   kernels) run 400 collective_kernels.json python bench.py --collective-kernels ;;
+  treepmc)  # the fused tree alone at C4's shape (tools/tree_pmc.py): kernel stats, then FETCH / WRITE passes
+    run 300 tree_prof.txt rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/tree_prof" -o run \
+      -- python3 tools/tree_pmc.py 40
+    for ctr in FETCH_SIZE WRITE_SIZE; do
+      run 300 "tree_pmc_$ctr.txt" rocprofv3 --pmc $ctr --output-format csv -d "$PWD/$OUT/tree_pmc_$ctr" -o run \
+        -- python3 tools/tree_pmc.py 40
+    done ;;
   sweep) run 600 sweep.json python bench.py --sweep --no-cpu-baseline ;;
   e2e) run 300 e2e.json python bench.py --e2e --no-cpu-baseline ;;
   probe) run 400 mstream_probe.jsonl python tools/mstream_probe.py ${PROBE_ARGS:-} ;;
