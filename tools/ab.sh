@@ -1,0 +1,42 @@
+#!/bin/bash
+# Product-API A/B runs behind the occupancy-cap and XCD-run policy, on the GPU box:
+#   gpurun -- bash tools/ab.sh cap    C2 / mstream m=3,7 / collective-kernel rows vs CHR_WG_PER_CU_{VEC,TREE}
+#   gpurun -- bash tools/ab.sh runs   C2 with the policy XCD map vs 256 KiB runs, 3 alternating rounds
+# Results land under gpurun_out/cap/ or gpurun_out/ab_runs/ (copied to profiles/r02/occupancy_cap/, ab_runs/).
+set -u -o pipefail
+cd "$(dirname "$0")/.."
+export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
+frac() { python -c "import json,sys;d=json.load(open(sys.argv[1]));print(d['value'], d['roofline']['frac'])" "$1"; }
+case "${1:-}" in
+cap)
+  mkdir -p gpurun_out/cap
+  for r in 1 2; do
+    for c in 0 10 12 14 16; do
+      CHR_WG_PER_CU_VEC=$c timeout -k 10 120 python bench.py --steps 200 --warmup 20 --no-cpu-baseline \
+        > gpurun_out/cap/c2_cap${c}_r${r}.json 2>/dev/null || exit 1
+      echo "c2 cap=$c r=$r $(frac gpurun_out/cap/c2_cap${c}_r${r}.json)"
+    done
+  done
+  for c in 0 12 10; do
+    CHR_WG_PER_CU_VEC=$c timeout -k 10 300 python tools/mstream_probe.py --ms 3,7 --mib 256 --layouts sep --sets 1,8 \
+      > gpurun_out/cap/mstream_cap${c}.jsonl 2>/dev/null || exit 1
+    echo "mstream cap=$c"; cut -c1-300 gpurun_out/cap/mstream_cap${c}.jsonl
+  done
+  for c in 0 8 10 12; do
+    CHR_WG_PER_CU_TREE=$c timeout -k 10 400 python bench.py --collective-kernels > gpurun_out/cap/ck_tree_cap${c}.json \
+      2>/dev/null || exit 1
+    echo "tree cap=$c $(python -c "import json;d=json.load(open('gpurun_out/cap/ck_tree_cap${c}.json'))['collective_kernels']['rows'];print({k: v['frac'] for k, v in d.items()})")"
+  done ;;
+runs)
+  mkdir -p gpurun_out/ab_runs
+  for r in 1 2 3; do
+    for v in policy 256; do
+      if [ "$v" = policy ]; then unset CHR_XCD_RUN_KIB; else export CHR_XCD_RUN_KIB=$v; fi
+      timeout -k 10 120 python bench.py --steps 200 --warmup 20 --no-cpu-baseline \
+        > gpurun_out/ab_runs/c2_${v}_r${r}.json 2>/dev/null || exit 1
+      echo "c2 runs=$v r=$r $(frac gpurun_out/ab_runs/c2_${v}_r${r}.json)"
+    done
+  done ;;
+*) echo "usage: tools/ab.sh cap|runs"; exit 2 ;;
+esac
+echo AB_DONE
