@@ -201,7 +201,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce_tree_scalar(TreeScalarArgs a)
 // cap, take 256 KiB runs (focus18 below).
 template <int NL>
 constexpr size_t tree_xcd_run_kib() {
-    return NL <= 2 ? 256 : 512;
+    return NL <= 2 ? 256 : NL <= 4 ? 512 : 1024;
 }
 
 // Vectors per lane per trip and resident workgroups per CU (nt_lds_bytes; 0 = uncapped) of
@@ -213,7 +213,10 @@ constexpr size_t tree_xcd_run_kib() {
 // 6 HBM-cold sets): 2 leaves at 128 MiB U = 4 uncapped 0.774-0.783 -> 0.801-0.804 with 12 per CU and
 // 256 KiB runs (U = 2 at 16 per CU ties, 0.800-0.817); 4 leaves at 64 MiB U = 4 uncapped 0.741-0.750
 // -> U = 2 at 12 per CU 0.774-0.781.  3 leaves (not measured) follow the 3-input bucket (m = 2):
-// U = 2 at 16 per CU.
+// U = 2 at 16 per CU.  At U = 1 the 8-leaf C4 slice then preferred 12 per CU with longer XCD runs
+// (focus20, microbench_focus20_tree_runs.txt, 2 rounds, 16 MiB pieces): 16 per CU / 512 KiB
+// 0.760-0.761 cold, 0.752-0.754 warm -> 12 per CU / 1 MiB 0.772-0.775 / 0.758-0.761 (2 MiB runs
+// read 0.779-0.782 but leave pieces under 16 MiB unmapped, where the identity loses ~4 %).
 template <int NL, bool NT>
 constexpr int tree_u() {
     if constexpr (!NT) return NL <= 4 ? 4 : 2;  // cache-warm (plain) launches: the round-1 shapes
@@ -221,7 +224,7 @@ constexpr int tree_u() {
 }
 template <int NL>
 constexpr int tree_wg_per_cu() {
-    return NL == 2 || NL == 4 ? 12 : 16;
+    return NL == 3 ? 16 : 12;
 }
 
 template <int DT, int OP, int NL, int BL, bool NT>

@@ -1409,6 +1409,25 @@ int main(int argc, char** argv) {
         layout_mode();
         return 0;
     }
+    if (argc > 1 && std::string(argv[1]) == "focus20") {  // XCD run length for the U = 1 tree shape
+        for (int r = 0; r < 2; ++r)
+            for (int sets : {16, 4}) {
+                const size_t piece = 16 << 20, nvec = piece / 16;
+                Sets S = make_sets(17, nvec, sets);
+                for (unsigned run_kib : {0u, 128u, 256u, 512u, 1024u, 2048u}) {
+                    uint32_t cs = 0;
+                    while (run_kib && ((size_t)2 << cs) * (64 * 1 * 16) <= (size_t)run_kib * 1024 && cs < 16) ++cs;
+                    for (int cap : {12, 16, 20}) {
+                        char name[128];
+                        std::snprintf(name, sizeof name, "tree8x2 U=1 cap=%d run=%uKiB sets=%d", cap, run_kib, sets);
+                        report_moved(name, 2.0 * 9 * piece, tree8x2_time<1, true, 64>(S, nvec, sets, lds_for_cap(cap), cs));
+                    }
+                }
+                free_sets(S);
+                std::printf("--\n");
+            }
+        return 0;
+    }
     if (argc > 1 && std::string(argv[1]) == "focus19") {
         for (int r = 0; r < 2; ++r) {
             for (size_t mib : {2, 4, 8}) {
