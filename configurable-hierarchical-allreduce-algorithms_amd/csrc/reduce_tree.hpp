@@ -197,11 +197,11 @@ __global__ __launch_bounds__(kBlock) void k_reduce_tree_scalar(TreeScalarArgs a)
 // XCD runs for streaming (nt) tree launches (profiles/r02/xcd_runs/ab_tree_*.json, C4 slice of 2
 // batched 8-leaf trees, HBM-cold, identity -> 512 KiB): 8 MiB pieces 0.571 -> 0.634, 16 MiB
 // 0.668 -> 0.700, 32 MiB 0.719 -> 0.750; fused reductions of a whole C4 call 0.676 -> 0.719.
-// Two leaves move the m = 1 bucket's traffic (2 reads + 1 write) and, like it under the 12-per-CU
-// cap, take 256 KiB runs (focus18 below).
+// Two leaves move the m = 1 bucket's traffic (2 reads + 1 write) and keep the identity (focus18's
+// microbench lead for 256 KiB runs under a cap is not product-verified; see tree_u below).
 template <int NL>
 constexpr size_t tree_xcd_run_kib() {
-    return NL <= 2 ? 256 : NL <= 4 ? 512 : 1024;
+    return NL <= 2 ? 0 : 512;
 }
 
 // Vectors per lane per trip and resident workgroups per CU (nt_lds_bytes; 0 = uncapped) of
@@ -210,21 +210,22 @@ constexpr size_t tree_xcd_run_kib() {
 // uncapped's 0.739-0.750 on the C4 slice (2 x 8 leaves x 16 MiB, 4.5 and 1.1 GiB rotations, 2
 // rounds: microbench_focus17_tree_u_cap.txt), so trees of 5+ leaves take that shape.  The small
 // trees of the N = 2 / N = 4 flat schedules (focus18, microbench_focus18_small_trees.txt, 2 rounds,
-// 6 HBM-cold sets): 2 leaves at 128 MiB U = 4 uncapped 0.774-0.783 -> 0.801-0.804 with 12 per CU and
-// 256 KiB runs (U = 2 at 16 per CU ties, 0.800-0.817); 4 leaves at 64 MiB U = 4 uncapped 0.741-0.750
-// -> U = 2 at 12 per CU 0.774-0.781.  3 leaves (not measured) follow the 3-input bucket (m = 2):
-// U = 2 at 16 per CU.  At U = 1 the 8-leaf C4 slice then preferred 12 per CU with longer XCD runs
-// (focus20, microbench_focus20_tree_runs.txt, 2 rounds, 16 MiB pieces): 16 per CU / 512 KiB
-// 0.760-0.761 cold, 0.752-0.754 warm -> 12 per CU / 1 MiB 0.772-0.775 / 0.758-0.761 (2 MiB runs
-// read 0.779-0.782 but leave pieces under 16 MiB unmapped, where the identity loses ~4 %).
+// 6 HBM-cold sets) showed 2 leaves at 128 MiB U = 4 uncapped 0.774-0.783 -> 0.801-0.804 with 12 per
+// CU and 256 KiB runs, and 4 leaves at 64 MiB 0.741-0.750 -> 0.774-0.781 at U = 2 with 12 per CU,
+// but the microbench over-predicted the 8-leaf change below, and no product A/B of the 2- and
+// 4-leaf shapes exists yet, so trees of <= 4 leaves keep the round-1 shapes (U = 4, uncapped).
+// For the U = 1 8-leaf tree the microbench preferred 12 per CU with 1-2 MiB
+// XCD runs (focus20: 0.760 -> 0.772-0.782 on the C4 slice), but the same-box product A/B over the
+// whole C4/C5 calls reversed it (profiles/r02/ab_tree/: 16 per CU / 512 KiB 0.7245-0.7255 (C4),
+// 0.703-0.709 (C5) against 0.695-0.697 / 0.688), so 16 / 512 KiB stays.
 template <int NL, bool NT>
 constexpr int tree_u() {
     if constexpr (!NT) return NL <= 4 ? 4 : 2;  // cache-warm (plain) launches: the round-1 shapes
-    return NL == 2 ? 4 : NL <= 4 ? 2 : 1;
+    return NL <= 4 ? 4 : 1;
 }
 template <int NL>
 constexpr int tree_wg_per_cu() {
-    return NL == 3 ? 16 : 12;
+    return NL <= 4 ? 0 : 16;
 }
 
 template <int DT, int OP, int NL, int BL, bool NT>

@@ -37,6 +37,16 @@ runs)
       echo "c2 runs=$v r=$r $(frac gpurun_out/ab_runs/c2_${v}_r${r}.json)"
     done
   done ;;
-*) echo "usage: tools/ab.sh cap|runs"; exit 2 ;;
+tree)  # the tree shape: policy vs the previous one (16 per CU, 512 KiB runs), collective-kernel rows, alternating
+  mkdir -p gpurun_out/ab_tree
+  for r in 1 2; do
+    for v in prev policy; do
+      if [ "$v" = prev ]; then export CHR_WG_PER_CU_TREE=16 CHR_XCD_RUN_KIB=512; else unset CHR_WG_PER_CU_TREE CHR_XCD_RUN_KIB; fi
+      timeout -k 10 400 python bench.py --collective-kernels > gpurun_out/ab_tree/ck_${v}_r${r}.json 2>/dev/null || exit 1
+      echo "tree $v r=$r $(python -c "import json;d=json.load(open('gpurun_out/ab_tree/ck_${v}_r${r}.json'))['collective_kernels']['rows'];print({k[:-0 or None]: v['frac'] for k, v in d.items() if 'copies' not in k})")"
+    done
+  done
+  unset CHR_WG_PER_CU_TREE CHR_XCD_RUN_KIB ;;
+*) echo "usage: tools/ab.sh cap|runs|tree"; exit 2 ;;
 esac
 echo AB_DONE
