@@ -134,8 +134,9 @@ def test_rccl_world2_reduce_scatter_and_allreduce():
 
 
 def test_rccl_world8_c4_c5_geometries():
-    _run(8, [("ar", 4, 4, 8 * 4096, "f32", False, 0), ("ar", 4, 4, 8 * 4096, "bf16", False, 4),
-             ("ar", 2, 2, 8 * 4096, "f32", False, 3), ("ar", 3, 4, 8 * 2048, "bf16", False, 2),
+    # 8 processes over RCCL's socket transport cost seconds per case on a loaded box; the (n, k, b)
+    # grid itself is covered bit-exact on the loopback transport (test_gpu_collectives.py goldens)
+    _run(8, [("ar", 4, 4, 8 * 4096, "bf16", False, 4), ("ar", 3, 4, 8 * 2048, "bf16", False, 2),
              ("ar", 4, 8, 8 * 1024, "f32", False, 0), ("rs", 4, 4, 4000, "f32", False, 3)], timeout=600)
 
 
@@ -146,9 +147,8 @@ def test_rccl_mpich_baselines_world5_and_8():
              ("rx", 2, 1, 777, "bf16", False, 0), ("krsag", 2, 0, 30011, "f32", False, 0),
              ("rm", 2, 0, 4097, "f32", False, 0)]
     _run(5, cases)
-    _run(8, cases[:1] + [("rx", 4, 0, 1 << 16, "f32", False, 0), ("rsag", 0, 0, 1 << 16, "bf16", False, 0),
-                         ("krsag", 2, 1, 1 << 16, "f32", False, 0), ("rm", 3, 0, 12345, "bf16", False, 0)],
-         timeout=600)
+    _run(8, cases[:1] + [("rx", 4, 0, 1 << 14, "f32", False, 0), ("krsag", 2, 1, 1 << 14, "f32", False, 0),
+                         ("rm", 3, 0, 12345, "bf16", False, 0)], timeout=600)
 
 
 def test_rccl_mpich_reduce_scatter_baselines_world5_and_8():
@@ -158,9 +158,8 @@ def test_rccl_mpich_reduce_scatter_baselines_world5_and_8():
              ("rs_doubling", 0, 0, 777, "bf16", False, 0), ("rs_pairwise", 0, 0, 3000, "f32", True, 0),
              ("rs_radix", 2, 0, 64, "i32", True, 0)]
     _run(5, cases)
-    _run(8, [("rs_radix", 4, 0, 1 << 14, "f32", False, 0), ("rs_doubling", 0, 0, 5000, "f32", False, 0),
-             ("rs_halving", 0, 0, 4096, "bf16", True, 0), ("rs_pairwise", 0, 0, 1 << 14, "f32", False, 0)],
-         timeout=600)
+    _run(8, [("rs_radix", 4, 0, 1 << 12, "f32", False, 0), ("rs_doubling", 0, 0, 5000, "f32", False, 0),
+             ("rs_halving", 0, 0, 4096, "bf16", True, 0)], timeout=600)
 
 
 def test_rccl_allgather_world4_and_8():
