@@ -136,16 +136,22 @@ def cpu_baseline_collective(world, k, b, gpu_count, gpu_es):
                       f"({what}), {reps} calls, max over ranks: {t * 1e3:.1f} ms per call (nproc={os.cpu_count()})"}
 
 
-def pmc_traffic(kernel_key):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if any."""
-    path = os.path.join(REPO, "profiles", "pmc_latest.json")
+C2_KERNEL_SYMBOL = "void chr::k_reduce_vec<0, 0, 1, 4, true, true, 64>(chr::VecArgs)"
+
+
+def pmc_traffic(kernel_key, symbol, root=REPO):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_latest.json), or
+    (None, why) when that entry was measured on another kernel symbol or before its sources last
+    changed (tools/pmc_provenance.py)."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import pmc_provenance
+
     try:
-        with open(path) as f:
-            d = json.load(f)
-        e = d["kernels"][kernel_key]
-        return e["hbm_bytes_per_launch"]
-    except Exception:
-        return None
+        with open(os.path.join(root, "profiles", "pmc_latest.json")) as f:
+            entry = json.load(f)["kernels"].get(kernel_key)
+    except Exception as e:
+        return None, f"profiles/pmc_latest.json unreadable: {e}"
+    return pmc_provenance.current_traffic(entry, kernel_key, symbol, root)
 
 
 # ---- N = 1: bucket reduction (C2) ----------------------------------------------------------------
@@ -201,7 +207,7 @@ def bench_bucket(args, cpu):
     bytes_per_step = 3 * 4 * n
     ms_per_step = total_ms / args.steps
     achieved = bytes_per_step / (avg_kern_ms * 1e-3) / 1e9
-    traffic = pmc_traffic("reduce_f32_sum_m1_64MiB")
+    traffic, stale = pmc_traffic("reduce_f32_sum_m1_64MiB", C2_KERNEL_SYMBOL)
     line = {
         "metric": METRIC, "value": round(bytes_per_step / (ms_per_step * 1e-3) / 1e9, 2), "unit": "GB/s",
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
@@ -211,11 +217,13 @@ def bench_bucket(args, cpu):
                    "buffer_sets": NSETS, "untimed_launches": touch, "parallelism": "replicas"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "kernel": "chr::k_reduce_vec<f32,SUM,M=1,U=4,NT,ACC0,64 threads>", "algorithmic_bytes_per_launch": bytes_per_step,
+                     "kernel": C2_KERNEL_SYMBOL, "algorithmic_bytes_per_launch": bytes_per_step,
                      "avg_kernel_ms": round(avg_kern_ms, 5)},
         "cpu_baseline": cpu,
         "host_wall_s": round(wall, 4),
     }
+    if stale:
+        line["roofline"]["traffic_stale"] = stale
     if cpu:
         line["gpu_vs_cpu"] = round(line["value"] / cpu["value"], 1)
         if "all_cores" in cpu:

@@ -54,27 +54,37 @@ hipError_t launch_fill(void* buf, size_t n, int dtype, int pattern, uint64_t see
 //   CHR_REDUCE_NT            0 / 1 forces plain / non-temporal loads+stores; unset = by size
 //   CHR_REDUCE_NT_MIN_BYTES  bytes streamed by one call from which NT is used (128 MiB for
 //                            bucket launches, 64 MiB for tree launches; the variable sets both)
-//   CHR_REDUCE_ACC0          0 / 1 forces the first accumulator slot nt / default policy
-//                            under NT; unset = default policy for m >= 2 or large buckets
-//   CHR_REDUCE_ACC0_MIN_BYTES  bucket size from which m = 1 uses it too (0: always)
-//   CHR_REDUCE_BLOCK         threads per workgroup of the vector kernels: 64 or 256;
-//                            unset = 64 for NT calls, 256 otherwise
 //   CHR_WG_PER_CU_VEC        streaming (NT) bucket launches: at most this many workgroups resident
 //   CHR_WG_PER_CU_TREE       per CU, capped through dynamic LDS (0 = uncapped); unset = policy
 //                            (nt_lds_bytes in reduce_common.hpp); likewise for the tree kernel
 struct ReduceTuning {
     int xcd_run_kib;        // -1: policy
     size_t max_launch_vec;  // 0: the grid limit; else cap on 16-B vectors per launch / tree segment
-    int block;
     int nt_mode;
     size_t nt_min_bytes;       // bucket launches
     size_t tree_nt_min_bytes;  // tree launches
-    int acc0_mode;
-    size_t acc0_min_bytes;
     int wg_per_cu_vec;   // -1: policy
     int wg_per_cu_tree;  // -1: policy
     unsigned lds_per_cu; // bytes of LDS per CU (device attribute; 160 KiB on gfx950)
+    unsigned lds_per_block;  // bytes of LDS one workgroup may allocate (device attribute)
 };
 ReduceTuning& reduce_tuning();
+
+// Streaming launches issued on this host thread while a CoresidentScope is open share the GPU with
+// RCCL's kernels and leave them room: at most kCoresidentWgPerCu resident workgroups per CU
+// (stream_wg_cap in reduce_common.hpp, which gives the measurements).
+constexpr int kCoresidentWgPerCu = 12;
+int& coresident_depth();  // per host thread (reduce_kernels.hip)
+struct CoresidentScope {
+    bool on;
+    explicit CoresidentScope(bool enable) : on(enable) {
+        if (on) ++coresident_depth();
+    }
+    ~CoresidentScope() {
+        if (on) --coresident_depth();
+    }
+    CoresidentScope(const CoresidentScope&) = delete;
+    CoresidentScope& operator=(const CoresidentScope&) = delete;
+};
 
 }  // namespace chr

@@ -535,7 +535,12 @@ int enqueue_plan(chr_comm* c, const Plan& p, const void* send, void* recv, int d
         if (!ec || !ed) return CHR_ERR_HIP;
         if ((rc = hip_code(hipEventRecord(ec, c->stream))) || (rc = hip_code(hipStreamWaitEvent(c->cstream, ec, 0))))
             return rc;
-        if ((rc = run_locals(s.post, B, dtype, op, c->cstream, &c->prof))) return rc;
+        {
+            // RCCL's kernels run beside these launches: streaming reductions leave them room on every
+            // CU (reduce_common.hpp kCoresidentWgPerCu)
+            chr::CoresidentScope beside_rccl(c->nranks > 1);
+            if ((rc = run_locals(s.post, B, dtype, op, c->cstream, &c->prof))) return rc;
+        }
         if ((rc = hip_code(hipEventRecord(ed, c->cstream)))) return rc;
         last_comp = (int)t;
     }
@@ -1017,6 +1022,17 @@ int chr_get_unique_id(chr_unique_id* id) {
 
 int chr_comm_init_rank(chr_comm** out, int nranks, const chr_unique_id* id, int rank, int device) {
     if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks) return CHR_ERR_INVALID_ARG;
+    if (std::getenv("CHR_DEBUG")) {  // the library defaults it to 0 at load (api.cpp chr_default_ipc_mode)
+        static bool warned = false;
+        const char* ipc = std::getenv("HSA_ENABLE_IPC_MODE_LEGACY");
+        if (!warned && nranks > 1 && (!ipc || std::strcmp(ipc, "0") != 0)) {
+            std::fprintf(stderr,
+                         "[chiara] HSA_ENABLE_IPC_MODE_LEGACY=%s: RCCL's IPC transport needs 0 (dmabuf) on this "
+                         "driver; expect hipIpcGetMemHandle failures\n",
+                         ipc ? ipc : "(unset)");
+            warned = true;
+        }
+    }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return CHR_ERR_NO_DEVICE;
     if (device < 0 || device >= ndev) return CHR_ERR_INVALID_ARG;

@@ -155,13 +155,40 @@ inline uint32_t xcd_run_shift(size_t policy_kib, size_t trip_bytes) {
     return cs;
 }
 
-// Dynamic LDS per workgroup that leaves at most `cap` workgroups resident per CU (the kernels use
-// no LDS; the allocation only caps occupancy).  env >= 0 overrides the policy; 0 = uncapped.
+// Dynamic LDS per workgroup that caps the workgroups resident per CU (the kernels use no LDS; the
+// allocation only caps occupancy).  env >= 0 overrides the policy (and stream_wg_cap below); 0 =
+// uncapped.  Clamped to the
+// per-workgroup limit (a cap of 1 asks for the whole CU).  Measured residency of one-wave workgroups
+// per `cap` (tools/coresidency_probe --census, profiles/r03/coresidency/census.jsonl): 8 -> 8,
+// 10 -> 9, 12 -> 11, 13 -> 12, 14 -> 14, 16 -> 16, uncapped -> 32 (the wave-slot limit).
+inline int stream_wg_cap(int env, int policy);
 inline unsigned nt_lds_bytes(int env, int policy) {
     const unsigned lds = reduce_tuning().lds_per_cu;
-    const int cap = env >= 0 ? env : policy;
+    const int cap = stream_wg_cap(env, policy);
     if (cap <= 0 || lds == 0) return 0;
-    return (lds / (unsigned)cap) & ~255u;
+    const unsigned b = (lds / (unsigned)cap) & ~255u;
+    const unsigned lim = reduce_tuning().lds_per_block;
+    return lim && b > lim ? lim & ~255u : b;
+}
+
+// Launches that share the GPU with RCCL's kernels.  Inside an overlapped collective the fused
+// reductions of one pipeline slice run on the compute stream while RCCL's send/recv kernel of the
+// next slice runs on the transfer stream, and RCCL's kernel needs a CU with room for 256 threads at
+// ~288 VGPRs per wave plus 19 744 B of LDS (torch's RCCL) or 37 664 B (ROCm 7.2's).  With a
+// streaming reduction resident on every CU, a kernel of that footprint was admitted within 3-31 us
+// of its submission when the reduction ran at cap <= 12 (11 resident workgroups per CU), but only
+// once the reduction launch drained (median ~170 us into a 200 us launch) at cap 14, 16 or uncapped
+// (tools/coresidency_probe, profiles/r03/coresidency/).  Alone, the 8-leaf tree runs as fast at 12
+// as at 16 in that probe, but the whole-call in-collective rows measured 2-3 % lower, so the
+// tighter cap applies only where RCCL runs beside the launch: the executor opens a CoresidentScope
+// around the local ops it puts on the compute stream of a multi-rank overlapped collective, and every
+// streaming launch issued on that thread meanwhile takes at most kCoresidentWgPerCu (uncapped
+// policies included; CoresidentScope in chr_internal.hpp).  An explicit CHR_WG_PER_CU_VEC / _TREE
+// still wins.
+inline int stream_wg_cap(int env, int policy) {
+    if (env >= 0) return env;
+    if (coresident_depth() > 0 && (policy <= 0 || policy > kCoresidentWgPerCu)) return kCoresidentWgPerCu;
+    return policy;
 }
 
 // Materialise a wave-uniform pointer (a kernel argument) in SGPRs at this point: an empty asm

@@ -16,44 +16,46 @@ namespace chr {
 template <int DT>
 static hipError_t vec_all_ops(const VecArgs& a, int op, int m, hipStream_t s) {
     switch (op) {
-    case CHR_SUM: return launch_vec_op<DT, CHR_SUM, false>(a, m, s);
-    case CHR_PROD: return launch_vec_op<DT, CHR_PROD, false>(a, m, s);
-    case CHR_MAX: return launch_vec_op<DT, CHR_MAX, false>(a, m, s);
-    case CHR_MIN: return launch_vec_op<DT, CHR_MIN, false>(a, m, s);
-    case CHR_LAND: return launch_vec_op<DT, CHR_LAND, false>(a, m, s);
-    case CHR_LOR: return launch_vec_op<DT, CHR_LOR, false>(a, m, s);
-    case CHR_LXOR: return launch_vec_op<DT, CHR_LXOR, false>(a, m, s);
-    case CHR_BAND: return launch_vec_op<DT, CHR_BAND, false>(a, m, s);
-    case CHR_BOR: return launch_vec_op<DT, CHR_BOR, false>(a, m, s);
-    case CHR_BXOR: return launch_vec_op<DT, CHR_BXOR, false>(a, m, s);
+    case CHR_SUM: return launch_vec_op<DT, CHR_SUM>(a, m, s);
+    case CHR_PROD: return launch_vec_op<DT, CHR_PROD>(a, m, s);
+    case CHR_MAX: return launch_vec_op<DT, CHR_MAX>(a, m, s);
+    case CHR_MIN: return launch_vec_op<DT, CHR_MIN>(a, m, s);
+    case CHR_LAND: return launch_vec_op<DT, CHR_LAND>(a, m, s);
+    case CHR_LOR: return launch_vec_op<DT, CHR_LOR>(a, m, s);
+    case CHR_LXOR: return launch_vec_op<DT, CHR_LXOR>(a, m, s);
+    // the bitwise ops see no element boundaries (apply_vec works on whole dwords): int32's
+    // kernels serve every width
+    case CHR_BAND: return launch_vec_op<CHR_INT32, CHR_BAND>(a, m, s);
+    case CHR_BOR: return launch_vec_op<CHR_INT32, CHR_BOR>(a, m, s);
+    case CHR_BXOR: return launch_vec_op<CHR_INT32, CHR_BXOR>(a, m, s);
     default: return hipErrorInvalidValue;
     }
 }
 
 template <int DT>
 static hipError_t vec_minmax(const VecArgs& a, int op, int m, hipStream_t s) {
-    if (op == CHR_MAX) return launch_vec_op<DT, CHR_MAX, false>(a, m, s);
-    if (op == CHR_MIN) return launch_vec_op<DT, CHR_MIN, false>(a, m, s);
+    if (op == CHR_MAX) return launch_vec_op<DT, CHR_MAX>(a, m, s);
+    if (op == CHR_MIN) return launch_vec_op<DT, CHR_MIN>(a, m, s);
     return hipErrorInvalidValue;
 }
 
 static hipError_t vec_i32_logic(const VecArgs& a, int op, int m, hipStream_t s) {
     switch (op) {
-    case CHR_LAND: return launch_vec_op<CHR_INT32, CHR_LAND, false>(a, m, s);
-    case CHR_LOR: return launch_vec_op<CHR_INT32, CHR_LOR, false>(a, m, s);
-    case CHR_LXOR: return launch_vec_op<CHR_INT32, CHR_LXOR, false>(a, m, s);
-    case CHR_BAND: return launch_vec_op<CHR_INT32, CHR_BAND, false>(a, m, s);
-    case CHR_BOR: return launch_vec_op<CHR_INT32, CHR_BOR, false>(a, m, s);
-    case CHR_BXOR: return launch_vec_op<CHR_INT32, CHR_BXOR, false>(a, m, s);
+    case CHR_LAND: return launch_vec_op<CHR_INT32, CHR_LAND>(a, m, s);
+    case CHR_LOR: return launch_vec_op<CHR_INT32, CHR_LOR>(a, m, s);
+    case CHR_LXOR: return launch_vec_op<CHR_INT32, CHR_LXOR>(a, m, s);
+    case CHR_BAND: return launch_vec_op<CHR_INT32, CHR_BAND>(a, m, s);
+    case CHR_BOR: return launch_vec_op<CHR_INT32, CHR_BOR>(a, m, s);
+    case CHR_BXOR: return launch_vec_op<CHR_INT32, CHR_BXOR>(a, m, s);
     default: return hipErrorInvalidValue;
     }
 }
 
 template <int DT>
 static hipError_t vec_logic(const VecArgs& a, int op, int m, hipStream_t s) {
-    if (op == CHR_LAND) return launch_vec_op<DT, CHR_LAND, false>(a, m, s);
-    if (op == CHR_LOR) return launch_vec_op<DT, CHR_LOR, false>(a, m, s);
-    if (op == CHR_LXOR) return launch_vec_op<DT, CHR_LXOR, false>(a, m, s);
+    if (op == CHR_LAND) return launch_vec_op<DT, CHR_LAND>(a, m, s);
+    if (op == CHR_LOR) return launch_vec_op<DT, CHR_LOR>(a, m, s);
+    if (op == CHR_LXOR) return launch_vec_op<DT, CHR_LXOR>(a, m, s);
     return hipErrorInvalidValue;
 }
 

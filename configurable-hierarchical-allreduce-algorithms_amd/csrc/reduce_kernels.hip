@@ -88,9 +88,14 @@ void canon_op(int dtype, int op, bool running_first, int* kdt, int* kop) {
     }
 }
 
-// kernel types compiled in this translation unit (all tuning variants); the rest: reduce_int.hip
+// kernel types compiled in this translation unit; the rest: reduce_int.hip
 static bool in_core_tu(int kdt, int kop) {
     return (is_float_dtype(kdt) || kdt == CHR_INT32) && ((kop >= CHR_SUM && kop <= CHR_MIN) || kop >= kMaxSw);
+}
+
+int& coresident_depth() {
+    static thread_local int depth = 0;
+    return depth;
 }
 
 ReduceTuning& reduce_tuning() {
@@ -109,22 +114,19 @@ ReduceTuning& reduce_tuning() {
         // plain 0.572-0.577 cold, 0.651-0.657 vs 0.599-0.666 warm; 2 MiB pieces tie;
         // profiles/r02/occupancy_cap/microbench_focus19_nt_threshold.txt)
         r.tree_nt_min_bytes = s ? r.nt_min_bytes : (size_t)64 << 20;
-        s = std::getenv("CHR_REDUCE_ACC0");   // 0 / 1 / unset = by fan-in and size
-        r.acc0_mode = s ? std::atoi(s) : -1;
-        s = std::getenv("CHR_REDUCE_ACC0_MIN_BYTES");
-        r.acc0_min_bytes = s ? (size_t)std::atoll(s) : 0;
-        s = std::getenv("CHR_REDUCE_BLOCK");  // 64 / 256 / unset = by policy (launch_vec_m)
-        r.block = s ? (std::atoi(s) == 64 ? 64 : 256) : 0;
         s = std::getenv("CHR_WG_PER_CU_VEC");
         r.wg_per_cu_vec = s ? std::max(0, std::atoi(s)) : -1;
         s = std::getenv("CHR_WG_PER_CU_TREE");
         r.wg_per_cu_tree = s ? std::max(0, std::atoi(s)) : -1;
-        int dev = 0, lds = 0;
+        int dev = 0, lds = 0, blk = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess ||
             lds <= 0)
             lds = 0;  // unknown: no cap
+        if (hipDeviceGetAttribute(&blk, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess || blk <= 0)
+            blk = 0;
         r.lds_per_cu = (unsigned)lds;
+        r.lds_per_block = (unsigned)blk;
         return r;
     }();
     return t;
@@ -135,16 +137,16 @@ ReduceTuning& reduce_tuning() {
 template <int DT>
 static hipError_t launch_vec_dt(const VecArgs& a, int m, int op, hipStream_t s) {
     switch (op) {
-    case CHR_SUM: return launch_vec_op<DT, CHR_SUM, true>(a, m, s);
-    case CHR_PROD: return launch_vec_op<DT, CHR_PROD, true>(a, m, s);
-    case CHR_MAX: return launch_vec_op<DT, CHR_MAX, true>(a, m, s);
-    case CHR_MIN: return launch_vec_op<DT, CHR_MIN, true>(a, m, s);
+    case CHR_SUM: return launch_vec_op<DT, CHR_SUM>(a, m, s);
+    case CHR_PROD: return launch_vec_op<DT, CHR_PROD>(a, m, s);
+    case CHR_MAX: return launch_vec_op<DT, CHR_MAX>(a, m, s);
+    case CHR_MIN: return launch_vec_op<DT, CHR_MIN>(a, m, s);
     case kMaxSw:
         if constexpr (DT == CHR_INT32) return hipErrorInvalidValue;
-        else return launch_vec_op<DT, kMaxSw, true>(a, m, s);
+        else return launch_vec_op<DT, kMaxSw>(a, m, s);
     case kMinSw:
         if constexpr (DT == CHR_INT32) return hipErrorInvalidValue;
-        else return launch_vec_op<DT, kMinSw, true>(a, m, s);
+        else return launch_vec_op<DT, kMinSw>(a, m, s);
     default: return hipErrorInvalidValue;
     }
 }

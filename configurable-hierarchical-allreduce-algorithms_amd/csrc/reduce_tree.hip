@@ -8,10 +8,10 @@ namespace chr {
 template <int DT>
 static hipError_t launch_tree_dt(const TreeArgs& a, const TreeScalarArgs* sa, int op, hipStream_t s) {
     switch (op) {
-    case CHR_SUM: return launch_tree_op<DT, CHR_SUM, true>(a, sa, s);
-    case CHR_PROD: return launch_tree_op<DT, CHR_PROD, true>(a, sa, s);
-    case CHR_MAX: return launch_tree_op<DT, CHR_MAX, true>(a, sa, s);
-    case CHR_MIN: return launch_tree_op<DT, CHR_MIN, true>(a, sa, s);
+    case CHR_SUM: return launch_tree_op<DT, CHR_SUM>(a, sa, s);
+    case CHR_PROD: return launch_tree_op<DT, CHR_PROD>(a, sa, s);
+    case CHR_MAX: return launch_tree_op<DT, CHR_MAX>(a, sa, s);
+    case CHR_MIN: return launch_tree_op<DT, CHR_MIN>(a, sa, s);
     default: return hipErrorInvalidValue;
     }
 }

@@ -217,7 +217,9 @@ constexpr size_t tree_xcd_run_kib() {
 // For the U = 1 8-leaf tree the microbench preferred 12 per CU with 1-2 MiB
 // XCD runs (focus20: 0.760 -> 0.772-0.782 on the C4 slice), but the same-box product A/B over the
 // whole C4/C5 calls reversed it (profiles/r02/ab_tree/: 16 per CU / 512 KiB 0.7245-0.7255 (C4),
-// 0.703-0.709 (C5) against 0.695-0.697 / 0.688), so 16 / 512 KiB stays.
+// 0.703-0.709 (C5) against 0.695-0.697 / 0.688), so 16 / 512 KiB stays -- except beside RCCL
+// (stream_wg_cap), where every tree takes kCoresidentWgPerCu: at 16 or uncapped RCCL's kernel waits
+// for the tree launch to drain (profiles/r03/coresidency/).
 template <int NL, bool NT>
 constexpr int tree_u() {
     if constexpr (!NT) return NL <= 4 ? 4 : 2;  // cache-warm (plain) launches: the round-1 shapes
@@ -252,41 +254,52 @@ inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
     return hipGetLastError();
 }
 
-// FULL: the CHR_REDUCE_BLOCK override is honoured (both workgroup sizes compiled); otherwise the
-// policy shapes only (nt: one wave; plain: 256 threads), as in reduce_vec.hpp.
-template <int DT, int OP, int NL, bool FULL>
-inline hipError_t launch_tree_nl(const TreeArgs& a, const TreeScalarArgs* sa, hipStream_t s) {
-    if (sa) {
-        const size_t trips = (sa->n + kBlock - 1) / kBlock;
-        const int grid = (int)(trips < 2048 ? trips : 2048);
-        hipLaunchKernelGGL((k_reduce_tree_scalar<DT, OP, NL>), dim3(grid), dim3(kBlock), 0, s, *sa);
-        return hipGetLastError();
+template <int DT, int OP, int NL>
+inline hipError_t launch_tree_scalar_nl(const TreeScalarArgs& sa, hipStream_t s) {
+    const size_t trips = (sa.n + kBlock - 1) / kBlock;
+    const int grid = (int)(trips < 2048 ? trips : 2048);
+    hipLaunchKernelGGL((k_reduce_tree_scalar<DT, OP, NL>), dim3(grid), dim3(kBlock), 0, s, sa);
+    return hipGetLastError();
+}
+
+// Scalar (any alignment) trees only.
+template <int DT, int OP>
+inline hipError_t launch_tree_scalar_op(const TreeScalarArgs& sa, hipStream_t s) {
+    switch (sa.nl) {
+    case 2: return launch_tree_scalar_nl<DT, OP, 2>(sa, s);
+    case 3: return launch_tree_scalar_nl<DT, OP, 3>(sa, s);
+    case 4: return launch_tree_scalar_nl<DT, OP, 4>(sa, s);
+    case 5: return launch_tree_scalar_nl<DT, OP, 5>(sa, s);
+    case 6: return launch_tree_scalar_nl<DT, OP, 6>(sa, s);
+    case 7: return launch_tree_scalar_nl<DT, OP, 7>(sa, s);
+    case 8: return launch_tree_scalar_nl<DT, OP, 8>(sa, s);
+    default: return hipErrorInvalidValue;
     }
+}
+
+// The policy shapes only (nt: one wave; plain: 256 threads), as in reduce_vec.hpp.
+template <int DT, int OP, int NL>
+inline hipError_t launch_tree_nl(const TreeArgs& a, const TreeScalarArgs* sa, hipStream_t s) {
+    if (sa) return launch_tree_scalar_nl<DT, OP, NL>(*sa, s);
     // as launch_vec_m: streaming calls (>= 64 MiB for trees) nt with one-wave workgroups
     const ReduceTuning& t = reduce_tuning();
     size_t nvec = 0;
     for (int j = 0; j < a.nseg; ++j) nvec += a.seg[j].nvec;
     const size_t call_bytes = (size_t)(a.nl + 1) * nvec * 16;
     const bool nt = t.nt_mode == 1 || (t.nt_mode < 0 && call_bytes >= t.tree_nt_min_bytes);
-    if constexpr (!FULL) {
-        return nt ? launch_tree_vec<DT, OP, NL, 64, true>(a, s) : launch_tree_vec<DT, OP, NL, 256, false>(a, s);
-    } else {
-        const int bl = t.block ? t.block : nt ? 64 : 256;
-        if (bl == 64) return nt ? launch_tree_vec<DT, OP, NL, 64, true>(a, s) : launch_tree_vec<DT, OP, NL, 64, false>(a, s);
-        return nt ? launch_tree_vec<DT, OP, NL, 256, true>(a, s) : launch_tree_vec<DT, OP, NL, 256, false>(a, s);
-    }
+    return nt ? launch_tree_vec<DT, OP, NL, 64, true>(a, s) : launch_tree_vec<DT, OP, NL, 256, false>(a, s);
 }
 
-template <int DT, int OP, bool FULL>
+template <int DT, int OP>
 inline hipError_t launch_tree_op(const TreeArgs& a, const TreeScalarArgs* sa, hipStream_t s) {
     switch (sa ? sa->nl : a.nl) {
-    case 2: return launch_tree_nl<DT, OP, 2, FULL>(a, sa, s);
-    case 3: return launch_tree_nl<DT, OP, 3, FULL>(a, sa, s);
-    case 4: return launch_tree_nl<DT, OP, 4, FULL>(a, sa, s);
-    case 5: return launch_tree_nl<DT, OP, 5, FULL>(a, sa, s);
-    case 6: return launch_tree_nl<DT, OP, 6, FULL>(a, sa, s);
-    case 7: return launch_tree_nl<DT, OP, 7, FULL>(a, sa, s);
-    case 8: return launch_tree_nl<DT, OP, 8, FULL>(a, sa, s);
+    case 2: return launch_tree_nl<DT, OP, 2>(a, sa, s);
+    case 3: return launch_tree_nl<DT, OP, 3>(a, sa, s);
+    case 4: return launch_tree_nl<DT, OP, 4>(a, sa, s);
+    case 5: return launch_tree_nl<DT, OP, 5>(a, sa, s);
+    case 6: return launch_tree_nl<DT, OP, 6>(a, sa, s);
+    case 7: return launch_tree_nl<DT, OP, 7>(a, sa, s);
+    case 8: return launch_tree_nl<DT, OP, 8>(a, sa, s);
     default: return hipErrorInvalidValue;
     }
 }

@@ -120,13 +120,13 @@ constexpr size_t vec_xcd_run_kib() {
     return M == 1 ? 256 : M == 2 ? 0 : 512;
 }
 
-// Resident workgroups per CU for streaming launches (nt_lds_bytes); 0 = uncapped.  Uncapped, a
-// CU holds ~20-32 one-wave workgroups, each with (m+1)*U*1 KiB of loads in flight the moment it
-// starts; 12 per CU measured best for m <= 3 through the product API (profiles/r02/occupancy_cap/,
-// 2 rounds, bench.py C2: 0.815 -> 0.823-0.826; m = 3 at 256 MiB 0.893 -> 0.924 with a 1.25 GiB
-// rotation, 0.814 -> 0.830 with 10 GiB; 16 and 10 per CU lose or tie).  Wider fan-in takes 16 per CU
-// with U = 1 (vec_u_nt below); the tree kernel gains nothing at 8-12 (collective rows within
-// noise) and stays uncapped.
+// Resident workgroups per CU for streaming launches (nt_lds_bytes; 0 = uncapped).  Uncapped, a CU
+// holds 32 one-wave workgroups, each with (m+1)*U*1 KiB of loads in flight the moment it starts;
+// cap 12 (11 resident, census in nt_lds_bytes) measured best for m <= 3 through the product API
+// (profiles/r02/occupancy_cap/, 2 rounds, bench.py C2: 0.815 -> 0.823-0.826; m = 3 at 256 MiB 0.893 ->
+// 0.924 with a 1.25 GiB rotation, 0.814 -> 0.830 with 10 GiB; 16 and 10 per CU lose or tie).  Wider
+// fan-in takes 12 with U = 1 (vec_u_nt below); m = 2 takes 16 (0.817-0.830 in the microbench), or 12
+// beside RCCL (stream_wg_cap).
 template <int M>
 constexpr int vec_wg_per_cu() {
     return M == 2 ? 16 : 12;
@@ -176,7 +176,9 @@ inline hipError_t for_each_launch_piece(VecArgs a, L launch) {
 
 // Policy (profiles/r01/block_ab_*): calls that stream >= 128 MiB run non-temporal with
 // one-wave workgroups and the first accumulator slot temporal (ACC0); smaller, cache-warm
-// calls keep plain accesses and 256-thread workgroups.
+// calls keep plain accesses and 256-thread workgroups.  Only these two shapes are compiled into
+// the library; the design-space variants (other workgroup sizes, all-nt accumulators) live in
+// tools/reduce_microbench.hip, which instantiates the kernel templates directly.
 template <int DT, int OP, int M, int BL, bool NT, bool ACC0>
 inline hipError_t launch_vec_mb_one(VecArgs a, hipStream_t s) {
     constexpr int U = vec_u<M, NT>();
@@ -187,41 +189,26 @@ inline hipError_t launch_vec_mb_one(VecArgs a, hipStream_t s) {
     });
 }
 
-// FULL: every tuning variant (CHR_REDUCE_BLOCK / CHR_REDUCE_ACC0 overrides) is compiled, for the
-// floating types and int32; the other integer types compile the two policy shapes only (nt: one
-// wave + ACC0; plain: 256 threads) and ignore those two overrides.
-template <int DT, int OP, int M, int BL>
-inline hipError_t launch_vec_mb(const VecArgs& a, bool nt, bool acc0, hipStream_t s) {
-    if (!nt) return launch_vec_mb_one<DT, OP, M, BL, false, false>(a, s);
-    return acc0 ? launch_vec_mb_one<DT, OP, M, BL, true, true>(a, s) : launch_vec_mb_one<DT, OP, M, BL, true, false>(a, s);
-}
-
-template <int DT, int OP, int M, bool FULL>
+template <int DT, int OP, int M>
 inline hipError_t launch_vec_m(const VecArgs& a, hipStream_t s) {
     const ReduceTuning& t = reduce_tuning();
     const size_t call_bytes = (size_t)(M + 2) * a.nvec * 16;
     const bool nt = t.nt_mode == 1 || (t.nt_mode < 0 && call_bytes >= t.nt_min_bytes);
-    if constexpr (!FULL) {
-        if (nt) return launch_vec_mb_one<DT, OP, M, 64, true, true>(a, s);
-        return launch_vec_mb_one<DT, OP, M, 256, false, false>(a, s);
-    } else {
-        const bool acc0 = t.acc0_mode == 1 || (t.acc0_mode < 0 && (M >= 2 || a.nvec * 16 >= t.acc0_min_bytes));
-        const int bl = t.block ? t.block : nt ? 64 : 256;
-        return bl == 64 ? launch_vec_mb<DT, OP, M, 64>(a, nt, acc0, s) : launch_vec_mb<DT, OP, M, 256>(a, nt, acc0, s);
-    }
+    if (nt) return launch_vec_mb_one<DT, OP, M, 64, true, true>(a, s);
+    return launch_vec_mb_one<DT, OP, M, 256, false, false>(a, s);
 }
 
-template <int DT, int OP, bool FULL>
+template <int DT, int OP>
 inline hipError_t launch_vec_op(const VecArgs& a, int m, hipStream_t s) {
     switch (m) {
-    case 1: return launch_vec_m<DT, OP, 1, FULL>(a, s);
-    case 2: return launch_vec_m<DT, OP, 2, FULL>(a, s);
-    case 3: return launch_vec_m<DT, OP, 3, FULL>(a, s);
-    case 4: return launch_vec_m<DT, OP, 4, FULL>(a, s);
-    case 5: return launch_vec_m<DT, OP, 5, FULL>(a, s);
-    case 6: return launch_vec_m<DT, OP, 6, FULL>(a, s);
-    case 7: return launch_vec_m<DT, OP, 7, FULL>(a, s);
-    case 8: return launch_vec_m<DT, OP, 8, FULL>(a, s);
+    case 1: return launch_vec_m<DT, OP, 1>(a, s);
+    case 2: return launch_vec_m<DT, OP, 2>(a, s);
+    case 3: return launch_vec_m<DT, OP, 3>(a, s);
+    case 4: return launch_vec_m<DT, OP, 4>(a, s);
+    case 5: return launch_vec_m<DT, OP, 5>(a, s);
+    case 6: return launch_vec_m<DT, OP, 6>(a, s);
+    case 7: return launch_vec_m<DT, OP, 7>(a, s);
+    case 8: return launch_vec_m<DT, OP, 8>(a, s);
     default: return hipErrorInvalidValue;
     }
 }

@@ -60,3 +60,33 @@ def test_reduce_tree_rejects_bad_args_without_device():
     leaves = (ctypes.c_void_p * 2)(0x1000, 0x2000)
     assert ca.lib().chr_reduce_tree(0x3000, leaves, 2, bytes([0, 1]), None, 0, 11, ca.SUM, None) == 1  # bad dtype
     assert ca.lib().chr_reduce_tree(0x3000, None, 2, bytes([0, 1]), None, 0, ca.FLOAT32, ca.SUM, None) == 1
+
+
+def _ipc_env_after_dlopen(preset):
+    """Loads libchiara.so into a fresh process (no torch, no chiara_amd) and reads the C-level
+    environment afterwards: the library's ELF constructor sets the dmabuf-IPC default."""
+    code = (
+        "import ctypes, sys\n"
+        f"ctypes.CDLL({_lib.LIB_PATH!r})\n"
+        "libc = ctypes.CDLL(None)\n"
+        "libc.getenv.restype = ctypes.c_char_p\n"
+        "v = libc.getenv(b'HSA_ENABLE_IPC_MODE_LEGACY')\n"
+        "print(v.decode() if v is not None else 'UNSET')\n"
+    )
+    env = {k: v for k, v in os.environ.items() if k != "HSA_ENABLE_IPC_MODE_LEGACY"}
+    if preset is not None:
+        env["HSA_ENABLE_IPC_MODE_LEGACY"] = preset
+    return subprocess.check_output(["python3", "-c", code], env=env).decode().strip()
+
+
+def test_library_defaults_ipc_mode_at_load():
+    assert _ipc_env_after_dlopen(None) == "0"
+    assert _ipc_env_after_dlopen("1") == "1"  # the caller's value is kept
+
+
+def test_package_defaults_ipc_mode_before_torch():
+    code = "import os, chiara_amd; print(os.environ['HSA_ENABLE_IPC_MODE_LEGACY'])"
+    env = {k: v for k, v in os.environ.items() if k != "HSA_ENABLE_IPC_MODE_LEGACY"}
+    env["PYTHONPATH"] = _lib.PKG_ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    out = subprocess.check_output(["python3", "-c", code], env=env, cwd=REPO).decode().strip()
+    assert out == "0"

@@ -14,13 +14,18 @@ import json
 import os
 import sys
 
+import pmc_provenance
+
 
 def per_launch(d, counter, needle):
     for f in sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)):
-        vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(f))
-                if needle in r["Kernel_Name"] and r["Counter_Name"] == counter]
-        if vals:
-            return sum(vals) / len(vals), len(vals), f
+        rows = [r for r in csv.DictReader(open(f)) if needle in r["Kernel_Name"] and r["Counter_Name"] == counter]
+        if rows:
+            names = sorted({r["Kernel_Name"] for r in rows})
+            if len(names) != 1:
+                raise SystemExit(f"{needle} matches several kernels under {d}: {names}")
+            vals = [float(r["Counter_Value"]) for r in rows]
+            return sum(vals) / len(vals), len(vals), f, names[0]
     raise SystemExit(f"no {counter} rows for {needle} under {d}")
 
 
@@ -29,8 +34,10 @@ def main():
     out = sys.argv[5] if len(sys.argv) > 5 and sys.argv[5] != "-" else os.path.join(os.path.dirname(__file__), "..", "profiles",
                                                                "pmc_latest.json")
     needle = sys.argv[6] if len(sys.argv) > 6 else "k_reduce_vec"
-    fetch_kb, nf, ff = per_launch(fdir, "FETCH_SIZE", needle)
-    write_kb, nw, wf = per_launch(wdir, "WRITE_SIZE", needle)
+    fetch_kb, nf, ff, sym = per_launch(fdir, "FETCH_SIZE", needle)
+    write_kb, nw, wf, sym_w = per_launch(wdir, "WRITE_SIZE", needle)
+    if sym != sym_w:
+        raise SystemExit(f"the two passes measured different kernels: {sym!r} vs {sym_w!r}")
     read_b = fetch_kb * 1024 * 2
     write_b = write_kb * 1024
     try:
@@ -44,6 +51,9 @@ def main():
         "hbm_bytes_per_launch": read_b + write_b, "algorithmic_bytes_per_launch": alg,
         "traffic_over_algorithmic": (read_b + write_b) / alg, "launches": [nf, nw],
         "sources": [os.path.relpath(ff), os.path.relpath(wf)],
+        # provenance: bench.py reports this figure only for this symbol built from these sources
+        "kernel_symbol": sym, "kernel_sources": pmc_provenance.KERNEL_SOURCES[key],
+        "sources_sha256_16": pmc_provenance.sources_hash(key),
     }
     json.dump(d, open(out, "w"), indent=1)
     print(json.dumps(d["kernels"][key], indent=1))
