@@ -10,6 +10,29 @@ for p in (REPO, PKG_DIR, os.path.join(REPO, "oracle"), os.path.join(REPO, "tests
         sys.path.insert(0, p)
 
 
+_DURATIONS = []
+GPU_SUITE_BUDGET_S = 600  # the driver's -m gpu step is killed at 900 s; keep >= 30 % headroom
+
+
+def pytest_runtest_logreport(report):
+    if report.when == "call" or (report.when == "setup" and report.failed):
+        _DURATIONS.append((report.duration, report.nodeid))
+
+
+def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    """Per-test durations in the run's log, the slowest first, and the total against the GPU suite's
+    time budget."""
+    if not _DURATIONS:
+        return
+    total = sum(d for d, _ in _DURATIONS)
+    tr = terminalreporter
+    tr.write_sep("-", f"chiara test durations: {len(_DURATIONS)} tests, {total:.1f} s in calls")
+    for d, nodeid in sorted(_DURATIONS, reverse=True)[:15]:
+        tr.write_line(f"{d:8.2f}s  {nodeid}")
+    if getattr(config.option, "markexpr", "") == "gpu" and total > GPU_SUITE_BUDGET_S:
+        tr.write_line(f"WARNING: the GPU suite took {total:.0f} s, over its {GPU_SUITE_BUDGET_S} s budget")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu on the GPU box)")
     config.addinivalue_line("markers", "slow: larger CPU cases")

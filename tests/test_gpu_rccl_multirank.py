@@ -133,44 +133,54 @@ def test_rccl_world2_reduce_scatter_and_allreduce():
              ("ar", 2, 2, 1 << 14, "f32", True, 2)])
 
 
-def test_rccl_world8_c4_c5_geometries():
-    # 8 processes over RCCL's socket transport cost seconds per case on a loaded box; the (n, k, b)
-    # grid itself is covered bit-exact on the loopback transport (test_gpu_collectives.py goldens)
-    _run(8, [("ar", 4, 4, 8 * 4096, "bf16", False, 4), ("ar", 3, 4, 8 * 2048, "bf16", False, 2),
-             ("ar", 4, 8, 8 * 1024, "f32", False, 0), ("rs", 4, 4, 4000, "f32", False, 3)], timeout=600)
+# Every process session pays python + torch start-up and RCCL's socket bootstrap (~10-20 s at 8 ranks
+# on a loaded box), so the cases of one world size share one session (the suite's
+# time budget); the assertion message lists every failing (rank, mode, k, b, rc, ok).
+
+# C4/C5 geometries; the (n, k, b) grid itself is covered bit-exact on the loopback transport
+# (test_gpu_collectives.py goldens)
+W8_GEOMETRIES = [("ar", 4, 4, 8 * 4096, "bf16", False, 4), ("ar", 3, 4, 8 * 2048, "bf16", False, 2),
+                 ("ar", 4, 8, 8 * 1024, "f32", False, 0), ("rs", 4, 4, 4000, "f32", False, 3)]
+# testing/main.cpp's baselines over RCCL: non-power-of-two (fold/unfold) at 5 ranks, and 8 ranks
+MPICH_W5 = [("ring", 0, 0, 100003, "f32", False, 0), ("rd", 0, 0, 4099, "f32", False, 0),
+            ("rsag", 0, 0, 65537, "f32", True, 0), ("rx", 3, 0, 20000, "f32", False, 0),
+            ("rx", 2, 1, 777, "bf16", False, 0), ("krsag", 2, 0, 30011, "f32", False, 0),
+            ("rm", 2, 0, 4097, "f32", False, 0)]
+MPICH_W8 = MPICH_W5[:1] + [("rx", 4, 0, 1 << 14, "f32", False, 0), ("krsag", 2, 1, 1 << 14, "f32", False, 0),
+                           ("rm", 3, 0, 12345, "bf16", False, 0)]
+# testing/mpich_implementations/reduce_scatter/'s four baselines: 5 ranks (folds, recursive doubling's
+# relays) and 8, host-staged and device buffers
+RS_MPICH_W5 = [("rs_radix", 3, 0, 4099, "f32", False, 0), ("rs_halving", 0, 0, 1001, "f32", False, 0),
+               ("rs_doubling", 0, 0, 777, "bf16", False, 0), ("rs_pairwise", 0, 0, 3000, "f32", True, 0),
+               ("rs_radix", 2, 0, 64, "i32", True, 0)]
+RS_MPICH_W8 = [("rs_radix", 4, 0, 1 << 12, "f32", False, 0), ("rs_doubling", 0, 0, 5000, "f32", False, 0),
+               ("rs_halving", 0, 0, 4096, "bf16", True, 0)]
+ALLGATHER_W4 = [("ag", 2, 2, 1 << 16, "f32", False, 0), ("ag", 3, 4, 1001, "bf16", True, 0)]
+ALLGATHER_W8 = [("ag", 4, 4, 1 << 16, "f32", False, 0), ("ag", 8, 2, 4097, "i32", False, 0)]
+# the reference's own messages end to end (bcast + left-over k-Bruck at C4; k-nomial scatter for
+# reduce-scatter)
+EXACT_W8 = [("ar", 4, 4, 1 << 18, "f32", False, 0, 3, True), ("ar", 2, 8, 8 * 1001, "bf16", False, 0, 3, True),
+            ("ar", 2, 2, 1 << 16, "f32", True, 0, 3, False), ("rs", 4, 8, 1 << 14, "f32", False, 0, 3, True),
+            ("rs", 2, 4, 999, "f32", False, 0, 3, True)]
 
 
-def test_rccl_mpich_baselines_world5_and_8():
-    """testing/main.cpp's baselines over RCCL, non-power-of-two (fold/unfold) and 8 ranks."""
-    cases = [("ring", 0, 0, 100003, "f32", False, 0), ("rd", 0, 0, 4099, "f32", False, 0),
-             ("rsag", 0, 0, 65537, "f32", True, 0), ("rx", 3, 0, 20000, "f32", False, 0),
-             ("rx", 2, 1, 777, "bf16", False, 0), ("krsag", 2, 0, 30011, "f32", False, 0),
-             ("rm", 2, 0, 4097, "f32", False, 0)]
-    _run(5, cases)
-    _run(8, cases[:1] + [("rx", 4, 0, 1 << 14, "f32", False, 0), ("krsag", 2, 1, 1 << 14, "f32", False, 0),
-                         ("rm", 3, 0, 12345, "bf16", False, 0)], timeout=600)
+def test_rccl_world8_geometries_baselines_allgather_exact():
+    """8 ranks over RCCL, one session: C4/C5 geometries, the MPICH allreduce and reduce-scatter
+    baselines, allgather_radix_batch, and the exact schedule (the reference's messages): bit-exact
+    vs the oracle."""
+    _run(8, W8_GEOMETRIES + MPICH_W8 + RS_MPICH_W8 + ALLGATHER_W8 + EXACT_W8, timeout=800)
 
 
-def test_rccl_mpich_reduce_scatter_baselines_world5_and_8():
-    """testing/mpich_implementations/reduce_scatter/'s four baselines over RCCL: 5 ranks (folds,
-    recursive doubling's relays) and 8, host-staged and device buffers: bit-exact vs the oracle."""
-    cases = [("rs_radix", 3, 0, 4099, "f32", False, 0), ("rs_halving", 0, 0, 1001, "f32", False, 0),
-             ("rs_doubling", 0, 0, 777, "bf16", False, 0), ("rs_pairwise", 0, 0, 3000, "f32", True, 0),
-             ("rs_radix", 2, 0, 64, "i32", True, 0)]
-    _run(5, cases)
-    _run(8, [("rs_radix", 4, 0, 1 << 12, "f32", False, 0), ("rs_doubling", 0, 0, 5000, "f32", False, 0),
-             ("rs_halving", 0, 0, 4096, "bf16", True, 0)], timeout=600)
-
-
-def test_rccl_allgather_world4_and_8():
-    _run(4, [("ag", 2, 2, 1 << 16, "f32", False, 0), ("ag", 3, 4, 1001, "bf16", True, 0)])
-    _run(8, [("ag", 4, 4, 1 << 16, "f32", False, 0), ("ag", 8, 2, 4097, "i32", False, 0)], timeout=600)
+def test_rccl_world5_mpich_baselines():
+    """The MPICH allreduce and reduce-scatter baselines at 5 ranks (non-power-of-two folds), one session."""
+    _run(5, MPICH_W5 + RS_MPICH_W5)
 
 
 def test_rccl_schedules_and_overlap_world4():
     """The two-stream executor (overlap on/off) under all six schedules, allreduce and
-    reduce-scatter, 4 ranks over RCCL: bit-exact vs the oracle."""
-    cases = []
+    reduce-scatter, 4 ranks over RCCL (and allgather_radix_batch in the same session): bit-exact vs
+    the oracle."""
+    cases = list(ALLGATHER_W4)
     for sched in (0, 1, 2, 3, 4, 5):
         for ov in (True, False):
             cases.append(("ar", 4, 4, 1 << 18, "f32", False, 4, sched, ov))
@@ -190,14 +200,6 @@ def test_rccl_auto_schedule_world4():
              ("rs", 2, 2, 1 << 15, "f32", False, 0, A, True), ("rs", 4, 4, 4000, "f32", False, 0, A, True, True),
              ("ar", 4, 4, 1 << 14, "f32", True, 0, A, True), ("ar", 2, 4, 8 * 1001, "bf16", False, 3, A, False)]
     _run(4, cases, timeout=600)
-
-
-def test_rccl_exact_schedule_world8():
-    """The reference's own messages end to end (bcast + left-over k-Bruck at C4; k-nomial
-    scatter for reduce-scatter), 8 ranks over RCCL: bit-exact vs the oracle."""
-    _run(8, [("ar", 4, 4, 1 << 18, "f32", False, 0, 3, True), ("ar", 2, 8, 8 * 1001, "bf16", False, 0, 3, True),
-             ("ar", 2, 2, 1 << 16, "f32", True, 0, 3, False), ("rs", 4, 8, 1 << 14, "f32", False, 0, 3, True),
-             ("rs", 2, 4, 999, "f32", False, 0, 3, True)], timeout=600)
 
 
 def _phase_worker(rank, world, port, q):
