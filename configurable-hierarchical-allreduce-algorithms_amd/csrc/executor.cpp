@@ -14,6 +14,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <cctype>
 #include <chrono>
 #include <condition_variable>
@@ -89,6 +90,10 @@ int nccl_code(ncclResult_t r) {
 // launch stream around each reduction, summed when read.
 struct ReduceProfile {
     bool on = false;
+    // span: the caller brackets whole phases with events (record_span) and the launches only add
+    // their algorithmic bytes and count -- the local group's mode, whose launches may run on two
+    // streams at once
+    bool span = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, spare;
     double ms = 0, bytes = 0;
     long launches = 0;
@@ -151,7 +156,8 @@ int run_local(const chr::LocalOp& op, const Bufs& B, int dtype, int rop, hipStre
     std::vector<const void*> ins;
     if (tree) ins.push_back(B.ptr(op.acc));  // leaf 0
     for (const chr::Ref& r : op.ins) ins.push_back(B.ptr(r));
-    const bool timed = prof && prof->on && !ins.empty();
+    const bool counted = prof && prof->on && !ins.empty();
+    const bool timed = counted && !prof->span;
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     if (timed) {
         ev = prof->take();
@@ -165,6 +171,8 @@ int run_local(const chr::LocalOp& op, const Bufs& B, int dtype, int rop, hipStre
     if (timed) {
         (void)hipEventRecord(ev.second, s);
         prof->pending.push_back(ev);
+    }
+    if (counted) {
         // algorithmic bytes: every operand read once, the result written once
         prof->bytes += (double)(ins.size() + (tree ? 1 : 2)) * op.count * B.es;
         prof->launches += 1;
@@ -175,20 +183,23 @@ int run_local(const chr::LocalOp& op, const Bufs& B, int dtype, int rop, hipStre
 // Consecutive L_TREE ops of one step (the flat schedule's chunks of one pipeline slice) run as ONE
 // batched launch when none writes what another reads or writes (an op's own in-place root over
 // its own leaf is element-wise and fine): fewer grid fills and drains per call
-// (launch_reduce_tree_multi).  Anything else runs op by op.
-bool overlaps(const chr::Ref& x, uint64_t xn, const chr::Ref& y, uint64_t yn) {
-    return x.buf == y.buf && x.off < y.off + yn && y.off < x.off + xn;
+// (launch_reduce_tree_multi).  Anything else runs op by op.  Overlap is decided on the resolved
+// byte ranges, not on (buffer, offset): under CHR_IN_PLACE the SEND and RECV buffers are one.
+bool overlaps(const Bufs& B, const chr::Ref& x, uint64_t xn, const chr::Ref& y, uint64_t yn) {
+    const char* px = B.ptr(x);
+    const char* py = B.ptr(y);
+    return px < py + yn * B.es && py < px + xn * B.es;
 }
 
-bool batchable(const std::vector<chr::LocalOp>& ops, size_t i0, size_t i1) {
+bool batchable(const std::vector<chr::LocalOp>& ops, size_t i0, size_t i1, const Bufs& B) {
     for (size_t i = i0; i < i1; ++i)
         for (size_t j = i0; j < i1; ++j) {
             if (i == j) continue;
             const chr::LocalOp& w = ops[i];
             const chr::LocalOp& r = ops[j];
-            if (overlaps(w.dst, w.count, r.dst, r.count) || overlaps(w.dst, w.count, r.acc, r.count)) return false;
+            if (overlaps(B, w.dst, w.count, r.dst, r.count) || overlaps(B, w.dst, w.count, r.acc, r.count)) return false;
             for (const chr::Ref& x : r.ins)
-                if (overlaps(w.dst, w.count, x, r.count)) return false;
+                if (overlaps(B, w.dst, w.count, x, r.count)) return false;
         }
     return true;
 }
@@ -212,7 +223,8 @@ int run_tree_batch(const std::vector<chr::LocalOp>& ops, size_t i0, size_t i1, c
         bytes += (double)(jb.nl + 1) * op.count * B.es;
     }
     if (jobs.empty()) return CHR_SUCCESS;
-    const bool timed = prof && prof->on;
+    const bool counted = prof && prof->on;
+    const bool timed = counted && !prof->span;
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     if (timed) {
         ev = prof->take();
@@ -222,6 +234,8 @@ int run_tree_batch(const std::vector<chr::LocalOp>& ops, size_t i0, size_t i1, c
     if (timed) {
         (void)hipEventRecord(ev.second, s);
         prof->pending.push_back(ev);
+    }
+    if (counted) {
         prof->bytes += bytes;
         prof->launches += 1;
     }
@@ -233,7 +247,7 @@ int run_locals(const std::vector<chr::LocalOp>& ops, const Bufs& B, int dtype, i
     for (size_t i = 0; i < ops.size();) {
         size_t j = i;
         while (j < ops.size() && ops[j].kind == chr::L_TREE && ops[j].ins.size() + 1 <= 8) ++j;
-        if (j - i >= 2 && batchable(ops, i, j)) {
+        if (j - i >= 2 && batchable(ops, i, j, B)) {
             if (int rc = run_tree_batch(ops, i, j, B, dtype, rop, s, prof)) return rc;
             i = j;
             continue;
@@ -263,6 +277,20 @@ int default_overlap() {
     static const int v = [] {
         const char* e = std::getenv("CHR_OVERLAP");
         return e ? (std::atoi(e) != 0) : 1;
+    }();
+    return v;
+}
+
+// CHR_DUAL_COMPUTE=1: local ops spread over two compute streams; default 0 (one).  Measured on the
+// local group's C4/C5 calls (whole-phase spans, 2 alternating rounds, profiles/r03/ab_dual/): one
+// stream 0.747-0.751 (C4) / 0.727-0.728 (C5) of the HBM peak, two streams 0.646-0.663 / 0.665-0.672:
+// two tree launches streaming 18 operands at once lose more HBM efficiency than the overlapped
+// ramp-up and drain win back, while back-to-back launches on one stream already overlap their
+// tails (no event between them).
+int default_dual() {
+    static const int v = [] {
+        const char* e = std::getenv("CHR_DUAL_COMPUTE");
+        return e ? (std::atoi(e) != 0) : 0;
     }();
     return v;
 }
@@ -353,6 +381,19 @@ struct chr_comm {
     ncclComm_t nccl = nullptr;
     hipStream_t stream = nullptr;   // RCCL transfers; the call completes on this stream
     hipStream_t cstream = nullptr;  // local ops (reductions, copies) when overlapping
+    // A second compute stream (CHR_DUAL_COMPUTE=1, default off; created on first use): consecutive
+    // steps' local ops alternate between cstream and cstream2, so when two slices' evaluations are
+    // ready at once one launch's ramp-up could overlap the other's drain (measured a loss on one GPU:
+    // default_dual).  Not used by the pipelined host
+    // windows, which already run four streams (transfers, compute, copy-in, copy-out: the box's
+    // GPU_MAX_HW_QUEUES is 4, and a fifth stream would share a hardware queue with one of them), nor
+    // inside captured graphs (launch_graph).
+    hipStream_t cstream2 = nullptr;
+    int dual = default_dual();
+    hipError_t compute2() {
+        if (cstream2) return hipSuccess;
+        return hipStreamCreateWithFlags(&cstream2, hipStreamDefault);
+    }
     std::vector<hipEvent_t> events;  // pool: 2 per step
     hipEvent_t event(size_t i) {
         while (events.size() <= i) {
@@ -447,7 +488,14 @@ struct chr_comm {
 
 struct chr_local_group {
     int nranks = 0, device = 0;
-    ReduceProfile prof;  // chr_local_group_profile: every rank's fused reductions, HIP events
+    // chr_local_group_profile: the fused reductions of every rank, timed as whole phases (from the
+    // end of a step's copies to the join of its reductions) with HIP events on the group's stream
+    ReduceProfile prof;
+    // The virtual ranks' local ops of one step are independent (each rank's own buffers): with
+    // CHR_DUAL_COMPUTE=1 they alternate between two compute streams, joined back into `stream` before
+    // the next step's copies; by default they run on `stream` (default_dual).
+    hipStream_t cs[2] = {nullptr, nullptr};
+    hipEvent_t ev_copy = nullptr, ev_done[2] = {nullptr, nullptr};
     int slices = 0;  // 0 = auto
     int sched = default_schedule() == CHR_SCHEDULE_AUTO ? (int)chr::SCHED_FLAT : default_schedule();  // no tuning
     hipStream_t stream = nullptr;
@@ -457,36 +505,56 @@ struct chr_local_group {
 
 namespace {
 
-int enqueue_plan(chr_comm* c, const Plan& p, const void* send, void* recv, int dtype, int op, bool* posted);
+int enqueue_plan(chr_comm* c, const Plan& p, const void* send, void* recv, int dtype, int op, bool* posted,
+                 bool allow_dual);
 
 // Enqueues a whole plan.  A failure after the first RCCL operation was posted aborts the
 // communicator: peers may already be waiting on this rank's messages.
-int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int dtype, int op) {
+int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int dtype, int op, bool allow_dual = true) {
     if (c->failed) return CHR_ERR_ABORTED;
     bool posted = false;
-    const int rc = enqueue_plan(c, p, send, recv, dtype, op, &posted);
+    const int rc = enqueue_plan(c, p, send, recv, dtype, op, &posted, allow_dual);
     if (rc && posted) c->abort_comm();
     return rc;
 }
 
-int enqueue_plan(chr_comm* c, const Plan& p, const void* send, void* recv, int dtype, int op, bool* posted) {
+int enqueue_plan(chr_comm* c, const Plan& p, const void* send, void* recv, int dtype, int op, bool* posted,
+                 bool allow_dual) {
     const size_t es = chr::dtype_size(dtype);
     hipError_t e = c->reserve_scratch(p.acc_elems * es, p.stage_elems * es);
     if (e != hipSuccess) return hip_code(e);
     Bufs B{(const char*)send, (char*)recv, (char*)c->acc.p, (char*)c->stage.p, es};
     int rc;
     if ((rc = run_locals(p.pre, B, dtype, op, c->stream, &c->prof))) return rc;
-    // Two streams: transfers on c->stream, local ops on c->cstream.  A step's transfers wait
-    // only for the local ops of step comm_wait (schedule.cpp analyze_deps); local ops wait
-    // for their own step's transfers.  The call ends with c->stream waiting for the last ops.
+    // Transfers on c->stream, local ops on c->cstream (and c->cstream2: consecutive local steps
+    // alternate).  A step's transfers wait for the local ops of its comm_deps, a step's local ops for
+    // its own transfers and its local_deps (schedule.cpp analyze_deps): per compute stream, only the
+    // latest such step on it needs an event wait, since each stream runs in order.  The call ends
+    // with c->stream waiting for the last ops of each compute stream.
     const bool two = c->overlap && c->cstream;
-    int waited = -1, last_comp = -1;
+    hipStream_t cs[2] = {c->cstream, nullptr};
+    if (two && allow_dual && c->dual && c->nranks > 1) {
+        if (hipError_t e2 = c->compute2(); e2 != hipSuccess) return hip_code(e2);
+        cs[1] = c->cstream2;
+    }
+    const int ncs = cs[1] ? 2 : 1;
+    std::vector<int8_t> on(p.steps.size(), -1);  // compute stream that ran each step's local ops
+    int xfer_waited[2] = {-1, -1}, last_on[2] = {-1, -1}, nlocal = 0;
+    std::vector<std::array<int, 2>> local_waited(ncs, std::array<int, 2>{-1, -1});
+    auto latest_on = [&](const std::vector<int>& deps, int k) {
+        for (size_t i = deps.size(); i-- > 0;)
+            if (on[(size_t)deps[i]] == k) return deps[i];
+        return -1;
+    };
     for (size_t t = 0; t < p.steps.size(); ++t) {
         const chr::Step& s = p.steps[t];
-        if (two && s.comm_wait > waited) {
-            hipEvent_t e = c->event(2 * (size_t)s.comm_wait + 1);
-            if (!e || (rc = hip_code(hipStreamWaitEvent(c->stream, e, 0)))) return e ? rc : CHR_ERR_HIP;
-            waited = s.comm_wait;
+        for (int k = 0; two && k < ncs; ++k) {
+            const int d = latest_on(s.comm_deps, k);
+            if (d > xfer_waited[k]) {
+                hipEvent_t e = c->event(2 * (size_t)d + 1);
+                if (!e || (rc = hip_code(hipStreamWaitEvent(c->stream, e, 0)))) return e ? rc : CHR_ERR_HIP;
+                xfer_waited[k] = d;
+            }
         }
         const bool xfers = !s.sends.empty() || !s.recvs.empty() || !s.allgathers.empty();
         const bool timed = c->prof.on && xfers;
@@ -533,20 +601,33 @@ int enqueue_plan(chr_comm* c, const Plan& p, const void* send, void* recv, int d
         }
         hipEvent_t ec = c->event(2 * t), ed = c->event(2 * t + 1);
         if (!ec || !ed) return CHR_ERR_HIP;
-        if ((rc = hip_code(hipEventRecord(ec, c->stream))) || (rc = hip_code(hipStreamWaitEvent(c->cstream, ec, 0))))
+        const int k = nlocal++ % ncs;
+        hipStream_t cst = cs[k];
+        if ((rc = hip_code(hipEventRecord(ec, c->stream))) || (rc = hip_code(hipStreamWaitEvent(cst, ec, 0))))
             return rc;
+        for (int k2 = 0; k2 < ncs; ++k2) {  // the other compute stream's conflicting local ops
+            if (k2 == k) continue;
+            const int d = latest_on(s.local_deps, k2);
+            if (d > local_waited[k][k2]) {
+                hipEvent_t e = c->event(2 * (size_t)d + 1);
+                if (!e || (rc = hip_code(hipStreamWaitEvent(cst, e, 0)))) return e ? rc : CHR_ERR_HIP;
+                local_waited[k][k2] = d;
+            }
+        }
         {
             // RCCL's kernels run beside these launches: streaming reductions leave them room on every
             // CU (reduce_common.hpp kCoresidentWgPerCu)
             chr::CoresidentScope beside_rccl(c->nranks > 1);
-            if ((rc = run_locals(s.post, B, dtype, op, c->cstream, &c->prof))) return rc;
+            if ((rc = run_locals(s.post, B, dtype, op, cst, &c->prof))) return rc;
         }
-        if ((rc = hip_code(hipEventRecord(ed, c->cstream)))) return rc;
-        last_comp = (int)t;
+        if ((rc = hip_code(hipEventRecord(ed, cst)))) return rc;
+        on[t] = (int8_t)k;
+        last_on[k] = (int)t;
     }
-    if (two && last_comp > waited) {
-        if ((rc = hip_code(hipStreamWaitEvent(c->stream, c->event(2 * (size_t)last_comp + 1), 0)))) return rc;
-    }
+    for (int k = 0; two && k < ncs; ++k)
+        if (last_on[k] > xfer_waited[k] &&
+            (rc = hip_code(hipStreamWaitEvent(c->stream, c->event(2 * (size_t)last_on[k] + 1), 0))))
+            return rc;
     return CHR_SUCCESS;
 }
 
@@ -565,7 +646,9 @@ int launch_graph(chr_comm* c, const Plan& p, const void* send, void* recv, int d
     if (it == c->gexec.end()) {
         if (!c->event(2 * p.steps.size() + 1)) return CHR_ERR_HIP;  // the event pool, created outside the capture
         if ((e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal)) != hipSuccess) return hip_code(e);
-        const int rc = enqueue_rccl(c, p, send, recv, dtype, op);
+        // one compute stream in a graph: graphs serve small, latency-bound calls, and a replay of a
+        // capture forked over two compute streams hung on the test box (4 RCCL ranks sharing one GPU)
+        const int rc = enqueue_rccl(c, p, send, recv, dtype, op, /*allow_dual=*/false);
         hipGraph_t g = nullptr;
         e = hipStreamEndCapture(c->stream, &g);
         if (rc || e != hipSuccess) {
@@ -618,8 +701,49 @@ int wait_call(chr_comm* c) {
             c->abort_comm();  // RCCL kernels poll the abort flag and exit
             (void)hipStreamSynchronize(c->stream);
             (void)hipStreamSynchronize(c->cstream);
+            if (c->cstream2) (void)hipStreamSynchronize(c->cstream2);
             return CHR_ERR_TIMEOUT;
         }
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
+// wait_call for one event (the main thread: may abort the communicator).  Used before a copy to or
+// from pageable host memory that depends on a collective: such a copy returns only once HIP has
+// staged it, so issued first it would block inside HIP -- beyond the timeout -- if a peer is lost.
+int wait_event(chr_comm* c, hipEvent_t ev) {
+    if (c->timeout_ms <= 0) return CHR_SUCCESS;  // no timeout: let the copy itself wait, as before
+    using clk = std::chrono::steady_clock;
+    const auto limit = clk::now() + std::chrono::milliseconds(c->timeout_ms);
+    for (int spin = 0;; ++spin) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) return CHR_SUCCESS;
+        if (q != hipErrorNotReady) return hip_code(q);
+        ncclResult_t ae = ncclSuccess;
+        if (spin % 64 == 0 && c->nccl && ncclCommGetAsyncError(c->nccl, &ae) == ncclSuccess && ae != ncclSuccess &&
+            ae != ncclInProgress) {
+            c->abort_comm();
+            return CHR_ERR_RCCL;
+        }
+        if (clk::now() >= limit) {
+            c->abort_comm();
+            return CHR_ERR_TIMEOUT;
+        }
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
+// The copy-out thread's wait for an event under the communicator's timeout.  It never touches the
+// RCCL communicator (the issuing thread owns it and does any abort): it reports CHR_ERR_TIMEOUT.
+int wait_event_poll(hipEvent_t ev, int timeout_ms) {
+    if (timeout_ms <= 0) return CHR_SUCCESS;
+    using clk = std::chrono::steady_clock;
+    const auto limit = clk::now() + std::chrono::milliseconds(timeout_ms);
+    for (int spin = 0;; ++spin) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) return CHR_SUCCESS;
+        if (q != hipErrorNotReady) return hip_code(q);
+        if (clk::now() >= limit) return CHR_ERR_TIMEOUT;
         if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
 }
@@ -653,6 +777,8 @@ int run_host_windows(chr_comm* c, int sched, int slices, int mode, const void* i
     if (w == 0 || w >= block) return -1;
     hipError_t e = c->host_pipeline_init();
     if (e != hipSuccess) return hip_code(e);
+    int rc;
+    if ((rc = wait_call(c))) return rc;  // earlier _async work, under the timeout
     const size_t out_rows = mode == chr::MODE_ALLREDUCE ? n : 1;
     for (int i = 0; i < 2; ++i) {
         if ((e = c->wsend[i].reserve(n * w * es, c->stream)) != hipSuccess) return hip_code(e);
@@ -661,13 +787,14 @@ int run_host_windows(chr_comm* c, int sched, int slices, int mode, const void* i
     const char* hsrc = (const char*)input;
     char* hdst = (char*)recv;
     const size_t nwin = (block + w - 1) / w;
+    const int timeout_ms = c->timeout_ms;
 
     std::mutex mu;
     std::condition_variable cv;
     size_t coll_enqueued = 0, out_enqueued = 0;  // windows handed over, under mu
     bool stop = false;                           // the issuing thread failed: copy-out ends
     int out_rc = CHR_SUCCESS;                    // the copy-out thread's first error
-    std::thread copy_out([&] {
+    auto copy_out_loop = [&] {
         if (hipSetDevice(c->device) != hipSuccess) {
             std::lock_guard<std::mutex> g(mu);
             out_rc = CHR_ERR_HIP;
@@ -682,60 +809,97 @@ int run_host_windows(chr_comm* c, int sched, int slices, int mode, const void* i
             }
             const int i = (int)(j & 1);
             const size_t off = j * w, wj = std::min(w, block - off);
-            hipError_t ee = hipStreamWaitEvent(c->hout, c->ev_coll[i], 0);
-            if (ee == hipSuccess)
+            // with a timeout, the collective first: a pageable copy would block inside HIP
+            int wrc = wait_event_poll(c->ev_coll[i], timeout_ms);
+            hipError_t ee = hipSuccess;
+            if (!wrc) ee = hipStreamWaitEvent(c->hout, c->ev_coll[i], 0);
+            if (!wrc && ee == hipSuccess)
                 ee = hipMemcpy2DAsync(hdst + off * es, block * es, c->wrecv[i].p, wj * es, wj * es, out_rows,
-                                      hipMemcpyDeviceToHost, c->hout);
-            if (ee == hipSuccess) ee = hipEventRecord(c->ev_out[i], c->hout);
+                                      hipMemcpyDefault, c->hout);
+            if (!wrc && ee == hipSuccess) ee = hipEventRecord(c->ev_out[i], c->hout);
             std::lock_guard<std::mutex> g(mu);
-            if (ee != hipSuccess) {
-                out_rc = hip_code(ee);
+            if (wrc || ee != hipSuccess) {
+                out_rc = wrc ? wrc : hip_code(ee);
                 cv.notify_all();
                 return;
             }
             out_enqueued = j + 1;
             cv.notify_all();
         }
-    });
+    };
+    // The copy-out side runs on a second host thread; if one cannot be started, it runs after the
+    // issuing loop on this one (no overlap of the two PCIe directions, same bits) -- no exception
+    // crosses the C ABI.
+    std::thread copy_out;
+    try {
+        copy_out = std::thread(copy_out_loop);
+    } catch (const std::exception&) {
+        copy_out = std::thread();
+    }
+    const bool threaded = copy_out.joinable();
     auto issue = [&]() -> int {
         for (size_t j = 0; j < nwin; ++j) {
             const int i = (int)(j & 1);
             const size_t off = j * w, wj = std::min(w, block - off);
             // window j reuses window j-2's buffers: its copy-in waits for j-2's collective, and
             // the collective for j-2's copy-out, once the copy-out thread has enqueued it
-            if (j >= 2 && (e = hipStreamWaitEvent(c->hin, c->ev_coll[i], 0)) != hipSuccess) return hip_code(e);
-            if ((e = hipMemcpy2DAsync(c->wsend[i].p, wj * es, hsrc + off * es, block * es, wj * es, n,
-                                      hipMemcpyHostToDevice, c->hin)) != hipSuccess)
+            if (j >= 2) {
+                int r2;
+                if ((r2 = wait_event(c, c->ev_coll[i]))) return r2;  // with a timeout: before the pageable copy
+                if ((e = hipStreamWaitEvent(c->hin, c->ev_coll[i], 0)) != hipSuccess) return hip_code(e);
+            }
+            if ((e = hipMemcpy2DAsync(c->wsend[i].p, wj * es, hsrc + off * es, block * es, wj * es, n, hipMemcpyDefault,
+                                      c->hin)) != hipSuccess)
                 return hip_code(e);
             if ((e = hipEventRecord(c->ev_in[i], c->hin)) != hipSuccess) return hip_code(e);
             if ((e = hipStreamWaitEvent(c->stream, c->ev_in[i], 0)) != hipSuccess) return hip_code(e);
             if (j >= 2) {
-                std::unique_lock<std::mutex> g(mu);
-                cv.wait(g, [&] { return out_rc != CHR_SUCCESS || out_enqueued >= j - 1; });
-                if (out_rc != CHR_SUCCESS) return out_rc;
+                if (threaded) {
+                    std::unique_lock<std::mutex> g(mu);
+                    auto ready = [&] { return out_rc != CHR_SUCCESS || out_enqueued >= j - 1; };
+                    if (timeout_ms > 0) {
+                        // the copy-out thread gives up after the same timeout; this is the backstop
+                        if (!cv.wait_for(g, std::chrono::milliseconds(2 * (int64_t)timeout_ms + 1000), ready))
+                            return CHR_ERR_TIMEOUT;
+                    } else {
+                        cv.wait(g, ready);
+                    }
+                    if (out_rc != CHR_SUCCESS) return out_rc;
+                }
                 if ((e = hipStreamWaitEvent(c->stream, c->ev_out[i], 0)) != hipSuccess) return hip_code(e);
             }
             const Plan& p = c->plan(mode, k, b, mode == chr::MODE_ALLREDUCE ? n * wj : wj, es, sched, slices);
             if (p.error) return p.error;
-            int rc = enqueue_rccl(c, p, c->wsend[i].p, c->wrecv[i].p, dtype, op);
-            if (rc) return rc;
+            int r = enqueue_rccl(c, p, c->wsend[i].p, c->wrecv[i].p, dtype, op, /*allow_dual=*/false);
+            if (r) return r;
             if ((e = hipEventRecord(c->ev_coll[i], c->stream)) != hipSuccess) return hip_code(e);
+            if (!threaded) {  // this thread copies window j out itself
+                if ((r = wait_event(c, c->ev_coll[i]))) return r;
+                if ((e = hipStreamWaitEvent(c->hout, c->ev_coll[i], 0)) != hipSuccess ||
+                    (e = hipMemcpy2DAsync(hdst + off * es, block * es, c->wrecv[i].p, wj * es, wj * es, out_rows,
+                                          hipMemcpyDefault, c->hout)) != hipSuccess ||
+                    (e = hipEventRecord(c->ev_out[i], c->hout)) != hipSuccess)
+                    return hip_code(e);
+                continue;
+            }
             std::lock_guard<std::mutex> g(mu);
             coll_enqueued = j + 1;
             cv.notify_all();
         }
         return CHR_SUCCESS;
     };
-    int rc = issue();
+    rc = issue();
     if (rc) {
+        if (!c->failed && (rc == CHR_ERR_TIMEOUT || rc == CHR_ERR_RCCL)) c->abort_comm();  // peers may be posted
         std::lock_guard<std::mutex> g(mu);
         stop = true;
         cv.notify_all();
     }
     if (!rc) rc = wait_call(c);  // the last collective, under the communicator's timeout
-    copy_out.join();
+    if (threaded) copy_out.join();
     const int rc_out = hip_code(hipStreamSynchronize(c->hout));
     if (rc) return rc;
+    if (out_rc && !c->failed) c->abort_comm();  // the copy-out side timed out: peers may still be posted
     return out_rc ? out_rc : rc_out;
 }
 
@@ -754,6 +918,14 @@ int run_collective(chr_comm* c, int sched, int slices, int mode, const void* sen
     hipError_t e = hipSetDevice(c->device);
     if (e != hipSuccess) return hip_code(e);
     const bool dev_in = is_device_ptr(input), dev_out = is_device_ptr(recv);
+    // Pipelined staging splits a call into window collectives.  Whether it does is a function of the
+    // communicator's setting and the call's arguments only -- never of where this rank's buffers
+    // live -- so every rank issues the same number of RCCL collectives even when one passes host
+    // memory and another device memory (device buffers are then staged device to device).
+    if (sync) {
+        const int rc = run_host_windows(c, sched, slices, mode, input, recv, count, dtype, op, k, b);
+        if (rc >= 0) return rc;
+    }
     if (dev_in && dev_out) {
         int rc = c->graphs && !c->prof.on ? launch_graph(c, p, input, recv, dtype, op)
                                           : enqueue_rccl(c, p, input, recv, dtype, op);
@@ -761,13 +933,13 @@ int run_collective(chr_comm* c, int sched, int slices, int mode, const void* sen
         return wait_call(c);
     }
     if (!sync) return CHR_ERR_UNSUPPORTED;  // async needs device-resident buffers
-    if (!dev_in && !dev_out) {
-        const int rc = run_host_windows(c, sched, slices, mode, input, recv, count, dtype, op, k, b);
-        if (rc >= 0) return rc;
-    }
-    // Host-memory contract of the reference: stage through HBM (PCIe H2D / D2H).
+    // Host-memory contract of the reference: stage through HBM (PCIe H2D / D2H).  With a timeout
+    // set, every copy to or from pageable memory is issued only after what it depends on has
+    // completed (wait_call), since such a copy blocks inside HIP until it is staged.
     const void* dsend = input;
     void* drecv = recv;
+    int rc;
+    if ((rc = wait_call(c))) return rc;  // earlier _async work
     if (!dev_in) {
         if ((e = c->hsend.reserve(p.send_elems * es, c->stream)) != hipSuccess) return hip_code(e);
         if ((e = hipMemcpyAsync(c->hsend.p, input, p.send_elems * es, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
@@ -778,11 +950,13 @@ int run_collective(chr_comm* c, int sched, int slices, int mode, const void* sen
         if ((e = c->hrecv.reserve(p.recv_elems * es, c->stream)) != hipSuccess) return hip_code(e);
         drecv = c->hrecv.p;
     }
-    int rc = enqueue_rccl(c, p, dsend, drecv, dtype, op);
+    rc = enqueue_rccl(c, p, dsend, drecv, dtype, op);
     if (rc) return rc;
-    if (!dev_out &&
-        (e = hipMemcpyAsync(recv, drecv, p.recv_elems * es, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
-        return hip_code(e);
+    if (!dev_out) {
+        if (c->timeout_ms > 0 && (rc = wait_call(c))) return rc;  // the collective, under the timeout
+        if ((e = hipMemcpyAsync(recv, drecv, p.recv_elems * es, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+            return hip_code(e);
+    }
     return wait_call(c);
 }
 
@@ -960,8 +1134,39 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
         B[r] = Bufs{(const char*)in, (char*)recvs[r], (char*)g->acc[r].p, (char*)g->stage[r].p, es};
     }
     int rc;
-    for (int r = 0; r < n; ++r)
-        if ((rc = run_locals(P[r].pre, B[r], dtype, op, g->stream, &g->prof))) return rc;
+    // One phase of local ops of all ranks: on the two compute streams when the group has them, joined
+    // back into the group's stream; while profiling, bracketed by events on the group's stream.
+    const bool dual = g->cs[0] && g->cs[1];
+    auto phase = [&](auto&& ops_of) -> int {
+        bool any = false;
+        for (int r = 0; r < n && !any; ++r) any = !ops_of(r).empty();
+        if (!any) return CHR_SUCCESS;
+        std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+        if (g->prof.on) {
+            ev = g->prof.take();
+            if ((rc = hip_code(hipEventRecord(ev.first, g->stream)))) return rc;
+        }
+        if (!dual) {
+            for (int r = 0; r < n; ++r)
+                if ((rc = run_locals(ops_of(r), B[r], dtype, op, g->stream, &g->prof))) return rc;
+        } else {
+            if ((rc = hip_code(hipEventRecord(g->ev_copy, g->stream)))) return rc;
+            for (int k = 0; k < 2; ++k)
+                if ((rc = hip_code(hipStreamWaitEvent(g->cs[k], g->ev_copy, 0)))) return rc;
+            for (int r = 0; r < n; ++r)
+                if ((rc = run_locals(ops_of(r), B[r], dtype, op, g->cs[r & 1], &g->prof))) return rc;
+            for (int k = 0; k < 2; ++k)
+                if ((rc = hip_code(hipEventRecord(g->ev_done[k], g->cs[k]))) ||
+                    (rc = hip_code(hipStreamWaitEvent(g->stream, g->ev_done[k], 0))))
+                    return rc;
+        }
+        if (g->prof.on) {
+            if ((rc = hip_code(hipEventRecord(ev.second, g->stream)))) return rc;
+            g->prof.pending.push_back(ev);
+        }
+        return CHR_SUCCESS;
+    };
+    if ((rc = phase([&](int r) -> const std::vector<chr::LocalOp>& { return P[r].pre; }))) return rc;
     const size_t nsteps = P[0].steps.size();
     for (size_t si = 0; si < nsteps; ++si) {
         // Loopback transport: each receive takes the next unmatched send of its peer to
@@ -1001,8 +1206,8 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
                                             x.count * es, hipMemcpyDeviceToDevice, g->stream)) != hipSuccess)
                         return hip_code(e);
                 }
-        for (int r = 0; r < n; ++r)
-            if ((rc = run_locals(P[r].steps[si].post, B[r], dtype, op, g->stream, &g->prof))) return rc;
+        if ((rc = phase([&](int r) -> const std::vector<chr::LocalOp>& { return P[r].steps[si].post; })))
+            return rc;
     }
     return hip_code(hipStreamSynchronize(g->stream));
 }
@@ -1069,8 +1274,10 @@ int chr_comm_destroy(chr_comm* c) {
     c->hrecv.release();
     c->host_pipeline_release();
     if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+    if (c->cstream2) (void)hipStreamSynchronize(c->cstream2);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
+    if (c->cstream2) (void)hipStreamDestroy(c->cstream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return CHR_SUCCESS;
@@ -1100,6 +1307,7 @@ int chr_comm_abort(chr_comm* c) {
     c->abort_comm();
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+    if (c->cstream2) (void)hipStreamSynchronize(c->cstream2);
     return CHR_SUCCESS;
 }
 
@@ -1245,9 +1453,20 @@ int chr_local_group_create(chr_local_group** out, int nranks, int device) {
     g->device = device;
     g->acc.resize(nranks);
     g->stage.resize(nranks);
+    g->prof.span = true;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&g->stream, hipStreamDefault);
-    if (e != hipSuccess) return hip_code(e);
+    if (e == hipSuccess && default_dual()) {
+        for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+            e = hipStreamCreateWithFlags(&g->cs[k], hipStreamNonBlocking);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&g->ev_done[k], hipEventDisableTiming);
+        }
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&g->ev_copy, hipEventDisableTiming);
+    }
+    if (e != hipSuccess) {
+        chr_local_group_destroy(g.release());
+        return hip_code(e);
+    }
     *out = g.release();
     return CHR_SUCCESS;
 }
@@ -1278,9 +1497,16 @@ int chr_local_group_destroy(chr_local_group* g) {
     if (!g) return CHR_SUCCESS;
     (void)hipSetDevice(g->device);
     if (g->stream) (void)hipStreamSynchronize(g->stream);
+    for (int k = 0; k < 2; ++k)
+        if (g->cs[k]) (void)hipStreamSynchronize(g->cs[k]);
     g->prof.release();
     for (auto& d : g->acc) d.release();
     for (auto& d : g->stage) d.release();
+    for (int k = 0; k < 2; ++k) {
+        if (g->ev_done[k]) (void)hipEventDestroy(g->ev_done[k]);
+        if (g->cs[k]) (void)hipStreamDestroy(g->cs[k]);
+    }
+    if (g->ev_copy) (void)hipEventDestroy(g->ev_copy);
     if (g->stream) (void)hipStreamDestroy(g->stream);
     delete g;
     return CHR_SUCCESS;

@@ -188,7 +188,7 @@ struct Ctx {
     MPI_Op bf16_sum = MPI_OP_NULL;
 };
 
-inline int init(Ctx* c) {
+inline int init(Ctx* c, const Options& o) {
     MPI_Comm_rank(MPI_COMM_WORLD, &c->rank);
     MPI_Comm_size(MPI_COMM_WORLD, &c->nprocs);
     MPI_Comm local;
@@ -206,8 +206,10 @@ inline int init(Ctx* c) {
     if (c->rank == 0 && chr_get_unique_id(&id) != CHR_SUCCESS) return CHR_ERR_RCCL;
     MPI_Bcast(&id, sizeof(id), MPI_BYTE, 0, MPI_COMM_WORLD);
     int rc = chr_comm_init_rank(&c->comm, c->nprocs, &id, c->rank, c->device);
-    // mem=host on every rank (one CLI): pipelined host staging, as the shim does (chiara.h)
-    if (rc == CHR_SUCCESS && !std::getenv("CHR_HOST_WINDOW_MIB")) rc = chr_comm_set_host_pipeline(c->comm, 32);
+    // mem=host on every rank (one CLI): pipelined host staging, as the shim does (chiara.h); the
+    // device-resident runs keep one collective per call
+    if (rc == CHR_SUCCESS && o.mem == "host" && !std::getenv("CHR_HOST_WINDOW_MIB"))
+        rc = chr_comm_set_host_pipeline(c->comm, 32);
     MPI_Type_contiguous(2, MPI_BYTE, &c->bf16);
     MPI_Type_commit(&c->bf16);
     MPI_Op_create(bf16_sum_op, 1, &c->bf16_sum);

@@ -89,7 +89,7 @@ int main(int argc, char** argv) {
         MPI_Finalize();
         return EXIT_FAILURE;
     }
-    if (init(&c) != CHR_SUCCESS) {
+    if (init(&c, o) != CHR_SUCCESS) {
         std::fprintf(stderr, "rank %d: communicator init failed\n", c.rank);
         MPI_Abort(MPI_COMM_WORLD, 1);
     }

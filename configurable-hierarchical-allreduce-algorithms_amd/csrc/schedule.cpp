@@ -687,6 +687,20 @@ static void op_regions(const LocalOp& op, std::vector<Region>* rd, std::vector<R
     for (const Ref& x : op.ins) rd->push_back({x.buf, x.off, x.off + op.count});
     wr->push_back({op.dst.buf, op.dst.off, op.dst.off + op.count});
 }
+static bool conflict(const std::vector<Region>& wr_a, const std::vector<Region>& rd_a, const std::vector<Region>& rd_b,
+                     const std::vector<Region>& wr_b) {
+    for (const Region& a : wr_a) {
+        for (const Region& b : rd_b)
+            if (overlap(a, b)) return true;  // RAW
+        for (const Region& b : wr_b)
+            if (overlap(a, b)) return true;  // WAW
+    }
+    for (const Region& a : rd_a)
+        for (const Region& b : wr_b)
+            if (overlap(a, b)) return true;  // WAR
+    return false;
+}
+
 static void analyze_deps(Plan& p) {
     const size_t ns = p.steps.size();
     std::vector<std::vector<Region>> prd(ns), pwr(ns);
@@ -700,18 +714,15 @@ static void analyze_deps(Plan& p) {
             crd.push_back({x.ref.buf, x.ref.off + (uint64_t)p.rank * x.count, x.ref.off + (uint64_t)(p.rank + 1) * x.count});
             cwr.push_back({x.ref.buf, x.ref.off, x.ref.off + (uint64_t)p.g.nranks * x.count});
         }
-        int w = -1;
-        for (size_t u = t; u-- > 0 && w < 0;) {
-            bool c = false;
-            for (const Region& a : pwr[u]) {
-                for (const Region& b : crd) c = c || overlap(a, b);  // RAW
-                for (const Region& b : cwr) c = c || overlap(a, b);  // WAW
-            }
-            for (const Region& a : prd[u])
-                for (const Region& b : cwr) c = c || overlap(a, b);  // WAR
-            if (c) w = (int)u;
+        Step& st = p.steps[t];
+        st.comm_deps.clear();
+        st.local_deps.clear();
+        for (size_t u = 0; u < t; ++u) {
+            if (pwr[u].empty() && prd[u].empty()) continue;
+            if (conflict(pwr[u], prd[u], crd, cwr)) st.comm_deps.push_back((int)u);
+            if (conflict(pwr[u], prd[u], prd[t], pwr[t])) st.local_deps.push_back((int)u);
         }
-        p.steps[t].comm_wait = w;
+        st.comm_wait = st.comm_deps.empty() ? -1 : st.comm_deps.back();
     }
 }
 

@@ -423,52 +423,68 @@ def test_rccl_graph_cache_survives_scratch_growth_world4():
 
 def _timeout_worker(rank, world, port, q):
     """One rank returns early (never enters the collective); the others must get an error code
-    within their timeout instead of hanging, and their communicators must report aborted."""
+    within their timeout instead of hanging, and their communicators must report aborted.  Three
+    scenarios, each on a fresh communicator: device buffers; host (pageable) buffers through the
+    pipelined windows, whose copy-out thread issues pageable D2H copies (those used to
+    block inside HIP past the timeout); host buffers in one H2D / collective / D2H."""
     _setup(rank)
     import time
 
+    import numpy as np
     import torch
     import torch.distributed as dist
 
     import chiara_amd as ca
 
-    comm = _init_worker(rank, world, port)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     dev = torch.device("cuda:0")
-    res = None
-    try:
-        # warm the connections with one good call
-        x = torch.ones(1 << 16, dtype=torch.float32, device=dev)
-        y = torch.zeros_like(x)
-        assert ca.all_reduce_radix_batch(x, y, x.numel(), ca.FLOAT32, ca.SUM, comm, 4, 4) == 0
-        assert float(y[5].item()) == world
-        comm.set_timeout(5000)
-        if rank == world - 1:
-            dist.barrier()  # waits until the others have given up
-            comm.abort()    # it bailed out: release its side without blocking
-            res = (rank, 0, 0.0, comm.aborted, ca.all_reduce_radix_batch(x, y, x.numel(), ca.FLOAT32, ca.SUM, comm,
-                                                                         4, 4))
-        else:
-            t0 = time.perf_counter()
-            rc = ca.all_reduce_radix_batch(x, y, x.numel(), ca.FLOAT32, ca.SUM, comm, 4, 4)
-            el = time.perf_counter() - t0
-            again = ca.all_reduce_radix_batch(x, y, x.numel(), ca.FLOAT32, ca.SUM, comm, 4, 4)
-            res = (rank, rc, el, comm.aborted, again)
-            dist.barrier()
-    finally:
-        comm.destroy()
-        dist.destroy_process_group()
-    q.put(res)
+    out = []
+    for scenario in ("device", "host_windows", "host_single"):
+        comm = ca.Comm.from_torch_distributed(device=0)
+        try:
+            n = 1 << 20  # 4 MiB per rank: 4 windows of 1 MiB per rank with set_host_pipeline(1)
+            if scenario == "device":
+                x = torch.ones(n, dtype=torch.float32, device=dev)
+                y = torch.zeros_like(x)
+            else:
+                x = np.ones(n, dtype=np.float32)
+                y = np.zeros(n, dtype=np.float32)
+            comm.set_host_pipeline(1 if scenario == "host_windows" else 0)
+            # warm the connections with one good call
+            assert ca.all_reduce_radix_batch(x, y, n, ca.FLOAT32, ca.SUM, comm, 4, 4) == 0
+            assert float(y[5]) == world
+            comm.set_timeout(5000)
+            if rank == world - 1:
+                dist.barrier()  # waits until the others have given up
+                comm.abort()    # it bailed out: release its side without blocking
+                out.append((scenario, rank, 0, 0.0, comm.aborted,
+                            ca.all_reduce_radix_batch(x, y, n, ca.FLOAT32, ca.SUM, comm, 4, 4)))
+            else:
+                t0 = time.perf_counter()
+                rc = ca.all_reduce_radix_batch(x, y, n, ca.FLOAT32, ca.SUM, comm, 4, 4)
+                el = time.perf_counter() - t0
+                again = ca.all_reduce_radix_batch(x, y, n, ca.FLOAT32, ca.SUM, comm, 4, 4)
+                out.append((scenario, rank, rc, el, comm.aborted, again))
+                dist.barrier()
+        finally:
+            comm.destroy()
+    dist.destroy_process_group()
+    q.put(out)
 
 
 def test_rccl_lost_peer_times_out_world4():
     import chiara_amd as ca
 
-    res = sorted(_spawn(_timeout_worker, 4, timeout=240))
-    for rank, rc, el, aborted, again in res[:-1]:
-        assert rc in (ca.ERR_TIMEOUT, ca.ERR_RCCL), (rank, rc)
-        assert 4.0 <= el <= 60.0, (rank, el)
-        assert aborted and again == ca.ERR_ABORTED, (rank, aborted, again)
-    assert res[-1][3] and res[-1][4] == ca.ERR_ABORTED
+    res = _spawn(_timeout_worker, 4, timeout=300)
+    rows = [r for per_rank in res for r in per_rank]
+    assert len(rows) == 4 * 3
+    for scenario, rank, rc, el, aborted, again in rows:
+        if rank == 3:
+            assert aborted and again == ca.ERR_ABORTED, (scenario, rank)
+            continue
+        assert rc in (ca.ERR_TIMEOUT, ca.ERR_RCCL), (scenario, rank, rc)
+        assert 4.0 <= el <= 60.0, (scenario, rank, el)
+        assert aborted and again == ca.ERR_ABORTED, (scenario, rank, aborted, again)
 
 
 def _fullsize_worker(rank, world, port, q, dtype, slices):
