@@ -29,16 +29,24 @@ UINT16 = UNSIGNED_SHORT = 7
 UINT32 = UNSIGNED = 8
 INT64 = LONG = LONG_LONG = 9
 UINT64 = UNSIGNED_LONG = 10
-# ops (chr_op): MPI's predefined ops; the logical and bitwise ones on integer types only
+# MPI's MAXLOC / MINLOC pair types ({value; int index} C structs) and the C99 complex types
+FLOAT_INT, DOUBLE_INT, LONG_INT, TWO_INT, SHORT_INT = 11, 12, 13, 14, 15
+C_FLOAT_COMPLEX = C_COMPLEX = 16
+C_DOUBLE_COMPLEX = 17
+# ops (chr_op): MPI's predefined ops with MPICH's (type, op) table: the logical and bitwise ones on
+# integer types only (logical also on float / double), MAXLOC / MINLOC on the pair types only, SUM /
+# PROD on the complex types only
 SUM, PROD, MAX, MIN = 0, 1, 2, 3
 LAND, LOR, LXOR, BAND, BOR, BXOR = 4, 5, 6, 7, 8, 9
+MAXLOC, MINLOC = 10, 11
 SUCCESS = 0
 ERR_RCCL, ERR_TIMEOUT, ERR_ABORTED = 5, 9, 10
 IN_PLACE = object()  # MPI_IN_PLACE analogue
 _IN_PLACE_PTR = 1     # CHR_IN_PLACE
 
 DTYPE_SIZE = {FLOAT32: 4, FLOAT64: 8, INT32: 4, BFLOAT16: 2, INT8: 1, UINT8: 1, INT16: 2, UINT16: 2, UINT32: 4,
-              INT64: 8, UINT64: 8}
+              INT64: 8, UINT64: 8, FLOAT_INT: 8, DOUBLE_INT: 16, LONG_INT: 16, TWO_INT: 8, SHORT_INT: 8,
+              C_FLOAT_COMPLEX: 8, C_DOUBLE_COMPLEX: 16}
 MODE_ALLREDUCE, MODE_REDUCE_SCATTER = 0, 1
 # MPICH baselines (testing/mpich_implementations/all_reduce/), chr_mode numbering
 MODE_MPICH_RING, MODE_MPICH_RD, MODE_MPICH_RSAG, MODE_MPICH_RECEXCH = 2, 3, 4, 5
@@ -460,7 +468,10 @@ def parse_plan(text):
             plan["pre"].append(local(tok[1:]))
         elif tok[0] == "step":
             wait = int(tok[3].split("=")[1]) if len(tok) > 3 and tok[3].startswith("wait=") else -1
-            cur = {"label": tok[2], "wait": wait, "sends": [], "recvs": [], "allgathers": [], "post": []}
+            kv = dict(t.split("=", 1) for t in tok[4:] if "=" in t)
+            deps = lambda v: [] if v in (None, "-") else [int(x) for x in v.split(",")]  # noqa: E731
+            cur = {"label": tok[2], "wait": wait, "deps": deps(kv.get("deps")), "ldeps": deps(kv.get("ldeps")),
+                   "sends": [], "recvs": [], "allgathers": [], "post": []}
             plan["steps"].append(cur)
         elif tok[0] in ("send", "recv"):
             cur[tok[0] + "s"].append((int(tok[1]), (tok[2], int(tok[3])), int(tok[4])))

@@ -10,8 +10,10 @@
 // library's MPI_Allreduce / MPI_Reduce_scatter_block on the same inputs.  The expectation comes from
 // MPICH itself: a pair MPICH's MPI_Reduce_local accepts must succeed through the shim with the
 // library's result (exact: integer data, and floats holding small integers, so every association
-// rounds the same); a pair it rejects must come back as an MPI error class, as must user ops,
-// MPI_MAXLOC/MINLOC and non-contiguous types.  Prints one JSON line; exit status 0 = all agree.
+// rounds the same); a pair it rejects must come back as an MPI error class, as must user ops and
+// the long-double types.  The MAXLOC / MINLOC pair types and the C complex types are in the table:
+// buffers are laid out at MPI's extent (MPI_DOUBLE_INT: 16 B an element, of which 12 are data).
+// Prints one JSON line; exit status 0 = all agree.
 #include <mpi.h>
 
 #include <cstdint>
@@ -41,15 +43,37 @@ uint64_t mix(uint64_t x) {
 struct TypeCase {
     MPI_Datatype t;
     const char* name;
-    int kind;  // 0 integer (random bits), 1 float, 2 double, 3 bool (0/1)
+    int kind;  // 0 integer (random bits), 1 float, 2 double, 3 bool (0/1), 4 pair {value; int}, 5 complex
+    int vsize; // pairs: bytes of the value (4 float / 8 double / 8 long / 4 int / 2 short); complex: of a part
+    bool vfloat;
 };
+
+void put_small(char* p, int v, int vsize, bool vfloat) {
+    if (vfloat && vsize == 4) {
+        const float f = (float)v;
+        std::memcpy(p, &f, 4);
+    } else if (vfloat) {
+        const double d = (double)v;
+        std::memcpy(p, &d, 8);
+    } else {
+        const int64_t w = v;
+        std::memcpy(p, &w, vsize);  // little endian: the low bytes
+    }
+}
 
 void fill(std::vector<char>& buf, int n, const TypeCase& tc, int tsize, int rank, int salt) {
     buf.assign((size_t)n * tsize, 0);
     for (int i = 0; i < n; ++i) {
         const uint64_t u = mix(((uint64_t)rank << 40) ^ ((uint64_t)salt << 20) ^ (uint64_t)i);
         char* p = buf.data() + (size_t)i * tsize;
-        if (tc.kind == 1) {  // small integers in [-3, 4], zeros included: every sum/product is exact
+        if (tc.kind == 4) {  // pair: value in [-3, 4] (ties are frequent), index in [0, 64); padding zero
+            put_small(p, (int)(u % 8) - 3, tc.vsize, tc.vfloat);
+            const int32_t idx = (int32_t)((u >> 8) & 63);
+            std::memcpy(p + (tc.vsize == 8 ? 8 : 4), &idx, 4);
+        } else if (tc.kind == 5) {  // complex: small integer parts, so every sum and product is exact
+            put_small(p, (int)(u % 8) - 3, tc.vsize, true);
+            put_small(p + tc.vsize, (int)((u >> 8) % 8) - 3, tc.vsize, true);
+        } else if (tc.kind == 1) {  // small integers in [-3, 4], zeros included: every sum/product is exact
             const float f = (float)((int)(u % 8) - 3);
             std::memcpy(p, &f, 4);
         } else if (tc.kind == 2) {
@@ -84,12 +108,17 @@ int main(int argc, char** argv) {
         {MPI_UINT8_T, "MPI_UINT8_T", 0}, {MPI_INT16_T, "MPI_INT16_T", 0}, {MPI_UINT16_T, "MPI_UINT16_T", 0},
         {MPI_INT32_T, "MPI_INT32_T", 0}, {MPI_UINT32_T, "MPI_UINT32_T", 0}, {MPI_INT64_T, "MPI_INT64_T", 0},
         {MPI_UINT64_T, "MPI_UINT64_T", 0}, {MPI_FLOAT, "MPI_FLOAT", 1}, {MPI_DOUBLE, "MPI_DOUBLE", 2},
-        {MPI_BYTE, "MPI_BYTE", 0}, {MPI_C_BOOL, "MPI_C_BOOL", 3}};
+        {MPI_BYTE, "MPI_BYTE", 0}, {MPI_C_BOOL, "MPI_C_BOOL", 3},
+        {MPI_FLOAT_INT, "MPI_FLOAT_INT", 4, 4, true}, {MPI_DOUBLE_INT, "MPI_DOUBLE_INT", 4, 8, true},
+        {MPI_LONG_INT, "MPI_LONG_INT", 4, 8, false}, {MPI_2INT, "MPI_2INT", 4, 4, false},
+        {MPI_SHORT_INT, "MPI_SHORT_INT", 4, 2, false}, {MPI_C_FLOAT_COMPLEX, "MPI_C_FLOAT_COMPLEX", 5, 4, true},
+        {MPI_C_COMPLEX, "MPI_C_COMPLEX", 5, 4, true}, {MPI_C_DOUBLE_COMPLEX, "MPI_C_DOUBLE_COMPLEX", 5, 8, true}};
     const struct {
         MPI_Op op;
         const char* name;
     } ops[] = {{MPI_SUM, "SUM"},   {MPI_PROD, "PROD"}, {MPI_MAX, "MAX"},   {MPI_MIN, "MIN"},  {MPI_LAND, "LAND"},
-               {MPI_LOR, "LOR"},   {MPI_LXOR, "LXOR"}, {MPI_BAND, "BAND"}, {MPI_BOR, "BOR"},  {MPI_BXOR, "BXOR"}};
+               {MPI_LOR, "LOR"},   {MPI_LXOR, "LXOR"}, {MPI_BAND, "BAND"}, {MPI_BOR, "BOR"},  {MPI_BXOR, "BXOR"},
+               {MPI_MAXLOC, "MAXLOC"}, {MPI_MINLOC, "MINLOC"}};
     const int per = 37, count = per * n;
     int pairs = 0, supported = 0, bad = 0;
     std::string failures;
@@ -99,8 +128,9 @@ int main(int argc, char** argv) {
     };
     int salt = 0;
     for (const TypeCase& tc : types) {
-        int tsize = 0;
-        MPI_Type_size(tc.t, &tsize);
+        MPI_Aint lb = 0, ext = 0;
+        MPI_Type_get_extent(tc.t, &lb, &ext);
+        const int tsize = (int)ext;  // the element stride of a buffer
         for (const auto& o : ops) {
             ++pairs;
             ++salt;
@@ -139,8 +169,11 @@ int main(int argc, char** argv) {
         if (all_reduce_radix_batch(a.data(), r.data(), 4 * n, MPI_INT, uop, MPI_COMM_WORLD, 2, 1) == MPI_SUCCESS)
             fail("user op accepted");
         MPI_Op_free(&uop);
-        if (all_reduce_radix_batch(a.data(), r.data(), 4 * n, MPI_2INT, MPI_MAXLOC, MPI_COMM_WORLD, 2, 1) == MPI_SUCCESS)
-            fail("MPI_MAXLOC accepted");
+        if (all_reduce_radix_batch(a.data(), r.data(), 4 * n, MPI_INT, MPI_MAXLOC, MPI_COMM_WORLD, 2, 1) == MPI_SUCCESS)
+            fail("MPI_MAXLOC on MPI_INT accepted");
+        if (all_reduce_radix_batch(a.data(), r.data(), 4 * n, MPI_LONG_DOUBLE_INT, MPI_MAXLOC, MPI_COMM_WORLD, 2, 1) ==
+            MPI_SUCCESS)
+            fail("MPI_LONG_DOUBLE_INT accepted");
         if (all_reduce_radix_batch(a.data(), r.data(), 4 * n, MPI_LONG_DOUBLE, MPI_SUM, MPI_COMM_WORLD, 2, 1) ==
             MPI_SUCCESS)
             fail("MPI_LONG_DOUBLE accepted");

@@ -28,6 +28,37 @@ __device__ __forceinline__ uint32_t f2bf_pk(float lo, float hi) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2));
 }
 
+// MPI's pair types for MAXLOC / MINLOC and the C99 complex types, as element types of the kernels.
+// A pair element is carried as its raw 32-bit words (the C struct {value; int index} MPI defines,
+// padding included): MPICH replaces a whole element when the incoming one wins (padding bytes and
+// all, tests/golden/pairs_reduce_local.npz), and a word copy does the same, where a struct copy may
+// drop padding.  Value and index are read out of the words.
+template <int NW>
+struct RawPair {
+    uint32_t w[NW];
+};
+struct PairFI : RawPair<2> {};  // {float v; int i;}        8 B
+struct PairDI : RawPair<4> {};  // {double v; int i;}      16 B (4 B padding)
+struct PairLI : RawPair<4> {};  // {long v; int i;}        16 B (4 B padding)
+struct Pair2I : RawPair<2> {};  // {int v; int i;}          8 B
+struct PairSI : RawPair<2> {};  // {short v; int i;}        8 B (2 B padding after v)
+struct CplxF { float re, im; };
+struct CplxD { double re, im; };
+static_assert(sizeof(PairFI) == 8 && sizeof(PairDI) == 16 && sizeof(PairLI) == 16 && sizeof(Pair2I) == 8 &&
+                  sizeof(PairSI) == 8 && sizeof(CplxF) == 8 && sizeof(CplxD) == 16,
+              "pair / complex layouts");
+__host__ __device__ __forceinline__ float pair_value(const PairFI& p) { return __builtin_bit_cast(float, p.w[0]); }
+__host__ __device__ __forceinline__ double pair_value(const PairDI& p) {
+    return __builtin_bit_cast(double, (uint64_t)p.w[0] | ((uint64_t)p.w[1] << 32));
+}
+__host__ __device__ __forceinline__ int64_t pair_value(const PairLI& p) {
+    return (int64_t)((uint64_t)p.w[0] | ((uint64_t)p.w[1] << 32));
+}
+__host__ __device__ __forceinline__ int32_t pair_value(const Pair2I& p) { return (int32_t)p.w[0]; }
+__host__ __device__ __forceinline__ int16_t pair_value(const PairSI& p) { return (int16_t)(p.w[0] & 0xFFFFu); }
+template <int NW>
+__host__ __device__ __forceinline__ constexpr int pair_index_word() { return NW == 2 ? 1 : 2; }
+
 template <int DT> struct DTy;
 template <> struct DTy<CHR_FLOAT32> { using T = float; };
 template <> struct DTy<CHR_FLOAT64> { using T = double; };
@@ -40,6 +71,18 @@ template <> struct DTy<CHR_UINT16> { using T = uint16_t; };
 template <> struct DTy<CHR_UINT32> { using T = uint32_t; };
 template <> struct DTy<CHR_INT64> { using T = int64_t; };
 template <> struct DTy<CHR_UINT64> { using T = uint64_t; };
+template <> struct DTy<CHR_FLOAT_INT> { using T = PairFI; };
+template <> struct DTy<CHR_DOUBLE_INT> { using T = PairDI; };
+template <> struct DTy<CHR_LONG_INT> { using T = PairLI; };
+template <> struct DTy<CHR_2INT> { using T = Pair2I; };
+template <> struct DTy<CHR_SHORT_INT> { using T = PairSI; };
+template <> struct DTy<CHR_C_FLOAT_COMPLEX> { using T = CplxF; };
+template <> struct DTy<CHR_C_DOUBLE_COMPLEX> { using T = CplxD; };
+
+template <int DT>
+constexpr bool is_pair_dt() { return DT >= CHR_FLOAT_INT && DT <= CHR_SHORT_INT; }
+template <int DT>
+constexpr bool is_complex_dt() { return DT == CHR_C_FLOAT_COMPLEX || DT == CHR_C_DOUBLE_COMPLEX; }
 
 template <int DT>
 constexpr bool is_float_dt() { return DT == CHR_FLOAT32 || DT == CHR_FLOAT64 || DT == CHR_BFLOAT16; }
@@ -50,6 +93,49 @@ constexpr bool is_float_dt() { return DT == CHR_FLOAT32 || DT == CHR_FLOAT64 || 
 // op), so only MAX/MIN need their own instantiations (they differ on ties such as -0/+0
 // and on NaN compares).
 constexpr int kMaxSw = 16, kMinSw = 17;
+// The same for MAXLOC / MINLOC on the pairs with a floating value: a NaN compare keeps inout, and a
+// tie keeps inout's value bits (-0 vs +0), so the operand order shows.
+constexpr int kMaxLocSw = 18, kMinLocSw = 19;
+
+// C99 Annex G complex multiplication (libgcc's __mulsc3 / __muldc3, what MPICH's `a = a * b` on
+// `float _Complex` compiles to): (a + bi)(c + di), products rounded one by one (the library is
+// built with -ffp-contract=off), and the infinity recovery when both parts come out NaN.  The
+// result is the same with the operands exchanged (every term is a commuting product or sum).
+template <typename F>
+__device__ __forceinline__ void cmul(F a, F b, F c, F d, F* re, F* im) {
+    const F ac = a * c, bd = b * d, ad = a * d, bc = b * c;
+    F x = ac - bd, y = ad + bc;
+    if (__builtin_isnan(x) && __builtin_isnan(y)) {
+        bool recalc = false;
+        if (__builtin_isinf(a) || __builtin_isinf(b)) {
+            a = __builtin_copysign(__builtin_isinf(a) ? (F)1 : (F)0, a);
+            b = __builtin_copysign(__builtin_isinf(b) ? (F)1 : (F)0, b);
+            if (__builtin_isnan(c)) c = __builtin_copysign((F)0, c);
+            if (__builtin_isnan(d)) d = __builtin_copysign((F)0, d);
+            recalc = true;
+        }
+        if (__builtin_isinf(c) || __builtin_isinf(d)) {
+            c = __builtin_copysign(__builtin_isinf(c) ? (F)1 : (F)0, c);
+            d = __builtin_copysign(__builtin_isinf(d) ? (F)1 : (F)0, d);
+            if (__builtin_isnan(a)) a = __builtin_copysign((F)0, a);
+            if (__builtin_isnan(b)) b = __builtin_copysign((F)0, b);
+            recalc = true;
+        }
+        if (!recalc && (__builtin_isinf(ac) || __builtin_isinf(bd) || __builtin_isinf(ad) || __builtin_isinf(bc))) {
+            if (__builtin_isnan(a)) a = __builtin_copysign((F)0, a);
+            if (__builtin_isnan(b)) b = __builtin_copysign((F)0, b);
+            if (__builtin_isnan(c)) c = __builtin_copysign((F)0, c);
+            if (__builtin_isnan(d)) d = __builtin_copysign((F)0, d);
+            recalc = true;
+        }
+        if (recalc) {
+            x = __builtin_inf() * (a * c - b * d);
+            y = __builtin_inf() * (a * d + b * c);
+        }
+    }
+    *re = x;
+    *im = y;
+}
 
 // MPI_Reduce_local(in = x, inout = y): MPICH 3.3.2's loop is inout = OP(inout, in) with
 // MAX(p, q) = p > q ? p : q (MPIR_OP_TYPE_REDUCE_CASE, a = inoutvec, b = invec), so MAX/MIN
@@ -57,7 +143,33 @@ constexpr int kMaxSw = 16, kMinSw = 17;
 // `in` operand and the result takes the place of the incoming buffer: OP(x, y).
 template <int DT, int OP>
 __device__ __forceinline__ typename DTy<DT>::T apply(typename DTy<DT>::T x, typename DTy<DT>::T y) {
-    if constexpr (DT == CHR_BFLOAT16) {
+    if constexpr (is_pair_dt<DT>()) {
+        // MPICH's MAXLOC / MINLOC loop (a = inout, b = in): equal values keep a's words with the
+        // lower index, a strictly better b replaces a (the whole element), else a stays
+        if constexpr (OP == kMaxLocSw) return apply<DT, CHR_MAXLOC>(y, x);
+        else if constexpr (OP == kMinLocSw) return apply<DT, CHR_MINLOC>(y, x);
+        else {
+            using T = typename DTy<DT>::T;
+            constexpr int IW = pair_index_word<sizeof(T) / 4>();
+            const auto vx = pair_value(x), vy = pair_value(y);
+            T r = y;
+            if (vy == vx) {
+                const int32_t ix = (int32_t)x.w[IW], iy = (int32_t)y.w[IW];
+                r.w[IW] = (uint32_t)(ix < iy ? ix : iy);
+            } else if (OP == CHR_MAXLOC ? vy < vx : vy > vx) {
+                r = x;
+            }
+            return r;
+        }    } else if constexpr (is_complex_dt<DT>()) {
+        typename DTy<DT>::T r;
+        if constexpr (OP == CHR_SUM) {
+            r.re = y.re + x.re;
+            r.im = y.im + x.im;
+        } else {
+            cmul(y.re, y.im, x.re, x.im, &r.re, &r.im);
+        }
+        return r;
+    } else if constexpr (DT == CHR_BFLOAT16) {
         const float fx = bf2f(x), fy = bf2f(y);
         if constexpr (OP == CHR_SUM) return f2bf(fy + fx);
         else if constexpr (OP == CHR_PROD) return f2bf(fy * fx);

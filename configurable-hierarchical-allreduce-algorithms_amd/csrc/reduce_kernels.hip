@@ -46,9 +46,15 @@ size_t dtype_size(int dtype) {
     case CHR_INT16: case CHR_UINT16: return 2;
     case CHR_UINT32: return 4;
     case CHR_INT64: case CHR_UINT64: return 8;
+    // the pair and complex types: the C struct, i.e. MPI's extent (the element stride of a buffer)
+    case CHR_FLOAT_INT: case CHR_2INT: case CHR_SHORT_INT: case CHR_C_FLOAT_COMPLEX: return 8;
+    case CHR_DOUBLE_INT: case CHR_LONG_INT: case CHR_C_DOUBLE_COMPLEX: return 16;
     default: return 0;
     }
 }
+
+static bool is_pair_dtype(int dtype) { return dtype >= CHR_FLOAT_INT && dtype <= CHR_SHORT_INT; }
+static bool is_complex_dtype(int dtype) { return dtype == CHR_C_FLOAT_COMPLEX || dtype == CHR_C_DOUBLE_COMPLEX; }
 
 static bool is_float_dtype(int dtype) {
     return dtype == CHR_FLOAT32 || dtype == CHR_FLOAT64 || dtype == CHR_BFLOAT16;
@@ -60,6 +66,11 @@ static bool is_float_dtype(int dtype) {
 // library's own type: arithmetic and MAX/MIN only.
 bool valid_dtype_op(int dtype, int op) {
     if (!dtype_size(dtype)) return false;
+    // MPICH 3.3.2's table for the pair and complex types (oracle/ref_pairs_probe table,
+    // tests/golden/pairs_manifest.json): MAXLOC / MINLOC on the pairs only, SUM / PROD on complex only
+    if (is_pair_dtype(dtype)) return op == CHR_MAXLOC || op == CHR_MINLOC;
+    if (is_complex_dtype(dtype)) return op == CHR_SUM || op == CHR_PROD;
+    if (op == CHR_MAXLOC || op == CHR_MINLOC) return false;
     if (op >= CHR_SUM && op <= CHR_MIN) return true;
     if (op >= CHR_LAND && op <= CHR_LXOR) return dtype != CHR_BFLOAT16;
     return op >= CHR_BAND && op <= CHR_BXOR && !is_float_dtype(dtype);
@@ -71,6 +82,12 @@ bool valid_dtype_op(int dtype, int op) {
 // changes MAX/MIN results only for floating types (ties of -0/+0, NaN compares).
 void canon_op(int dtype, int op, bool running_first, int* kdt, int* kop) {
     *kop = op;
+    if (is_pair_dtype(dtype) || is_complex_dtype(dtype)) {
+        *kdt = dtype;
+        if (running_first && (dtype == CHR_FLOAT_INT || dtype == CHR_DOUBLE_INT))  // ties of -0/+0, NaN
+            *kop = op == CHR_MAXLOC ? kMaxLocSw : op == CHR_MINLOC ? kMinLocSw : op;
+        return;
+    }
     if (is_float_dtype(dtype)) {
         *kdt = dtype;
         if (running_first && (op == CHR_MAX || op == CHR_MIN)) *kop = op == CHR_MAX ? kMaxSw : kMinSw;
@@ -90,7 +107,8 @@ void canon_op(int dtype, int op, bool running_first, int* kdt, int* kop) {
 
 // kernel types compiled in this translation unit; the rest: reduce_int.hip
 static bool in_core_tu(int kdt, int kop) {
-    return (is_float_dtype(kdt) || kdt == CHR_INT32) && ((kop >= CHR_SUM && kop <= CHR_MIN) || kop >= kMaxSw);
+    return (is_float_dtype(kdt) || kdt == CHR_INT32) && ((kop >= CHR_SUM && kop <= CHR_MIN) || kop == kMaxSw ||
+                                                         kop == kMinSw);
 }
 
 int& coresident_depth() {
@@ -178,6 +196,7 @@ static hipError_t launch_scalar(void* out, const void* acc, const void* const* i
     a.m = m;
     a.n = n;
     for (int j = 0; j < m; ++j) a.ins[j] = ins[j];
+    if (is_pair_dtype(kdt) || is_complex_dtype(kdt)) return launch_scalar_pair(a, kdt, kop, s);
     if (!in_core_tu(kdt, kop)) return launch_scalar_int(a, kdt, kop, s);
     switch (kdt) {
     case CHR_FLOAT32: return launch_scalar_dt<CHR_FLOAT32>(a, kop, s);
@@ -209,7 +228,9 @@ static hipError_t launch_group(void* out, const void* acc, const void* const* in
         a.acc = (const u32x4*)((const char*)acc + head * es);
         for (int j = 0; j < m; ++j) a.ins[j] = (const u32x4*)((const char*)ins[j] + head * es);
         a.nvec = nvec;
-        if (!in_core_tu(dtype, op)) {
+        if (is_pair_dtype(dtype) || is_complex_dtype(dtype)) {
+            err = launch_vec_pair(a, dtype, op, m, s);
+        } else if (!in_core_tu(dtype, op)) {
             err = launch_vec_int(a, dtype, op, m, s);
         } else {
             switch (dtype) {
@@ -259,8 +280,90 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     return x ^ (x >> 31);
 }
 
+__device__ __forceinline__ float gen_f32(uint64_t seed, uint64_t rank, uint64_t i) {
+    return (float)(splitmix64(seed ^ (rank << 40) ^ i) >> 40) * (1.0f / 8388608.0f) - 1.0f;
+}
+__device__ __forceinline__ double gen_f64(uint64_t seed, uint64_t rank, uint64_t i) {
+    return (double)(splitmix64(seed ^ (rank << 40) ^ i) >> 11) * (1.0 / 4503599627370496.0) - 1.0;
+}
+
+// The pair and complex types (oracle/chiara_oracle.c orc_fill_pair, the same formulas): pair value a
+// small integer in [-4, 3] (uniform / sparse), rank*count + i with index = rank (seq), or for the
+// floating pairs {+0, -0, 1, -1, 0.5, NaN with a per-rank payload} (ties); index from 6 random bits;
+// complex: U[-1,1) parts from elements 2g and 2g + 1 of the float generator, rank*count + i and its
+// negation (seq), the float ties values.  Padding bytes zero.
+__device__ void fill_pair(char* elem, int dtype, int pattern, uint64_t seed, uint64_t rank, uint64_t count_for_seq,
+                          uint64_t g) {
+    const float ft[8] = {0.0f, -0.0f, 1.0f, -1.0f, 0.0f, -0.0f, 0.5f, 0.0f};
+    const uint64_t key = splitmix64(seed ^ (rank << 40) ^ g);
+    const unsigned sel = (unsigned)(key >> 61);
+    const uint32_t pay = (uint32_t)(rank + 1) & 0x3Fu;
+    const int32_t small = (int32_t)(key >> 61) - 4;
+    const int32_t idx = pattern == 1 ? (int32_t)rank : (int32_t)((key >> 32) & 0x3F);
+    const int32_t seq = (int32_t)(uint32_t)(rank * count_for_seq + g);
+    uint32_t w[4] = {0, 0, 0, 0};
+    switch (dtype) {
+    case CHR_FLOAT_INT: {
+        const float v = pattern == 1 ? (float)seq : pattern == 2 ? ft[sel] : (float)small;
+        w[0] = pattern == 2 && sel == 7 ? (0x7FC00000u | (pay << 16) | pay) : __float_as_uint(v);
+        w[1] = (uint32_t)idx;
+        break;
+    }
+    case CHR_DOUBLE_INT: {
+        const double v = pattern == 1 ? (double)seq : pattern == 2 ? (double)ft[sel] : (double)small;
+        const uint64_t u = pattern == 2 && sel == 7 ? (0x7FF8000000000000ull | ((uint64_t)pay << 40) | pay)
+                                                     : (uint64_t)__double_as_longlong(v);
+        w[0] = (uint32_t)u;
+        w[1] = (uint32_t)(u >> 32);
+        w[2] = (uint32_t)idx;
+        break;
+    }
+    case CHR_LONG_INT: {
+        const uint64_t u = (uint64_t)(int64_t)(pattern == 1 ? seq : small);
+        w[0] = (uint32_t)u;
+        w[1] = (uint32_t)(u >> 32);
+        w[2] = (uint32_t)idx;
+        break;
+    }
+    case CHR_2INT:
+        w[0] = (uint32_t)(pattern == 1 ? seq : small);
+        w[1] = (uint32_t)idx;
+        break;
+    case CHR_SHORT_INT:
+        w[0] = (uint32_t)(uint16_t)(int16_t)(pattern == 1 ? seq : small);
+        w[1] = (uint32_t)idx;
+        break;
+    case CHR_C_FLOAT_COMPLEX: {
+        const float re = pattern == 1 ? (float)seq : pattern == 2 ? ft[sel] : gen_f32(seed, rank, 2 * g);
+        const float im = pattern == 1 ? -(float)seq : pattern == 2 ? ft[(key >> 58) & 7] : gen_f32(seed, rank, 2 * g + 1);
+        w[0] = __float_as_uint(re);
+        w[1] = __float_as_uint(im);
+        break;
+    }
+    default: {  // CHR_C_DOUBLE_COMPLEX
+        const double re = pattern == 1 ? (double)seq : pattern == 2 ? (double)ft[sel] : gen_f64(seed, rank, 2 * g);
+        const double im = pattern == 1 ? -(double)seq : pattern == 2 ? (double)ft[(key >> 58) & 7]
+                                                                     : gen_f64(seed, rank, 2 * g + 1);
+        const uint64_t ur = (uint64_t)__double_as_longlong(re), ui = (uint64_t)__double_as_longlong(im);
+        w[0] = (uint32_t)ur;
+        w[1] = (uint32_t)(ur >> 32);
+        w[2] = (uint32_t)ui;
+        w[3] = (uint32_t)(ui >> 32);
+        break;
+    }
+    }
+    const int nw = dtype == CHR_DOUBLE_INT || dtype == CHR_LONG_INT || dtype == CHR_C_DOUBLE_COMPLEX ? 4 : 2;
+    for (int k = 0; k < nw; ++k) ((uint32_t*)elem)[k] = w[k];
+}
+
 __global__ __launch_bounds__(kBlock) void k_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed,
                                                  uint64_t rank, uint64_t count_for_seq) {
+    if (dtype >= CHR_FLOAT_INT) {
+        const size_t es = dtype == CHR_DOUBLE_INT || dtype == CHR_LONG_INT || dtype == CHR_C_DOUBLE_COMPLEX ? 16 : 8;
+        for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kBlock)
+            fill_pair((char*)buf + i * es, dtype, pattern, seed, rank, count_for_seq, i);
+        return;
+    }
     const int es = dtype == CHR_INT8 || dtype == CHR_UINT8 ? 1 : dtype == CHR_INT16 || dtype == CHR_UINT16 ? 2
                    : dtype == CHR_UINT32 || (dtype == CHR_INT32 && pattern == 3) ? 4
                    : dtype == CHR_INT64 || dtype == CHR_UINT64 ? 8 : 0;

@@ -18,6 +18,7 @@ static hipError_t launch_tree_dt(const TreeArgs& a, const TreeScalarArgs* sa, in
 
 // dtype, op: the kernel type and op (canon_op)
 static hipError_t launch_tree_any(const TreeArgs& a, const TreeScalarArgs* sa, int dtype, int op, hipStream_t s) {
+    if (dtype >= CHR_FLOAT_INT && dtype <= CHR_C_DOUBLE_COMPLEX) return launch_tree_pair(a, sa, dtype, op, s);
     const bool core = (dtype == CHR_FLOAT32 || dtype == CHR_FLOAT64 || dtype == CHR_BFLOAT16 || dtype == CHR_INT32) &&
                       op <= CHR_MIN;
     if (!core) return launch_tree_int(a, sa, dtype, op, s);

@@ -59,7 +59,14 @@ constexpr size_t kMaxSegVec = (size_t)1 << 26;
 
 template <int OP>
 constexpr int swapped_op() {
-    return OP == CHR_MAX ? kMaxSw : OP == CHR_MIN ? kMinSw : OP;
+    return OP == CHR_MAX ? kMaxSw : OP == CHR_MIN ? kMinSw : OP == CHR_MAXLOC ? kMaxLocSw : OP == CHR_MINLOC ? kMinLocSw : OP;
+}
+// Whether MPI_Reduce_local(running, next) can differ bitwise from MPI_Reduce_local(next, running):
+// MAX / MIN on floating types and MAXLOC / MINLOC on floating-valued pairs (ties, -0 / +0, NaN).
+template <int DT, int OP>
+constexpr bool order_sensitive() {
+    return (is_float_dt<DT>() && (OP == CHR_MAX || OP == CHR_MIN)) ||
+           ((DT == CHR_FLOAT_INT || DT == CHR_DOUBLE_INT) && (OP == CHR_MAXLOC || OP == CHR_MINLOC));
 }
 
 // Generic over the value carried per lane (W values of type V, combined with F).  The stack
@@ -95,7 +102,7 @@ template <int DT, int OP>
 struct VecOp {
     template <bool SW>
     __device__ __forceinline__ static u32x4 ap(u32x4 in, u32x4 run) {
-        if constexpr (SW && is_float_dt<DT>()) return apply_vec<DT, swapped_op<OP>()>(in, run);
+        if constexpr (SW && order_sensitive<DT, OP>()) return apply_vec<DT, swapped_op<OP>()>(in, run);
         else return apply_vec<DT, OP>(in, run);
     }
 };
@@ -105,7 +112,7 @@ struct ScalarOp {
     using T = typename DTy<DT>::T;
     template <bool SW>
     __device__ __forceinline__ static T ap(T in, T run) {
-        if constexpr (SW && is_float_dt<DT>()) return apply<DT, swapped_op<OP>()>(in, run);
+        if constexpr (SW && order_sensitive<DT, OP>()) return apply<DT, swapped_op<OP>()>(in, run);
         else return apply<DT, OP>(in, run);
     }
 };
@@ -232,7 +239,7 @@ constexpr int tree_wg_per_cu() {
 
 template <int DT, int OP, int NL, int BL, bool NT>
 inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
-    constexpr int U = tree_u<NL, NT>();
+    constexpr int U = is_complex_dt<DT>() && OP == CHR_PROD ? 1 : tree_u<NL, NT>();  // see vec_u_dt
     TreeArgs a = a_in;
     a.xrun = NT ? xcd_run_shift(tree_xcd_run_kib<NL>(), (size_t)BL * U * 16) : 0;
     size_t grid = 0;
@@ -287,7 +294,8 @@ inline hipError_t launch_tree_nl(const TreeArgs& a, const TreeScalarArgs* sa, hi
     for (int j = 0; j < a.nseg; ++j) nvec += a.seg[j].nvec;
     const size_t call_bytes = (size_t)(a.nl + 1) * nvec * 16;
     const bool nt = t.nt_mode == 1 || (t.nt_mode < 0 && call_bytes >= t.tree_nt_min_bytes);
-    return nt ? launch_tree_vec<DT, OP, NL, 64, true>(a, s) : launch_tree_vec<DT, OP, NL, 256, false>(a, s);
+    if constexpr (is_pair_dt<DT>() || is_complex_dt<DT>()) return launch_tree_vec<DT, OP, NL, 256, false>(a, s);  // as launch_vec_m
+    else return nt ? launch_tree_vec<DT, OP, NL, 64, true>(a, s) : launch_tree_vec<DT, OP, NL, 256, false>(a, s);
 }
 
 template <int DT, int OP>
@@ -306,6 +314,8 @@ inline hipError_t launch_tree_op(const TreeArgs& a, const TreeScalarArgs* sa, hi
 
 // The integer kernel types of reduce_tree_int.hip (kdt/kop from canon_op).
 hipError_t launch_tree_int(const TreeArgs& a, const TreeScalarArgs* sa, int kdt, int kop, hipStream_t s);
+// The pair (MAXLOC / MINLOC) and complex (SUM / PROD) types of reduce_tree_pair.hip.
+hipError_t launch_tree_pair(const TreeArgs& a, const TreeScalarArgs* sa, int kdt, int kop, hipStream_t s);
 
 
 }  // namespace chr

@@ -152,6 +152,11 @@ template <int M, bool NT>
 constexpr int vec_u() {
     return NT ? vec_u_nt<M>() : M <= 2 ? 4 : 2;
 }
+// Complex PROD (C99 Annex G multiplication per element) keeps one vector per lane per trip.
+template <int DT, int OP, int M, bool NT>
+constexpr int vec_u_dt() {
+    return is_complex_dt<DT>() && OP == CHR_PROD ? 1 : vec_u<M, NT>();
+}
 
 // A grid holds at most 2^31 threads here; larger calls (> 32 GiB per operand at BL = 64, U = 2)
 // run as consecutive launches over consecutive pieces.
@@ -181,7 +186,7 @@ inline hipError_t for_each_launch_piece(VecArgs a, L launch) {
 // tools/reduce_microbench.hip, which instantiates the kernel templates directly.
 template <int DT, int OP, int M, int BL, bool NT, bool ACC0>
 inline hipError_t launch_vec_mb_one(VecArgs a, hipStream_t s) {
-    constexpr int U = vec_u<M, NT>();
+    constexpr int U = vec_u_dt<DT, OP, M, NT>();
     a.xrun = NT ? xcd_run_shift(vec_xcd_run_kib<M>(), (size_t)BL * U * 16) : 0;
     const unsigned lds = NT ? nt_lds_bytes(reduce_tuning().wg_per_cu_vec, vec_wg_per_cu<M>()) : 0;
     return for_each_launch_piece<BL, U>(a, [&](const VecArgs& p, unsigned grid) {
@@ -191,11 +196,17 @@ inline hipError_t launch_vec_mb_one(VecArgs a, hipStream_t s) {
 
 template <int DT, int OP, int M>
 inline hipError_t launch_vec_m(const VecArgs& a, hipStream_t s) {
-    const ReduceTuning& t = reduce_tuning();
-    const size_t call_bytes = (size_t)(M + 2) * a.nvec * 16;
-    const bool nt = t.nt_mode == 1 || (t.nt_mode < 0 && call_bytes >= t.nt_min_bytes);
-    if (nt) return launch_vec_mb_one<DT, OP, M, 64, true, true>(a, s);
-    return launch_vec_mb_one<DT, OP, M, 256, false, false>(a, s);
+    // The pair and complex types (MAXLOC / MINLOC, complex SUM / PROD) are compiled in the plain
+    // shape only: a rarely used element type does not buy its own streaming instantiations.
+    if constexpr (is_pair_dt<DT>() || is_complex_dt<DT>()) {
+        return launch_vec_mb_one<DT, OP, M, 256, false, false>(a, s);
+    } else {
+        const ReduceTuning& t = reduce_tuning();
+        const size_t call_bytes = (size_t)(M + 2) * a.nvec * 16;
+        const bool nt = t.nt_mode == 1 || (t.nt_mode < 0 && call_bytes >= t.nt_min_bytes);
+        if (nt) return launch_vec_mb_one<DT, OP, M, 64, true, true>(a, s);
+        return launch_vec_mb_one<DT, OP, M, 256, false, false>(a, s);
+    }
 }
 
 template <int DT, int OP>
@@ -225,5 +236,8 @@ inline hipError_t launch_scalar_op(const ScalarArgs& a, hipStream_t s) {
 // Launches for the integer kernel types of reduce_int.hip (kdt/kop from canon_op).
 hipError_t launch_vec_int(const VecArgs& a, int kdt, int kop, int m, hipStream_t s);
 hipError_t launch_scalar_int(const ScalarArgs& a, int kdt, int kop, hipStream_t s);
+// The pair (MAXLOC / MINLOC) and complex (SUM / PROD) types of reduce_pair.hip.
+hipError_t launch_vec_pair(const VecArgs& a, int kdt, int kop, int m, hipStream_t s);
+hipError_t launch_scalar_pair(const ScalarArgs& a, int kdt, int kop, hipStream_t s);
 
 }  // namespace chr

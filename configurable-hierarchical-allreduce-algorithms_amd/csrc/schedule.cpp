@@ -971,7 +971,13 @@ std::string describe(const Plan& p) {
     }
     for (size_t i = 0; i < p.steps.size(); ++i) {
         const Step& s = p.steps[i];
-        o << "step " << i << " " << (s.label.empty() ? "-" : s.label) << " wait=" << s.comm_wait << "\n";
+        o << "step " << i << " " << (s.label.empty() ? "-" : s.label) << " wait=" << s.comm_wait;
+        for (const auto* v : {&s.comm_deps, &s.local_deps}) {
+            o << (v == &s.comm_deps ? " deps=" : " ldeps=");
+            for (size_t j = 0; j < v->size(); ++j) o << (j ? "," : "") << (*v)[j];
+            if (v->empty()) o << "-";
+        }
+        o << "\n";
         for (const Xfer& x : s.sends)
             o << "send " << x.peer << " " << buf_name(x.ref.buf) << " " << x.ref.off << " " << x.count << "\n";
         for (const Xfer& x : s.recvs)

@@ -73,8 +73,9 @@ chr_comm* comm_for(MPI_Comm mc) {
 // MPI_Type_size, all_reduce_radix_batch.cpp:234-277); its arithmetic is MPICH's predefined-op loop
 // for the pair.  C integer types map by size and signedness (MPI_LONG is 64-bit on this LP64
 // platform); MPI_CHAR reduces as a signed char, as in MPICH.  MPI_BYTE takes the bitwise ops and
-// MPI_C_BOOL the logical ones (checked in valid_pair).  Everything else -- MPI_LONG_DOUBLE,
-// complex, pair types for MAXLOC/MINLOC, derived types -- is MPI_ERR_TYPE.
+// MPI_C_BOOL the logical ones (checked in map_pair).  The MAXLOC / MINLOC pair types and the C
+// complex types are supported; everything else -- MPI_LONG_DOUBLE and its pair / complex types,
+// derived types -- is MPI_ERR_TYPE.
 bool map_type(MPI_Datatype d, chr_dtype* out) {
     if (d == MPI_FLOAT) *out = CHR_FLOAT32;
     else if (d == MPI_DOUBLE) *out = CHR_FLOAT64;
@@ -88,12 +89,21 @@ bool map_type(MPI_Datatype d, chr_dtype* out) {
         *out = sizeof(long) == 8 || d != MPI_LONG ? CHR_INT64 : CHR_INT32;
     else if (d == MPI_UNSIGNED_LONG || d == MPI_UNSIGNED_LONG_LONG || d == MPI_UINT64_T)
         *out = sizeof(unsigned long) == 8 || d != MPI_UNSIGNED_LONG ? CHR_UINT64 : CHR_UINT32;
+    // MAXLOC / MINLOC pair types (the C structs MPI defines; element stride = MPI's extent) and the
+    // C complex types
+    else if (d == MPI_FLOAT_INT) *out = CHR_FLOAT_INT;
+    else if (d == MPI_DOUBLE_INT) *out = CHR_DOUBLE_INT;
+    else if (d == MPI_LONG_INT && sizeof(long) == 8) *out = CHR_LONG_INT;
+    else if (d == MPI_2INT) *out = CHR_2INT;
+    else if (d == MPI_SHORT_INT) *out = CHR_SHORT_INT;
+    else if (d == MPI_C_FLOAT_COMPLEX || d == MPI_C_COMPLEX) *out = CHR_C_FLOAT_COMPLEX;
+    else if (d == MPI_C_DOUBLE_COMPLEX) *out = CHR_C_DOUBLE_COMPLEX;
     else return false;
     return true;
 }
 
-// MPI predefined ops.  MPI_MAXLOC/MINLOC, MPI_REPLACE/NO_OP and user ops (MPI_Op_create: a host
-// function pointer the device cannot call) are MPI_ERR_OP.
+// MPI predefined ops.  MPI_REPLACE/NO_OP and user ops (MPI_Op_create: a host function pointer the
+// device cannot call) are MPI_ERR_OP.
 bool map_op(MPI_Op o, chr_op* out) {
     if (o == MPI_SUM) *out = CHR_SUM;
     else if (o == MPI_PROD) *out = CHR_PROD;
@@ -105,6 +115,8 @@ bool map_op(MPI_Op o, chr_op* out) {
     else if (o == MPI_BAND) *out = CHR_BAND;
     else if (o == MPI_BOR) *out = CHR_BOR;
     else if (o == MPI_BXOR) *out = CHR_BXOR;
+    else if (o == MPI_MAXLOC) *out = CHR_MAXLOC;
+    else if (o == MPI_MINLOC) *out = CHR_MINLOC;
     else return false;
     return true;
 }
@@ -120,6 +132,12 @@ int map_pair(MPI_Datatype d, MPI_Op o, chr_dtype* dt, chr_op* op) {
     if (d == MPI_BYTE && !bitwise) return MPI_ERR_OP;
     if (d == MPI_C_BOOL && !logical) return MPI_ERR_OP;
     if ((*dt == CHR_FLOAT32 || *dt == CHR_FLOAT64) && bitwise) return MPI_ERR_OP;
+    // MAXLOC / MINLOC only on the pair types, which take nothing else; complex takes SUM / PROD only
+    const bool loc = *op == CHR_MAXLOC || *op == CHR_MINLOC;
+    const bool pair = *dt >= CHR_FLOAT_INT && *dt <= CHR_SHORT_INT;
+    const bool cplx = *dt == CHR_C_FLOAT_COMPLEX || *dt == CHR_C_DOUBLE_COMPLEX;
+    if (loc != pair) return MPI_ERR_OP;
+    if (cplx && *op != CHR_SUM && *op != CHR_PROD) return MPI_ERR_OP;
     return 0;
 }
 

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define CHR_ABI_VERSION 4
+#define CHR_ABI_VERSION 5
 
 /* Element types.  The reference is generic over MPI_Datatype (all_reduce_radix_batch.cpp:202-204,
  * sizes from MPI_Type_size at :234-277); these are the MPI predefined types MPICH's
@@ -39,18 +39,31 @@ typedef enum {
     CHR_UINT16 = 7,    /* MPI_UNSIGNED_SHORT, MPI_UINT16_T */
     CHR_UINT32 = 8,    /* MPI_UNSIGNED, MPI_UINT32_T */
     CHR_INT64 = 9,     /* MPI_LONG, MPI_LONG_LONG, MPI_INT64_T */
-    CHR_UINT64 = 10    /* MPI_UNSIGNED_LONG, MPI_UNSIGNED_LONG_LONG, MPI_UINT64_T */
+    CHR_UINT64 = 10,   /* MPI_UNSIGNED_LONG, MPI_UNSIGNED_LONG_LONG, MPI_UINT64_T */
+    /* The value/index pair types of MPI_MAXLOC / MPI_MINLOC, one element = the C struct MPI defines
+     * ({value; int index}, naturally aligned; sizes below are the element stride, i.e. MPI's extent). */
+    CHR_FLOAT_INT = 11,   /* MPI_FLOAT_INT   {float; int}    8 B */
+    CHR_DOUBLE_INT = 12,  /* MPI_DOUBLE_INT  {double; int}  16 B (MPI_Type_size 12) */
+    CHR_LONG_INT = 13,    /* MPI_LONG_INT    {long; int}    16 B (MPI_Type_size 12) */
+    CHR_2INT = 14,        /* MPI_2INT        {int; int}      8 B */
+    CHR_SHORT_INT = 15,   /* MPI_SHORT_INT   {short; int}    8 B (MPI_Type_size 6) */
+    /* C99 complex types: SUM and PROD (C99 Annex G multiplication, as MPICH's C loop does) */
+    CHR_C_FLOAT_COMPLEX = 16,   /* MPI_C_FLOAT_COMPLEX (MPI_C_COMPLEX)  8 B */
+    CHR_C_DOUBLE_COMPLEX = 17   /* MPI_C_DOUBLE_COMPLEX                16 B */
 } chr_dtype;
 
 /* Reduction ops: MPI's predefined ops with MPICH 3.3.2's element semantics
- * (inout[i] = inout[i] OP in[i]).  SUM/PROD/MAX/MIN on every type; the logical ops (result 0 or
- * 1) on the integer types and on float/double (MPICH accepts those; C truth: NaN is true, -0
- * false); the bitwise ops on the integer types only.  MPI_MAXLOC/MINLOC and user ops (MPI_Op_create)
- * are not supported (CHR_ERR_INVALID_ARG; MPI_ERR_OP through the shim). */
+ * (inout[i] = inout[i] OP in[i]), and MPICH's table of which (type, op) pairs it accepts.  SUM/PROD/
+ * MAX/MIN on every integer and floating type; the logical ops (result 0 or 1) on the integer types
+ * and on float/double (MPICH accepts those; C truth: NaN is true, -0 false); the bitwise ops on the
+ * integer types only; MAXLOC/MINLOC on the five pair types only (equal values: the lower index wins,
+ * the inout element is kept otherwise; NaN compares keep inout); SUM/PROD on the complex types only.
+ * User ops (MPI_Op_create) are not supported (CHR_ERR_INVALID_ARG; MPI_ERR_OP through the shim). */
 typedef enum {
     CHR_SUM = 0, CHR_PROD = 1, CHR_MAX = 2, CHR_MIN = 3,
     CHR_LAND = 4, CHR_LOR = 5, CHR_LXOR = 6,  /* MPI_LAND, MPI_LOR, MPI_LXOR */
-    CHR_BAND = 7, CHR_BOR = 8, CHR_BXOR = 9   /* MPI_BAND, MPI_BOR, MPI_BXOR */
+    CHR_BAND = 7, CHR_BOR = 8, CHR_BXOR = 9,  /* MPI_BAND, MPI_BOR, MPI_BXOR */
+    CHR_MAXLOC = 10, CHR_MINLOC = 11          /* MPI_MAXLOC, MPI_MINLOC */
 } chr_op;
 
 typedef enum {

@@ -18,6 +18,7 @@
  */
 #include "chiara_oracle.h"
 
+#include <math.h>
 #include <stdlib.h>
 
 size_t orc_dtype_size(int dtype) {
@@ -30,7 +31,106 @@ size_t orc_dtype_size(int dtype) {
     case ORC_I16: case ORC_U16: return 2;
     case ORC_U32: return 4;
     case ORC_I64: case ORC_U64: return 8;
+    case ORC_FI: case ORC_2I: case ORC_SI: case ORC_CF: return 8;
+    case ORC_DI: case ORC_LI: case ORC_CD: return 16;
     default: return 0;
+    }
+}
+
+int orc_valid(int dtype, int op) {
+    if (!orc_dtype_size(dtype) || op < ORC_SUM || op > ORC_MINLOC) return 0;
+    if (dtype >= ORC_FI && dtype <= ORC_SI) return op == ORC_MAXLOC || op == ORC_MINLOC;
+    if (dtype == ORC_CF || dtype == ORC_CD) return op == ORC_SUM || op == ORC_PROD;
+    if (op >= ORC_MAXLOC) return 0;
+    if (dtype == ORC_BF16) return op <= ORC_MIN;
+    if (dtype == ORC_F32 || dtype == ORC_F64) return op <= ORC_LXOR;
+    return 1;
+}
+
+/* The pair and complex element structs (C layout, as MPI defines the types). */
+typedef struct { float v; int32_t i; } orc_fi;
+typedef struct { double v; int32_t i; } orc_di;
+typedef struct { int64_t v; int32_t i; } orc_li;
+typedef struct { int32_t v; int32_t i; } orc_2i;
+typedef struct { int16_t v; int32_t i; } orc_si;
+typedef struct { float re, im; } orc_cf;
+typedef struct { double re, im; } orc_cd;
+
+/* Pair and complex types: value = a small integer in [-4, 3] (UNIFORM / SPARSE; many ties, so
+ * MAXLOC's lower-index rule is exercised), rank*count + i (SEQ, index = rank), or for the floating
+ * pairs {+0, -0, 1, -1, 0.5, NaN with a per-rank payload} (TIES); index from 6 random bits.  Complex:
+ * U[-1,1) parts from elements 2g and 2g + 1 of the float generator (UNIFORM), rank*count + i and its
+ * negation (SEQ), the float TIES values.  Padding bytes are zero. */
+static void orc_fill_pair(void* elem, int dtype, int pattern, uint64_t seed, int rank, uint64_t count_for_seq,
+                          uint64_t g) {
+    static const float ft[8] = {0.0f, -0.0f, 1.0f, -1.0f, 0.0f, -0.0f, 0.5f, 0.0f};
+    const uint64_t key = orc_key(seed, (uint64_t)rank, g);
+    const unsigned sel = (unsigned)(key >> 61);
+    const uint32_t pay = (uint32_t)(rank + 1) & 0x3Fu;
+    const int32_t small = (int32_t)(key >> 61) - 4;
+    const int32_t idx = pattern == ORC_PAT_SEQ ? rank : (int32_t)((key >> 32) & 0x3F);
+    const int32_t seq = (int32_t)(uint32_t)((uint64_t)rank * count_for_seq + g);
+    memset(elem, 0, orc_dtype_size(dtype));
+    if (dtype == ORC_FI || dtype == ORC_DI) {
+        double v = pattern == ORC_PAT_SEQ ? (double)seq : (double)small;
+        int nan = 0;
+        if (pattern == ORC_PAT_TIES) {
+            v = (double)ft[sel];
+            nan = sel == 7;
+        }
+        if (dtype == ORC_FI) {
+            orc_fi* e = (orc_fi*)elem;
+            e->v = (float)v;
+            if (nan) {
+                uint32_t u = 0x7FC00000u | (pay << 16) | pay;
+                memcpy(&e->v, &u, 4);
+            } else if (pattern == ORC_PAT_TIES) {
+                memcpy(&e->v, &ft[sel], 4); /* keeps the sign of -0 */
+            }
+            e->i = idx;
+        } else {
+            orc_di* e = (orc_di*)elem;
+            e->v = v;
+            if (nan) {
+                uint64_t u = 0x7FF8000000000000ull | ((uint64_t)pay << 40) | pay;
+                memcpy(&e->v, &u, 8);
+            }
+            e->i = idx;
+        }
+        return;
+    }
+    {
+        const int64_t v = pattern == ORC_PAT_SEQ ? (int64_t)seq : (int64_t)small;
+        switch (dtype) {
+        case ORC_LI: ((orc_li*)elem)->v = v; ((orc_li*)elem)->i = idx; return;
+        case ORC_2I: ((orc_2i*)elem)->v = (int32_t)v; ((orc_2i*)elem)->i = idx; return;
+        case ORC_SI: ((orc_si*)elem)->v = (int16_t)v; ((orc_si*)elem)->i = idx; return;
+        }
+    }
+    if (dtype == ORC_CF) {
+        orc_cf* e = (orc_cf*)elem;
+        if (pattern == ORC_PAT_SEQ) {
+            e->re = (float)seq;
+            e->im = -(float)seq;
+        } else if (pattern == ORC_PAT_TIES) {
+            e->re = ft[sel];
+            e->im = ft[(key >> 58) & 7];
+        } else {
+            e->re = orc_gen_f32(seed, (uint64_t)rank, 2 * g);
+            e->im = orc_gen_f32(seed, (uint64_t)rank, 2 * g + 1);
+        }
+    } else if (dtype == ORC_CD) {
+        orc_cd* e = (orc_cd*)elem;
+        if (pattern == ORC_PAT_SEQ) {
+            e->re = (double)seq;
+            e->im = -(double)seq;
+        } else if (pattern == ORC_PAT_TIES) {
+            e->re = (double)ft[sel];
+            e->im = (double)ft[(key >> 58) & 7];
+        } else {
+            e->re = orc_gen_f64(seed, (uint64_t)rank, 2 * g);
+            e->im = orc_gen_f64(seed, (uint64_t)rank, 2 * g + 1);
+        }
     }
 }
 
@@ -39,7 +139,13 @@ size_t orc_dtype_size(int dtype) {
 void orc_fill_at(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int rank,
                  uint64_t count_for_seq, uint64_t start) {
     size_t i;
-    const size_t ies = (dtype >= ORC_I8 || (dtype == ORC_I32 && pattern == ORC_PAT_SPARSE)) ? orc_dtype_size(dtype) : 0;
+    const size_t ies = ((dtype >= ORC_I8 && dtype <= ORC_U64) || (dtype == ORC_I32 && pattern == ORC_PAT_SPARSE))
+                           ? orc_dtype_size(dtype) : 0;
+    if (dtype >= ORC_FI && dtype <= ORC_CD) {
+        const size_t es = orc_dtype_size(dtype);
+        for (i = 0; i < n; ++i) orc_fill_pair((char*)buf + i * es, dtype, pattern, seed, rank, count_for_seq, start + i);
+        return;
+    }
     for (i = 0; i < n; ++i) {
         const uint64_t g = start + i;
         if (ies) {
@@ -145,8 +251,99 @@ void orc_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int ra
     case ORC_BXOR: ORC_LOOP(T, (T)(y ^ x)); break;                                       \
     }
 
+/* MPICH 3.3.2's MAXLOC / MINLOC loop (src/mpi/coll/op/opmaxloc.c, opminloc.c; a = inoutvec,
+ * b = invec): `if (a.value == b.value) a.loc = MIN(a.loc, b.loc); else if (a.value < b.value) a = b;`
+ * (MINLOC: `>`).  Ties keep a's value bits (-0 vs +0), NaN compares keep a, a better b replaces the
+ * whole element.  Pinned by tests/golden/pairs_reduce_local.npz (MPICH's own outputs). */
+#define ORC_LOC_LOOP(T, BETTER)                                                      \
+    do {                                                                             \
+        const T* xs = (const T*)in;                                                  \
+        T* ys = (T*)inout;                                                           \
+        size_t i;                                                                    \
+        for (i = 0; i < n; ++i) {                                                    \
+            if (ys[i].v == xs[i].v) ys[i].i = xs[i].i < ys[i].i ? xs[i].i : ys[i].i; \
+            else if (BETTER) memcpy(&ys[i], &xs[i], sizeof(T)); /* padding too */    \
+        }                                                                            \
+    } while (0)
+#define ORC_LOC_CASE(T)                                        \
+    if (op == ORC_MAXLOC) ORC_LOC_LOOP(T, ys[i].v < xs[i].v);  \
+    else if (op == ORC_MINLOC) ORC_LOC_LOOP(T, ys[i].v > xs[i].v)
+
+/* C99 Annex G complex multiplication, as libgcc's __mulsc3 / __muldc3 restate it (what MPICH's
+ * `a = a * b` on `float _Complex` compiles to): products rounded one by one, and when both parts
+ * come out NaN, the infinity recovery of C11 G.5.1.  (a + bi) = inout, (c + di) = in. */
+#define ORC_CMUL(F, INF, a_, b_, c_, d_, re_, im_)                                                 \
+    do {                                                                                          \
+        F a = (a_), b = (b_), c = (c_), d = (d_);                                                 \
+        F ac = a * c, bd = b * d, ad = a * d, bc = b * c;                                         \
+        F x = ac - bd, y = ad + bc;                                                               \
+        if (isnan(x) && isnan(y)) {                                                               \
+            int recalc = 0;                                                                       \
+            if (isinf(a) || isinf(b)) {                                                           \
+                a = copysign(isinf(a) ? (F)1 : (F)0, a);                                          \
+                b = copysign(isinf(b) ? (F)1 : (F)0, b);                                          \
+                if (isnan(c)) c = copysign((F)0, c);                                              \
+                if (isnan(d)) d = copysign((F)0, d);                                              \
+                recalc = 1;                                                                       \
+            }                                                                                     \
+            if (isinf(c) || isinf(d)) {                                                           \
+                c = copysign(isinf(c) ? (F)1 : (F)0, c);                                          \
+                d = copysign(isinf(d) ? (F)1 : (F)0, d);                                          \
+                if (isnan(a)) a = copysign((F)0, a);                                              \
+                if (isnan(b)) b = copysign((F)0, b);                                              \
+                recalc = 1;                                                                       \
+            }                                                                                     \
+            if (!recalc && (isinf(ac) || isinf(bd) || isinf(ad) || isinf(bc))) {                  \
+                if (isnan(a)) a = copysign((F)0, a);                                              \
+                if (isnan(b)) b = copysign((F)0, b);                                              \
+                if (isnan(c)) c = copysign((F)0, c);                                              \
+                if (isnan(d)) d = copysign((F)0, d);                                              \
+                recalc = 1;                                                                       \
+            }                                                                                     \
+            if (recalc) {                                                                         \
+                x = (F)(INF) * (a * c - b * d);                                                   \
+                y = (F)(INF) * (a * d + b * c);                                                   \
+            }                                                                                     \
+        }                                                                                         \
+        (re_) = x;                                                                                \
+        (im_) = y;                                                                                \
+    } while (0)
+
 void orc_reduce_local(const void* in, void* inout, size_t n, int dtype, int op) {
     switch (dtype) {
+    case ORC_FI: ORC_LOC_CASE(orc_fi); break;
+    case ORC_DI: ORC_LOC_CASE(orc_di); break;
+    case ORC_LI: ORC_LOC_CASE(orc_li); break;
+    case ORC_2I: ORC_LOC_CASE(orc_2i); break;
+    case ORC_SI: ORC_LOC_CASE(orc_si); break;
+    case ORC_CF: {
+        const orc_cf* xs = (const orc_cf*)in;
+        orc_cf* ys = (orc_cf*)inout;
+        size_t i;
+        for (i = 0; i < n; ++i) {
+            if (op == ORC_SUM) {
+                ys[i].re = ys[i].re + xs[i].re;
+                ys[i].im = ys[i].im + xs[i].im;
+            } else {
+                ORC_CMUL(float, INFINITY, ys[i].re, ys[i].im, xs[i].re, xs[i].im, ys[i].re, ys[i].im);
+            }
+        }
+        break;
+    }
+    case ORC_CD: {
+        const orc_cd* xs = (const orc_cd*)in;
+        orc_cd* ys = (orc_cd*)inout;
+        size_t i;
+        for (i = 0; i < n; ++i) {
+            if (op == ORC_SUM) {
+                ys[i].re = ys[i].re + xs[i].re;
+                ys[i].im = ys[i].im + xs[i].im;
+            } else {
+                ORC_CMUL(double, INFINITY, ys[i].re, ys[i].im, xs[i].re, xs[i].im, ys[i].re, ys[i].im);
+            }
+        }
+        break;
+    }
     /* MPICH 3.3.2 also takes LAND/LOR/LXOR on float and double (probed: rc 0), C truth values. */
     case ORC_F32:
         if (op == ORC_SUM) ORC_LOOP(float, y + x);
@@ -318,9 +515,7 @@ static int orc_phases_0_2(orc_state* s, int nranks, int k_in, int b, size_t recv
     memset(s, 0, sizeof(*s));
     if (b < 1 || nranks < 1 || nranks % b != 0 || k_in < 2) return 1;
     s->es = orc_dtype_size(dtype);
-    if (!s->es || op < ORC_SUM || op > ORC_BXOR || (op > ORC_MIN && dtype == ORC_BF16) ||
-        (op > ORC_LXOR && (dtype == ORC_F32 || dtype == ORC_F64)))
-        return 1;
+    if (!s->es || !orc_valid(dtype, op)) return 1;
     s->nranks = nranks;
     s->b = b;
     s->recvcount = recvcount;

@@ -30,12 +30,21 @@ extern "C" {
 /* Same numbering as include/chiara.h (chr_dtype / chr_op). */
 enum {
     ORC_F32 = 0, ORC_F64 = 1, ORC_I32 = 2, ORC_BF16 = 3,
-    ORC_I8 = 4, ORC_U8 = 5, ORC_I16 = 6, ORC_U16 = 7, ORC_U32 = 8, ORC_I64 = 9, ORC_U64 = 10
+    ORC_I8 = 4, ORC_U8 = 5, ORC_I16 = 6, ORC_U16 = 7, ORC_U32 = 8, ORC_I64 = 9, ORC_U64 = 10,
+    /* MPI's pair types for MAXLOC / MINLOC ({value; int index} C structs, element = MPI extent) */
+    ORC_FI = 11, ORC_DI = 12, ORC_LI = 13, ORC_2I = 14, ORC_SI = 15,
+    /* MPI_C_FLOAT_COMPLEX, MPI_C_DOUBLE_COMPLEX */
+    ORC_CF = 16, ORC_CD = 17
 };
 enum {
     ORC_SUM = 0, ORC_PROD = 1, ORC_MAX = 2, ORC_MIN = 3,
-    ORC_LAND = 4, ORC_LOR = 5, ORC_LXOR = 6, ORC_BAND = 7, ORC_BOR = 8, ORC_BXOR = 9
+    ORC_LAND = 4, ORC_LOR = 5, ORC_LXOR = 6, ORC_BAND = 7, ORC_BOR = 8, ORC_BXOR = 9,
+    ORC_MAXLOC = 10, ORC_MINLOC = 11
 };
+
+/* MPICH 3.3.2's (type, op) table as MPI_Reduce_local applies it (probed; pairs and complex:
+ * oracle/ref_pairs_probe table, tests/golden/pairs_manifest.json); bf16 takes SUM/PROD/MAX/MIN. */
+int orc_valid(int dtype, int op);
 
 /* Input patterns for the generator. */
 enum {
@@ -88,7 +97,7 @@ static inline double orc_gen_f64(uint64_t seed, uint64_t rank, uint64_t i) {
     return (double)(u >> 11) * (1.0 / 4503599627370496.0) - 1.0;
 }
 
-size_t orc_dtype_size(int dtype);
+size_t orc_dtype_size(int dtype);  /* the element stride: MPI's extent for the pair types */
 
 /* Fill `n` elements of rank `rank`'s buffer.  `count_for_seq` is the per-rank element
  * count used by the SEQ pattern (value = rank*count_for_seq + i, wrapping int32). */

@@ -14,10 +14,28 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 DTYPES = {"f32": 0, "f64": 1, "i32": 2, "bf16": 3, "i8": 4, "u8": 5, "i16": 6, "u16": 7, "u32": 8, "i64": 9,
-          "u64": 10}
-OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "land": 4, "lor": 5, "lxor": 6, "band": 7, "bor": 8, "bxor": 9}
+          "u64": 10, "fi": 11, "di": 12, "li": 13, "2i": 14, "si": 15, "cf": 16, "cd": 17}
+OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "land": 4, "lor": 5, "lxor": 6, "band": 7, "bor": 8, "bxor": 9,
+       "maxloc": 10, "minloc": 11}
+
+
+def _pair(vfmt, ioff, size):
+    return np.dtype({"names": ["v", "i"], "formats": [vfmt, "<i4"], "offsets": [0, ioff], "itemsize": size})
+
+
 NP_DTYPES = {"f32": np.float32, "f64": np.float64, "i32": np.int32, "bf16": np.uint16, "i8": np.int8, "u8": np.uint8,
-             "i16": np.int16, "u16": np.uint16, "u32": np.uint32, "i64": np.int64, "u64": np.uint64}
+             "i16": np.int16, "u16": np.uint16, "u32": np.uint32, "i64": np.int64, "u64": np.uint64,
+             # MPI's MAXLOC / MINLOC pair types (C struct layouts) and the C complex types
+             "fi": _pair("<f4", 4, 8), "di": _pair("<f8", 8, 16), "li": _pair("<i8", 8, 16), "2i": _pair("<i4", 4, 8),
+             "si": _pair("<i2", 4, 8), "cf": np.complex64, "cd": np.complex128}
+PAIR_DTYPES = ("fi", "di", "li", "2i", "si")
+COMPLEX_DTYPES = ("cf", "cd")
+
+
+def valid(dtype, op):
+    """MPICH 3.3.2's (type, op) table (chiara_oracle.c orc_valid)."""
+    lib().orc_valid.restype = ctypes.c_int
+    return bool(lib().orc_valid(DTYPES[dtype], OPS[op]))
 INT_DTYPES = ("i32", "i8", "u8", "i16", "u16", "u32", "i64", "u64")
 PAT_UNIFORM, PAT_SEQ, PAT_TIES, PAT_SPARSE = 0, 1, 2, 3
 

@@ -81,6 +81,22 @@ def golden_types():
 
 
 @pytest.fixture(scope="session")
+def golden_pairtypes():
+    """Golden vectors of MPI's pair types (MAXLOC / MINLOC) and the C complex types (SUM / PROD) from
+    the reference compiled here, or MPI's own collective where the reference cannot address the
+    type (gen_golden.py pairs; modes ar_lib / rs_lib).  Outputs are stored as raw bytes."""
+    import json
+
+    import numpy as np
+
+    here = os.path.join(REPO, "tests", "golden")
+    with open(os.path.join(here, "pairtypes_manifest.json")) as f:
+        manifest = json.load(f)
+    arrays = np.load(os.path.join(here, "pairtypes_outputs.npz"), allow_pickle=False)
+    return manifest["cases"], arrays
+
+
+@pytest.fixture(scope="session")
 def golden_rsmpich():
     """Golden vectors of the MPICH baseline reduce-scatters that
     testing/mpich_implementations/reduce_scatter/main.cpp drives (gen_golden.py rsmpich)."""

@@ -198,6 +198,45 @@ def types_cases_for(n):
     return out
 
 
+def pairs_cases_for(n):
+    """MPI's pair types under MAXLOC / MINLOC and the C complex types under SUM / PROD through the
+    radix/batch collectives and three MPICH baselines (the reference is generic over MPI_Datatype x
+    MPI_Op, all_reduce_radix_batch.cpp:202-204; its arithmetic is MPICH's MPI_Reduce_local).  The
+    reference addresses its buffers with MPI_Type_size as the element stride (:238-256), which is the
+    C struct's size only for MPI_FLOAT_INT, MPI_2INT and the complex types; for MPI_DOUBLE_INT,
+    MPI_LONG_INT and MPI_SHORT_INT (size 12 / 12 / 6, extent 16 / 16 / 8) the expected output is MPI's
+    own collective instead (modes ar_lib / rs_lib; MAXLOC / MINLOC on these values are associative
+    and commutative, so every correct schedule gives those bits).  fi also runs the TIES pattern
+    (-0 / +0, NaN): MPICH keeps inout on ties and NaN compares, so the operand order shows."""
+    out = []
+
+    def add(mode, k, b, count, dt, op, pat, inplace):
+        cid = f"{mode}_n{n}_k{k}_b{b}_c{count}_{dt}_{op}_p{pat}_ip{inplace}"
+        out.append(dict(id=cid, mode=mode, n=n, k=k, b=b, count=count, dtype=dt, op=op,
+                        pattern=pat, seed=SEED, inplace=inplace))
+
+    ref_ok = {"fi": ("maxloc", "minloc"), "2i": ("maxloc", "minloc"), "cf": ("sum", "prod"), "cd": ("sum", "prod")}
+    for dt, ops in ref_ok.items():
+        for op in ops:
+            pats = [pyoracle.PAT_UNIFORM] + ([pyoracle.PAT_TIES] if dt == "fi" else [])
+            for pat in pats:
+                for i, b in enumerate(divisors(n)):
+                    k = (2, 3, 4)[i % 3]
+                    add("ar", k, b, n * 12 + (n if i % 2 else 0), dt, op, pat, i % 2)
+                    add("rs", k, b, 7 + i, dt, op, pat, 0)
+                add("rx", 3, 0, 40, dt, op, pat, 0)
+                add("ring", 0, 0, 3 * n + 5, dt, op, pat, 0)
+                add("rm", 2, 0, 33, dt, op, pat, 1)
+        add("ag", 2, 2 if n >= 4 and n % 2 == 0 else n, 9, dt, ops[0], pyoracle.PAT_UNIFORM, 0)
+    for dt in ("di", "li", "si"):
+        for op in ("maxloc", "minloc"):
+            for i, b in enumerate(divisors(n)):
+                k = (2, 3, 4)[i % 3]
+                add("ar_lib", k, b, n * 12 + (n if i % 2 else 0), dt, op, pyoracle.PAT_UNIFORM, 0)
+                add("rs_lib", k, b, 7 + i, dt, op, pyoracle.PAT_UNIFORM, 0)
+    return out
+
+
 def rsmpich_cases_for(n):
     """testing/mpich_implementations/reduce_scatter/: radix (k), recursive halving, recursive
     doubling (relays for non-powers of two) and pairwise, driven by that directory's main.cpp
@@ -260,6 +299,10 @@ def main():
         for n in (2, 3, 4, 6, 8):
             all_cases += types_cases_for(n)
         prefix = "types_"
+    elif which == "pairs":
+        for n in (2, 3, 4, 5, 6, 8):
+            all_cases += pairs_cases_for(n)
+        prefix = "pairtypes_"
     else:
         prefix = ""
         for n in (1, 2, 3, 4, 5, 6, 8, 9, 12, 16):
@@ -286,6 +329,23 @@ def main():
             npdt = pyoracle.NP_DTYPES[c["dtype"]]
             a = np.frombuffer(out, dtype=npdt)
             lb = np.frombuffer(libb, dtype=npdt)
+            if c["dtype"] in pyoracle.PAIR_DTYPES + pyoracle.COMPLEX_DTYPES:
+                # element-wise byte comparison (structured / complex elements)
+                isz = np.dtype(npdt).itemsize
+                ab = np.frombuffer(out, dtype=np.uint8).reshape(-1, isz)
+                lbb = np.frombuffer(libb, dtype=np.uint8).reshape(-1, isz)
+                rec["n_diff_vs_lib"] = int(np.count_nonzero((ab != lbb).any(axis=1)))
+                if c["dtype"] in pyoracle.COMPLEX_DTYPES:
+                    d = np.abs(a.astype(np.complex128) - lb.astype(np.complex128))
+                    rec["max_abs_diff_vs_lib"] = float(np.max(d[np.isfinite(d)])) if np.isfinite(d).any() else 0.0
+                else:
+                    rec["max_abs_diff_vs_lib"] = 0.0 if rec["n_diff_vs_lib"] == 0 else float("nan")
+                rec["stored"] = len(out) <= STORE_LIMIT
+                if rec["stored"]:
+                    arrays[c["id"]] = np.frombuffer(out, dtype=np.uint8).copy()
+                    arrays[c["id"] + "__lib"] = np.frombuffer(libb, dtype=np.uint8).copy()
+                manifest.append(rec)
+                continue
             if c["dtype"] == "bf16":
                 af = (a.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
                 lf = (lb.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
@@ -310,6 +370,10 @@ def main():
                 "Fugaku_experiments/{Allreduce,Reduce-scatter,Allgather} + testing/mpich_implementations/"
                 "all_reduce/{allreduce_ring,allreduce_recexch,allreduce_recursive_multiplying}.cpp, integer types "
                 "beyond int32 and the logical/bitwise ops" if which == "types" else
+                "Fugaku_experiments/{Allreduce,Reduce-scatter,Allgather} + testing/mpich_implementations/"
+                "all_reduce/{allreduce_ring,allreduce_recexch,allreduce_recursive_multiplying}.cpp, MPI pair types "
+                "(MAXLOC/MINLOC) and C complex types (SUM/PROD); ar_lib/rs_lib: MPI_Allreduce / "
+                "MPI_Reduce_scatter_block (see pairs_cases_for)" if which == "pairs" else
                 "testing/mpich_implementations/all_reduce/{allreduce_ring,allreduce_recursive_doubling,"
                 "allreduce_reduce_scatter_allgather,allreduce_recexch,allreduce_k_reduce_scatter_allgather,"
                 "allreduce_recursive_multiplying}.cpp" if which == "mpich" else

@@ -15,9 +15,11 @@ import pyoracle as po
 pytestmark = pytest.mark.gpu
 
 DT = {"f32": ca.FLOAT32, "f64": ca.FLOAT64, "i32": ca.INT32, "bf16": ca.BFLOAT16, "i8": ca.INT8, "u8": ca.UINT8,
-      "i16": ca.INT16, "u16": ca.UINT16, "u32": ca.UINT32, "i64": ca.INT64, "u64": ca.UINT64}
+      "i16": ca.INT16, "u16": ca.UINT16, "u32": ca.UINT32, "i64": ca.INT64, "u64": ca.UINT64,
+      "fi": ca.FLOAT_INT, "di": ca.DOUBLE_INT, "li": ca.LONG_INT, "2i": ca.TWO_INT, "si": ca.SHORT_INT,
+      "cf": ca.C_FLOAT_COMPLEX, "cd": ca.C_DOUBLE_COMPLEX}
 OP = {"sum": ca.SUM, "prod": ca.PROD, "max": ca.MAX, "min": ca.MIN, "land": ca.LAND, "lor": ca.LOR,
-      "lxor": ca.LXOR, "band": ca.BAND, "bor": ca.BOR, "bxor": ca.BXOR}
+      "lxor": ca.LXOR, "band": ca.BAND, "bor": ca.BOR, "bxor": ca.BXOR, "maxloc": ca.MAXLOC, "minloc": ca.MINLOC}
 
 
 @pytest.fixture(scope="module")
@@ -101,6 +103,49 @@ def test_local_group_exact_schedule_matches_reference_golden(gu, groups, golden)
             outs = run_local(gu, g, c["mode"], sends, c["k"], c["b"], c["dtype"], c["op"], bool(c["inplace"]))
         finally:
             g.set_schedule(ca.SCHEDULE_FLAT)
+        if hashlib.sha256(b"".join(o.tobytes() for o in outs)).hexdigest() != c["sha256"]:
+            bad.append(c["id"])
+    assert not bad, f"{len(bad)} device/reference mismatches, e.g. {bad[:5]}"
+
+
+def _golden_on_device(gu, groups, c, schedule):
+    """One golden case through the local group: the radix/batch collectives (ar_lib / rs_lib: the
+    same calls, compared with MPI's own collective) or an MPICH baseline; every rank's output."""
+    n, g = c["n"], groups(c["n"])
+    mode = {"ar_lib": "ar", "rs_lib": "rs"}.get(c["mode"], c["mode"])
+    if mode in ("ar", "rs", "ag"):
+        in_n = c["count"] * n if mode == "rs" else c["count"]
+        sends = [po.fill(in_n, c["dtype"], c["pattern"], c["seed"], r) for r in range(n)]
+        g.set_schedule(ca.SCHEDULE_EXACT if schedule == "exact" else ca.SCHEDULE_FLAT)
+        try:
+            return run_local(gu, g, mode, sends, c["k"], c["b"], c["dtype"], c["op"], bool(c["inplace"]))
+        finally:
+            g.set_schedule(ca.SCHEDULE_FLAT)
+    npdt = po.NP_DTYPES[c["dtype"]]
+    sends = [po.fill(c["count"], c["dtype"], c["pattern"], c["seed"], r) for r in range(n)]
+    d_send = [gu.to_dev(x) for x in sends]
+    if c["inplace"]:
+        d_recv, d_sendp = d_send, [ca.IN_PLACE] * n
+    else:
+        d_recv, d_sendp = [gu.empty_dev(x.nbytes) for x in sends], d_send
+    assert g.allreduce_mpich(MPICH_MODE[mode], d_sendp, d_recv, c["count"], DT[c["dtype"]], OP[c["op"]],
+                             c["k"], c["b"]) == 0, c["id"]
+    return [gu.from_dev(d, npdt, c["count"]) for d in d_recv]
+
+
+@pytest.mark.parametrize("schedule", ["flat", "exact"])
+def test_pair_and_complex_types_match_reference_golden(gu, groups, golden_pairtypes, schedule):
+    """MPI_MAXLOC / MPI_MINLOC on the five pair types and SUM / PROD on the C complex types (the
+    reference's generic MPI_Datatype x MPI_Op, all_reduce_radix_batch.cpp:202-204): every golden
+    case bit-exact on the device -- the reference run here under MPICH 3.3.2 for MPI_FLOAT_INT,
+    MPI_2INT and complex (the TIES pattern's -0 / +0 and NaN expose the operand order), MPI's own
+    collective for the types the reference mis-strides (gen_golden.py pairs_cases_for)."""
+    cases, _ = golden_pairtypes
+    bad = []
+    for c in cases:
+        if schedule == "exact" and c["mode"] not in ("ar", "rs", "ar_lib", "rs_lib"):
+            continue
+        outs = _golden_on_device(gu, groups, c, schedule)
         if hashlib.sha256(b"".join(o.tobytes() for o in outs)).hexdigest() != c["sha256"]:
             bad.append(c["id"])
     assert not bad, f"{len(bad)} device/reference mismatches, e.g. {bad[:5]}"

@@ -11,9 +11,11 @@ import pyoracle as po
 pytestmark = pytest.mark.gpu
 
 DT = {"f32": ca.FLOAT32, "f64": ca.FLOAT64, "i32": ca.INT32, "bf16": ca.BFLOAT16, "i8": ca.INT8, "u8": ca.UINT8,
-      "i16": ca.INT16, "u16": ca.UINT16, "u32": ca.UINT32, "i64": ca.INT64, "u64": ca.UINT64}
+      "i16": ca.INT16, "u16": ca.UINT16, "u32": ca.UINT32, "i64": ca.INT64, "u64": ca.UINT64,
+      "fi": ca.FLOAT_INT, "di": ca.DOUBLE_INT, "li": ca.LONG_INT, "2i": ca.TWO_INT, "si": ca.SHORT_INT,
+      "cf": ca.C_FLOAT_COMPLEX, "cd": ca.C_DOUBLE_COMPLEX}
 OP = {"sum": ca.SUM, "prod": ca.PROD, "max": ca.MAX, "min": ca.MIN, "land": ca.LAND, "lor": ca.LOR,
-      "lxor": ca.LXOR, "band": ca.BAND, "bor": ca.BOR, "bxor": ca.BXOR}
+      "lxor": ca.LXOR, "band": ca.BAND, "bor": ca.BOR, "bxor": ca.BXOR, "maxloc": ca.MAXLOC, "minloc": ca.MINLOC}
 INT_OPS = ("sum", "prod", "max", "min", "land", "lor", "lxor", "band", "bor", "bxor")
 
 
@@ -25,7 +27,15 @@ def gu():
 
 
 def _bits(a):
+    """Raw element bits (structured pair / complex elements: their bytes, padding included)."""
+    if a.dtype.names is not None or a.itemsize == 16:
+        return a.view(np.uint8)
     return a.view({1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[a.itemsize])
+
+
+def _bytes_copy(a):
+    """A copy that keeps padding bytes (a structured array's .copy() does not)."""
+    return a.view(np.uint8).copy().view(a.dtype)
 
 
 def _check_multi(gu, dtype, op, m, n, off=0, in_off=None, seed=5, pattern=0):
@@ -49,7 +59,7 @@ def _check_multi(gu, dtype, op, m, n, off=0, in_off=None, seed=5, pattern=0):
     assert rc == 0
     gu.sync()
     got = gu.from_dev(d_acc, npdt)[off:off + n]
-    ref = po.reduce_multi(acc.copy(), ins, dtype, op)
+    ref = po.reduce_multi(_bytes_copy(acc), ins, dtype, op)
     np.testing.assert_array_equal(_bits(got), _bits(ref))
 
 
@@ -215,3 +225,103 @@ def test_reduce_multi_running_first(gu, dtype, op, m):
 def test_reduce_multi_ex_rejects_bad_flags(gu):
     d = gu.empty_dev(64)
     assert ca.reduce_multi_ex(d, d, [d], 4, ca.FLOAT32, ca.MAX, 2, gu.stream()) == 1
+
+
+@pytest.mark.parametrize("dtype", ["fi", "di", "li", "2i", "si"])
+@pytest.mark.parametrize("op", ["maxloc", "minloc"])
+@pytest.mark.parametrize("m", [1, 3, 8, 9])
+def test_pair_types_maxloc_minloc(gu, dtype, op, m):
+    """MPI_MAXLOC / MPI_MINLOC on MPI's five pair types (MPICH's loop: equal values keep inout's
+    value with the lower index, a better incoming element replaces the whole element, NaN compares
+    keep inout): vector path (2 or 1 elements per 16-B vector), a ragged tail, a misaligned scalar
+    path; the floating pairs also on the TIES pattern (-0 / +0, NaN payloads)."""
+    pats = [po.PAT_UNIFORM] + ([po.PAT_TIES] if dtype in ("fi", "di") else [])
+    for pat in pats:
+        _check_multi(gu, dtype, op, m, 30011, pattern=pat)
+        _check_multi(gu, dtype, op, m, 501, off=1, in_off=1, pattern=pat)
+        _check_multi(gu, dtype, op, m, 377, off=1, in_off=2, pattern=pat)
+
+
+@pytest.mark.parametrize("dtype", ["cf", "cd"])
+@pytest.mark.parametrize("op", ["sum", "prod"])
+@pytest.mark.parametrize("m", [1, 2, 8, 9])
+def test_complex_types_sum_prod(gu, dtype, op, m):
+    """MPI_SUM / MPI_PROD on MPI_C_FLOAT_COMPLEX / MPI_C_DOUBLE_COMPLEX (C99 complex arithmetic, the
+    products rounded one by one): bit-exact on finite data."""
+    _check_multi(gu, dtype, op, m, 20011)
+    _check_multi(gu, dtype, op, m, 333, off=1, in_off=2)
+
+
+def test_complex_prod_special_values_match_mpich_fixture(gu):
+    """C99 Annex G multiplication (infinities recovered where the plain formula gives NaN + NaN i)
+    on MPICH's own fixture inputs (tests/golden/pairs_reduce_local.npz): the device result equals
+    MPICH's, NaN parts compared by NaN-ness (the sign / payload of an invalid operation's NaN is the
+    x86 default NaN on the CPU, not pinned by C)."""
+    import os
+
+    from test_pairs_oracle import complex_equal
+
+    fix = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "pairs_reduce_local.npz"))
+    for dtype, npdt in (("cf", np.complex64), ("cd", np.complex128)):
+        for op in ("sum", "prod"):
+            x = fix[f"{dtype}_{op}_in"].copy()
+            y = fix[f"{dtype}_{op}_inout"].copy()
+            d_x, d_y = gu.to_dev(x), gu.to_dev(y)
+            assert ca.reduce_local(d_x, d_y, x.size // np.dtype(npdt).itemsize, DT[dtype], OP[op], gu.stream()) == 0
+            gu.sync()
+            assert complex_equal(gu.from_dev(d_y, npdt), fix[f"{dtype}_{op}_out"].view(npdt)), (dtype, op)
+
+
+def test_pair_fixture_bit_exact_on_device(gu):
+    """MAXLOC / MINLOC on MPICH's own fixture inputs (integer extremes, ties, -0 / +0, infinities, NaN
+    payloads, padding bytes set to a marker): the device result equals MPICH's byte for byte."""
+    import os
+
+    fix = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "pairs_reduce_local.npz"))
+    for dtype in po.PAIR_DTYPES:
+        for op in ("maxloc", "minloc"):
+            x = fix[f"{dtype}_{op}_in"].copy()
+            y = fix[f"{dtype}_{op}_inout"].copy()
+            d_x, d_y = gu.to_dev(x), gu.to_dev(y)
+            n = x.size // po.NP_DTYPES[dtype].itemsize
+            assert ca.reduce_local(d_x, d_y, n, DT[dtype], OP[op], gu.stream()) == 0
+            gu.sync()
+            got = d_y.cpu().numpy()
+            assert np.array_equal(got, fix[f"{dtype}_{op}_out"]), (dtype, op)
+
+
+@pytest.mark.parametrize("dtype", ["fi", "di"])
+def test_pair_running_first_order(gu, dtype):
+    """chr_reduce_multi_ex(CHR_REDUCE_RUNNING_FIRST) on the floating pairs: MPICH_do_reduce's order,
+    MPI_Reduce_local(running, next) per step, differs bitwise from the default on ties (-0 / +0) and
+    NaN compares; checked against the oracle chained the same way."""
+    npdt = po.NP_DTYPES[dtype]
+    n, m = 20011, 5
+    acc = po.fill(n, dtype, po.PAT_TIES, 9, 0)
+    ins = [po.fill(n, dtype, po.PAT_TIES, 9, r + 1) for r in range(m)]
+    for op in ("maxloc", "minloc"):
+        run = _bytes_copy(acc)
+        for x in ins:
+            nxt = _bytes_copy(x)
+            po.reduce_local(run, nxt, dtype, op)  # MPI_Reduce_local(in = running, inout = next)
+            run = nxt
+        d_acc = gu.to_dev(acc)
+        d_ins = [gu.to_dev(x) for x in ins]
+        rc = ca.reduce_multi_ex(d_acc, d_acc, d_ins, n, DT[dtype], OP[op], ca.REDUCE_RUNNING_FIRST, gu.stream())
+        assert rc == 0
+        gu.sync()
+        assert np.array_equal(gu.from_dev(d_acc, npdt).view(np.uint8), run.view(np.uint8)), (dtype, op)
+        default = po.reduce_multi(_bytes_copy(acc), ins, dtype, op)
+        assert not np.array_equal(default.view(np.uint8), run.view(np.uint8))  # the order is visible
+
+
+def test_pair_and_complex_reject_other_ops(gu):
+    x = gu.empty_dev(256)
+    for dt in (ca.FLOAT_INT, ca.DOUBLE_INT, ca.LONG_INT, ca.TWO_INT, ca.SHORT_INT):
+        for op in (ca.SUM, ca.PROD, ca.MAX, ca.MIN, ca.LAND, ca.BAND):
+            assert ca.reduce_local(x, x, 4, dt, op, gu.stream()) == 1
+    for dt in (ca.C_FLOAT_COMPLEX, ca.C_DOUBLE_COMPLEX):
+        for op in (ca.MAX, ca.MIN, ca.LAND, ca.BXOR, ca.MAXLOC):
+            assert ca.reduce_local(x, x, 4, dt, op, gu.stream()) == 1
+    for dt in (ca.FLOAT32, ca.INT32, ca.BFLOAT16):
+        assert ca.reduce_local(x, x, 4, dt, ca.MAXLOC, gu.stream()) == 1

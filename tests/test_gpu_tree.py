@@ -15,9 +15,11 @@ from tree_util import random_program, tree_ref
 pytestmark = pytest.mark.gpu
 
 DT = {"f32": ca.FLOAT32, "f64": ca.FLOAT64, "i32": ca.INT32, "bf16": ca.BFLOAT16, "i8": ca.INT8, "u8": ca.UINT8,
-      "i16": ca.INT16, "u16": ca.UINT16, "u32": ca.UINT32, "i64": ca.INT64, "u64": ca.UINT64}
+      "i16": ca.INT16, "u16": ca.UINT16, "u32": ca.UINT32, "i64": ca.INT64, "u64": ca.UINT64,
+      "fi": ca.FLOAT_INT, "di": ca.DOUBLE_INT, "li": ca.LONG_INT, "2i": ca.TWO_INT, "si": ca.SHORT_INT,
+      "cf": ca.C_FLOAT_COMPLEX, "cd": ca.C_DOUBLE_COMPLEX}
 OP = {"sum": ca.SUM, "prod": ca.PROD, "max": ca.MAX, "min": ca.MIN, "land": ca.LAND, "lor": ca.LOR,
-      "lxor": ca.LXOR, "band": ca.BAND, "bor": ca.BOR, "bxor": ca.BXOR}
+      "lxor": ca.LXOR, "band": ca.BAND, "bor": ca.BOR, "bxor": ca.BXOR, "maxloc": ca.MAXLOC, "minloc": ca.MINLOC}
 
 
 @pytest.fixture(scope="module")
@@ -28,6 +30,8 @@ def gu():
 
 
 def _bits(a):
+    if a.dtype.names is not None or a.itemsize == 16:  # pair / complex elements: their bytes
+        return a.view(np.uint8)
     return a.view({1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[a.itemsize])
 
 
@@ -144,3 +148,19 @@ def test_batched_trees_bit_identical(gu, ntrees, n, off):
         got = gu.from_dev(outs[t], npdt)[off:off + n]
         want = tree_ref(leaves[t], progs[t][0], progs[t][1], "f32", "sum")
         np.testing.assert_array_equal(_bits(got), _bits(want))
+
+
+@pytest.mark.parametrize("dtype,op", [(d, o) for d in ("fi", "di", "li", "2i", "si") for o in ("maxloc", "minloc")] +
+                         [(d, o) for d in ("cf", "cd") for o in ("sum", "prod")])
+def test_tree_pair_and_complex_types(gu, dtype, op):
+    """The fused tree on MPI's pair types (MAXLOC / MINLOC) and the C complex types (SUM / PROD):
+    random programs with random swap bits (MPICH_do_reduce order per combine), 2..8 leaves, vector
+    path with a ragged tail and the misaligned scalar path; the floating pairs on TIES data, where
+    the swap bits change the result bits."""
+    rng = np.random.default_rng(hash((dtype, op)) & 0xFFFF)
+    pat = po.PAT_TIES if dtype in ("fi", "di") else po.PAT_UNIFORM
+    for nl in (2, 3, 5, 8):
+        comb, swaps = random_program(rng, nl)
+        _run(gu, dtype, op, comb, swaps, 4099, pattern=pat)
+        _run(gu, dtype, op, comb, swaps, 257, pattern=pat, off=1)
+    _run(gu, dtype, op, *C4_TREE, 8192 + 3, pattern=pat, inplace_leaf=0)

@@ -121,9 +121,11 @@ def test_block_window_property(mode, n, k, b, dtype):
 
 def _oracle_outputs(c):
     n, dt = c["n"], c["dtype"]
-    in_n = c["count"] * n if c["mode"] == "rs" else c["count"]
+    mode = {"ar_lib": "ar", "rs_lib": "rs"}.get(c["mode"], c["mode"])  # MPI's collective: same result
+    in_n = c["count"] * n if mode == "rs" else c["count"]
     sends = [po.fill(in_n, dt, c["pattern"], c["seed"], r) for r in range(n)]
     ip = bool(c["inplace"])
+    c = dict(c, mode=mode)
     if c["mode"] == "ar":
         return po.allreduce_radix_batch(sends, c["k"], c["b"], dt, c["op"], ip)
     if c["mode"] == "rs":
@@ -153,3 +155,20 @@ def test_oracle_matches_reference_on_integer_types_and_logical_bitwise_ops(golde
             if c["op"] == op:
                 vals |= set(np.unique(arrays[c["id"]]).tolist())
         assert vals == {0, 1}, (op, vals)
+
+
+def test_oracle_matches_reference_on_pair_and_complex_types(golden_pairtypes):
+    """MPI_MAXLOC / MPI_MINLOC on the five pair types and SUM / PROD on the C complex types through the
+    radix/batch collectives, allgather and three MPICH baselines: bit-exact vs the reference run here
+    under MPICH 3.3.2 (MPI_FLOAT_INT, MPI_2INT, complex; the TIES pattern's -0 / +0 and NaN make the
+    operand order visible) and vs MPI's own collective for MPI_DOUBLE_INT / MPI_LONG_INT /
+    MPI_SHORT_INT, whose MPI_Type_size (12 / 12 / 6) the reference would take for their stride
+    (all_reduce_radix_batch.cpp:238-256, gen_golden.py pairs_cases_for)."""
+    cases, arrays = golden_pairtypes
+    assert len(cases) > 700
+    assert {c["dtype"] for c in cases} == set(po.PAIR_DTYPES + po.COMPLEX_DTYPES)
+    bad = [c["id"] for c in cases
+           if hashlib.sha256(b"".join(o.tobytes() for o in _oracle_outputs(c))).hexdigest() != c["sha256"]]
+    assert not bad, bad[:5]
+    # without NaN / signed zeros the reference's MAXLOC / MINLOC equal MPI's collective (order-free)
+    assert all(c["n_diff_vs_lib"] == 0 for c in cases if c["dtype"] in ("fi", "2i") and c["pattern"] == 0)

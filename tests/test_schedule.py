@@ -358,3 +358,46 @@ def test_tiny_and_ragged_sizes_every_schedule(schedule):
                 want = f(sends, k, b, "f32", "sum")
                 for r in range(n):
                     np.testing.assert_array_equal(got[r].view(np.uint32), want[r].view(np.uint32))
+
+
+@pytest.mark.parametrize("schedule", [ca.SCHEDULE_FLAT, ca.SCHEDULE_EXACT, ca.SCHEDULE_REFERENCE])
+def test_plans_match_pair_and_complex_goldens(golden_pairtypes, schedule):
+    """MAXLOC / MINLOC on the pair types and complex SUM / PROD through the compiled plans (CPU plan
+    interpreter): the radix/batch and allgather goldens bit-exact under three schedules -- the TIES
+    pattern's -0 / +0 and NaN cases fix the operand order of every reduction."""
+    cases, _ = golden_pairtypes
+    bad, ran = [], 0
+    for c in cases:
+        mode = {"ar": "ar", "rs": "rs", "ag": "ag", "ar_lib": "ar", "rs_lib": "rs"}.get(c["mode"])
+        if mode is None:
+            continue
+        mm = {"ar": ca.MODE_ALLREDUCE, "rs": ca.MODE_REDUCE_SCATTER, "ag": ca.MODE_ALLGATHER}[mode]
+        outs = plan_sim.simulate(mm, _inputs(dict(c, mode=mode)), c["k"], c["b"], c["dtype"], c["op"],
+                                 bool(c["inplace"]), schedule=schedule)
+        ran += 1
+        if hashlib.sha256(b"".join(o.tobytes() for o in outs)).hexdigest() != c["sha256"]:
+            bad.append(c["id"])
+    assert ran > 400 and not bad, f"{len(bad)} plan/reference mismatches, e.g. {bad[:5]}"
+
+
+def test_plan_dependency_lists():
+    """Every step lists all earlier steps whose local ops conflict with its transfers (comm_deps, the
+    last of which is comm_wait) or with its own local ops (local_deps): what the executor needs to
+    spread local ops over two compute streams.  Checked here on the flat C4 plan: the evaluation of
+    slice s reads only slice s's receives, so no local step depends on another, and allgather s
+    depends on exactly the evaluation of slice s."""
+    p = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 1 << 24, 4))
+    assert [st["wait"] for st in p["steps"]] == [-1, -1, 0, 1, 2, 3]
+    assert [st["deps"] for st in p["steps"]] == [[], [], [0], [1], [2], [3]]
+    assert all(st["ldeps"] == [] for st in p["steps"])
+    for sched in (ca.SCHEDULE_REFERENCE, ca.SCHEDULE_EXACT):
+        for mode, count in ((ca.MODE_ALLREDUCE, 1 << 20), (ca.MODE_REDUCE_SCATTER, 1 << 17)):
+            for rank in range(8):
+                q = ca.parse_plan(ca.describe_plan(mode, 8, rank, 4, 4, count, 2, sched))
+                for t, st in enumerate(q["steps"]):
+                    assert st["deps"] == sorted(st["deps"]) and all(d < t for d in st["deps"] + st["ldeps"])
+                    assert st["wait"] == (st["deps"][-1] if st["deps"] else -1)
+                    assert all(q["steps"][d]["post"] for d in st["deps"] + st["ldeps"])
+    # the reference route's recexch phases fold into the same region step after step: local chains
+    r = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 16, 0, 2, 16, 1 << 16, 1, ca.SCHEDULE_REFERENCE))
+    assert any(st["ldeps"] for st in r["steps"])

@@ -12,7 +12,7 @@ def tree_ref(leaves, comb, swaps, dtype, op):
     swap bit MPI_Reduce_local(run, in) -> in (MPICH_do_reduce order)."""
     stack, ci = [], 0
     for j, leaf in enumerate(leaves):
-        stack.append(np.array(leaf, copy=True))
+        stack.append(leaf.view(np.uint8).copy().view(leaf.dtype))  # keeps padding bytes (pair types)
         for _ in range(comb[j]):
             x = stack.pop()
             run = stack.pop()
