@@ -1092,7 +1092,9 @@ int tune_schedule(chr_comm* c, int mode, const void* send, void* recv, size_t co
 
 int collective(chr_comm* c, int mode, const void* send, void* recv, size_t count, int dtype, int op, int k, int b,
                bool sync) {
-    if (!c || !chr::valid_dtype_op(dtype, op)) return CHR_ERR_INVALID_ARG;
+    // allgather moves elements of any type (its op is unused)
+    if (!c || !(mode == chr::MODE_ALLGATHER ? chr::dtype_size(dtype) != 0 : chr::valid_dtype_op(dtype, op)))
+        return CHR_ERR_INVALID_ARG;
     if (c->failed) return CHR_ERR_ABORTED;
     int sched = c->sched, slices = c->slices;
     if (sched == CHR_SCHEDULE_AUTO) {
@@ -1105,7 +1107,9 @@ int collective(chr_comm* c, int mode, const void* send, void* recv, size_t count
 
 int local_collective(chr_local_group* g, int mode, const void* const* sends, void* const* recvs, size_t count,
                      int dtype, int op, int k, int b) {
-    if (!g || !sends || !recvs || !chr::valid_dtype_op(dtype, op)) return CHR_ERR_INVALID_ARG;
+    if (!g || !sends || !recvs ||
+        !(mode == chr::MODE_ALLGATHER ? chr::dtype_size(dtype) != 0 : chr::valid_dtype_op(dtype, op)))
+        return CHR_ERR_INVALID_ARG;
     const int n = g->nranks;
     const int depth = pick_slices(g->slices, count, mode, n, b, chr::dtype_size(dtype), g->sched);
     auto key = std::make_tuple(mode, k, b, (uint64_t)count, (int)chr::dtype_size(dtype), depth, g->sched);
@@ -1396,7 +1400,7 @@ int chr_comm_set_graphs(chr_comm* c, int enable) {
 
 int chr_comm_tuned_schedule(const chr_comm* c, int mode, size_t count, chr_dtype dtype, int k, int b, int* schedule,
                             int* slices) {
-    if (!c || !schedule || !slices || !chr::valid_dtype_op(dtype, CHR_SUM)) return CHR_ERR_INVALID_ARG;
+    if (!c || !schedule || !slices || !chr::dtype_size(dtype)) return CHR_ERR_INVALID_ARG;
     auto it = c->tuned.find(std::make_tuple(mode, (uint64_t)count, (int)chr::dtype_size(dtype), k, b, c->slices,
                                             c->overlap));
     if (it == c->tuned.end()) return CHR_ERR_INVALID_ARG;
