@@ -827,9 +827,9 @@ int run_host_windows(chr_comm* c, int sched, int slices, int mode, const void* i
             cv.notify_all();
         }
     };
-    // The copy-out side runs on a second host thread; if one cannot be started, it runs after the
-    // issuing loop on this one (no overlap of the two PCIe directions, same bits) -- no exception
-    // crosses the C ABI.
+    // The copy-out side runs on a second host thread; if one cannot be started, the issuing loop
+    // copies each window out itself right after its collective (no overlap of the two PCIe
+    // directions, same bits) -- no exception crosses the C ABI.
     std::thread copy_out;
     try {
         copy_out = std::thread(copy_out_loop);

@@ -6,6 +6,7 @@
 // ((m+2) x bucket bytes per launch), buffers rotated so the working set exceeds the
 // 256 MiB Infinity Cache.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cstdio>
 
@@ -1374,6 +1375,88 @@ static void focus19(size_t piece, int sets) {
     free_sets(S);
 }
 
+// ---- focus21: back-to-back tree launches with the AQL barrier bit cleared ----------------------
+// hipExtAnyOrderLaunch lets the packet processor start launch i+1 while launch i drains; the flat
+// plan's consecutive slice evaluations touch disjoint memory, so only the ramp/drain gap is at stake.
+__global__ void k_spin_write(unsigned* p, unsigned v, long long ticks) {
+    const long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+    if (threadIdx.x == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ void k_read_to(const unsigned* p, unsigned* out) {
+    if (threadIdx.x == 0) out[0] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// What an any-order launch still waits for: (a) the kernel before it on the same stream, (b) an
+// event wait (barrier-AND packet) before it.  Prints the value the reader saw (1 = it waited).
+static void any_order_semantics() {
+    unsigned *flag, *out;
+    CK(hipMalloc(&flag, 256));
+    CK(hipMalloc(&out, 256));
+    hipStream_t sa, sb;
+    CK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+    hipEvent_t ev;
+    CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    for (uint32_t fl : {0u, (uint32_t)hipExtAnyOrderLaunch}) {
+        for (int r = 0; r < 3; ++r) {
+            CK(hipMemset(flag, 0, 256));
+            CK(hipMemset(out, 0xff, 256));
+            CK(hipDeviceSynchronize());
+            hipLaunchKernelGGL(k_spin_write, dim3(1), dim3(64), 0, sa, flag, 1u, 20000ll);  // ~200 us at 100 MHz
+            hipExtLaunchKernelGGL(k_read_to, dim3(1), dim3(64), 0, sa, nullptr, nullptr, fl, (const unsigned*)flag, out);
+            CK(hipStreamSynchronize(sa));
+            unsigned same = 0;
+            CK(hipMemcpy(&same, out, 4, hipMemcpyDeviceToHost));
+            CK(hipMemset(flag, 0, 256));
+            CK(hipMemset(out, 0xff, 256));
+            CK(hipDeviceSynchronize());
+            hipLaunchKernelGGL(k_spin_write, dim3(1), dim3(64), 0, sa, flag, 1u, 20000ll);
+            CK(hipEventRecord(ev, sa));
+            CK(hipStreamWaitEvent(sb, ev, 0));
+            hipExtLaunchKernelGGL(k_read_to, dim3(1), dim3(64), 0, sb, nullptr, nullptr, fl, (const unsigned*)flag, out);
+            CK(hipDeviceSynchronize());
+            unsigned cross = 0;
+            CK(hipMemcpy(&cross, out, 4, hipMemcpyDeviceToHost));
+            std::printf("semantics flags=%u rep=%d same-stream reader saw %u, after event wait saw %u\n", fl, r, same, cross);
+        }
+    }
+    std::fflush(stdout);
+    CK(hipEventDestroy(ev));
+    CK(hipStreamDestroy(sa));
+    CK(hipStreamDestroy(sb));
+    CK(hipFree(flag));
+    CK(hipFree(out));
+}
+
+template <int U>
+static double tree8x2_time_flags(Sets& S, size_t nvec, int sets, unsigned lds, uint32_t cs, uint32_t flags) {
+    return time_launches([&](int i) {
+        chr::TreeArgs a{};
+        const auto& b = S.bufs[i % sets];
+        a.nseg = 2;
+        a.nl = 8;
+        a.xrun = cs;
+        const uint32_t trips = (uint32_t)((nvec + 64 * U - 1) / (64 * U));
+        for (int j = 0; j < chr::kMaxTreeSegs; ++j) {
+            a.block0[j] = j < 2 ? j * trips : ~0u;
+            a.xfull[j] = j < 2 ? chr::xcd_full(trips, cs) : 0;
+        }
+        const int comb[8] = {0, 1, 1, 1, 0, 1, 1, 2};
+        for (int t2 = 0; t2 < 2; ++t2) {
+            chr::TreeSeg& g = a.seg[t2];
+            for (int l = 0; l < 8; ++l) g.leaves[l] = (const chr::u32x4*)b[9 * t2 + l];
+            g.out = (chr::u32x4*)b[9 * t2 + 8];
+            g.nvec = nvec;
+            g.comb = 0;
+            for (int l = 0; l < 8; ++l) g.comb |= (uint32_t)comb[l] << (2 * l);
+            g.swaps = 0;
+        }
+        hipExtLaunchKernelGGL((chr::k_reduce_tree<CHR_FLOAT32, CHR_SUM, 8, U, true, 64>), dim3(2 * trips), dim3(64), lds,
+                              0, nullptr, nullptr, flags, a);
+    }, 64);
+}
+
 template <bool NT, int BL, int U>
 static double vec1_time(Sets& S, size_t nvec, int sets, unsigned lds, uint32_t cs) {
     const unsigned G = (unsigned)(nvec / (BL * U));
@@ -1407,6 +1490,26 @@ int main(int argc, char** argv) {
     check();
     if (argc > 1 && std::string(argv[1]) == "layout") {
         layout_mode();
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus21") {  // barrier bit vs any-order launches, C4 slice shape
+        any_order_semantics();
+        for (int r = 0; r < 3; ++r)
+            for (size_t mib : {8, 16, 32})
+                for (int sets : {16, 4}) {
+                    const size_t piece = mib << 20, nvec = piece / 16;
+                    Sets S = make_sets(17, nvec, sets);
+                    uint32_t cs = 0;
+                    while (((size_t)2 << cs) * (64 * 1 * 16) <= (size_t)512 * 1024 && cs < 16) ++cs;
+                    for (uint32_t fl : {0u, (uint32_t)hipExtAnyOrderLaunch}) {
+                        char name[128];
+                        std::snprintf(name, sizeof name, "tree8x2 U=1 cap16 %s piece=%zuMiB sets=%d",
+                                      fl ? "any-order" : "ordered  ", mib, sets);
+                        report_moved(name, 2.0 * 9 * piece,
+                                     tree8x2_time_flags<1>(S, nvec, sets, lds_for_cap(16), cs, fl));
+                    }
+                    free_sets(S);
+                }
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus20") {  // XCD run length for the U = 1 tree shape
