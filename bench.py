@@ -359,21 +359,25 @@ def bench_collective_kernels(args):
         for r, x in enumerate(sends):
             ca.check(ca.fill(x, count, cdt, 0, SEED, r, stream=g.stream))
         for slices in (0, 8):
-            g.set_slices(slices)
-            ca.check(g.all_reduce_radix_batch(sends, recvs, count, cdt, ca.SUM, k, b))  # warm: plans, scratch
-            g.profile(True)
-            g.profile_read()
-            reps = 3
-            for _ in range(reps):
-                ca.check(g.all_reduce_radix_batch(sends, recvs, count, cdt, ca.SUM, k, b))
-            ms, by, launches = g.profile_read()
-            g.profile(False)
-            ach = by / (ms * 1e-3) / 1e9
-            rows[f"{'c4' if dname == 'f32' else 'c5'}_{dname}_slices_{slices or 'auto'}"] = {
-                "launches_per_call_all_ranks": launches // reps, "kernel_ms_per_call_all_ranks": round(ms / reps, 4),
-                "algorithmic_bytes_per_call_all_ranks": int(by / reps), "achieved_GBps": round(ach, 1),
-                "frac": round(ach / HBM_PEAK_GBPS, 4)}
+            for batched in (True, False):  # the ranks' trees of a step in shared grids, or one grid per rank
+                g.set_slices(slices)
+                g.set_batching(batched)
+                ca.check(g.all_reduce_radix_batch(sends, recvs, count, cdt, ca.SUM, k, b))  # warm: plans, scratch
+                g.profile(True)
+                g.profile_read()
+                reps = 3
+                for _ in range(reps):
+                    ca.check(g.all_reduce_radix_batch(sends, recvs, count, cdt, ca.SUM, k, b))
+                ms, by, launches = g.profile_read()
+                g.profile(False)
+                ach = by / (ms * 1e-3) / 1e9
+                rows[f"{'c4' if dname == 'f32' else 'c5'}_{dname}_slices_{slices or 'auto'}"
+                     f"{'' if batched else '_per_rank_launches'}"] = {
+                    "launches_per_call_all_ranks": launches // reps, "kernel_ms_per_call_all_ranks": round(ms / reps, 4),
+                    "algorithmic_bytes_per_call_all_ranks": int(by / reps), "achieved_GBps": round(ach, 1),
+                    "frac": round(ach / HBM_PEAK_GBPS, 4)}
         g.set_slices(0)
+        g.set_batching(True)
         del sends, recvs
         torch.cuda.empty_cache()
     g.destroy()
@@ -385,8 +389,11 @@ def bench_collective_kernels(args):
                 rows[key] = replay_rank_trees(ca, torch, dev, cdt, es, (1 << 30) // es, n, k, b, slices, recv_copies)
                 torch.cuda.empty_cache()
     emit({"collective_kernels": {"workload": "all_reduce_radix_batch fused reductions, 8 virtual ranks, k=4, b=4, "
-                                             "1 GiB per rank, flat schedule (batched trees); *_rank0_alone rows: "
-                                             "rank 0's own trees on its own send/recv/STAGE only", "rows": rows}})
+                                             "1 GiB per rank, flat schedule, each reduce phase of a call timed as one "
+                                             "span; the ranks' trees of a step share grids of up to 8 trees "
+                                             "(*_per_rank_launches: one grid per rank and step, as each GPU of a "
+                                             "node launches); *_rank0_alone rows: rank 0's own trees on its own "
+                                             "send/recv/STAGE only", "rows": rows}})
 
 
 def replay_rank_trees(ca, torch, dev, cdt, es, count, n, k, b, slices, recv_copies, reps=5):

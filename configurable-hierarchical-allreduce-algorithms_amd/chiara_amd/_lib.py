@@ -89,6 +89,7 @@ def _load():
         "chr_reduce_scatter_mpich_async": ([vp, vp, sz, i, i, vp, i, i], i),
         "chr_local_reduce_scatter_mpich": ([vp, pp, pp, sz, i, i, i, i], i),
         "chr_local_group_profile": ([vp, i], i),
+        "chr_local_group_set_batching": ([vp, i], i),
         "chr_local_group_profile_read": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(ctypes.c_long), i], i),
     }
@@ -122,5 +123,5 @@ EXPORTED = [
     "chr_comm_tuned_schedule", "chr_comm_set_graphs", "chr_comm_set_host_pipeline", "chr_comm_set_timeout", "chr_comm_abort",
     "chr_comm_synchronize", "chr_comm_is_aborted", "chr_reduce_tree_batch", "chr_local_group_profile",
     "chr_local_group_profile_read", "chr_reduce_scatter_mpich", "chr_reduce_scatter_mpich_async",
-    "chr_local_reduce_scatter_mpich",
+    "chr_local_reduce_scatter_mpich", "chr_local_group_set_batching",
 ]

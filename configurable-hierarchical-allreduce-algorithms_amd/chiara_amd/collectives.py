@@ -263,6 +263,10 @@ class LocalGroup:
     def set_schedule(self, schedule):
         check(lib().chr_local_group_set_schedule(self._h, int(schedule)))
 
+    def set_batching(self, enable):
+        """Virtual ranks' tree evaluations of one step share launches (default on); same bits."""
+        check(lib().chr_local_group_set_batching(self._h, int(bool(enable))))
+
     def profile(self, enable=True):
         """Time every virtual rank's fused reduction launches (HIP events)."""
         check(lib().chr_local_group_profile(self._h, 1 if enable else 0))

@@ -204,9 +204,12 @@ bool batchable(const std::vector<chr::LocalOp>& ops, size_t i0, size_t i1, const
     return true;
 }
 
-int run_tree_batch(const std::vector<chr::LocalOp>& ops, size_t i0, size_t i1, const Bufs& B, int dtype, int rop,
-                   hipStream_t s, ReduceProfile* prof) {
-    std::vector<chr::TreeJob> jobs;
+// Trees per batched launch (reduce_tree.hpp kMaxTreeSegs).
+constexpr size_t kTreeSegsPerLaunch = 8;
+
+// The tree ops [i0, i1) as resolved jobs for launch_reduce_tree_multi; returns their algorithmic bytes.
+double tree_jobs(const std::vector<chr::LocalOp>& ops, size_t i0, size_t i1, const Bufs& B,
+                 std::vector<chr::TreeJob>* jobs) {
     double bytes = 0;
     for (size_t i = i0; i < i1; ++i) {
         const chr::LocalOp& op = ops[i];
@@ -219,9 +222,14 @@ int run_tree_batch(const std::vector<chr::LocalOp>& ops, size_t i0, size_t i1, c
         jb.comb = op.comb.data();
         jb.swaps = op.swaps.empty() ? nullptr : op.swaps.data();
         jb.n = op.count;
-        jobs.push_back(jb);
+        jobs->push_back(jb);
         bytes += (double)(jb.nl + 1) * op.count * B.es;
     }
+    return bytes;
+}
+
+int launch_tree_jobs(const std::vector<chr::TreeJob>& jobs, double bytes, int dtype, int rop, hipStream_t s,
+                     ReduceProfile* prof) {
     if (jobs.empty()) return CHR_SUCCESS;
     const bool counted = prof && prof->on;
     const bool timed = counted && !prof->span;
@@ -237,9 +245,38 @@ int run_tree_batch(const std::vector<chr::LocalOp>& ops, size_t i0, size_t i1, c
     }
     if (counted) {
         prof->bytes += bytes;
-        prof->launches += 1;
+        // vector launches: launch_reduce_tree_multi packs up to kTreeSegsPerLaunch trees of one leaf count per grid
+        prof->launches += (long)((jobs.size() + kTreeSegsPerLaunch - 1) / kTreeSegsPerLaunch);
     }
     return rc;
+}
+
+int run_tree_batch(const std::vector<chr::LocalOp>& ops, size_t i0, size_t i1, const Bufs& B, int dtype, int rop,
+                   hipStream_t s, ReduceProfile* prof) {
+    std::vector<chr::TreeJob> jobs;
+    const double bytes = tree_jobs(ops, i0, i1, B, &jobs);
+    return launch_tree_jobs(jobs, bytes, dtype, rop, s, prof);
+}
+
+// Whether every op of `ops` is a tree of <= 8 leaves and the list is one batchable run (run_locals
+// would issue it as a single launch_reduce_tree_multi call).
+bool one_tree_run(const std::vector<chr::LocalOp>& ops, const Bufs& B) {
+    for (const chr::LocalOp& op : ops)
+        if (op.kind != chr::L_TREE || op.ins.size() + 1 > 8) return false;
+    return ops.size() < 2 || batchable(ops, 0, ops.size(), B);
+}
+
+// Whether job x writes memory job y reads or writes (resolved byte ranges).
+bool job_conflict(const chr::TreeJob& x, const chr::TreeJob& y, size_t es) {
+    auto hit = [&](const void* a, const void* b) {
+        const char* pa = (const char*)a;
+        const char* pb = (const char*)b;
+        return pa < pb + y.n * es && pb < pa + x.n * es;
+    };
+    if (hit(x.out, y.out)) return true;
+    for (int j = 0; j < y.nl; ++j)
+        if (hit(x.out, y.leaves[j])) return true;
+    return false;
 }
 
 int run_locals(const std::vector<chr::LocalOp>& ops, const Bufs& B, int dtype, int rop, hipStream_t s,
@@ -291,6 +328,15 @@ int default_dual() {
     static const int v = [] {
         const char* e = std::getenv("CHR_DUAL_COMPUTE");
         return e ? (std::atoi(e) != 0) : 0;
+    }();
+    return v;
+}
+
+// CHR_LG_BATCH=0: a local group launches each virtual rank's trees separately; default 1
+int default_lg_batch() {
+    static const int v = [] {
+        const char* e = std::getenv("CHR_LG_BATCH");
+        return e ? (std::atoi(e) != 0) : 1;
     }();
     return v;
 }
@@ -497,6 +543,9 @@ struct chr_local_group {
     hipStream_t cs[2] = {nullptr, nullptr};
     hipEvent_t ev_copy = nullptr, ev_done[2] = {nullptr, nullptr};
     int slices = 0;  // 0 = auto
+    // chr_local_group_set_batching: the virtual ranks' tree evaluations of one step share launches
+    // (CHR_LG_BATCH=0 turns it off; default on)
+    int batch_ranks = default_lg_batch();
     int sched = default_schedule() == CHR_SCHEDULE_AUTO ? (int)chr::SCHED_FLAT : default_schedule();  // no tuning
     hipStream_t stream = nullptr;
     std::vector<DevBuf> acc, stage;
@@ -1151,8 +1200,35 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
             if ((rc = hip_code(hipEventRecord(ev.first, g->stream)))) return rc;
         }
         if (!dual) {
-            for (int r = 0; r < n; ++r)
-                if ((rc = run_locals(ops_of(r), B[r], dtype, op, g->stream, &g->prof))) return rc;
+            // The virtual ranks' local ops of one step touch only their own buffers.  When every rank's
+            // ops are one batchable run of trees (the flat schedules' slice evaluations), all ranks'
+            // trees go to one launch_reduce_tree_multi call: one grid per 8 trees instead of one per
+            // rank, so the step pays the fixed cost of a launch -- ~4.5 us between back-to-back grids
+            // on one stream plus ~3-4 us of fill and drain (tools/reduce_microbench focus22/23,
+            // profiles/r03/launch_timeline/) -- once per 8 trees.  A real node has one rank per GPU
+            // and so one launch per rank per slice; rows measured there are the rank-alone replays of
+            // bench.py --collective-kernels.
+            std::vector<chr::TreeJob> jobs;
+            double bytes = 0;
+            bool merged = g->batch_ranks && n > 1;
+            for (int r = 0; r < n && merged; ++r) {
+                const std::vector<chr::LocalOp>& ops = ops_of(r);
+                if (!one_tree_run(ops, B[r])) {
+                    merged = false;
+                    break;
+                }
+                const size_t j0 = jobs.size();
+                bytes += tree_jobs(ops, 0, ops.size(), B[r], &jobs);
+                for (size_t x = 0; x < j0 && merged; ++x)  // earlier ranks' trees vs this rank's
+                    for (size_t y = j0; y < jobs.size() && merged; ++y)
+                        merged = !job_conflict(jobs[x], jobs[y], es) && !job_conflict(jobs[y], jobs[x], es);
+            }
+            if (merged) {
+                if ((rc = launch_tree_jobs(jobs, bytes, dtype, op, g->stream, &g->prof))) return rc;
+            } else {
+                for (int r = 0; r < n; ++r)
+                    if ((rc = run_locals(ops_of(r), B[r], dtype, op, g->stream, &g->prof))) return rc;
+            }
         } else {
             if ((rc = hip_code(hipEventRecord(g->ev_copy, g->stream)))) return rc;
             for (int k = 0; k < 2; ++k)
@@ -1412,6 +1488,12 @@ int chr_comm_tuned_schedule(const chr_comm* c, int mode, size_t count, chr_dtype
 int chr_local_group_set_schedule(chr_local_group* g, int schedule) {
     if (!g || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_FLAT_SEQ) return CHR_ERR_INVALID_ARG;
     g->sched = schedule;
+    return CHR_SUCCESS;
+}
+
+int chr_local_group_set_batching(chr_local_group* g, int enable) {
+    if (!g) return CHR_ERR_INVALID_ARG;
+    g->batch_ranks = enable != 0;
     return CHR_SUCCESS;
 }
 

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define CHR_ABI_VERSION 5
+#define CHR_ABI_VERSION 6
 
 /* Element types.  The reference is generic over MPI_Datatype (all_reduce_radix_batch.cpp:202-204,
  * sizes from MPI_Type_size at :234-277); these are the MPI predefined types MPICH's
@@ -290,6 +290,11 @@ int chr_local_group_destroy(chr_local_group* group);
 int chr_local_group_stream(const chr_local_group* group, hipStream_t* stream);
 int chr_local_group_set_slices(chr_local_group* group, int slices);
 int chr_local_group_set_schedule(chr_local_group* group, int schedule);
+/* Whether the virtual ranks' tree evaluations of one step share launches (default 1; env
+ * CHR_LG_BATCH=0 sets the default to 0).  The ranks' trees are independent, so the bits are the
+ * same either way; batched, a step pays a grid's fixed launch cost once per 8 trees instead of once
+ * per rank.  No reference counterpart (the virtual-rank group is this library's own). */
+int chr_local_group_set_batching(chr_local_group* group, int enable);
 /* Timing of every virtual rank's fused reductions (HIP events on the group's stream), as
  * chr_comm_profile / chr_comm_profile_read: the collective's own kernels at full size with the
  * leaves just written by the loopback copies, one rank at a time. */

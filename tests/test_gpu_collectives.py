@@ -458,6 +458,35 @@ def test_schedules_bit_identical(gu, groups, n, k, b, dtype):
             np.testing.assert_array_equal(outs[sch][r].view(np.uint8), want[r].view(np.uint8))
 
 
+@pytest.mark.parametrize("n,k,b,dtype,slices,inplace", [(8, 4, 4, "f32", 0, False), (8, 4, 4, "bf16", 8, True),
+                                                         (8, 2, 2, "f32", 3, False), (5, 2, 5, "i32", 2, True),
+                                                         (4, 4, 4, "f64", 1, False)])
+def test_local_group_cross_rank_batching_bit_identical(gu, groups, n, k, b, dtype, slices, inplace):
+    """The virtual ranks' trees of one step share launches (chr_local_group_set_batching, default
+    on) or run rank by rank: identical bits, equal to the oracle; allreduce (optionally in place,
+    an odd per-rank count for scalar heads and tails) and reduce-scatter."""
+    count = (3 << 20) + 8 * n + 5
+    count -= count % n
+    sends = [po.fill(count, dtype, po.PAT_UNIFORM, 9, r) for r in range(n)]
+    g = groups(n)
+    got = {}
+    try:
+        g.set_slices(slices)
+        for on in (True, False):
+            g.set_batching(on)
+            got[on] = (run_local(gu, g, "ar", sends, k, b, dtype, "sum", inplace),
+                       run_local(gu, g, "rs", sends, k, b, dtype, "sum"))
+    finally:
+        g.set_batching(True)
+        g.set_slices(0)
+    want_ar = po.allreduce_radix_batch(sends, k, b, dtype, "sum")
+    want_rs = po.reduce_scatter_radix_batch(sends, k, b, dtype, "sum")
+    for on in (True, False):
+        for r in range(n):
+            np.testing.assert_array_equal(got[on][0][r].view(np.uint8), want_ar[r].view(np.uint8))
+            np.testing.assert_array_equal(got[on][1][r].view(np.uint8), want_rs[r].view(np.uint8))
+
+
 @pytest.mark.parametrize("n,k,b", [(2, 2, 2), (2, 2, 1), (8, 4, 4), (8, 8, 8)])
 def test_balanced_reduce_scatter_equals_owner_lane(gu, groups, n, k, b):
     """Reduce-scatter: balanced (own block evaluated locally) and owner-lane plans, 4 MiB

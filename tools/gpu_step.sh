@@ -3,5 +3,5 @@
 set -u -o pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out
-timeout -k 10 400 tools/reduce_microbench focus21 > gpurun_out/focus21.txt 2>&1 || exit 1
-N=4 bash tools/gpu.sh rehearse || exit 1
+export TESTS="tests/test_gpu_collectives.py" TAG=collectives TEST_LIMIT=600
+bash tools/gpu.sh tests kernels || exit 1

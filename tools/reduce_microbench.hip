@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 
+#include <algorithm>
 #include <cstdio>
 
 #include "chiara.h"
@@ -1457,6 +1458,168 @@ static double tree8x2_time_flags(Sets& S, size_t nvec, int sets, unsigned lds, u
     }, 64);
 }
 
+// ---- focus22: where a tree launch loses time against its steady rate -------------------------
+// The product's 8-leaf tree body (k_reduce_tree<f32, SUM, 8, U, nt, 64>, C4's program) with each
+// workgroup's start and end (after its stores are acknowledged) on the 100 MHz wall clock and its
+// XCC.  Launches run back to back on one stream, as the flat plan's slice evaluations do on a
+// rank's compute stream; from the stamps: ramp (first start -> steady completion rate), tail
+// (95 % done -> last end), per-XCD finish spread and the bubble between consecutive launches.
+// SAUX: the root's store. -1 = the product's (global_store ... nt); >= 0 = a buffer store with that
+// cache-policy aux (gfx950 CPol: sc0 = 1, nt = 2, sc1 = 16); -2 = no store (diagnostic: what the
+// end-of-kernel gap costs without dirty lines to write back; the result is not written).
+template <int U, int SAUX = -1>
+__global__ __launch_bounds__(64) void k_tree_stamped(chr::TreeArgs a, unsigned long long* st) {
+    const unsigned long long t0 = wall_clock64();
+    const uint32_t b = blockIdx.x, xrun = a.xrun;
+    int s = 0;
+    uint32_t b0 = 0, xfull = a.xfull[0];
+#pragma unroll
+    for (int j = 1; j < chr::kMaxTreeSegs; ++j)
+        if (b >= a.block0[j]) {
+            s = j;
+            b0 = a.block0[j];
+            xfull = a.xfull[j];
+        }
+    const chr::TreeSeg& g = a.seg[s];
+    const size_t trip = chr::xcd_trip(b - b0, xfull, xrun);
+    const size_t base = trip * 64 * U + threadIdx.x;
+    if ((trip + 1) * 64 * U <= g.nvec) {
+        chr::u32x4 x[8][U];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[j][u] = chr::ld<true>(&g.leaves[j][base + (size_t)u * 64]);
+        __builtin_amdgcn_sched_barrier(0);
+        chr::u32x4 r[U];
+        chr::tree_eval<chr::u32x4, 8, U, chr::VecOp<CHR_FLOAT32, CHR_SUM>>(x, r, g.comb, g.swaps);
+        if constexpr (SAUX == -1) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) chr::st<true>(&g.out[base + (size_t)u * 64], r[u]);
+        } else if constexpr (SAUX >= 0) {
+            const __amdgpu_buffer_rsrc_t ro =
+                __builtin_amdgcn_make_buffer_rsrc((void*)(g.out + trip * 64 * U), 0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                __builtin_amdgcn_raw_buffer_store_b128(r[u], ro, (unsigned)((threadIdx.x + u * 64) * 16), 0, SAUX);
+        } else {
+            if (r[0][0] == 0x7fc00001u && r[0][1] == 0x7fc00002u) g.out[base] = r[0];
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long t1 = wall_clock64();
+    if (threadIdx.x == 0) {
+        st[3 * (size_t)b] = t0;
+        st[3 * (size_t)b + 1] = t1;
+        st[3 * (size_t)b + 2] = __smid();
+    }
+}
+
+template <int SAUX = -1>
+static void focus22(size_t piece, int sets, int cap, int nlaunch, uint32_t flags = 0, const char* label = "product",
+                    bool synced_too = true) {
+    constexpr int U = 1;
+    const size_t nvec = piece / 16;
+    Sets S = make_sets(17, nvec, sets);
+    uint32_t cs = 0;
+    while (((size_t)2 << cs) * (64 * U * 16) <= (size_t)512 * 1024 && cs < 16) ++cs;
+    const uint32_t trips = (uint32_t)((nvec + 64 * U - 1) / (64 * U));
+    const size_t grid = 2 * (size_t)trips;
+    unsigned long long* st = nullptr;
+    CK(hipMalloc(&st, 3 * grid * nlaunch * sizeof(unsigned long long)));
+    int khz = 0;
+    CK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0));
+    const double us_per_tick = 1e3 / khz;
+    auto args = [&](int i) {
+        chr::TreeArgs a{};
+        const auto& bb = S.bufs[i % sets];
+        a.nseg = 2;
+        a.nl = 8;
+        a.xrun = cs;
+        for (int j = 0; j < chr::kMaxTreeSegs; ++j) {
+            a.block0[j] = j < 2 ? j * trips : ~0u;
+            a.xfull[j] = j < 2 ? chr::xcd_full(trips, cs) : 0;
+        }
+        const int comb[8] = {0, 1, 1, 1, 0, 1, 1, 2};
+        for (int t2 = 0; t2 < 2; ++t2) {
+            chr::TreeSeg& g = a.seg[t2];
+            for (int l = 0; l < 8; ++l) g.leaves[l] = (const chr::u32x4*)bb[9 * t2 + l];
+            g.out = (chr::u32x4*)bb[9 * t2 + 8];
+            g.nvec = nvec;
+            g.comb = 0;
+            for (int l = 0; l < 8; ++l) g.comb |= (uint32_t)comb[l] << (2 * l);
+            g.swaps = 0;
+        }
+        return a;
+    };
+    const unsigned lds = lds_for_cap(cap);
+    for (int mode = 0; mode < (synced_too ? 2 : 1); ++mode) {  // 0: back to back on one stream; 1: host sync between
+        for (int i = 0; i < 4; ++i)
+            hipExtLaunchKernelGGL(k_tree_stamped<U, SAUX>, dim3((unsigned)grid), dim3(64), lds, 0, nullptr, nullptr, flags,
+                                  args(i), st);
+        CK(hipDeviceSynchronize());
+        std::vector<hipEvent_t> ev(nlaunch + 1);
+        for (auto& e : ev) CK(hipEventCreate(&e));
+        CK(hipEventRecord(ev[0], 0));
+        for (int i = 0; i < nlaunch; ++i) {
+            hipExtLaunchKernelGGL(k_tree_stamped<U, SAUX>, dim3((unsigned)grid), dim3(64), lds, 0, nullptr, nullptr, flags,
+                                  args(i + 4), st + 3 * grid * i);
+            CK(hipEventRecord(ev[i + 1], 0));
+            if (mode == 1) CK(hipEventSynchronize(ev[i + 1]));
+        }
+        CK(hipDeviceSynchronize());
+        std::vector<unsigned long long> h(3 * grid * nlaunch);
+        CK(hipMemcpy(h.data(), st, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        const double bytes = 2.0 * 9 * piece;
+        unsigned long long prev_end = 0;
+        for (int i = 0; i < nlaunch; ++i) {
+            const unsigned long long* p = h.data() + 3 * grid * i;
+            unsigned long long tmin = ~0ull, tmax = 0, smin = ~0ull;
+            std::vector<unsigned long long> ends(grid);
+            unsigned long long xend[16] = {}, xstart[16];
+            for (auto& x : xstart) x = ~0ull;
+            for (size_t w = 0; w < grid; ++w) {
+                const unsigned long long t0 = p[3 * w], t1 = p[3 * w + 1];
+                const unsigned xcc = (unsigned)(p[3 * w + 2] >> 6) & 15u;  // __smid: XCC | SE (2 bits) | CU (4 bits)
+                tmin = std::min(tmin, t0);
+                tmax = std::max(tmax, t1);
+                smin = std::min(smin, t1);
+                ends[w] = t1;
+                xend[xcc] = std::max(xend[xcc], t1);
+                xstart[xcc] = std::min(xstart[xcc], t0);
+            }
+            std::sort(ends.begin(), ends.end());
+            auto at = [&](double f) { return (ends[(size_t)std::min<double>(grid - 1, f * grid)] - tmin) * us_per_tick; };
+            const double span = (tmax - tmin) * us_per_tick;
+            // steady rate: workgroups completed between 20 % and 80 % over that time
+            const double t20 = at(0.2), t80 = at(0.8);
+            const double ideal = (t80 - t20) / 0.6;
+            double xe_min = 1e30, xe_max = 0, xs_max = 0;
+            for (int x = 0; x < 16; ++x) {
+                if (!xend[x]) continue;
+                xe_min = std::min(xe_min, (xend[x] - tmin) * us_per_tick);
+                xe_max = std::max(xe_max, (xend[x] - tmin) * us_per_tick);
+                xs_max = std::max(xs_max, (xstart[x] - tmin) * us_per_tick);
+            }
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+            std::printf("{\"focus22\": \"%s\", \"mode\": \"%s\", \"piece_mib\": %zu, \"sets\": %d, \"cap\": %d, \"launch\": %d, "
+                        "\"event_us\": %.2f, \"span_us\": %.2f, \"gap_from_prev_us\": %.2f, \"ideal_us\": %.2f, "
+                        "\"first_end_us\": %.2f, \"t5\": %.2f, \"t20\": %.2f, \"t50\": %.2f, \"t80\": %.2f, \"t95\": %.2f, "
+                        "\"t99\": %.2f, \"xcd_first_start_max_us\": %.2f, \"xcd_end_min_us\": %.2f, \"xcd_end_max_us\": %.2f, "
+                        "\"frac_event\": %.4f, \"frac_span\": %.4f, \"frac_steady\": %.4f}\n",
+                        label, mode ? "synced" : "back_to_back", piece >> 20, sets, cap, i, ms * 1e3, span,
+                        prev_end ? (tmin - prev_end) * us_per_tick : -1.0, ideal, (smin - tmin) * us_per_tick, at(0.05),
+                        t20, at(0.5), t80, at(0.95), at(0.99), xs_max, xe_min, xe_max, bytes / (ms * 1e-3) / 8e12,
+                        bytes / (span * 1e-6) / 8e12, bytes / (ideal * 1e-6) / 8e12);
+            prev_end = tmax;
+        }
+        std::fflush(stdout);
+        for (auto& e : ev) CK(hipEventDestroy(e));
+    }
+    CK(hipFree(st));
+    free_sets(S);
+}
+
 template <bool NT, int BL, int U>
 static double vec1_time(Sets& S, size_t nvec, int sets, unsigned lds, uint32_t cs) {
     const unsigned G = (unsigned)(nvec / (BL * U));
@@ -1490,6 +1653,25 @@ int main(int argc, char** argv) {
     check();
     if (argc > 1 && std::string(argv[1]) == "layout") {
         layout_mode();
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus23") {  // what the ~4 us between back-to-back launches is
+        for (int r = 0; r < 2; ++r)
+            for (size_t mib : {16, 8}) {
+                focus22<-1>(mib << 20, 4, 16, 8, 0, "product", false);
+                focus22<-1>(mib << 20, 4, 16, 8, hipExtAnyOrderLaunch, "product_any_order", false);
+                focus22<-2>(mib << 20, 4, 16, 8, 0, "no_store", false);
+                focus22<2>(mib << 20, 4, 16, 8, 0, "buf_nt", false);
+                focus22<0>(mib << 20, 4, 16, 8, 0, "buf_plain", false);
+                focus22<19>(mib << 20, 4, 16, 8, 0, "buf_nt_sc0_sc1", false);
+                focus22<18>(mib << 20, 4, 16, 8, 0, "buf_nt_sc1", false);
+                focus22<3>(mib << 20, 4, 16, 8, 0, "buf_nt_sc0", false);
+            }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus22") {  // timeline of C4-slice tree launches
+        for (size_t mib : {16, 8, 32})
+            for (int cap : {16, 12}) focus22(mib << 20, 4, cap, 8);
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus21") {  // barrier bit vs any-order launches, C4 slice shape
