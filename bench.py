@@ -55,6 +55,9 @@ def parse():
     p.add_argument("--collective-kernels", action="store_true",
                    help="N=1: the fused reductions of the C4/C5 collectives at full size (8 virtual ranks, "
                         "loopback transport), HIP-event timed against the HBM roofline")
+    p.add_argument("--collective-kernels-small", action="store_true",
+                   help="N=1: the same for the N=2 / N=4 lines' allreduces (1 GiB per rank) and C3's reduce-scatter "
+                        "(2 ranks, 256 MiB send): the 2- and 4-leaf trees")
     return p.parse_args()
 
 
@@ -394,6 +397,53 @@ def bench_collective_kernels(args):
                                              "(*_per_rank_launches: one grid per rank and step, as each GPU of a "
                                              "node launches); *_rank0_alone rows: rank 0's own trees on its own "
                                              "send/recv/STAGE only", "rows": rows}})
+
+
+def bench_collective_kernels_small(args):
+    """The fused reductions of the smaller multi-GPU configs, on virtual ranks as above: the N=2 and
+    N=4 lines' allreduces (1 GiB fp32 per rank, b = N, k = min(4, N): 2- and 4-leaf trees) and C3
+    (reduce-scatter, 2 ranks, 256 MiB fp32 send buffer, radix 2, b = 1 and 2: 2-leaf trees), each
+    with the ranks' trees of a step in shared grids and with one grid per rank."""
+    import torch
+
+    import chiara_amd as ca
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    rows = {}
+    cases = [("ar_n2_k2_b2", "ar", 2, 2, 2, 1 << 28), ("ar_n4_k4_b4", "ar", 4, 4, 4, 1 << 28),
+             ("c3_rs_n2_k2_b1", "rs", 2, 2, 1, 1 << 25), ("c3_rs_n2_k2_b2", "rs", 2, 2, 2, 1 << 25)]
+    for name, mode, n, k, b, cnt in cases:
+        g = ca.LocalGroup(n, 0)
+        total = cnt if mode == "ar" else cnt * n  # send elements per rank
+        sends = [torch.empty(total * 4, dtype=torch.uint8, device=dev) for _ in range(n)]
+        recvs = [torch.empty(cnt * 4, dtype=torch.uint8, device=dev) for _ in range(n)]
+        for r, x in enumerate(sends):
+            ca.check(ca.fill(x, total, ca.FLOAT32, 0, SEED, r, stream=g.stream))
+        fn = g.all_reduce_radix_batch if mode == "ar" else g.reduce_scatter_radix_batch
+        for batched in (True, False):
+            g.set_batching(batched)
+            ca.check(fn(sends, recvs, cnt, ca.FLOAT32, ca.SUM, k, b))  # warm: plans, scratch
+            g.profile(True)
+            g.profile_read()
+            reps = 5
+            for _ in range(reps):
+                ca.check(fn(sends, recvs, cnt, ca.FLOAT32, ca.SUM, k, b))
+            ms, by, launches = g.profile_read()
+            g.profile(False)
+            ach = by / (ms * 1e-3) / 1e9
+            rows[name + ("" if batched else "_per_rank_launches")] = {
+                "launches_per_call_all_ranks": launches // reps, "kernel_ms_per_call_all_ranks": round(ms / reps, 4),
+                "algorithmic_bytes_per_call_all_ranks": int(by / reps), "achieved_GBps": round(ach, 1),
+                "frac": round(ach / HBM_PEAK_GBPS, 4)}
+        g.destroy()
+        del sends, recvs
+        torch.cuda.empty_cache()
+    knobs = {k: v for k, v in os.environ.items() if k.startswith("CHR_")}
+    emit({"collective_kernels_small": {"workload": "fused reductions of the N=2 / N=4 allreduce lines (1 GiB fp32 per "
+                                                   "rank) and C3 (reduce-scatter, 2 ranks, 256 MiB send), virtual "
+                                                   "ranks on one GPU, each reduce phase timed as one span",
+                                       "env": knobs, "rows": rows}})
 
 
 def replay_rank_trees(ca, torch, dev, cdt, es, count, n, k, b, slices, recv_copies, reps=5):
@@ -844,6 +894,9 @@ def _main():
         return
     if args.collective_kernels:
         bench_collective_kernels(args)
+        return
+    if args.collective_kernels_small:
+        bench_collective_kernels_small(args)
         return
     cpu = None if args.no_cpu_baseline else cpu_baseline(args.cpu_seconds)
     bench_bucket(args, cpu)
