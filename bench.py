@@ -554,7 +554,7 @@ def bench_allreduce(args):
         comm.set_schedule(metric_sched)
     ca.check(ca.all_reduce_radix_batch(send, recv, count, dt, ca.SUM, comm, k, b))
     tuned = comm.tuned_schedule(ca.MODE_ALLREDUCE, count, dt, k, b) if metric_sched is not None else None
-    sched_names = {0: "reference", 1: "balanced", 2: "flat", 3: "exact", 4: "flat_ag", 5: "flat_seq"}
+    sched_names = {0: "reference", 1: "balanced", 2: "flat", 3: "exact", 4: "flat_ag", 5: "flat_seq", 7: "flat_1shot"}
     for _ in range(args.warmup):
         ca.check(ca.all_reduce_radix_batch(send, recv, count, dt, ca.SUM, comm, k, b, async_op=True))
     ca.check(comm.synchronize())
@@ -758,15 +758,19 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
         comm.set_schedule(restore)
     if out.get("aborted"):
         return out
-    out["small_messages"] = small_messages(ca, torch, dist, comm, dt, k, b, world, dev)
+    out["small_messages"] = small_messages(ca, torch, dist, comm, dt, k, b, world, dev, restore)
     out.update(baseline_configs(args, ca, torch, dist, comm, world, dev, steps, warm))
     return out
 
 
-def small_messages(ca, torch, dist, comm, dt, k, b, world, dev):
-    """Latency of blocking calls (the reference harness's pattern) at small buffers, issued eagerly
-    and replayed from captured HIP graphs (chr_comm_set_graphs): us per call, max over ranks."""
+def small_messages(ca, torch, dist, comm, dt, k, b, world, dev, current):
+    """Latency of blocking calls (the reference harness's pattern) at small buffers: us per call, max
+    over ranks, with the communicator's schedule (the metric's AUTO, whose choice is reported) issued
+    eagerly and replayed from captured HIP graphs (chr_comm_set_graphs), and eagerly under FLAT
+    (gather + allgather: two exchange steps) and FLAT_1SHOT (one step, every rank reduces the whole
+    buffer)."""
     es = 4 if dt == ca.FLOAT32 else 2
+    names = {0: "reference", 1: "balanced", 2: "flat", 3: "exact", 4: "flat_ag", 5: "flat_seq", 7: "flat_1shot"}
     res = {}
     try:
         for nbytes in (4 << 10, 256 << 10, 4 << 20):
@@ -775,14 +779,21 @@ def small_messages(ca, torch, dist, comm, dt, k, b, world, dev):
             r = torch.empty(count * es, dtype=torch.uint8, device=dev)
             ca.check(ca.fill(s, count, dt, 0, SEED, int(os.environ["RANK"]), stream=comm.stream))
             row = {}
-            for name, g in (("eager_us", False), ("graph_us", True)):
+            for name, g, sch in (("eager_us", False, current), ("graph_us", True, current),
+                                 ("flat_eager_us", False, ca.SCHEDULE_FLAT),
+                                 ("flat_1shot_eager_us", False, ca.SCHEDULE_FLAT_1SHOT)):
                 comm.set_graphs(g)
+                comm.set_schedule(sch)
                 try:
                     el = _timed_max(torch, dist, lambda: ca.check(ca.all_reduce_radix_batch(s, r, count, dt, ca.SUM, comm,
                                                                                              k, b)), 50, 3)
                 finally:
                     comm.set_graphs(False)
+                    comm.set_schedule(current)
                 row[name] = round(el / 50 * 1e6, 1)
+            tuned = comm.tuned_schedule(ca.MODE_ALLREDUCE, count, dt, k, b) if current == ca.SCHEDULE_AUTO else None
+            if tuned is not None:
+                row["auto_choice"] = f"{names.get(tuned[0], tuned[0])}, {tuned[1]} slices"
             res[f"{nbytes >> 10}KiB"] = row
     except Exception as e:  # context only
         res["error"] = str(e)[:200]

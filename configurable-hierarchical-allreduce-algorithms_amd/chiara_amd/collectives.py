@@ -56,7 +56,8 @@ MODE_ALLGATHER = 8
 MODE_MPICH_RS_RADIX, MODE_MPICH_RS_HALVING, MODE_MPICH_RS_DOUBLING, MODE_MPICH_RS_PAIRWISE = 9, 10, 11, 12
 RS_MODES = (1, 9, 10, 11, 12)  # count = recvcount, send = nranks * recvcount
 SCHEDULE_REFERENCE, SCHEDULE_BALANCED, SCHEDULE_FLAT, SCHEDULE_EXACT, SCHEDULE_FLAT_AG, SCHEDULE_FLAT_SEQ = 0, 1, 2, 3, 4, 5
-SCHEDULE_AUTO = 6  # measured choice among FLAT / FLAT_SEQ / FLAT_AG and the pipeline depth (Comm only)
+SCHEDULE_AUTO = 6  # measured choice among FLAT / FLAT_SEQ / FLAT_AG (/ FLAT_1SHOT) and the depth (Comm only)
+SCHEDULE_FLAT_1SHOT = 7  # allreduce: one exchange step, every rank evaluates the whole buffer (small messages)
 REDUCE_RUNNING_FIRST = 1  # chr_reduce_multi_ex flag (MPICH_do_reduce operand order)
 
 
@@ -163,7 +164,8 @@ class Comm:
 
     def set_schedule(self, schedule):
         """SCHEDULE_REFERENCE / SCHEDULE_BALANCED / SCHEDULE_FLAT / SCHEDULE_EXACT / SCHEDULE_FLAT_AG /
-        SCHEDULE_FLAT_SEQ / SCHEDULE_AUTO: where reductions are evaluated (never what they compute)."""
+        SCHEDULE_FLAT_SEQ / SCHEDULE_FLAT_1SHOT / SCHEDULE_AUTO: where reductions are evaluated (never what
+        they compute)."""
         check(lib().chr_comm_set_schedule(self._h, int(schedule)))
 
     def set_graphs(self, enable):

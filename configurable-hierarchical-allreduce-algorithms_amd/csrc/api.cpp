@@ -128,7 +128,7 @@ long chr_plan_describe(chr_mode mode, int nranks, int rank, int k, int b, size_t
 long chr_plan_describe_ex(chr_mode mode, int nranks, int rank, int k, int b, size_t count, int slices, int schedule,
                           char* buf, size_t len) {
     if (mode < CHR_MODE_ALLREDUCE || mode > CHR_MODE_MPICH_RS_PAIRWISE) return -1;
-    if (schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_FLAT_SEQ) return -1;
+    if (!chr::plan_schedule(schedule)) return -1;
     const std::string s = chr::describe(chr::build_plan((chr::Mode)mode, nranks, rank, k, b, count, slices, schedule));
     if (buf && len) {
         const size_t c = s.size() < len - 1 ? s.size() : len - 1;

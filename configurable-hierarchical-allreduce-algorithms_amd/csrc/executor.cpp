@@ -378,6 +378,7 @@ int default_schedule() {
         if (s == "exact" || s == "3") return (int)chr::SCHED_EXACT;
         if (s == "flat_ag" || s == "4") return (int)chr::SCHED_FLAT_AG;
         if (s == "flat_seq" || s == "5") return (int)chr::SCHED_FLAT_SEQ;
+        if (s == "flat_1shot" || s == "7") return (int)chr::SCHED_FLAT_1SHOT;
         if (s == "auto" || s == "6") return CHR_SCHEDULE_AUTO;
         return (int)chr::SCHED_FLAT;
     }();
@@ -394,8 +395,14 @@ int default_schedule() {
 constexpr uint64_t kMinFlatPieceBytes = (uint64_t)16 << 20;
 
 bool flat_family(int sched) {
-    return sched == chr::SCHED_FLAT || sched == chr::SCHED_FLAT_AG || sched == chr::SCHED_FLAT_SEQ;
+    return sched == chr::SCHED_FLAT || sched == chr::SCHED_FLAT_AG || sched == chr::SCHED_FLAT_SEQ ||
+           sched == chr::SCHED_FLAT_1SHOT;
 }
+
+// SCHED_FLAT_1SHOT moves (n-1) S per rank instead of 2 (n-1)/n S: a latency trade for small calls.  AUTO
+// times it only up to this many bytes per rank (8 GPUs at ~350 GB/s of xGMI per direction: the
+// extra 1.75 S costs one RCCL group's ~15 us of latency near S = 3 MB).
+constexpr uint64_t kOneShotMaxBytes = (uint64_t)8 << 20;
 
 int pick_slices(int setting, uint64_t count, int mode, int nranks, int b, size_t es, int sched) {
     if (chr::is_mpich(mode) || mode == chr::MODE_ALLGATHER) return 1;  // unpipelined schedules
@@ -410,7 +417,9 @@ int pick_slices(int setting, uint64_t count, int mode, int nranks, int b, size_t
     const uint64_t irc_bytes = recvcount * (uint64_t)(b > 0 ? b : 1) * es;
     int P = chr::auto_slices(irc_bytes);
     if (flat_family(sched)) {
-        const uint64_t piece = mode == chr::MODE_ALLREDUCE ? irc_bytes / n : recvcount * es;
+        const uint64_t piece = mode == chr::MODE_ALLREDUCE && sched != chr::SCHED_FLAT_1SHOT ? irc_bytes / n
+                               : mode == chr::MODE_ALLREDUCE                                ? irc_bytes
+                                                                                            : recvcount * es;
         const int cap = (int)std::max<uint64_t>(1, piece / kMinFlatPieceBytes);
         P = std::min(P, cap);
     }
@@ -1091,6 +1100,8 @@ int tune_schedule(chr_comm* c, int mode, const void* send, void* recv, size_t co
     }
     for (int sc : {(int)chr::SCHED_FLAT, (int)chr::SCHED_FLAT_SEQ, (int)chr::SCHED_FLAT_AG})
         for (int d : depths) cand.push_back({sc, d});
+    if (mode == chr::MODE_ALLREDUCE && (uint64_t)count * es <= kOneShotMaxBytes)
+        for (int d : depths) cand.push_back({(int)chr::SCHED_FLAT_1SHOT, d});
     std::vector<float> ms(cand.size(), 0.f);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     hipError_t e = hipSuccess;
@@ -1453,7 +1464,7 @@ int chr_comm_set_overlap(chr_comm* c, int enable) {
 }
 
 int chr_comm_set_schedule(chr_comm* c, int schedule) {
-    if (!c || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_AUTO) return CHR_ERR_INVALID_ARG;
+    if (!c || !(chr::plan_schedule(schedule) || schedule == CHR_SCHEDULE_AUTO)) return CHR_ERR_INVALID_ARG;
     c->sched = schedule;
     return CHR_SUCCESS;
 }
@@ -1486,7 +1497,7 @@ int chr_comm_tuned_schedule(const chr_comm* c, int mode, size_t count, chr_dtype
 }
 
 int chr_local_group_set_schedule(chr_local_group* g, int schedule) {
-    if (!g || schedule < CHR_SCHEDULE_REFERENCE || schedule > CHR_SCHEDULE_FLAT_SEQ) return CHR_ERR_INVALID_ARG;
+    if (!g || !chr::plan_schedule(schedule)) return CHR_ERR_INVALID_ARG;
     g->sched = schedule;
     return CHR_SUCCESS;
 }

@@ -5,6 +5,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "reduce_common.hpp"
 
 namespace chr {
@@ -107,13 +109,35 @@ struct VecOp {
     }
 };
 
+// The scalar kernel's stack slots: the element type itself, except for the pair and complex
+// structs, which ride the slots as vectors of their 32-bit words and are bit-cast to the struct only
+// inside a combine.  With the structs themselves as slot values, the slot selects of tree_eval were
+// miscompiled for C_FLOAT_COMPLEX at depth 4 (a leaf's words shifted by one: tests/test_gpu_tree.py
+// ::test_tree_scalar_path_pair_and_complex_every_program, round 3).
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+template <int NW> struct WordsOf;
+template <> struct WordsOf<2> { using V = u32x2; };
+template <> struct WordsOf<4> { using V = u32x4; };
+template <int DT, bool WORDS = is_pair_dt<DT>() || is_complex_dt<DT>()>
+struct SlotOf {
+    using V = typename DTy<DT>::T;
+};
+template <int DT>
+struct SlotOf<DT, true> {
+    using V = typename WordsOf<sizeof(typename DTy<DT>::T) / 4>::V;
+};
+template <int DT>
+using slot_t = typename SlotOf<DT>::V;
+
 template <int DT, int OP>
 struct ScalarOp {
     using T = typename DTy<DT>::T;
+    using V = slot_t<DT>;
     template <bool SW>
-    __device__ __forceinline__ static T ap(T in, T run) {
-        if constexpr (SW && order_sensitive<DT, OP>()) return apply<DT, swapped_op<OP>()>(in, run);
-        else return apply<DT, OP>(in, run);
+    __device__ __forceinline__ static V ap(V in, V run) {
+        constexpr int O = SW && order_sensitive<DT, OP>() ? swapped_op<OP>() : OP;
+        if constexpr (std::is_same_v<V, T>) return apply<DT, O>(in, run);
+        else return __builtin_bit_cast(V, apply<DT, O>(__builtin_bit_cast(T, in), __builtin_bit_cast(T, run)));
     }
 };
 
@@ -191,13 +215,14 @@ struct TreeScalarArgs {
 template <int DT, int OP, int NL>
 __global__ __launch_bounds__(kBlock) void k_reduce_tree_scalar(TreeScalarArgs a) {
     using T = typename DTy<DT>::T;
+    using V = slot_t<DT>;
     for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < a.n; i += (size_t)gridDim.x * kBlock) {
-        T x[NL][1];
+        V x[NL][1];
 #pragma unroll
-        for (int j = 0; j < NL; ++j) x[j][0] = ((const T*)a.leaves[j])[i];
-        T r[1];
-        tree_eval<T, NL, 1, ScalarOp<DT, OP>>(x, r, a.comb, a.swaps);
-        ((T*)a.out)[i] = r[0];
+        for (int j = 0; j < NL; ++j) x[j][0] = __builtin_bit_cast(V, ((const T*)a.leaves[j])[i]);
+        V r[1];
+        tree_eval<V, NL, 1, ScalarOp<DT, OP>>(x, r, a.comb, a.swaps);
+        ((T*)a.out)[i] = __builtin_bit_cast(T, r[0]);
     }
 }
 

@@ -616,7 +616,7 @@ int auto_slices(uint64_t irc_bytes) {
 }
 
 Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, int slices, bool coll_ag = false,
-                     bool merge = true);
+                     bool merge = true, bool oneshot = false);
 static Plan build_plan_impl(Mode mode, int n, int me, int k_in, int b, uint64_t count, int slices, int sched);
 
 // The fused kernel takes at most kPlanFanIn inputs per pass (kMaxFanIn, reduce_kernels.hip)
@@ -788,8 +788,10 @@ static Plan build_plan_impl(Mode mode, int n, int me, int k_in, int b, uint64_t 
     p.recv_elems = mode == MODE_ALLREDUCE ? g.total : recvcount;
     p.acc_elems = g.total;
     if (g.total == 0) return p;
-    if ((sched == SCHED_FLAT || sched == SCHED_FLAT_AG || sched == SCHED_FLAT_SEQ) && n > 1) {
-        Plan f = build_plan_flat(mode, n, me, k_in, b, g, slices, sched == SCHED_FLAT_AG, sched != SCHED_FLAT_SEQ);
+    if ((sched == SCHED_FLAT || sched == SCHED_FLAT_AG || sched == SCHED_FLAT_SEQ || sched == SCHED_FLAT_1SHOT) &&
+        n > 1) {
+        Plan f = build_plan_flat(mode, n, me, k_in, b, g, slices, sched == SCHED_FLAT_AG, sched != SCHED_FLAT_SEQ,
+                                 sched == SCHED_FLAT_1SHOT && mode == MODE_ALLREDUCE);
         if (!f.error) return f;
     }
 
@@ -1884,12 +1886,15 @@ bool tree_enabled() {
 
 }  // namespace
 
-Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, int slices, bool coll_ag, bool merge) {
+// oneshot (allreduce): every rank's "piece" is the whole slice -- it receives every peer's whole
+// slice of every chunk and evaluates all of it, so no allgather follows (SCHED_FLAT_1SHOT).
+Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, int slices, bool coll_ag, bool merge,
+                     bool oneshot) {
     Plan p;
     p.mode = mode;
     p.rank = me;
     p.g = g;
-    p.sched = coll_ag ? SCHED_FLAT_AG : merge ? SCHED_FLAT : SCHED_FLAT_SEQ;
+    p.sched = oneshot ? SCHED_FLAT_1SHOT : coll_ag ? SCHED_FLAT_AG : merge ? SCHED_FLAT : SCHED_FLAT_SEQ;
     // 1. the reference-order plans of every rank at recvcount = 1, executed symbolically
     const uint64_t cnt1 = mode == MODE_ALLREDUCE ? (uint64_t)n : 1;
     std::vector<Plan> ref;
@@ -1962,7 +1967,7 @@ Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, 
         const uint64_t hi = s2 == P - 1 ? span : (span * (s2 + 1) / P) / G * G;
         const uint64_t len = hi - lo;
         // slots: 64-element multiples, +64 for the per-chunk phase shift below
-        const uint64_t stride = ((mode == MODE_ALLREDUCE ? len / (uint64_t)n + 64 : len) + 127) / 64 * 64;
+        const uint64_t stride = ((mode == MODE_ALLREDUCE && !oneshot ? len / (uint64_t)n + 64 : len) + 127) / 64 * 64;
         sl[s2] = {lo, len, stage, stride};
         stage += slots * stride;
     }
@@ -1970,6 +1975,11 @@ Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, 
     // piece q of a slice (allreduce): 64-element aligned cut into n
     auto cut = [&](const Sl& c, uint64_t i) { return i >= (uint64_t)n ? c.len : (c.len * i / (uint64_t)n) / 64 * 64; };
     auto piece = [&](const Sl& c, int q, uint64_t* a, uint64_t* l) {
+        if (oneshot) {  // every rank evaluates the whole slice
+            *a = 0;
+            *l = c.len;
+            return;
+        }
         *a = cut(c, (uint64_t)q);
         *l = cut(c, (uint64_t)q + 1) - *a;
     };
@@ -2072,6 +2082,10 @@ Plan build_plan_flat(Mode mode, int n, int me, int k, int b, const Geometry& g, 
         st.label = std::string(kind == F_GATHER ? "gather" : "fdist") + "/s" + std::to_string(s2);
         emit(kind, sl[s2], st);
     };
+    if (oneshot) {  // P gather steps, each followed by the whole slice's evaluation; nothing to distribute
+        for (int s2 = 0; s2 < P; ++s2) add(F_GATHER, s2);
+        return p;
+    }
     if (merge && mode == MODE_ALLREDUCE) {
         // One RCCL group per step t: gather of slice t together with the allgather of slice t-2.
         // Slice t-2 was reduced (compute stream) while step t-1's group was on the links, so the

@@ -147,9 +147,17 @@ void recexch_count_offset(int nranks, int max_phases, int k, std::vector<int>* c
 //                    (pure data movement, so the bits are unchanged) where the pieces are equal
 //   SCHED_FLAT_SEQ   SCHED_FLAT with gather and allgather in separate RCCL groups (2P groups per
 //                    call instead of P + 2; the ordering before the merged groups)
+//   SCHED_FLAT_1SHOT allreduce: every rank gathers the whole buffer from every peer and evaluates
+//                    every chunk's tree itself -- one exchange step instead of gather + allgather,
+//                    (n-1) S bytes per rank instead of 2 (n-1)/n S: the latency-bound small-message
+//                    variant.  Reduce-scatter: SCHED_FLAT (already one step).
+//   (6 is CHR_SCHEDULE_AUTO, the executor's measured choice, not a plan.)
 enum Sched : int {
-    SCHED_REFERENCE = 0, SCHED_BALANCED = 1, SCHED_FLAT = 2, SCHED_EXACT = 3, SCHED_FLAT_AG = 4, SCHED_FLAT_SEQ = 5
+    SCHED_REFERENCE = 0, SCHED_BALANCED = 1, SCHED_FLAT = 2, SCHED_EXACT = 3, SCHED_FLAT_AG = 4, SCHED_FLAT_SEQ = 5,
+    SCHED_FLAT_1SHOT = 7
 };
+// A schedule a plan can be built for (every Sched value; not CHR_SCHEDULE_AUTO).
+inline bool plan_schedule(int s) { return (s >= SCHED_REFERENCE && s <= SCHED_FLAT_SEQ) || s == SCHED_FLAT_1SHOT; }
 Plan build_plan(Mode mode, int nranks, int rank, int k, int b, uint64_t count, int slices = 1,
                 int sched = SCHED_FLAT);
 int auto_slices(uint64_t irc_bytes);

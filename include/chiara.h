@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define CHR_ABI_VERSION 6
+#define CHR_ABI_VERSION 7
 
 /* Element types.  The reference is generic over MPI_Datatype (all_reduce_radix_batch.cpp:202-204,
  * sizes from MPI_Type_size at :234-277); these are the MPI predefined types MPICH's
@@ -190,20 +190,27 @@ int chr_comm_set_slices(chr_comm* comm, int slices);
  *                           movement only, so identical bits
  *   CHR_SCHEDULE_FLAT_SEQ   FLAT with its gather and allgather in separate RCCL groups (FLAT
  *                           merges the gather of slice t with the allgather of slice t-2)
- * Env CHR_SCHEDULE=reference|balanced|flat|exact|flat_ag|flat_seq|auto sets the default.  DESIGN.md §5. */
+ * Env CHR_SCHEDULE=reference|balanced|flat|exact|flat_ag|flat_seq|auto|flat_1shot sets the default.  DESIGN.md §5. */
 #define CHR_SCHEDULE_REFERENCE 0
 #define CHR_SCHEDULE_BALANCED 1
 #define CHR_SCHEDULE_FLAT 2
 #define CHR_SCHEDULE_EXACT 3
 #define CHR_SCHEDULE_FLAT_AG 4
 #define CHR_SCHEDULE_FLAT_SEQ 5
-/*   CHR_SCHEDULE_AUTO       chooses among FLAT, FLAT_SEQ and FLAT_AG and the pipeline depth by
+/*   CHR_SCHEDULE_AUTO       chooses among FLAT, FLAT_SEQ and FLAT_AG (and FLAT_1SHOT for
+ *                           allreduces of <= 8 MiB per rank) and the pipeline depth by
  *                           measurement: on the first device-resident call for a (collective,
  *                           count, dtype, k, b) every candidate runs a few complete collectives,
  *                           the ranks agree on the slowest rank's times (one ncclAllReduce) and
  *                           the fastest is kept.  Same bits as every other schedule.  Host-staged
  *                           calls and the other collectives use FLAT. */
 #define CHR_SCHEDULE_AUTO 6
+/*   CHR_SCHEDULE_FLAT_1SHOT allreduce: every rank receives the whole buffer from every peer in one
+ *                           exchange step and evaluates every chunk's expression tree itself (no
+ *                           allgather): one RCCL group per slice instead of two, (n-1)·S bytes per
+ *                           rank instead of 2(n-1)/n·S -- the latency-bound small-message variant of
+ *                           FLAT.  Reduce-scatter runs FLAT (already one step).  Same bits. */
+#define CHR_SCHEDULE_FLAT_1SHOT 7
 int chr_comm_set_schedule(chr_comm* comm, int schedule);
 /* What CHR_SCHEDULE_AUTO chose for a collective already called with these arguments
  * (mode: 0 allreduce_radix_batch, 1 reduce_scatter_radix_batch; count as passed). */

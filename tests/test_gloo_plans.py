@@ -94,7 +94,8 @@ def test_gloo_world2():
              (ca.MODE_ALLREDUCE, 2, 2, 2 * 4096, "f32", 4), (ca.MODE_REDUCE_SCATTER, 2, 1, 4096, "f32", 3),
              (ca.MODE_ALLREDUCE, 2, 2, 2 * 1000, "f32", 1, ca.SCHEDULE_EXACT),
              (ca.MODE_REDUCE_SCATTER, 2, 2, 4096, "f32", 1, ca.SCHEDULE_EXACT),
-             (ca.MODE_ALLREDUCE, 2, 2, 2 * 4096, "f32", 3, ca.SCHEDULE_FLAT_AG)])
+             (ca.MODE_ALLREDUCE, 2, 2, 2 * 4096, "f32", 3, ca.SCHEDULE_FLAT_AG),
+             (ca.MODE_ALLREDUCE, 2, 2, 2 * 1000, "f32", 2, ca.SCHEDULE_FLAT_1SHOT)])
 
 
 @pytest.mark.slow
@@ -106,4 +107,6 @@ def test_gloo_world4():
              (ca.MODE_ALLREDUCE, 4, 4, 4 * 2048, "f32", 3), (ca.MODE_REDUCE_SCATTER, 2, 2, 1500, "bf16", 2),
              (ca.MODE_ALLREDUCE, 2, 4, 4 * 333, "f32", 1, ca.SCHEDULE_EXACT),
              (ca.MODE_REDUCE_SCATTER, 4, 4, 50, "f32", 1, ca.SCHEDULE_EXACT),
-             (ca.MODE_ALLREDUCE, 4, 4, 4 * 4096, "bf16", 2, ca.SCHEDULE_FLAT_AG)])
+             (ca.MODE_ALLREDUCE, 4, 4, 4 * 4096, "bf16", 2, ca.SCHEDULE_FLAT_AG),
+             (ca.MODE_ALLREDUCE, 2, 4, 4 * 333, "f32", 1, ca.SCHEDULE_FLAT_1SHOT),
+             (ca.MODE_ALLREDUCE, 4, 4, 4 * 2048, "bf16", 3, ca.SCHEDULE_FLAT_1SHOT)])

@@ -18,6 +18,9 @@ DT = {"f32": ca.FLOAT32, "f64": ca.FLOAT64, "i32": ca.INT32, "bf16": ca.BFLOAT16
       "i16": ca.INT16, "u16": ca.UINT16, "u32": ca.UINT32, "i64": ca.INT64, "u64": ca.UINT64,
       "fi": ca.FLOAT_INT, "di": ca.DOUBLE_INT, "li": ca.LONG_INT, "2i": ca.TWO_INT, "si": ca.SHORT_INT,
       "cf": ca.C_FLOAT_COMPLEX, "cd": ca.C_DOUBLE_COMPLEX}
+SCHEDULES = {"flat": ca.SCHEDULE_FLAT, "balanced": ca.SCHEDULE_BALANCED, "reference": ca.SCHEDULE_REFERENCE,
+             "exact": ca.SCHEDULE_EXACT, "flat_ag": ca.SCHEDULE_FLAT_AG, "flat_seq": ca.SCHEDULE_FLAT_SEQ,
+             "flat_1shot": ca.SCHEDULE_FLAT_1SHOT}
 OP = {"sum": ca.SUM, "prod": ca.PROD, "max": ca.MAX, "min": ca.MIN, "land": ca.LAND, "lor": ca.LOR,
       "lxor": ca.LXOR, "band": ca.BAND, "bor": ca.BOR, "bxor": ca.BXOR, "maxloc": ca.MAXLOC, "minloc": ca.MINLOC}
 
@@ -87,8 +90,10 @@ def test_local_group_matches_reference_golden(gu, groups, golden):
     assert not bad, f"{len(bad)} device/reference mismatches, e.g. {bad[:5]}"
 
 
-def test_local_group_exact_schedule_matches_reference_golden(gu, groups, golden):
-    """The exact schedule (reference messages end to end) on the device, every radix/batch golden case."""
+@pytest.mark.parametrize("schedule", ["exact", "flat_1shot"])
+def test_local_group_exact_schedule_matches_reference_golden(gu, groups, golden, schedule):
+    """The exact schedule (reference messages end to end) and the one-shot flat schedule (every rank
+    evaluates the whole buffer) on the device, every radix/batch golden case."""
     cases, _ = golden
     bad = []
     for c in cases:
@@ -98,7 +103,7 @@ def test_local_group_exact_schedule_matches_reference_golden(gu, groups, golden)
         in_n = c["count"] * n if c["mode"] == "rs" else c["count"]
         sends = [po.fill(in_n, c["dtype"], c["pattern"], c["seed"], r) for r in range(n)]
         g = groups(n)
-        g.set_schedule(ca.SCHEDULE_EXACT)
+        g.set_schedule(SCHEDULES[schedule])
         try:
             outs = run_local(gu, g, c["mode"], sends, c["k"], c["b"], c["dtype"], c["op"], bool(c["inplace"]))
         finally:
@@ -445,7 +450,7 @@ def test_schedules_bit_identical(gu, groups, n, k, b, dtype):
     outs = {}
     try:
         for sch in (ca.SCHEDULE_FLAT, ca.SCHEDULE_BALANCED, ca.SCHEDULE_REFERENCE, ca.SCHEDULE_EXACT,
-                    ca.SCHEDULE_FLAT_AG, ca.SCHEDULE_FLAT_SEQ):
+                    ca.SCHEDULE_FLAT_AG, ca.SCHEDULE_FLAT_SEQ, ca.SCHEDULE_FLAT_1SHOT):
             g.set_schedule(sch)
             g.set_slices(3)
             outs[sch] = run_local(gu, g, "ar", sends, k, b, dtype, "sum")
@@ -505,8 +510,6 @@ def test_balanced_reduce_scatter_equals_owner_lane(gu, groups, n, k, b):
         g.set_schedule(ca.SCHEDULE_FLAT)
 
 
-SCHEDULES = {"flat": ca.SCHEDULE_FLAT, "balanced": ca.SCHEDULE_BALANCED, "reference": ca.SCHEDULE_REFERENCE,
-             "exact": ca.SCHEDULE_EXACT, "flat_ag": ca.SCHEDULE_FLAT_AG, "flat_seq": ca.SCHEDULE_FLAT_SEQ}
 
 
 @pytest.mark.parametrize("schedule", sorted(SCHEDULES))

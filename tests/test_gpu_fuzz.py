@@ -35,7 +35,7 @@ PAIRS = [("f32", "sum"), ("f32", "sum"), ("f32", "max"), ("f32", "min"), ("f32",
          ("bf16", "max"), ("f64", "sum"), ("i32", "sum"), ("i32", "max"), ("i64", "bxor"), ("u8", "min"),
          ("i16", "land"), ("u32", "bor"), ("f32", "lor"), ("u64", "sum"), ("i8", "prod")]
 SCHED = [ca.SCHEDULE_FLAT, ca.SCHEDULE_REFERENCE, ca.SCHEDULE_BALANCED, ca.SCHEDULE_EXACT, ca.SCHEDULE_FLAT_AG,
-         ca.SCHEDULE_FLAT_SEQ]
+         ca.SCHEDULE_FLAT_SEQ, ca.SCHEDULE_FLAT_1SHOT]
 MPICH = {{"ring": ca.MODE_MPICH_RING, "rd": ca.MODE_MPICH_RD, "rsag": ca.MODE_MPICH_RSAG, "rx": ca.MODE_MPICH_RECEXCH,
          "krsag": ca.MODE_MPICH_KRSAG, "rm": ca.MODE_MPICH_RMULT}}
 MPICH_RS = {{"rs_radix": ca.MODE_MPICH_RS_RADIX, "rs_halving": ca.MODE_MPICH_RS_HALVING,

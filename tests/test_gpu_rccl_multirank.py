@@ -101,7 +101,8 @@ def _worker(rank, world, port, cases, q):
                 tuned = comm.tuned_schedule(ca.MODE_ALLREDUCE if mode == "ar" else ca.MODE_REDUCE_SCATTER, count, cdt,
                                             k, b)
                 ok = ok and ((tuned is None) == host)
-                ok = ok and (tuned is None or tuned[0] in (ca.SCHEDULE_FLAT, ca.SCHEDULE_FLAT_SEQ, ca.SCHEDULE_FLAT_AG))
+                ok = ok and (tuned is None or tuned[0] in (ca.SCHEDULE_FLAT, ca.SCHEDULE_FLAT_SEQ, ca.SCHEDULE_FLAT_AG,
+                                                           ca.SCHEDULE_FLAT_1SHOT))
             q.put((rank, mode, k, b, rc, ok))
     finally:
         comm.destroy()
@@ -177,15 +178,17 @@ def test_rccl_world5_mpich_baselines():
 
 
 def test_rccl_schedules_and_overlap_world4():
-    """The two-stream executor (overlap on/off) under all six schedules, allreduce and
+    """The two-stream executor (overlap on/off) under all seven schedules, allreduce and
     reduce-scatter, 4 ranks over RCCL (and allgather_radix_batch in the same session): bit-exact vs
     the oracle."""
     cases = list(ALLGATHER_W4)
-    for sched in (0, 1, 2, 3, 4, 5):
+    for sched in (0, 1, 2, 3, 4, 5, 7):
         for ov in (True, False):
             cases.append(("ar", 4, 4, 1 << 18, "f32", False, 4, sched, ov))
             cases.append(("rs", 2, 2, 1 << 15, "f32", False, 3, sched, ov))
     cases.append(("ar", 2, 4, 1 << 18, "bf16", False, 5, 2, True))  # multi-phase tree, flat
+    cases.append(("ar", 2, 4, 8 * 1001, "bf16", False, 2, 7, True, True))  # multi-phase tree, one-shot, in place
+    cases.append(("ar", 4, 4, 1 << 14, "f32", True, 1, 7, True))  # one-shot, host-staged
     _run(4, cases, timeout=600)
 
 

@@ -5,6 +5,8 @@ builds one chunk across phases (all_reduce_radix_batch.cpp:332, :364, :446, :529
 CPU side evaluates the same post-order program with the oracle's MPI_Reduce_local
 restatement, one call per combine.  Bar: bit-exact for every dtype and op, including the
 running-value-first (swap) combines and ties/NaN data (pattern 2)."""
+import zlib
+
 import numpy as np
 import pytest
 
@@ -157,10 +159,64 @@ def test_tree_pair_and_complex_types(gu, dtype, op):
     random programs with random swap bits (MPICH_do_reduce order per combine), 2..8 leaves, vector
     path with a ragged tail and the misaligned scalar path; the floating pairs on TIES data, where
     the swap bits change the result bits."""
-    rng = np.random.default_rng(hash((dtype, op)) & 0xFFFF)
+    rng = np.random.default_rng(zlib.crc32(f"{dtype}-{op}".encode()))
     pat = po.PAT_TIES if dtype in ("fi", "di") else po.PAT_UNIFORM
     for nl in (2, 3, 5, 8):
         comb, swaps = random_program(rng, nl)
         _run(gu, dtype, op, comb, swaps, 4099, pattern=pat)
         _run(gu, dtype, op, comb, swaps, 257, pattern=pat, off=1)
     _run(gu, dtype, op, *C4_TREE, 8192 + 3, pattern=pat, inplace_leaf=0)
+
+
+def all_programs(nl, max_depth=4):
+    """Every valid post-order program with nl leaves and stack depth <= max_depth."""
+    out = []
+
+    def rec(j, depth, comb):
+        depth += 1
+        if depth > max_depth:
+            return
+        if j == nl - 1:
+            out.append(comb + [depth - 1])
+            return
+        for c in range(0, min(3, depth - 1) + 1):
+            rec(j + 1, depth - c, comb + [c])
+
+    rec(0, 0, [])
+    return out
+
+
+@pytest.mark.parametrize("dtype,op", [(d, o) for d in ("fi", "di", "li", "2i", "si") for o in ("maxloc", "minloc")] +
+                         [(d, o) for d in ("cf", "cd") for o in ("sum", "prod")])
+def test_tree_scalar_path_pair_and_complex_every_program(gu, dtype, op):
+    """The scalar tree kernel (operands not 16-B congruent: leaves shifted by the element's
+    alignment against the output) on the pair and complex types, EVERY program of 4, 5 and 8 leaves
+    with stack depth <= 4 (5 + 13 + 233), swap bits drawn per program: bit-exact vs the oracle.  A
+    random 8-leaf depth-4 program once exposed a miscompile of struct-typed stack slots
+    (C_FLOAT_COMPLEX, a leaf's words shifted by one); the slots now hold word vectors."""
+    npdt = po.NP_DTYPES[dtype]
+    es = np.dtype(npdt).itemsize
+    shift = 8 if es == 16 else 4  # the element's own alignment (double / long: 8, float / int: 4)
+    n = 5
+    pat = po.PAT_TIES if dtype in ("fi", "di") else po.PAT_UNIFORM
+    rng = np.random.default_rng(zlib.crc32(f"every-{dtype}-{op}".encode()))
+    bad = []
+    for nl in (4, 5, 8):
+        leaves = [po.fill(n, dtype, pat, 23 + nl, r) for r in range(nl)]
+        d = []
+        for x in leaves:
+            t = gu.empty_dev(n * es + shift)
+            t[shift:shift + n * es] = gu.to_dev(x)
+            d.append(t)
+        out = gu.empty_dev(n * es)
+        for comb in all_programs(nl):
+            swaps = [int(v) for v in rng.integers(0, 2, nl - 1)]
+            rc = ca.reduce_tree(out.data_ptr(), [t.data_ptr() + shift for t in d], comb, swaps, n, DT[dtype], OP[op],
+                                gu.stream())
+            assert rc == 0
+            gu.sync()
+            got = gu.from_dev(out, npdt, n)
+            ref = tree_ref(leaves, comb, swaps, dtype, op)
+            if not np.array_equal(_bits(got), _bits(ref)):
+                bad.append((nl, comb, swaps))
+    assert not bad, f"{len(bad)} programs differ, e.g. {bad[:3]}"

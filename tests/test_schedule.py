@@ -30,6 +30,45 @@ def test_plans_match_reference_golden(golden):
     assert not bad, f"{len(bad)} plan/reference mismatches, e.g. {bad[:5]}"
 
 
+def test_one_shot_plans_match_reference_golden(golden):
+    """SCHEDULE_FLAT_1SHOT (every rank receives the whole buffer from every peer and evaluates
+    every chunk's tree itself): every golden case, pipelined at depth 2, bit-exact."""
+    cases, _ = golden
+    bad = []
+    for c in cases:
+        if c["count"] * c["n"] > (1 << 16):
+            continue
+        mode = {"ar": ca.MODE_ALLREDUCE, "rs": ca.MODE_REDUCE_SCATTER, "ag": ca.MODE_ALLGATHER}[c["mode"]]
+        if mode == ca.MODE_ALLGATHER:
+            continue
+        outs = plan_sim.simulate(mode, _inputs(c), c["k"], c["b"], c["dtype"], c["op"], bool(c["inplace"]), slices=2,
+                                 schedule=ca.SCHEDULE_FLAT_1SHOT)
+        h = hashlib.sha256(b"".join(o.tobytes() for o in outs)).hexdigest()
+        if h != c["sha256"]:
+            bad.append(c["id"])
+    assert not bad, f"{len(bad)} one-shot plan/reference mismatches, e.g. {bad[:5]}"
+
+
+@pytest.mark.parametrize("n,k,b", [(8, 4, 4), (8, 2, 2), (8, 4, 8), (4, 4, 4), (2, 2, 2), (6, 2, 3), (16, 4, 4)])
+def test_one_shot_plan_shape_and_traffic(n, k, b):
+    """One exchange step per slice and no allgather: each rank sends its whole buffer to every peer,
+    (n-1)·S bytes, against 2(n-1)/n·S for FLAT; the reduce-scatter plan is FLAT's."""
+    count = n * 4096
+    for rank in range(n):
+        p = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, n, rank, k, b, count, 3, ca.SCHEDULE_FLAT_1SHOT))
+        assert p["header"]["schedule"] == ca.SCHEDULE_FLAT_1SHOT and p["header"]["steps"] == 3
+        sent = sum(cnt for st in p["steps"] for _, _, cnt in st["sends"])
+        assert sent == (n - 1) * count
+        for st in p["steps"]:
+            assert {peer for peer, _, _ in st["sends"]} == set(range(n)) - {rank}
+        f = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, n, rank, k, b, count, 3, ca.SCHEDULE_FLAT))
+        flat_sent = sum(cnt for st in f["steps"] for _, _, cnt in st["sends"])  # pieces are 64-element cuts
+        assert abs(flat_sent - 2 * (n - 1) * count // n) <= 2 * n * 64 * 3 * (n // b)
+        rs1 = ca.describe_plan(ca.MODE_REDUCE_SCATTER, n, rank, k, b, 4096, 2, ca.SCHEDULE_FLAT_1SHOT)
+        rsf = ca.describe_plan(ca.MODE_REDUCE_SCATTER, n, rank, k, b, 4096, 2, ca.SCHEDULE_FLAT)
+        assert rs1 == rsf
+
+
 @pytest.mark.parametrize("n,k,b", [(8, 4, 4), (8, 2, 2), (8, 4, 8), (8, 3, 4), (2, 2, 1), (2, 2, 2), (16, 4, 4),
                                    (32, 4, 4), (24, 3, 4), (12, 5, 6), (20, 3, 5), (27, 3, 3)])
 def test_plans_match_oracle_wider_grid(n, k, b):
@@ -343,7 +382,7 @@ def test_flat_rccl_allgather_unequal_pieces_fall_back_to_p2p():
 
 
 @pytest.mark.parametrize("schedule", [ca.SCHEDULE_REFERENCE, ca.SCHEDULE_BALANCED, ca.SCHEDULE_FLAT, ca.SCHEDULE_EXACT,
-                                      ca.SCHEDULE_FLAT_AG, ca.SCHEDULE_FLAT_SEQ])
+                                      ca.SCHEDULE_FLAT_AG, ca.SCHEDULE_FLAT_SEQ, ca.SCHEDULE_FLAT_1SHOT])
 def test_tiny_and_ragged_sizes_every_schedule(schedule):
     """One element per rank, odd per-rank counts, reduce-scatter recvcount 1/3/5: plans of every
     schedule reproduce the oracle bit-exactly (the GPU twin is in test_gpu_collectives.py)."""
@@ -360,7 +399,8 @@ def test_tiny_and_ragged_sizes_every_schedule(schedule):
                     np.testing.assert_array_equal(got[r].view(np.uint32), want[r].view(np.uint32))
 
 
-@pytest.mark.parametrize("schedule", [ca.SCHEDULE_FLAT, ca.SCHEDULE_EXACT, ca.SCHEDULE_REFERENCE])
+@pytest.mark.parametrize("schedule", [ca.SCHEDULE_FLAT, ca.SCHEDULE_EXACT, ca.SCHEDULE_REFERENCE,
+                                      ca.SCHEDULE_FLAT_1SHOT])
 def test_plans_match_pair_and_complex_goldens(golden_pairtypes, schedule):
     """MAXLOC / MINLOC on the pair types and complex SUM / PROD through the compiled plans (CPU plan
     interpreter): the radix/batch and allgather goldens bit-exact under three schedules -- the TIES

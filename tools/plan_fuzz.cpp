@@ -63,7 +63,7 @@ int main(int argc, char** argv) {
                 for (int k = 2; k <= 9; ++k)
                     for (unsigned long long per : {1ull, 3ull, 64ull, 1000ull})
                         for (int slices : {1, 3, 8})
-                            for (int sched = 0; sched <= 5; ++sched) {
+                            for (int sched : {0, 1, 2, 3, 4, 5, (int)SCHED_FLAT_1SHOT}) {
                                 if ((is_mpich(mode) || mode == MODE_ALLGATHER) && (sched != SCHED_FLAT || slices != 1))
                                     continue;
                                 const unsigned long long count =
