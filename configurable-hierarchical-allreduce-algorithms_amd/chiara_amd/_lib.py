@@ -90,6 +90,10 @@ def _load():
         "chr_local_reduce_scatter_mpich": ([vp, pp, pp, sz, i, i, i, i], i),
         "chr_local_group_profile": ([vp, i], i),
         "chr_local_group_set_batching": ([vp, i], i),
+        "chr_intra_reduce_scatter_radix_batch": ([vp, vp, sz, i, i, vp, i, i], i),
+        "chr_inter_reduce_linear": ([vp, vp, sz, i, i, vp, i], i),
+        "chr_intra_scatter_radix_batch": ([vp, sz, i, vp, vp, i, i], i),
+        "chr_local_phase_collective": ([vp, i, pp, pp, sz, i, i, i, i], i),
         "chr_local_group_profile_read": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(ctypes.c_long), i], i),
     }
@@ -124,4 +128,6 @@ EXPORTED = [
     "chr_comm_synchronize", "chr_comm_is_aborted", "chr_reduce_tree_batch", "chr_local_group_profile",
     "chr_local_group_profile_read", "chr_reduce_scatter_mpich", "chr_reduce_scatter_mpich_async",
     "chr_local_reduce_scatter_mpich", "chr_local_group_set_batching",
+    "chr_intra_reduce_scatter_radix_batch", "chr_inter_reduce_linear", "chr_intra_scatter_radix_batch",
+    "chr_local_phase_collective",
 ]

@@ -40,6 +40,7 @@ SUM, PROD, MAX, MIN = 0, 1, 2, 3
 LAND, LOR, LXOR, BAND, BOR, BXOR = 4, 5, 6, 7, 8, 9
 MAXLOC, MINLOC = 10, 11
 SUCCESS = 0
+ERR_INVALID_ARG, ERR_COUNT_NOT_DIVISIBLE, ERR_BATCH_NOT_DIVISOR = 1, 2, 3
 ERR_RCCL, ERR_TIMEOUT, ERR_ABORTED = 5, 9, 10
 IN_PLACE = object()  # MPI_IN_PLACE analogue
 _IN_PLACE_PTR = 1     # CHR_IN_PLACE
@@ -55,6 +56,10 @@ MODE_ALLGATHER = 8
 # MPICH baseline reduce-scatters (testing/mpich_implementations/reduce_scatter/)
 MODE_MPICH_RS_RADIX, MODE_MPICH_RS_HALVING, MODE_MPICH_RS_DOUBLING, MODE_MPICH_RS_PAIRWISE = 9, 10, 11, 12
 RS_MODES = (1, 9, 10, 11, 12)  # count = recvcount, send = nranks * recvcount
+# CHiArA's phases as stand-alone collectives (testing/custom_implementations/work_dir/reduce_scatter/;
+# count = recvcount)
+MODE_INTRA_REDUCE_SCATTER, MODE_INTER_REDUCE_LINEAR, MODE_INTRA_SCATTER = 13, 14, 15
+PHASE_MODES = (13, 14, 15)
 SCHEDULE_REFERENCE, SCHEDULE_BALANCED, SCHEDULE_FLAT, SCHEDULE_EXACT, SCHEDULE_FLAT_AG, SCHEDULE_FLAT_SEQ = 0, 1, 2, 3, 4, 5
 SCHEDULE_AUTO = 6  # measured choice among FLAT / FLAT_SEQ / FLAT_AG (/ FLAT_1SHOT) and the depth (Comm only)
 SCHEDULE_FLAT_1SHOT = 7  # allreduce: one exchange step, every rank evaluates the whole buffer (small messages)
@@ -301,6 +306,13 @@ class LocalGroup:
         R = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in recvbufs])
         return lib().chr_local_reduce_scatter_mpich(self._h, S, R, recvcount, datatype, op, algo, k)
 
+    def phase_collective(self, mode, sendbufs, recvbufs, recvcount, datatype, op, k, b):
+        """mode: MODE_INTRA_REDUCE_SCATTER / MODE_INTER_REDUCE_LINEAR / MODE_INTRA_SCATTER (the stand-alone
+        phases; a rank whose plan reads no input may pass None)."""
+        S = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in sendbufs])
+        R = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in recvbufs])
+        return lib().chr_local_phase_collective(self._h, mode, S, R, recvcount, datatype, op, k, b)
+
     def allreduce_mpich(self, algo, sendbufs, recvbufs, count, datatype, op, k=2, single_phase_recv=0):
         """algo: MODE_MPICH_RING / _RD / _RSAG / _RECEXCH."""
         S = (ctypes.c_void_p * self.nranks)(*[_addr(x) for x in sendbufs])
@@ -403,6 +415,27 @@ def MPICH_reduce_scatter_rec_doubling(sendbuf, recvbuf, recvcount, datatype, op,
 def MPICH_reduce_scatter_pairwise(sendbuf, recvbuf, recvcount, datatype, op, comm, async_op=False):
     """reduce_scatter_pairwise.cpp:4."""
     return _mpich_rs(MODE_MPICH_RS_PAIRWISE, sendbuf, recvbuf, recvcount, datatype, op, comm, 0, async_op)
+
+
+# ---- CHiArA's phases as stand-alone collectives (testing/custom_implementations/work_dir/reduce_scatter/) ----
+
+def intra_reduce_scatter_radix_batch(sendbuf, recvbuf, recvcount, datatype, op, comm, k, b):
+    """intra_reduce_scatter_radix.cpp:208 -- phase 1: per stage, the group's radix-k recexch reduce-scatter
+    of IRC-element chunks; recvbuf[s * IRC] gets chunk s * b + lane (the leftover stage's for lanes < nu)."""
+    return lib().chr_intra_reduce_scatter_radix_batch(_addr(sendbuf), _addr(recvbuf), recvcount, datatype, op,
+                                                      comm.handle, k, b)
+
+
+def inter_reduce_linear(sendbuf, recvbuf, recvcount, datatype, op, comm, b):
+    """inter_linear_reduce.cpp:11 -- phase 2: the lane's root node of iteration i (node i * b + lane) folds
+    every node's chunk i in ascending node order into recvbuf."""
+    return lib().chr_inter_reduce_linear(_addr(sendbuf), _addr(recvbuf), recvcount, datatype, op, comm.handle, b)
+
+
+def intra_scatter_radix_batch(sendbuf, recvcount, datatype, recvbuf, comm, k, b):
+    """intra_scatter_radix_batch.cpp:10 -- the reduce-scatter's phase 3: the node root's b blocks go to the
+    node's ranks through a k-nomial tree (same argument order as the reference)."""
+    return lib().chr_intra_scatter_radix_batch(_addr(sendbuf), recvcount, datatype, _addr(recvbuf), comm.handle, k, b)
 
 
 def reduce_multi_ex(out, acc, ins, count, datatype, op, flags, stream=None):

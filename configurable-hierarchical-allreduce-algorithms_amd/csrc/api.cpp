@@ -121,13 +121,13 @@ int chr_fill(void* buf, size_t n, chr_dtype dtype, int pattern, uint64_t seed, i
 
 long chr_plan_describe(chr_mode mode, int nranks, int rank, int k, int b, size_t count, int slices, char* buf,
                        size_t len) {
-    if (mode < CHR_MODE_ALLREDUCE || mode > CHR_MODE_MPICH_RS_PAIRWISE) return -1;
+    if (mode < CHR_MODE_ALLREDUCE || mode > CHR_MODE_INTRA_SCATTER) return -1;
     return chr_plan_describe_ex(mode, nranks, rank, k, b, count, slices, CHR_SCHEDULE_FLAT, buf, len);
 }
 
 long chr_plan_describe_ex(chr_mode mode, int nranks, int rank, int k, int b, size_t count, int slices, int schedule,
                           char* buf, size_t len) {
-    if (mode < CHR_MODE_ALLREDUCE || mode > CHR_MODE_MPICH_RS_PAIRWISE) return -1;
+    if (mode < CHR_MODE_ALLREDUCE || mode > CHR_MODE_INTRA_SCATTER) return -1;
     if (!chr::plan_schedule(schedule)) return -1;
     const std::string s = chr::describe(chr::build_plan((chr::Mode)mode, nranks, rank, k, b, count, slices, schedule));
     if (buf && len) {

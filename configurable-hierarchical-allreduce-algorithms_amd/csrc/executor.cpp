@@ -405,7 +405,7 @@ bool flat_family(int sched) {
 constexpr uint64_t kOneShotMaxBytes = (uint64_t)8 << 20;
 
 int pick_slices(int setting, uint64_t count, int mode, int nranks, int b, size_t es, int sched) {
-    if (chr::is_mpich(mode) || mode == chr::MODE_ALLGATHER) return 1;  // unpipelined schedules
+    if (chr::is_unpipelined(mode)) return 1;  // unpipelined schedules
     if (setting > 0) return setting;
     static const int env = [] {
         const char* v = std::getenv("CHR_SLICES");
@@ -961,6 +961,13 @@ int run_host_windows(chr_comm* c, int sched, int slices, int mode, const void* i
     return out_rc ? out_rc : rc_out;
 }
 
+// The (dtype, op) pairs a mode accepts: the data-movement collectives (allgather, the stand-alone
+// intra scatter) move elements of any type and ignore op.
+bool valid_args(int mode, int dtype, int op) {
+    if (mode == chr::MODE_ALLGATHER || mode == chr::MODE_INTRA_SCATTER) return chr::dtype_size(dtype) != 0;
+    return chr::valid_dtype_op(dtype, op);
+}
+
 int run_collective(chr_comm* c, int sched, int slices, int mode, const void* send, void* recv, size_t count, int dtype,
                    int op, int k, int b, bool sync) {
     const Plan& p = c->plan(mode, k, b, count, chr::dtype_size(dtype), sched, slices);
@@ -969,13 +976,14 @@ int run_collective(chr_comm* c, int sched, int slices, int mode, const void* sen
     if (!recv) return CHR_ERR_INVALID_ARG;
     const size_t es = chr::dtype_size(dtype);
     const bool inplace = send == CHR_IN_PLACE;
+    if (inplace && (mode == chr::MODE_INTER_LINEAR || mode == chr::MODE_INTRA_SCATTER)) return CHR_ERR_INVALID_ARG;
     const void* input = !inplace ? send
                         : mode == chr::MODE_ALLGATHER ? (const void*)((char*)recv + (size_t)c->rank * count * es)
                                                       : (const void*)recv;
-    if (!input) return CHR_ERR_INVALID_ARG;
+    if (!input && p.send_elems) return CHR_ERR_INVALID_ARG;  // a rank whose plan reads no input may pass NULL
     hipError_t e = hipSetDevice(c->device);
     if (e != hipSuccess) return hip_code(e);
-    const bool dev_in = is_device_ptr(input), dev_out = is_device_ptr(recv);
+    const bool dev_out = is_device_ptr(recv), dev_in = p.send_elems ? is_device_ptr(input) : dev_out;
     // Pipelined staging splits a call into window collectives.  Whether it does is a function of the
     // communicator's setting and the call's arguments only -- never of where this rank's buffers
     // live -- so every rank issues the same number of RCCL collectives even when one passes host
@@ -998,7 +1006,7 @@ int run_collective(chr_comm* c, int sched, int slices, int mode, const void* sen
     void* drecv = recv;
     int rc;
     if ((rc = wait_call(c))) return rc;  // earlier _async work
-    if (!dev_in) {
+    if (!dev_in && p.send_elems) {
         if ((e = c->hsend.reserve(p.send_elems * es, c->stream)) != hipSuccess) return hip_code(e);
         if ((e = hipMemcpyAsync(c->hsend.p, input, p.send_elems * es, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
             return hip_code(e);
@@ -1010,7 +1018,7 @@ int run_collective(chr_comm* c, int sched, int slices, int mode, const void* sen
     }
     rc = enqueue_rccl(c, p, dsend, drecv, dtype, op);
     if (rc) return rc;
-    if (!dev_out) {
+    if (!dev_out && p.recv_elems) {
         if (c->timeout_ms > 0 && (rc = wait_call(c))) return rc;  // the collective, under the timeout
         if ((e = hipMemcpyAsync(recv, drecv, p.recv_elems * es, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
             return hip_code(e);
@@ -1052,7 +1060,7 @@ int tune_schedule(chr_comm* c, int mode, const void* send, void* recv, size_t co
                   int* sched_out, int* slices_out) {
     *sched_out = chr::SCHED_FLAT;
     *slices_out = c->slices;
-    if (chr::is_mpich(mode) || mode == chr::MODE_ALLGATHER || c->nranks < 2) return CHR_SUCCESS;
+    if (chr::is_unpipelined(mode) || c->nranks < 2) return CHR_SUCCESS;
     if (c->failed) return CHR_ERR_ABORTED;
     const size_t es = chr::dtype_size(dtype);
     auto key = std::make_tuple(mode, (uint64_t)count, (int)es, k, b, c->slices, c->overlap);
@@ -1153,8 +1161,7 @@ int tune_schedule(chr_comm* c, int mode, const void* send, void* recv, size_t co
 int collective(chr_comm* c, int mode, const void* send, void* recv, size_t count, int dtype, int op, int k, int b,
                bool sync) {
     // allgather moves elements of any type (its op is unused)
-    if (!c || !(mode == chr::MODE_ALLGATHER ? chr::dtype_size(dtype) != 0 : chr::valid_dtype_op(dtype, op)))
-        return CHR_ERR_INVALID_ARG;
+    if (!c || !valid_args(mode, dtype, op)) return CHR_ERR_INVALID_ARG;
     if (c->failed) return CHR_ERR_ABORTED;
     int sched = c->sched, slices = c->slices;
     if (sched == CHR_SCHEDULE_AUTO) {
@@ -1167,9 +1174,7 @@ int collective(chr_comm* c, int mode, const void* send, void* recv, size_t count
 
 int local_collective(chr_local_group* g, int mode, const void* const* sends, void* const* recvs, size_t count,
                      int dtype, int op, int k, int b) {
-    if (!g || !sends || !recvs ||
-        !(mode == chr::MODE_ALLGATHER ? chr::dtype_size(dtype) != 0 : chr::valid_dtype_op(dtype, op)))
-        return CHR_ERR_INVALID_ARG;
+    if (!g || !sends || !recvs || !valid_args(mode, dtype, op)) return CHR_ERR_INVALID_ARG;
     const int n = g->nranks;
     const int depth = pick_slices(g->slices, count, mode, n, b, chr::dtype_size(dtype), g->sched);
     auto key = std::make_tuple(mode, k, b, (uint64_t)count, (int)chr::dtype_size(dtype), depth, g->sched);
@@ -1191,10 +1196,12 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
         if (!recvs[r]) return CHR_ERR_INVALID_ARG;
         if ((e = g->acc[r].reserve(P[r].acc_elems * es, g->stream)) != hipSuccess) return hip_code(e);
         if ((e = g->stage[r].reserve(P[r].stage_elems * es, g->stream)) != hipSuccess) return hip_code(e);
+        if (sends[r] == CHR_IN_PLACE && (mode == chr::MODE_INTER_LINEAR || mode == chr::MODE_INTRA_SCATTER))
+            return CHR_ERR_INVALID_ARG;
         const void* in = sends[r] != CHR_IN_PLACE ? sends[r]
                          : mode == chr::MODE_ALLGATHER ? (const void*)((char*)recvs[r] + (size_t)r * count * es)
                                                        : (const void*)recvs[r];
-        if (!in || !is_device_ptr(in) || !is_device_ptr(recvs[r])) return CHR_ERR_INVALID_ARG;
+        if ((P[r].send_elems && (!in || !is_device_ptr(in))) || !is_device_ptr(recvs[r])) return CHR_ERR_INVALID_ARG;
         B[r] = Bufs{(const char*)in, (char*)recvs[r], (char*)g->acc[r].p, (char*)g->stage[r].p, es};
     }
     int rc;
@@ -1682,6 +1689,28 @@ int chr_allgather_radix_batch_async(const void* send, size_t sendcount, chr_dtyp
 int chr_local_allgather_radix_batch(chr_local_group* g, const void* const* sends, void* const* recvs, size_t sendcount,
                                     chr_dtype dtype, int k, int b) {
     return local_collective(g, chr::MODE_ALLGATHER, sends, recvs, sendcount, dtype, CHR_SUM, k, b);
+}
+
+int chr_intra_reduce_scatter_radix_batch(const void* send, void* recv, size_t recvcount, chr_dtype dtype, chr_op op,
+                                         chr_comm* comm, int k, int b) {
+    return collective(comm, chr::MODE_INTRA_RS, send, recv, recvcount, dtype, op, k, b, true);
+}
+
+int chr_inter_reduce_linear(const void* send, void* recv, size_t recvcount, chr_dtype dtype, chr_op op, chr_comm* comm,
+                            int b) {
+    return collective(comm, chr::MODE_INTER_LINEAR, send, recv, recvcount, dtype, op, 2, b, true);
+}
+
+int chr_intra_scatter_radix_batch(const void* send, size_t recvcount, chr_dtype dtype, void* recv, chr_comm* comm,
+                                  int k, int b) {
+    return collective(comm, chr::MODE_INTRA_SCATTER, send, recv, recvcount, dtype, CHR_SUM, k, b, true);
+}
+
+int chr_local_phase_collective(chr_local_group* g, chr_mode mode, const void* const* sends, void* const* recvs,
+                               size_t recvcount, chr_dtype dtype, chr_op op, int k, int b) {
+    if (!chr::is_phase(mode)) return CHR_ERR_INVALID_ARG;
+    return local_collective(g, mode, sends, recvs, recvcount, dtype, mode == CHR_MODE_INTRA_SCATTER ? CHR_SUM : op,
+                            mode == CHR_MODE_INTER_REDUCE_LINEAR ? 2 : k, b);
 }
 
 }  // extern "C"

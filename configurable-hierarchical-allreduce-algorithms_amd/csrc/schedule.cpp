@@ -739,6 +739,7 @@ static Plan build_plan_impl(Mode mode, int n, int me, int k_in, int b, uint64_t 
     const bool balance = sched == SCHED_BALANCED;
     if (is_mpich(mode)) return build_plan_mpich(mode, n, me, k_in, b, count);
     if (mode == MODE_ALLGATHER) return build_plan_allgather(n, me, k_in, b, count);
+    if (is_phase(mode)) return build_plan_phase(mode, n, me, k_in, b, count);
     Plan p;
     p.mode = mode;
     p.rank = me;
@@ -1712,6 +1713,212 @@ Plan build_plan_allgather(int n, int me, int k, int b, uint64_t count) {
             s.recvs.push_back({peers[j].second, {BUF_RECV, (uint64_t)peers[j].second * count}, count});
         }
     }
+    return p;
+}
+
+}  // namespace chr
+
+// ==== CHiArA's phases as stand-alone collectives ==============================================
+// testing/custom_implementations/work_dir/reduce_scatter/ keeps each phase of the hierarchical
+// reduce-scatter as its own function (each with a DEBUG_MODE self-test main).  Ranks form nnodes =
+// n / b groups of b: node = rank / b, lane = rank % b, IRC = recvcount * b, nstages = nnodes / b,
+// nu = nnodes % b.  The plans keep the reference's buffers: ACC is tmp_results (stage-major, as the
+// reference lays it out), STAGE its tmp_recvbuf / tmp.
+namespace chr {
+namespace {
+
+// intra_reduce_scatter_radix.cpp:208-541.  Recexch over the group's b lanes (tables of lane, b):
+// step 1 folds the non-participants' whole buffers once (:274-311); then, per stage, step 2 runs
+// the phases from the highest digit down, exchanging with the k-1 neighbours the count/offset
+// regions in units of IRC and folding each received region into the own one in neighbour order
+// (:314-356), and step 3 copies the lane's chunk out and returns the non-participants' (:359-386).
+// The leftover stage (nu != 0) does the same on regions clipped to its nu chunks (:400-500).  A
+// phase's k-1 exchanges read the neighbours' regions and write the own one, which are disjoint, so
+// they share one group and one fused reduction, in the reference's operand order.
+void build_intra_rs(Plan& p, int n, int me, int k_in, int b, uint64_t rc) {
+    const int node = me / b, lane = me % b, base = node * b, nnodes = n / b, nstages = nnodes / b, nu = nnodes % b;
+    const uint64_t irc = rc * (uint64_t)b, total = rc * (uint64_t)n, blk = irc * (uint64_t)b;
+    p.send_elems = total;
+    p.recv_elems = (uint64_t)(nstages + (lane < nu ? 1 : 0)) * irc;
+    Recexch x;
+    if (recexch_neighbors(lane, b, k_in, &x)) {
+        p.error = 1;
+        return;
+    }
+    const int k = x.k, nph = x.step2_nphases;
+    const bool part = x.step1_sendto == -1;
+    std::vector<int> cnt, off;
+    recexch_count_offset(b, std::max(nph, 1), k, &cnt, &off);
+    auto need = [&](uint64_t e) { p.stage_elems = std::max(p.stage_elems, e); };
+    auto add = [&](const char* label) -> Step& {
+        p.steps.emplace_back();
+        p.steps.back().label = label;
+        return p.steps.back();
+    };
+    if (part) {
+        p.pre.push_back(make_copy({BUF_ACC, 0}, {BUF_SEND, 0}, total, 277));  // :274-280
+        p.acc_elems = total;
+    }
+    {
+        Step& s = add("irs-step1");
+        if (!part) {
+            s.sends.push_back({base + x.step1_sendto, {BUF_SEND, 0}, total});  // :290
+        } else if (x.step1_nrecvs) {
+            std::vector<Ref> ins;
+            for (int i = 0; i < x.step1_nrecvs; ++i) {
+                s.recvs.push_back({base + x.step1_recvfrom[i], {BUF_STAGE, (uint64_t)i * total}, total});
+                ins.push_back({BUF_STAGE, (uint64_t)i * total});
+            }
+            need((uint64_t)x.step1_nrecvs * total);
+            s.post.push_back(make_reduce({BUF_ACC, 0}, {BUF_ACC, 0}, ins, total, 303));
+        }
+    }
+    // one stage's phases and return; `lim` clips every region to the leftover stage's nu chunks
+    auto stage = [&](uint64_t sb, uint64_t lim, uint64_t out_off, bool left) {
+        auto clip = [&](int c, int o, uint64_t* len) {  // (offset, length) of a count/offset region
+            const uint64_t ro = (uint64_t)o * irc, rl = (uint64_t)c * irc;
+            *len = ro < lim ? std::min(rl, lim - ro) : 0;
+            return ro;
+        };
+        for (int ph = nph - 1; ph >= 0; --ph) {
+            Step& s = add(left ? "irs-phase-left" : "irs-phase");
+            if (!part) continue;
+            uint64_t mlen = 0;
+            const uint64_t moff = clip(cnt[ph * b + lane], off[ph * b + lane], &mlen);
+            std::vector<Ref> ins;
+            for (int i = 0; i < k - 1; ++i) {
+                const int dst = x.step2_nbrs[ph][i];
+                uint64_t slen = 0;
+                const uint64_t soff = clip(cnt[ph * b + dst], off[ph * b + dst], &slen);
+                if (slen) s.sends.push_back({base + dst, {BUF_ACC, sb + soff}, slen});
+                if (mlen) {
+                    s.recvs.push_back({base + dst, {BUF_STAGE, (uint64_t)i * blk}, mlen});
+                    ins.push_back({BUF_STAGE, (uint64_t)i * blk});
+                }
+            }
+            if (mlen) {
+                need((uint64_t)(k - 1) * blk);
+                s.post.push_back(make_reduce({BUF_ACC, sb + moff}, {BUF_ACC, sb + moff}, ins, mlen, left ? 464 : 348));
+            }
+        }
+        Step& s = add(left ? "irs-step3-left" : "irs-step3");
+        const bool mine = (uint64_t)lane * irc < lim;  // the leftover stage's chunk exists for lanes < nu
+        if (!part) {
+            if (mine) s.recvs.push_back({base + x.step1_sendto, {BUF_RECV, out_off}, irc});  // :370 / :488
+        } else {
+            for (int i = 0; i < x.step1_nrecvs; ++i)
+                if ((uint64_t)x.step1_recvfrom[i] * irc < lim)
+                    s.sends.push_back({base + x.step1_recvfrom[i], {BUF_ACC, sb + (uint64_t)x.step1_recvfrom[i] * irc}, irc});
+            if (mine) s.post.push_back(make_copy({BUF_RECV, out_off}, {BUF_ACC, sb + (uint64_t)lane * irc}, irc, 360));
+        }
+    };
+    for (int st = 0; st < nstages; ++st) stage((uint64_t)st * blk, blk, (uint64_t)st * irc, false);
+    if (nu) stage((uint64_t)nstages * blk, (uint64_t)nu * irc, (uint64_t)nstages * irc, true);
+}
+
+// inter_linear_reduce.cpp:11-73.  For iteration i the lane's root is node i * b + lane: it starts
+// from its own chunk i and folds the other nodes' chunk i in ascending node order (MPI_Recv +
+// MPI_Reduce_local, :55-63); the others send it theirs (:67).  A rank is the root of at most
+// one iteration and all messages of all iterations are independent, so they share one group and
+// the root's folds are one fused reduction.
+void build_inter_linear(Plan& p, int n, int me, int b, uint64_t rc) {
+    const int node = me / b, lane = me % b, nnodes = n / b, niters = nnodes / b + (nnodes % b ? 1 : 0);
+    const uint64_t irc = rc * (uint64_t)b;
+    p.send_elems = (uint64_t)niters * irc;
+    Step& s = p.steps.emplace_back();
+    s.label = "ilr";
+    for (int i = 0; i < niters; ++i) {
+        const int root_node = i * b + lane;
+        if (root_node >= nnodes) continue;  // :48
+        const Ref chunk{BUF_SEND, (uint64_t)i * irc};
+        if (node != root_node) {
+            s.sends.push_back({root_node * b + lane, chunk, irc});
+            continue;
+        }
+        p.recv_elems = irc;
+        std::vector<Ref> ins;
+        for (int j = 0; j < nnodes; ++j) {
+            if (j == node) continue;
+            const Ref slot{BUF_STAGE, (uint64_t)ins.size() * irc};
+            s.recvs.push_back({j * b + lane, slot, irc});
+            ins.push_back(slot);
+        }
+        p.stage_elems = (uint64_t)ins.size() * irc;
+        if (ins.empty()) s.post.push_back(make_copy({BUF_RECV, 0}, chunk, irc, 53));  // :53
+        else s.post.push_back(make_reduce({BUF_RECV, 0}, chunk, ins, irc, 63));
+    }
+}
+
+// intra_scatter_radix_batch.cpp:10-110.  The node root (lane node % b) lays its b blocks out in
+// normalised order (slot (lane - root) mod b, :40-46); from the largest delta = k^(nphases-1) down,
+// every group leader sends each child subgroup's blocks to the child's leader (:65-83) and the
+// child leaders receive them (:84-97); each rank copies its block out at the end (:103-105).
+void build_intra_scatter(Plan& p, int n, int me, int k, int b, uint64_t rc) {
+    (void)n;
+    const int node = me / b, lane = me % b, root = node % b, shift = (lane - root + b) % b;
+    p.send_elems = lane == root ? (uint64_t)b * rc : 0;
+    p.recv_elems = rc;
+    p.stage_elems = (uint64_t)b * rc;
+    if (lane == root) {  // real slot j -> normalised slot (j - root) mod b: two runs
+        p.pre.push_back(make_copy({BUF_STAGE, 0}, {BUF_SEND, (uint64_t)root * rc}, (uint64_t)(b - root) * rc, 44));
+        if (root) p.pre.push_back(make_copy({BUF_STAGE, (uint64_t)(b - root) * rc}, {BUF_SEND, 0}, (uint64_t)root * rc, 44));
+    }
+    int nphases = 0;
+    for (int t = b - 1; t > 0; t /= k) ++nphases;  // ceil(log_k b), :31-32
+    int delta = 1;
+    for (int i = 1; i < nphases; ++i) delta *= k;
+    auto peer = [&](int norm) { return node * b + (norm + root) % b; };
+    for (int ph = nphases - 1; ph >= 0; --ph) {
+        Step& s = p.steps.emplace_back();
+        s.label = "isc";
+        const int group = delta * k, gstart = (shift / group) * group, gend = std::min(gstart + group, b);
+        const int offset = shift - gstart;
+        if (offset == 0) {
+            for (int j = 1; j < k; ++j) {
+                const int child = gstart + j * delta;
+                if (child >= gend) break;
+                const int subtree = std::min(delta, gend - child);
+                s.sends.push_back({peer(child), {BUF_STAGE, (uint64_t)child * rc}, (uint64_t)subtree * rc});
+            }
+        } else if (offset % delta == 0 && offset < group) {
+            const int subtree = std::min(delta, gend - shift);
+            s.recvs.push_back({peer(gstart), {BUF_STAGE, (uint64_t)shift * rc}, (uint64_t)subtree * rc});
+        }
+        delta = ph > 0 ? delta / k : delta;
+    }
+    Step& s = p.steps.emplace_back();
+    s.label = "isc-out";
+    s.post.push_back(make_copy({BUF_RECV, 0}, {BUF_STAGE, (uint64_t)shift * rc}, rc, 103));
+}
+
+}  // namespace
+
+Plan build_plan_phase(Mode mode, int n, int me, int k, int b, uint64_t rc) {
+    Plan p;
+    p.mode = mode;
+    p.rank = me;
+    if (!is_phase(mode) || n < 1 || me < 0 || me >= n || b < 1 || b > n || (mode != MODE_INTER_LINEAR && k < 2)) {
+        p.error = 1;  // CHR_ERR_INVALID_ARG
+        return p;
+    }
+    if (n % b) {
+        p.error = 3;  // CHR_ERR_BATCH_NOT_DIVISOR
+        return p;
+    }
+    Geometry& g = p.g;
+    g.nranks = n;
+    g.k = k;
+    g.b = b;
+    g.nnodes = n / b;
+    g.nstages = g.nnodes / b;
+    g.nu = g.nnodes % b;
+    g.recvcount = rc;
+    g.irc = rc * (uint64_t)b;
+    g.total = rc;  // zero: nothing to do
+    if (rc == 0) return p;
+    if (mode == MODE_INTRA_RS) build_intra_rs(p, n, me, k, b, rc);
+    else if (mode == MODE_INTER_LINEAR) build_inter_linear(p, n, me, b, rc);
+    else build_intra_scatter(p, n, me, k, b, rc);
     return p;
 }
 

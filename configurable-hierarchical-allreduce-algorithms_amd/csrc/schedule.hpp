@@ -96,10 +96,18 @@ enum Mode : int {
     MODE_MPICH_RS_RADIX = 9,     // reduce_scatter_radix.cpp:204 (k)
     MODE_MPICH_RS_HALVING = 10,  // reduce_scatter_recursive_halving.cpp:7
     MODE_MPICH_RS_DOUBLING = 11, // reduce_scatter_recursive_doubling.cpp:10
-    MODE_MPICH_RS_PAIRWISE = 12  // reduce_scatter_pairwise.cpp:4
+    MODE_MPICH_RS_PAIRWISE = 12, // reduce_scatter_pairwise.cpp:4
+    // CHiArA's phases as stand-alone functions (testing/custom_implementations/work_dir/reduce_scatter/;
+    // count = recvcount)
+    MODE_INTRA_RS = 13,          // intra_reduce_scatter_radix.cpp:208 (k, b)
+    MODE_INTER_LINEAR = 14,      // inter_linear_reduce.cpp:11 (b)
+    MODE_INTRA_SCATTER = 15      // intra_scatter_radix_batch.cpp:10 (k, b)
 };
 inline bool is_mpich_rs(int mode) { return mode >= MODE_MPICH_RS_RADIX && mode <= MODE_MPICH_RS_PAIRWISE; }
 inline bool is_mpich(int mode) { return (mode >= MODE_MPICH_RING && mode <= MODE_MPICH_RMULT) || is_mpich_rs(mode); }
+inline bool is_phase(int mode) { return mode >= MODE_INTRA_RS && mode <= MODE_INTRA_SCATTER; }
+// Modes compiled as one unsliced plan (no pipeline depth, no schedule choice).
+inline bool is_unpipelined(int mode) { return is_mpich(mode) || mode == MODE_ALLGATHER || is_phase(mode); }
 
 struct Geometry {
     int nranks = 0, b = 0, k = 0, nnodes = 0, nstages = 0, nu = 0, nph = 0;
@@ -165,6 +173,8 @@ int auto_slices(uint64_t irc_bytes);
 // reduce-scatters (count = recvcount).
 Plan build_plan_mpich(Mode mode, int nranks, int rank, int k, int aux, uint64_t count);
 Plan build_plan_allgather(int nranks, int rank, int k, int b, uint64_t sendcount);
+// The stand-alone phases (MODE_INTRA_RS / MODE_INTER_LINEAR / MODE_INTRA_SCATTER; count = recvcount).
+Plan build_plan_phase(Mode mode, int nranks, int rank, int k, int b, uint64_t recvcount);
 std::string describe(const Plan& p);
 // Phase of a step label for the per-phase timers: slice suffixes and super-step tags dropped,
 // distinct phase names joined by '+' ("t3,phase0/s0,lane/s1" -> "phase0+lane").

@@ -20,6 +20,10 @@
 //       replace testing/mpich_implementations/reduce_scatter/reduce_scatter_{radix.cpp:204,
 //       recursive_halving.cpp:7, recursive_doubling.cpp:10, pairwise.cpp:4}: the baselines that
 //       directory's main.cpp times
+//   intra_reduce_scatter_radix_batch, inter_reduce_linear, intra_scatter_radix_batch
+//       replace testing/custom_implementations/work_dir/reduce_scatter/{intra_reduce_scatter_radix.cpp:208,
+//       inter_linear_reduce.cpp:11, intra_scatter_radix_batch.cpp:10}: CHiArA's phases as stand-alone
+//       functions, so their DEBUG_MODE self-test mains run on libchiara
 //
 // One chr_comm per MPI communicator, created on first use (RCCL unique id broadcast with
 // MPI_Bcast, device = node-local rank mod visible GPUs) and cached as an MPI attribute.
@@ -268,4 +272,43 @@ int MPICH_reduce_scatter_rec_doubling(const void* sendbuf, void* recvbuf, MPI_Ai
 int MPICH_reduce_scatter_pairwise(const void* sendbuf, void* recvbuf, MPI_Aint recvcount, MPI_Datatype datatype,
                                   MPI_Op op, MPI_Comm comm) {
     return mpich_rs_call(CHR_MODE_MPICH_RS_PAIRWISE, sendbuf, recvbuf, recvcount, datatype, op, comm, 0);
+}
+
+// CHiArA's phases as stand-alone functions (testing/custom_implementations/work_dir/reduce_scatter/)
+int intra_reduce_scatter_radix_batch(const void* sendbuf, void* recvbuf, MPI_Aint recvcount, MPI_Datatype datatype,
+                                     MPI_Op op, MPI_Comm comm, int k, int b) {
+    chr_dtype dt;
+    chr_op o;
+    if (int err = map_pair(datatype, op, &dt, &o)) return err;
+    if (recvcount < 0) return MPI_ERR_COUNT;
+    chr_comm* c = comm_for(comm);
+    if (!c) return MPI_ERR_OTHER;
+    const void* send = sendbuf == MPI_IN_PLACE ? CHR_IN_PLACE : sendbuf;
+    return to_mpi(chr_intra_reduce_scatter_radix_batch(send, recvbuf, (size_t)recvcount, dt, o, c, k, b));
+}
+
+int inter_reduce_linear(const void* sendbuf, void* recvbuf, MPI_Aint recvcount, MPI_Datatype datatype, MPI_Op op,
+                        MPI_Comm comm, int b) {
+    chr_dtype dt;
+    chr_op o;
+    if (int err = map_pair(datatype, op, &dt, &o)) return err;
+    if (recvcount < 0) return MPI_ERR_COUNT;
+    chr_comm* c = comm_for(comm);
+    if (!c) return MPI_ERR_OTHER;
+    return to_mpi(chr_inter_reduce_linear(sendbuf, recvbuf, (size_t)recvcount, dt, o, c, b));
+}
+
+// Data movement only: any contiguous type, moved as bytes (as allgather_radix_batch).  Non-roots may
+// pass a NULL sendbuf (the reference's self-test does, intra_scatter_radix_batch.cpp:213).
+int intra_scatter_radix_batch(char* sendbuf, int recvcount, MPI_Datatype datatype, char* recvbuf, MPI_Comm comm, int k,
+                              int b) {
+    if (recvcount < 0) return MPI_ERR_COUNT;
+    int tsize = 0;
+    MPI_Aint lb = 0, extent = 0;
+    if (MPI_Type_size(datatype, &tsize) != MPI_SUCCESS || MPI_Type_get_extent(datatype, &lb, &extent) != MPI_SUCCESS ||
+        tsize <= 0 || lb != 0 || extent != tsize)
+        return MPI_ERR_TYPE;
+    chr_comm* c = comm_for(comm);
+    if (!c) return MPI_ERR_OTHER;
+    return to_mpi(chr_intra_scatter_radix_batch(sendbuf, (size_t)recvcount * (size_t)tsize, CHR_UINT8, recvbuf, c, k, b));
 }

@@ -338,7 +338,12 @@ typedef enum {
     CHR_MODE_MPICH_RS_RADIX = 9,    /* reduce_scatter_radix.cpp:204 (k) */
     CHR_MODE_MPICH_RS_HALVING = 10, /* reduce_scatter_recursive_halving.cpp:7 */
     CHR_MODE_MPICH_RS_DOUBLING = 11,/* reduce_scatter_recursive_doubling.cpp:10 */
-    CHR_MODE_MPICH_RS_PAIRWISE = 12 /* reduce_scatter_pairwise.cpp:4 */
+    CHR_MODE_MPICH_RS_PAIRWISE = 12,/* reduce_scatter_pairwise.cpp:4 */
+    /* CHiArA's building blocks, stand-alone (testing/custom_implementations/work_dir/reduce_scatter/;
+     * count = recvcount) */
+    CHR_MODE_INTRA_REDUCE_SCATTER = 13, /* intra_reduce_scatter_radix.cpp:208 (k, b): phase 1 */
+    CHR_MODE_INTER_REDUCE_LINEAR = 14,  /* inter_linear_reduce.cpp:11 (b): phase 2 */
+    CHR_MODE_INTRA_SCATTER = 15         /* intra_scatter_radix_batch.cpp:10 (k, b): RS phase 3 */
 } chr_mode;
 long chr_plan_describe(chr_mode mode, int nranks, int rank, int k, int b, size_t count,
                        int slices, char* buf, size_t len);
@@ -391,6 +396,42 @@ int chr_reduce_scatter_mpich_async(const void* send, void* recv, size_t recvcoun
 int chr_local_reduce_scatter_mpich(chr_local_group* group, const void* const* sends,
                                    void* const* recvs, size_t recvcount, chr_dtype dtype, chr_op op,
                                    chr_mode algo, int k);
+
+/* ---- CHiArA's phases as stand-alone collectives ------------------------------------------
+ * testing/custom_implementations/work_dir/reduce_scatter/ keeps each phase of the hierarchical
+ * reduce-scatter as its own function with a DEBUG_MODE self-test main.  Ranks form nnodes = n / b
+ * groups of b (node = rank / b, lane = rank % b); IRC = recvcount * b; nstages = nnodes / b,
+ * nu = nnodes % b, niters = nstages + (nu != 0).  Results bit-identical to the reference's code on
+ * the same inputs; reductions on the fused HIP kernel, messages RCCL send/recv.
+ *
+ * Replaces  int intra_reduce_scatter_radix_batch(const void* sendbuf, void* recvbuf,
+ *             MPI_Aint recvcount, MPI_Datatype, MPI_Op, MPI_Comm, int k, int b)
+ *           (intra_reduce_scatter_radix.cpp:208-541; phase 1 of reduce_scatter_radix_batch.cpp).
+ * send: recvcount * n elements (recv under CHR_IN_PLACE); chunk c = send[c * IRC, +IRC).  Per
+ * stage s, the group's radix-k recexch reduces chunk s * b + lane over the group into
+ * recv[s * IRC, +IRC); the leftover stage's chunk nstages * b + lane only for lanes < nu (recv
+ * beyond what a rank writes is left untouched). */
+int chr_intra_reduce_scatter_radix_batch(const void* send, void* recv, size_t recvcount, chr_dtype dtype,
+                                         chr_op op, chr_comm* comm, int k, int b);
+/* Replaces  int inter_reduce_linear(const void* sendbuf, void* recvbuf, MPI_Aint recvcount,
+ *             MPI_Datatype, MPI_Op, MPI_Comm, int b)   (inter_linear_reduce.cpp:11-73; phase 2).
+ * send: niters chunks of IRC; for iteration i the lane's root node is i * b + lane (if < nnodes):
+ * recv[0, IRC) = own chunk i reduced with the other nodes' chunk i in ascending node order.  Ranks
+ * that are nobody's root leave recv untouched.  send may not be CHR_IN_PLACE (nor in the reference). */
+int chr_inter_reduce_linear(const void* send, void* recv, size_t recvcount, chr_dtype dtype, chr_op op,
+                            chr_comm* comm, int b);
+/* Replaces  int intra_scatter_radix_batch(char* sendbuf, int recvcount, MPI_Datatype,
+ *             char* recvbuf, MPI_Comm, int k, int b)  (intra_scatter_radix_batch.cpp:10-110; RS phase 3).
+ * The node root (lane node % b) holds b blocks of recvcount in send; every rank of the node gets
+ * block `lane` in recv through a k-nomial tree.  send is read on node roots only (may be NULL
+ * elsewhere).  Data movement only: any dtype. */
+int chr_intra_scatter_radix_batch(const void* send, size_t recvcount, chr_dtype dtype, void* recv,
+                                  chr_comm* comm, int k, int b);
+/* All three on virtual ranks (mode = CHR_MODE_INTRA_REDUCE_SCATTER / _INTER_REDUCE_LINEAR /
+ * _INTRA_SCATTER; op is unused by the scatter, k by the linear reduce). */
+int chr_local_phase_collective(chr_local_group* group, chr_mode mode, const void* const* sends,
+                               void* const* recvs, size_t recvcount, chr_dtype dtype, chr_op op, int k,
+                               int b);
 
 /* ---- utilities -------------------------------------------------------------------------- */
 /* Synthetic inputs on the device with the shared generator (oracle/chiara_oracle.h):

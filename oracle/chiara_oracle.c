@@ -1304,3 +1304,122 @@ int orc_reduce_scatter_radix(int n, int k_in, size_t rc, int dtype, int op, cons
     orc_rs_store(n, rc, es, res, recv);
     return 0;
 }
+
+/* ---- CHiArA's phases as stand-alone functions: testing/custom_implementations/work_dir/reduce_scatter/ ---- */
+
+/* intra_reduce_scatter_radix.cpp:208-541, bulk-synchronous per group.  A participant's tmp_results
+ * starts as its input (:274-280) and folds its step-1 senders' whole buffers in step1_recvfrom order
+ * (:292-311).  Per stage, every step-2 phase (highest digit first) folds, in neighbour order, the
+ * neighbours' copies of the participant's own count/offset region (:317-356) -- all taken before any
+ * rank of the group reduces in that phase; the leftover stage clips every region to its nu chunks
+ * (:400-475).  Step 3: participants copy their chunk out (:360 / :478), non-participants receive it
+ * from their step-1 partner (:370 / :488). */
+int orc_intra_reduce_scatter(int n, int k, int b, size_t rc, int dtype, int op, const void* const* send,
+                             void* const* recv) {
+    size_t es = orc_dtype_size(dtype), irc, total, blk;
+    int nnodes, nstages, nu, node, l, i, ph, st;
+    orc_recexch_t* x;
+    int *cnt, *off;
+    char **tres, **snap;
+    if (n < 1 || !es || k < 2 || b < 1) return 1;
+    if (n % b) return 3;
+    nnodes = n / b;
+    nstages = nnodes / b;
+    nu = nnodes % b;
+    irc = rc * (size_t)b;
+    total = rc * (size_t)n;
+    blk = irc * (size_t)b;
+    x = (orc_recexch_t*)calloc((size_t)b, sizeof(orc_recexch_t));
+    tres = (char**)calloc((size_t)b, sizeof(char*));
+    snap = (char**)calloc((size_t)b, sizeof(char*));
+    cnt = (int*)calloc(64 * (size_t)b + 1, sizeof(int));
+    off = (int*)calloc(64 * (size_t)b + 1, sizeof(int));
+    for (l = 0; l < b; l++) orc_recexch_neighbors(l, b, k, &x[l]);
+    orc_recexch_count_offset(b, x[0].step2_nphases > 0 ? x[0].step2_nphases : 1, x[0].k, cnt, off);
+    for (node = 0; node < nnodes; node++) {
+        const int base = node * b;
+        for (l = 0; l < b; l++) {
+            tres[l] = NULL;
+            if (x[l].step1_sendto != -1) continue;
+            tres[l] = (char*)malloc(total * es + 1);
+            snap[l] = (char*)malloc(total * es + 1);
+            memcpy(tres[l], orc_rs_input(send, recv, base + l), total * es);
+            for (i = 0; i < x[l].step1_nrecvs; i++)
+                orc_reduce_local(orc_rs_input(send, recv, base + x[l].step1_recvfrom[i]), tres[l], total, dtype, op);
+        }
+        for (st = 0; st <= nstages; st++) {
+            const size_t sb = (size_t)st * blk, lim = st < nstages ? blk : (size_t)nu * irc;
+            if (st == nstages && nu == 0) break;
+            for (ph = x[0].step2_nphases - 1; ph >= 0; ph--) {
+                for (l = 0; l < b; l++)
+                    if (tres[l]) memcpy(snap[l], tres[l], total * es);
+                for (l = 0; l < b; l++) {
+                    size_t mo, ml;
+                    if (!tres[l]) continue;
+                    mo = (size_t)off[ph * b + l] * irc;
+                    ml = (size_t)cnt[ph * b + l] * irc;
+                    if (mo >= lim) continue;
+                    if (ml > lim - mo) ml = lim - mo;
+                    for (i = 0; i < x[l].k - 1; i++)
+                        orc_reduce_local(snap[x[l].step2_nbrs[ph][i]] + (sb + mo) * es, tres[l] + (sb + mo) * es, ml,
+                                         dtype, op);
+                }
+            }
+            for (l = 0; l < b; l++) {
+                const int owner = x[l].step1_sendto == -1 ? l : x[l].step1_sendto;
+                if ((size_t)l * irc >= lim) continue;
+                memcpy((char*)recv[base + l] + (size_t)st * irc * es, tres[owner] + (sb + (size_t)l * irc) * es,
+                       irc * es);
+            }
+        }
+        for (l = 0; l < b; l++) {
+            free(tres[l]);
+            if (tres[l]) free(snap[l]);
+        }
+    }
+    free(x);
+    free(tres);
+    free(snap);
+    free(cnt);
+    free(off);
+    return 0;
+}
+
+/* inter_linear_reduce.cpp:11-73: root of iteration i = node i * b + lane (skipped past the last
+ * node, :48); recvbuf = own chunk i (:55), then MPI_Reduce_local(chunk i of node j, recvbuf) for
+ * j ascending, j != root (:58-63). */
+int orc_inter_reduce_linear(int n, int b, size_t rc, int dtype, int op, const void* const* send, void* const* recv) {
+    size_t es = orc_dtype_size(dtype), irc;
+    int nnodes, niters, r, i, j;
+    if (n < 1 || !es || b < 1) return 1;
+    if (n % b) return 3;
+    nnodes = n / b;
+    niters = nnodes / b + (nnodes % b ? 1 : 0);
+    irc = rc * (size_t)b;
+    for (r = 0; r < n; r++) {
+        const int node = r / b, lane = r % b;
+        for (i = 0; i < niters; i++) {
+            if (i * b + lane != node) continue;
+            memcpy(recv[r], (const char*)send[r] + (size_t)i * irc * es, irc * es);
+            for (j = 0; j < nnodes; j++)
+                if (j != node)
+                    orc_reduce_local((const char*)send[j * b + lane] + (size_t)i * irc * es, recv[r], irc, dtype, op);
+        }
+    }
+    return 0;
+}
+
+/* intra_scatter_radix_batch.cpp:10-110: the k-nomial tree only routes the blocks; every rank ends
+ * with block `lane` of its node root's (lane node % b) send buffer (the self-test's expectation,
+ * :226-233). */
+int orc_intra_scatter(int n, int k, int b, size_t rc, int dtype, const void* const* send, void* const* recv) {
+    size_t es = orc_dtype_size(dtype);
+    int r;
+    if (n < 1 || !es || k < 2 || b < 1) return 1;
+    if (n % b) return 3;
+    for (r = 0; r < n; r++) {
+        const int node = r / b, lane = r % b, root = node * b + node % b;
+        memcpy(recv[r], (const char*)send[root] + (size_t)lane * rc * es, rc * es);
+    }
+    return 0;
+}

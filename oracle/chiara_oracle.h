@@ -165,6 +165,21 @@ int orc_reduce_scatter_rec_doubling(int n, size_t rc, int dtype, int op, const v
 int orc_reduce_scatter_radix(int n, int k, size_t rc, int dtype, int op, const void* const* send,
                              void* const* recv);
 
+/* CHiArA's phases as stand-alone functions (testing/custom_implementations/work_dir/reduce_scatter/).
+ * Ranks form n / b groups of b (node = r / b, lane = r % b); IRC = rc * b; nstages = nnodes / b,
+ * nu = nnodes % b.  Each writes only what the reference writes into recv[r]; the rest of recv[r] is
+ * left as it was.
+ *   intra_reduce_scatter: send[r] (NULL: in place, recv[r]) holds rc * n elements; recv[r][s * IRC]
+ *     gets chunk s * b + lane reduced over the group (leftover stage: lanes < nu).
+ *   inter_reduce_linear: send[r] holds niters chunks of IRC; the root of iteration i (node i * b +
+ *     lane) gets its chunk i folded with every other node's chunk i in ascending node order.
+ *   intra_scatter: the node root's send (b blocks of rc) scattered, block `lane` to each rank; send[r]
+ *     is read on node roots only. */
+int orc_intra_reduce_scatter(int n, int k, int b, size_t rc, int dtype, int op, const void* const* send,
+                             void* const* recv);
+int orc_inter_reduce_linear(int n, int b, size_t rc, int dtype, int op, const void* const* send, void* const* recv);
+int orc_intra_scatter(int n, int k, int b, size_t rc, int dtype, const void* const* send, void* const* recv);
+
 #ifdef __cplusplus
 }
 #endif

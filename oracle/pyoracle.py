@@ -261,3 +261,54 @@ def mpich_reduce_scatter(algo, sends, dtype, op, k=2, inplace=False):
     if rc_:
         raise ValueError(f"oracle {algo} rejected (rc={rc_})")
     return [r[:rc] for r in recvs]
+
+
+PHASE_ALGOS = ("irs", "ilr", "isc")  # intra_reduce_scatter_radix / inter_linear_reduce / intra_scatter_radix_batch
+
+
+def phase_sizes(algo, n, b, rc):
+    """(input, output) elements per rank of the stand-alone phase `algo` (testing/custom_implementations/
+    work_dir/reduce_scatter/): ranks in n / b groups of b, IRC = rc * b, niters = ceil(nnodes / b)."""
+    nnodes = n // b
+    niters = nnodes // b + (1 if nnodes % b else 0)
+    if algo == "irs":
+        return rc * n, niters * rc * b
+    if algo == "ilr":
+        return niters * rc * b, rc * b
+    if algo == "isc":
+        return b * rc, rc
+    raise ValueError(algo)
+
+
+def phase_collective(algo, sends, dtype, op, k, b, rc, inplace=False):
+    """All ranks' recv buffers (output size, zero where the reference writes nothing) of the stand-alone
+    phase `algo`; sends: each rank's input (phase_sizes).  inplace: irs only (MPI_IN_PLACE)."""
+    L = lib()
+    vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    if not getattr(L, "_phase_ready", False):
+        L.orc_intra_reduce_scatter.argtypes = [i, i, i, sz, i, i, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+        L.orc_inter_reduce_linear.argtypes = [i, i, sz, i, i, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+        L.orc_intra_scatter.argtypes = [i, i, i, sz, i, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+        for fn in (L.orc_intra_reduce_scatter, L.orc_inter_reduce_linear, L.orc_intra_scatter):
+            fn.restype = i
+        L._phase_ready = True
+    n = len(sends)
+    _, out_n = phase_sizes(algo, n, b, rc)
+    npdt = sends[0].dtype
+    if inplace:
+        assert algo == "irs"
+        recvs = [s.copy() for s in sends]
+    else:
+        recvs = [np.zeros(max(out_n, 1), dtype=npdt) for _ in sends]
+    sp = _ptr_array([None] * n) if inplace else _ptr_array(sends)
+    rp = _ptr_array(recvs)
+    d = DTYPES[dtype]
+    if algo == "irs":
+        rc_ = L.orc_intra_reduce_scatter(n, k, b, rc, d, OPS[op], sp, rp)
+    elif algo == "ilr":
+        rc_ = L.orc_inter_reduce_linear(n, b, rc, d, OPS[op], sp, rp)
+    else:
+        rc_ = L.orc_intra_scatter(n, k, b, rc, d, sp, rp)
+    if rc_:
+        raise ValueError(f"oracle {algo} rejected (rc={rc_})")
+    return [r[:out_n] for r in recvs]

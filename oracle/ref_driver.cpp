@@ -13,7 +13,9 @@
 //   one case per line: id mode k b count dtype op pattern seed inplace
 //   mode: ar | rs | ag (radix_batch), ring | rd | rsag | rx | krsag | rm (MPICH baseline allreduces;
 //   rx and krsag use b as single_phase_recv), rs_radix | rs_halving | rs_doubling | rs_pairwise
-//   (MPICH baseline reduce-scatters, count = recvcount; rs_radix uses k)
+//   (MPICH baseline reduce-scatters, count = recvcount; rs_radix uses k), irs | ilr | isc (CHiArA's
+//   phases as stand-alone functions in testing/custom_implementations/work_dir/reduce_scatter/:
+//   intra_reduce_scatter_radix_batch, inter_reduce_linear, intra_scatter_radix_batch; count = recvcount)
 // For each case rank 0 writes <outdir>/<id>.out (all ranks' outputs, rank-major) and
 // <outdir>/<id>.lib (the MPI library collective's result on the same inputs).
 #include <mpi.h>
@@ -58,6 +60,14 @@ int MPICH_reduce_scatter_radix(const void* sendbuf, void* recvbuf, MPI_Aint recv
                                MPI_Op op, MPI_Comm comm, int k);
 int MPICH_reduce_scatter_pairwise(const void* sendbuf, void* recvbuf, MPI_Aint recvcount, MPI_Datatype datatype,
                                   MPI_Op op, MPI_Comm comm);
+
+// testing/custom_implementations/work_dir/reduce_scatter/ (CHiArA's phases, stand-alone)
+int intra_reduce_scatter_radix_batch(const void* sendbuf, void* recvbuf, MPI_Aint recvcount, MPI_Datatype datatype,
+                                     MPI_Op op, MPI_Comm comm, int k, int b);  // intra_reduce_scatter_radix.cpp:208
+int inter_reduce_linear(const void* sendbuf, void* recvbuf, MPI_Aint recvcount, MPI_Datatype datatype, MPI_Op op,
+                        MPI_Comm comm, int b);  // inter_linear_reduce.cpp:11
+int intra_scatter_radix_batch(char* sendbuf, int recvcount, MPI_Datatype datatype, char* recvbuf, MPI_Comm comm, int k,
+                              int b);  // intra_scatter_radix_batch.cpp:10
 
 // orc_reduce_local is the single definition of the bf16 op semantics.
 static void bf16_user_op(void* in, void* inout, int* len, MPI_Datatype*) {
@@ -154,10 +164,28 @@ int main(int argc, char** argv) {
         const bool rs_mode = mode == "rs" || mode.rfind("rs_", 0) == 0;  // rs_lib included
         size_t in_n = rs_mode ? (size_t)count * nprocs : (size_t)count;
         size_t out_n = (mode == "ag") ? (size_t)count * nprocs : (size_t)count;
+        const bool phase_mode = mode == "irs" || mode == "ilr" || mode == "isc";
+        if (phase_mode) {  // sizes as tests/../oracle/pyoracle.py phase_sizes
+            const size_t nnodes = (size_t)nprocs / b, niters = nnodes / b + (nnodes % b ? 1 : 0), irc = (size_t)count * b;
+            in_n = mode == "irs" ? (size_t)count * nprocs : mode == "ilr" ? niters * irc : (size_t)b * count;
+            out_n = mode == "irs" ? niters * irc : mode == "ilr" ? irc : (size_t)count;
+            if (in_n < out_n) in_n = out_n;  // recv is allocated with in_n elements
+        }
         std::vector<char> send(in_n * es), recv(in_n * es, 0), lib(out_n * es, 0);
         orc_fill(send.data(), in_n, dtype, pattern, seed, rank, in_n);
 
-        if (mode == "ar_lib" || mode == "rs_lib") {
+        if (phase_mode) {
+            // no library counterpart: .lib stays zero; recv starts zero, and what a rank does not write stays so
+            if (inplace) memcpy(recv.data(), send.data(), in_n * es);
+            MPI_Barrier(MPI_COMM_WORLD);
+            if (mode == "irs")
+                intra_reduce_scatter_radix_batch(inplace ? MPI_IN_PLACE : (const void*)send.data(), recv.data(),
+                                                 (MPI_Aint)count, mdt, mop, MPI_COMM_WORLD, k, b);
+            else if (mode == "ilr")
+                inter_reduce_linear(send.data(), recv.data(), (MPI_Aint)count, mdt, mop, MPI_COMM_WORLD, b);
+            else
+                intra_scatter_radix_batch(send.data(), (int)count, mdt, recv.data(), MPI_COMM_WORLD, k, b);
+        } else if (mode == "ar_lib" || mode == "rs_lib") {
             // MPI's own collective only: the expected output for the pair types whose MPI_Type_size is
             // not their extent (MPI_DOUBLE_INT, MPI_LONG_INT, MPI_SHORT_INT), where the reference's
             // byte arithmetic (all_reduce_radix_batch.cpp:238-256 takes MPI_Type_size as the element

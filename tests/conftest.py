@@ -109,3 +109,19 @@ def golden_rsmpich():
         manifest = json.load(f)
     arrays = np.load(os.path.join(here, "rsmpich_outputs.npz"), allow_pickle=False)
     return manifest["cases"], arrays
+
+
+@pytest.fixture(scope="session")
+def golden_phases():
+    """Golden vectors of CHiArA's phases as stand-alone functions (testing/custom_implementations/work_dir/
+    reduce_scatter/{intra_reduce_scatter_radix, inter_linear_reduce, intra_scatter_radix_batch}.cpp, compiled
+    unchanged against MPICH; gen_golden.py phases)."""
+    import json
+
+    import numpy as np
+
+    here = os.path.join(REPO, "tests", "golden")
+    with open(os.path.join(here, "phases_manifest.json")) as f:
+        manifest = json.load(f)
+    arrays = np.load(os.path.join(here, "phases_outputs.npz"), allow_pickle=False)
+    return manifest["cases"], arrays

@@ -270,6 +270,43 @@ def rsmpich_cases_for(n):
     return out
 
 
+def phases_cases_for(n):
+    """CHiArA's phases as stand-alone functions (testing/custom_implementations/work_dir/reduce_scatter/):
+    irs = intra_reduce_scatter_radix_batch (k, b), ilr = inter_reduce_linear (b), isc =
+    intra_scatter_radix_batch (k, b); count = recvcount.  Every divisor b of n (stages, leftover
+    stages, step-1 folds of b not a power of k), the self-tests' own parameters (irs: recvcount 1, k 2,
+    b 4; ilr: b 2; isc: k 7, b 9, recvcount 7)."""
+    out = []
+
+    def add(mode, k, b, count, dt, op, pat, inplace):
+        cid = f"{mode}_n{n}_k{k}_b{b}_c{count}_{dt}_{op}_p{pat}_ip{inplace}"
+        out.append(dict(id=cid, mode=mode, n=n, k=k, b=b, count=count, dtype=dt, op=op,
+                        pattern=pat, seed=SEED, inplace=inplace))
+
+    for b in divisors(n):
+        for k in (2, 3, 4):
+            add("irs", k, b, 3, "f32", "sum", pyoracle.PAT_UNIFORM, 0)
+            add("irs", k, b, 5, "i32", "sum", pyoracle.PAT_SEQ, k % 2)
+            add("isc", k, b, 5, "i32", "sum", pyoracle.PAT_SEQ, 0)
+        add("irs", 2, b, 16, "f64", "max", pyoracle.PAT_TIES, 0)
+        add("irs", 3, b, 16, "bf16", "sum", pyoracle.PAT_UNIFORM, 1)
+        add("irs", 4, b, 16, "f32", "min", pyoracle.PAT_TIES, 0)
+        add("irs", 2, b, 33, "u8", "bxor", pyoracle.PAT_UNIFORM, 0)
+        add("ilr", 0, b, 3, "f32", "sum", pyoracle.PAT_UNIFORM, 0)
+        add("ilr", 0, b, 7, "i32", "sum", pyoracle.PAT_SEQ, 0)
+        add("ilr", 0, b, 16, "f64", "max", pyoracle.PAT_TIES, 0)
+        add("ilr", 0, b, 16, "bf16", "sum", pyoracle.PAT_UNIFORM, 0)
+        add("isc", 2, b, 16, "f64", "sum", pyoracle.PAT_UNIFORM, 0)
+        add("isc", 5, b, 33, "u8", "sum", pyoracle.PAT_UNIFORM, 0)
+    if n % 4 == 0:
+        add("irs", 2, 4, 1, "i32", "sum", pyoracle.PAT_SEQ, 0)  # intra_reduce_scatter_radix.cpp:564-566
+    if n % 2 == 0:
+        add("ilr", 0, 2, 1, "i32", "sum", pyoracle.PAT_SEQ, 0)  # inter_linear_reduce.cpp:102-103
+    if n % 9 == 0:
+        add("isc", 7, 9, 7, "i32", "sum", pyoracle.PAT_SEQ, 0)  # intra_scatter_radix_batch.cpp:155-157
+    return out
+
+
 def run_n(n, cases, tmp):
     cf = os.path.join(tmp, f"cases_{n}.txt")
     with open(cf, "w") as f:
@@ -295,6 +332,10 @@ def main():
         for n in (1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 16):
             all_cases += rsmpich_cases_for(n)
         prefix = "rsmpich_"
+    elif which == "phases":
+        for n in (1, 2, 3, 4, 5, 6, 8, 9, 12, 16, 18):
+            all_cases += phases_cases_for(n)
+        prefix = "phases_"
     elif which == "types":
         for n in (2, 3, 4, 6, 8):
             all_cases += types_cases_for(n)
@@ -364,7 +405,9 @@ def main():
                 arrays[c["id"]] = a.copy()
                 arrays[c["id"] + "__lib"] = lb.copy()
             manifest.append(rec)
-    ref_desc = ("testing/mpich_implementations/reduce_scatter/{reduce_scatter_radix,"
+    ref_desc = ("testing/custom_implementations/work_dir/reduce_scatter/{intra_reduce_scatter_radix,"
+                "inter_linear_reduce,intra_scatter_radix_batch}.cpp" if which == "phases" else
+                "testing/mpich_implementations/reduce_scatter/{reduce_scatter_radix,"
                 "reduce_scatter_recursive_halving,reduce_scatter_recursive_doubling,reduce_scatter_pairwise}.cpp"
                 if which == "rsmpich" else
                 "Fugaku_experiments/{Allreduce,Reduce-scatter,Allgather} + testing/mpich_implementations/"

@@ -68,11 +68,14 @@ def run_local(st, op, dtype, rop):
 FAN_IN = 8  # kMaxFanIn in csrc/reduce_kernels.hip
 
 
-def execute(plans, sends, dtype, rop, inplace=False):
+def execute(plans, sends, dtype, rop, inplace=False, recv_init=None):
+    """recv_init: optional initial RECV buffer per rank (its size may exceed what the plan writes)."""
     n = len(plans)
     states = []
     for r in range(n):
-        if inplace and plans[r]["header"]["mode"] == ca.MODE_ALLGATHER:
+        if recv_init is not None and not inplace:
+            st = RankState(plans[r], sends[r], recv_init[r], dtype)
+        elif inplace and plans[r]["header"]["mode"] == ca.MODE_ALLGATHER:
             # MPI_IN_PLACE allgather: the own block already sits at recv + r*sendcount
             c = sends[r].size
             buf = np.zeros(plans[r]["header"]["recv"], dtype=sends[r].dtype)

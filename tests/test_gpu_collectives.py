@@ -579,3 +579,68 @@ def test_mpich_reduce_scatter_baselines_large(gu, groups, algo):
     assert groups(n).reduce_scatter_mpich(RS_MODE[algo], d_send, d_recv, rc, ca.FLOAT32, ca.SUM, 3) == 0
     for r in range(n):
         np.testing.assert_array_equal(gu.from_dev(d_recv[r], np.float32, rc).view(np.uint32), want[r].view(np.uint32))
+
+
+PHASE_MODE = {"irs": ca.MODE_INTRA_REDUCE_SCATTER, "ilr": ca.MODE_INTER_REDUCE_LINEAR, "isc": ca.MODE_INTRA_SCATTER}
+
+
+def _run_phase(gu, group, mode, sends, k, b, rc, dtype, op, inplace=False, null_unread=False):
+    """Every rank's recv buffer after the stand-alone phase `mode` on the device (recv starts zero, so
+    what a rank's plan does not write stays zero, as in the reference driver)."""
+    n = len(sends)
+    npdt = po.NP_DTYPES[dtype]
+    in_n, out_n = po.phase_sizes(mode, n, b, rc)
+    es = np.dtype(npdt).itemsize
+    if inplace:
+        d_recv = [gu.to_dev(s) for s in sends]
+        d_sendp = [ca.IN_PLACE] * n
+    else:
+        d_recv = [gu.to_dev(np.zeros(max(out_n, 1), dtype=npdt)) for _ in range(n)]
+        d_sendp = [gu.to_dev(s) for s in sends]
+        if null_unread and mode == "isc":  # only node roots read their send buffer
+            d_sendp = [d if (r % b) == (r // b) % b else None for r, d in enumerate(d_sendp)]
+    rc_ = group.phase_collective(PHASE_MODE[mode], d_sendp, d_recv, rc, DT[dtype], OP[op], k, b)
+    assert rc_ == 0, f"rc={rc_}"
+    return [gu.from_dev(d, npdt, out_n) for d in d_recv]
+
+
+def test_phases_match_reference_golden(gu, groups, golden_phases):
+    """CHiArA's phases as stand-alone functions (testing/custom_implementations/work_dir/reduce_scatter/:
+    intra_reduce_scatter_radix_batch, inter_reduce_linear, intra_scatter_radix_batch): every golden case
+    of the reference's own code bit-exact on the device (in place where the reference supports it;
+    non-roots of the scatter pass no send buffer, as its self-test does)."""
+    cases, _ = golden_phases
+    bad = []
+    for c in cases:
+        n = c["n"]
+        in_n, _ = po.phase_sizes(c["mode"], n, c["b"], c["count"])
+        sends = [po.fill(in_n, c["dtype"], c["pattern"], c["seed"], r) for r in range(n)]
+        outs = _run_phase(gu, groups(n), c["mode"], sends, c["k"] or 2, c["b"], c["count"], c["dtype"], c["op"],
+                          inplace=bool(c["inplace"]), null_unread=True)
+        if hashlib.sha256(b"".join(o.tobytes() for o in outs)).hexdigest() != c["sha256"]:
+            bad.append(c["id"])
+    assert not bad, f"{len(bad)} device/reference mismatches, e.g. {bad[:5]}"
+
+
+@pytest.mark.parametrize("mode,n,k,b", [("irs", 12, 2, 3), ("irs", 8, 4, 2), ("ilr", 12, 2, 2), ("isc", 9, 3, 9)])
+def test_phases_large(gu, groups, mode, n, k, b):
+    """MiB-sized chunks (the vector kernel paths, odd counts for the tails): bit-exact vs the oracle.
+    irs 12/3: one stage plus a leftover stage and step-1 folds (b = 3 is not a power of 2)."""
+    rc = (1 << 18) + 3
+    in_n, _ = po.phase_sizes(mode, n, b, rc)
+    sends = [po.fill(in_n, "f32", po.PAT_UNIFORM, 5, r) for r in range(n)]
+    want = po.phase_collective(mode, sends, "f32", "sum", k, b, rc)
+    got = _run_phase(gu, groups(n), mode, sends, k, b, rc, "f32", "sum")
+    for r in range(n):
+        np.testing.assert_array_equal(got[r].view(np.uint32), want[r].view(np.uint32))
+
+
+def test_phases_reject_in_place_where_the_reference_does(gu, groups):
+    """inter_reduce_linear and intra_scatter_radix_batch read sendbuf unconditionally (no MPI_IN_PLACE);
+    here CHR_IN_PLACE is an error instead of a crash.  n % b != 0 is CHR_ERR_BATCH_NOT_DIVISOR."""
+    n, b, rc = 4, 2, 8
+    d = [gu.to_dev(np.zeros(64, dtype=np.float32)) for _ in range(n)]
+    g = groups(n)
+    for mode in (ca.MODE_INTER_REDUCE_LINEAR, ca.MODE_INTRA_SCATTER):
+        assert g.phase_collective(mode, [ca.IN_PLACE] * n, d, rc, ca.FLOAT32, ca.SUM, 2, b) == ca.ERR_INVALID_ARG
+    assert g.phase_collective(ca.MODE_INTRA_REDUCE_SCATTER, d, d, rc, ca.FLOAT32, ca.SUM, 2, 3) == ca.ERR_BATCH_NOT_DIVISOR

@@ -173,3 +173,35 @@ def test_shim_over_mpi_datatype_op_table(tmp_path):
     # 31 types x 12 ops; MPICH accepts 226 of the pairs (the MAXLOC / MINLOC pair types and the C
     # complex types included)
     assert res["pairs"] == 372 and res["supported_by_mpich"] >= 226, res
+
+
+def _selftest_cases():
+    import json
+
+    with open(os.path.join(REPO, "tests", "golden", "selftest_outputs.json")) as f:
+        return sorted(json.load(f)["runs"].items())
+
+
+@pytest.mark.parametrize("name,run", _selftest_cases(), ids=[k for k, _ in _selftest_cases()])
+def test_reference_phase_selftests_on_mi355x(tmp_path, name, run):
+    """The DEBUG_MODE self-test mains of CHiArA's stand-alone phases (testing/custom_implementations/
+    work_dir/reduce_scatter/{intra_reduce_scatter_radix, inter_linear_reduce, intra_scatter_radix_batch}.cpp,
+    compiled unchanged with -DDEBUG_MODE; oracle/Makefile `selftests`), their function replaced through the
+    shim by libchiara's: every rank prints exactly the lines the reference's own build printed here
+    (tests/golden/selftest_outputs.json), the scatter's RESULT: PASS included."""
+    exe = os.path.join(REPO, "oracle", "_ref", f"selftest_{run['binary']}")
+    if not os.path.exists(exe) or not os.path.exists(MPIEXEC):
+        pytest.skip("self-test binary or MPICH not present")
+    n = run["nranks"]
+    cmd = [MPIEXEC, "-outfile-pattern", "out.%r"]
+    for r in range(n):
+        if r:
+            cmd.append(":")
+        cmd += ["-n", "1", "-env", "NCCL_HOSTID", f"chiara-selftest-{r}", "-env", "NCCL_SOCKET_IFNAME", "lo",
+                "-env", "NCCL_IB_DISABLE", "1", exe] + run["args"]
+    out = subprocess.run(cmd, cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    for r in range(n):
+        with open(tmp_path / f"out.{r}", encoding="utf-8") as f:
+            got = [ln.rstrip() for ln in f.read().splitlines()]
+        assert got == run["lines"][str(r)], (r, got, run["lines"][str(r)])

@@ -55,16 +55,16 @@ int main(int argc, char** argv) {
     const int modes[] = {MODE_ALLREDUCE,         MODE_REDUCE_SCATTER,    MODE_ALLGATHER,        MODE_MPICH_RING,
                          MODE_MPICH_RD,          MODE_MPICH_RSAG,        MODE_MPICH_RECEXCH,    MODE_MPICH_KRSAG,
                          MODE_MPICH_RMULT,       MODE_MPICH_RS_RADIX,    MODE_MPICH_RS_HALVING, MODE_MPICH_RS_DOUBLING,
-                         MODE_MPICH_RS_PAIRWISE};
+                         MODE_MPICH_RS_PAIRWISE, MODE_INTRA_RS,          MODE_INTER_LINEAR,     MODE_INTRA_SCATTER};
     for (int mode : modes)
         for (int n = 1; n <= max_n; ++n)
             for (int b = 1; b <= n; ++b) {
-                if (n % b && mode <= MODE_REDUCE_SCATTER) continue;
+                if (n % b && (mode <= MODE_REDUCE_SCATTER || is_phase(mode))) continue;
                 for (int k = 2; k <= 9; ++k)
                     for (unsigned long long per : {1ull, 3ull, 64ull, 1000ull})
                         for (int slices : {1, 3, 8})
                             for (int sched : {0, 1, 2, 3, 4, 5, (int)SCHED_FLAT_1SHOT}) {
-                                if ((is_mpich(mode) || mode == MODE_ALLGATHER) && (sched != SCHED_FLAT || slices != 1))
+                                if (is_unpipelined(mode) && (sched != SCHED_FLAT || slices != 1))
                                     continue;
                                 const unsigned long long count =
                                     mode == MODE_ALLREDUCE || is_mpich(mode) ? per * (unsigned long long)n : per;
