@@ -141,3 +141,40 @@ def test_plans_reject_bad_geometry():
         assert ca.parse_plan(ca.describe_plan(mode, 6, 0, 2, 4, 8))["header"]["error"] == 3  # 6 % 4
         assert ca.parse_plan(ca.describe_plan(mode, 4, 0, 2, 0, 8))["header"]["error"] == 1  # b = 0
     assert ca.parse_plan(ca.describe_plan(ca.MODE_INTRA_SCATTER, 4, 0, 1, 2, 8))["header"]["error"] == 1  # k < 2
+
+
+def test_reference_selftest_outputs_agree_with_the_oracle():
+    """tests/golden/selftest_outputs.json (the reference's DEBUG_MODE mains, run here; the GPU test runs
+    the same mains on libchiara) checked on CPU: the scatter's RESULT: PASS, and every AFTER buffer the
+    mains print equals the oracle on the mains' own inputs."""
+    import json
+    import os
+    import re
+
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    with open(os.path.join(here, "selftest_outputs.json")) as f:
+        runs = json.load(f)["runs"]
+    ints = lambda s: [int(x) for x in re.findall(r"-?\d+", s)]  # noqa: E731
+    for key, run in runs.items():
+        n, lines = run["nranks"], run["lines"]
+        if run["binary"] == "intra_scatter_radix_batch":
+            assert lines["0"][-1].startswith("RESULT: PASS"), key
+        elif run["binary"] == "inter_linear_reduce":
+            b, rc = (int(a) for a in run["args"])
+            in_n, out_n = po.phase_sizes("ilr", n, b, rc)
+            irc = rc * b
+            sends = [np.array([10000 * r + 100 * (i // irc) + i % irc for i in range(in_n)], dtype=np.int32)
+                     for r in range(n)]
+            want = po.phase_collective("ilr", sends, "i32", "sum", 2, b, rc)
+            for r in range(n):
+                after = lines[str(r)][lines[str(r)].index(f"== AFTER  rank {r} (rc=0) ==") + 2:]
+                got = [v for ln in after for v in ints(ln.split(":", 1)[1])][:irc]
+                root = any(i * b + r % b == r // b for i in range(in_n // irc))
+                assert got == (want[r].tolist() if root else [-777777] * irc), (key, r)
+        else:
+            rc, k, b = (int(a) for a in run["args"])
+            in_n, out_n = po.phase_sizes("irs", n, b, rc)
+            sends = [np.array([r + 1 + 100 * (i // (rc * b)) for i in range(in_n)], dtype=np.int32) for r in range(n)]
+            want = po.phase_collective("irs", sends, "i32", "sum", k, b, rc)
+            for r in range(n):
+                assert ints(lines[str(r)][-1]) == want[r].tolist(), (key, r)
