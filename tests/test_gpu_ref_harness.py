@@ -176,10 +176,15 @@ def test_shim_over_mpi_datatype_op_table(tmp_path):
 
 
 # One geometry per self-test main (each run starts n MPI processes, each with HIP and an RCCL
-# communicator, ~10-50 s): intra_reduce_scatter with step-1 folds (b = 3, k = 2), inter_linear_reduce with
-# a leftover iteration (nnodes = 3, b = 2), intra_scatter with a two-level k-nomial tree (k = 2, b = 4).
-# tests/golden/selftest_outputs.json holds more, all checked against the oracle on CPU (test_phases.py).
-SELFTEST_RUNS = ("intra_reduce_scatter_radix_n9_2_2_3", "inter_linear_reduce_n6_2_3", "intra_scatter_radix_batch_n8_2_4_3")
+# communicator): intra_reduce_scatter with step-1 folds (b = 3, k = 2), inter_linear_reduce with a leftover
+# iteration (nnodes = 3, b = 2), intra_scatter with a two-level k-nomial tree (k = 2, b = 4), and the DEBUG
+# mains of all_reduce_radix_batch.cpp and of the MPICH baselines at 6 ranks (non-power-of-two folds).
+# tests/golden/selftest_outputs.json holds more phase geometries, checked against the oracle on CPU.
+SELFTEST_RUNS = ("intra_reduce_scatter_radix_n9_2_2_3", "inter_linear_reduce_n6_2_3", "intra_scatter_radix_batch_n8_2_4_3",
+                 "all_reduce_radix_batch_n6_3_b2", "reduce_scatter_radix_n6_3", "reduce_scatter_recursive_halving_n6_2_2",
+                 "reduce_scatter_pairwise_n6_", "allreduce_ring_n6_", "allreduce_recursive_doubling_n6_",
+                 "allreduce_reduce_scatter_allgather_n6_", "allreduce_recexch_n6_", "allreduce_k_reduce_scatter_allgather_n6_",
+                 "allreduce_recursive_multiplying_n6_")
 
 
 def _selftest_cases():
@@ -190,19 +195,16 @@ def _selftest_cases():
     return [(k, runs[k]) for k in SELFTEST_RUNS]
 
 
-def _program_lines(text):
-    """The main's own lines: RCCL's rank-0 banner ("RCCL version : ...", "Librccl path : ...") and any
-    NCCL/RCCL log line are dropped (none of the mains prints " : " or "NCCL ")."""
-    return [ln.rstrip() for ln in text.splitlines() if " : " not in ln and "NCCL " not in ln]
-
-
 @pytest.mark.parametrize("name,run", _selftest_cases(), ids=list(SELFTEST_RUNS))
-def test_reference_phase_selftests_on_mi355x(tmp_path, name, run):
-    """The DEBUG_MODE self-test mains of CHiArA's stand-alone phases (testing/custom_implementations/
-    work_dir/reduce_scatter/{intra_reduce_scatter_radix, inter_linear_reduce, intra_scatter_radix_batch}.cpp,
-    compiled unchanged with -DDEBUG_MODE; oracle/Makefile `selftests`), their function replaced through the
-    shim by libchiara's: every rank prints exactly the lines the reference's own build printed here
-    (tests/golden/selftest_outputs.json), the scatter's RESULT: PASS included."""
+def test_reference_selftests_on_mi355x(tmp_path, name, run):
+    """The reference's DEBUG_MODE self-test mains, each compiled unchanged with -DDEBUG_MODE
+    (oracle/selftests.sh) with its algorithm function replaced through the shim by libchiara's: CHiArA's
+    stand-alone phases, all_reduce_radix_batch.cpp and the MPICH baselines.  Every rank prints exactly the
+    lines the reference's own build printed here, and writes the same files (tests/golden/selftest_outputs.json,
+    normalised by tests/selftest_util.py: wall-clock times masked) -- every PASS line, is_correct column and
+    printed buffer included."""
+    import selftest_util
+
     exe = os.path.join(REPO, "oracle", "_ref", f"selftest_{run['binary']}")
     if not os.path.exists(exe) or not os.path.exists(MPIEXEC):
         pytest.skip("self-test binary or MPICH not present")
@@ -216,6 +218,10 @@ def test_reference_phase_selftests_on_mi355x(tmp_path, name, run):
     out = subprocess.run(cmd, cwd=tmp_path, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     for r in range(n):
-        with open(tmp_path / f"out.{r}", encoding="utf-8") as f:
-            got = _program_lines(f.read())
+        path = tmp_path / f"out.{r}"
+        got = selftest_util.normalize(path.read_text(encoding="utf-8") if path.exists() else "")
         assert got == run["lines"][str(r)], (r, got, run["lines"][str(r)])
+    for fname, want in run.get("files", {}).items():
+        text = (tmp_path / fname).read_text(encoding="utf-8")
+        got = selftest_util.normalize_csv(text) if fname.endswith(".csv") else text.splitlines()
+        assert got == want, (fname, got[:10], want[:10])
