@@ -403,7 +403,10 @@ def bench_collective_kernels_small(args):
     """The fused reductions of the smaller multi-GPU configs, on virtual ranks as above: the N=2 and
     N=4 lines' allreduces (1 GiB fp32 per rank, b = N, k = min(4, N): 2- and 4-leaf trees) and C3
     (reduce-scatter, 2 ranks, 256 MiB fp32 send buffer, radix 2, b = 1 and 2: 2-leaf trees), each
-    with the ranks' trees of a step in shared grids and with one grid per rank."""
+    with the ranks' trees of a step in shared grids and with one grid per rank.  Also CHiArA's phases as
+    stand-alone collectives at 8 ranks, 1 GiB fp32 send buffer per rank: intra_reduce_scatter_radix_batch
+    (b = 2, k = 2: two stages of recexch folds, m = 1) and inter_reduce_linear (b = 2: the roots fold
+    nnodes - 1 = 3 chunks, m = 3), whose reductions run on k_reduce_vec (no trees: batching does not apply)."""
     import torch
 
     import chiara_amd as ca
@@ -412,16 +415,26 @@ def bench_collective_kernels_small(args):
     torch.cuda.set_device(dev)
     rows = {}
     cases = [("ar_n2_k2_b2", "ar", 2, 2, 2, 1 << 28), ("ar_n4_k4_b4", "ar", 4, 4, 4, 1 << 28),
-             ("c3_rs_n2_k2_b1", "rs", 2, 2, 1, 1 << 25), ("c3_rs_n2_k2_b2", "rs", 2, 2, 2, 1 << 25)]
+             ("c3_rs_n2_k2_b1", "rs", 2, 2, 1, 1 << 25), ("c3_rs_n2_k2_b2", "rs", 2, 2, 2, 1 << 25),
+             ("phase_intra_rs_n8_k2_b2", "irs", 8, 2, 2, 1 << 25), ("phase_inter_linear_n8_b2", "ilr", 8, 2, 2, 1 << 27)]
+    phase_mode = {"irs": ca.MODE_INTRA_REDUCE_SCATTER, "ilr": ca.MODE_INTER_REDUCE_LINEAR}
     for name, mode, n, k, b, cnt in cases:
         g = ca.LocalGroup(n, 0)
-        total = cnt if mode == "ar" else cnt * n  # send elements per rank
+        nnodes = n // b
+        niters = nnodes // b + (1 if nnodes % b else 0)
+        # send / recv elements per rank (the phases: intra_reduce_scatter_radix.cpp:241-247, inter_linear_reduce.cpp:39-46)
+        total, out = {"ar": (cnt, cnt), "rs": (cnt * n, cnt), "irs": (cnt * n, niters * cnt * b),
+                      "ilr": (niters * cnt * b, cnt * b)}[mode]
         sends = [torch.empty(total * 4, dtype=torch.uint8, device=dev) for _ in range(n)]
-        recvs = [torch.empty(cnt * 4, dtype=torch.uint8, device=dev) for _ in range(n)]
+        recvs = [torch.empty(out * 4, dtype=torch.uint8, device=dev) for _ in range(n)]
         for r, x in enumerate(sends):
             ca.check(ca.fill(x, total, ca.FLOAT32, 0, SEED, r, stream=g.stream))
-        fn = g.all_reduce_radix_batch if mode == "ar" else g.reduce_scatter_radix_batch
-        for batched in (True, False):
+        if mode in phase_mode:
+            def fn(S, R, c, dt, op, k_, b_, m=phase_mode[mode], g=g):
+                return g.phase_collective(m, S, R, c, dt, op, k_, b_)
+        else:
+            fn = g.all_reduce_radix_batch if mode == "ar" else g.reduce_scatter_radix_batch
+        for batched in ((True,) if mode in phase_mode else (True, False)):
             g.set_batching(batched)
             ca.check(fn(sends, recvs, cnt, ca.FLOAT32, ca.SUM, k, b))  # warm: plans, scratch
             g.profile(True)
@@ -441,8 +454,9 @@ def bench_collective_kernels_small(args):
         torch.cuda.empty_cache()
     knobs = {k: v for k, v in os.environ.items() if k.startswith("CHR_")}
     emit({"collective_kernels_small": {"workload": "fused reductions of the N=2 / N=4 allreduce lines (1 GiB fp32 per "
-                                                   "rank) and C3 (reduce-scatter, 2 ranks, 256 MiB send), virtual "
-                                                   "ranks on one GPU, each reduce phase timed as one span",
+                                                   "rank), C3 (reduce-scatter, 2 ranks, 256 MiB send) and the "
+                                                   "stand-alone phases (8 ranks, 1 GiB send), virtual ranks on one "
+                                                   "GPU, each reduce phase timed as one span",
                                        "env": knobs, "rows": rows}})
 
 
