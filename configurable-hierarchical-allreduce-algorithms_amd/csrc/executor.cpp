@@ -1209,11 +1209,16 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
     // back into the group's stream; while profiling, bracketed by events on the group's stream.
     const bool dual = g->cs[0] && g->cs[1];
     auto phase = [&](auto&& ops_of) -> int {
-        bool any = false;
-        for (int r = 0; r < n && !any; ++r) any = !ops_of(r).empty();
+        bool any = false, reduces = false;
+        for (int r = 0; r < n; ++r) {
+            any = any || !ops_of(r).empty();
+            for (const chr::LocalOp& op : ops_of(r)) reduces = reduces || op.kind == chr::L_REDUCE || op.kind == chr::L_TREE;
+        }
         if (!any) return CHR_SUCCESS;
+        // a phase of copies only (re-layouts, the stand-alone phases' copy-outs) is not a reduction span
+        const bool span = g->prof.on && reduces;
         std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-        if (g->prof.on) {
+        if (span) {
             ev = g->prof.take();
             if ((rc = hip_code(hipEventRecord(ev.first, g->stream)))) return rc;
         }
@@ -1258,7 +1263,7 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
                     (rc = hip_code(hipStreamWaitEvent(g->stream, g->ev_done[k], 0))))
                     return rc;
         }
-        if (g->prof.on) {
+        if (span) {
             if ((rc = hip_code(hipEventRecord(ev.second, g->stream)))) return rc;
             g->prof.pending.push_back(ev);
         }
