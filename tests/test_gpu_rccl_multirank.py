@@ -52,6 +52,8 @@ def _worker(rank, world, port, cases, q):
             cdt = {"f32": ca.FLOAT32, "bf16": ca.BFLOAT16, "i32": ca.INT32}[dtype]
             in_n = count * world if (mode == "rs" or mode.startswith("rs_")) else count
             out_n = count * world if mode == "ag" else count
+            if mode in po.PHASE_ALGOS:  # CHiArA's stand-alone phases (count = recvcount; k, b as given)
+                in_n, out_n = po.phase_sizes(mode, world, b, count)
             pat = po.PAT_TIES if mode == "rx" else 0  # recexch: operand-order sensitive data, MAX
             x = po.fill(in_n, dtype, pat, 4242, rank)
             if host:
@@ -64,7 +66,15 @@ def _worker(rank, world, port, cases, q):
                 out_t = torch.zeros(out_n * x.itemsize, dtype=torch.uint8, device=dev)
             dst = out if host else out_t
             allx = [po.fill(in_n, dtype, pat, 4242, r) for r in range(world)]
-            if mode == "ag":
+            if mode in po.PHASE_ALGOS:
+                if mode == "irs":
+                    rc = ca.intra_reduce_scatter_radix_batch(send, dst, count, cdt, ca.SUM, comm, k, b)
+                elif mode == "ilr":
+                    rc = ca.inter_reduce_linear(send, dst, count, cdt, ca.SUM, comm, b)
+                else:
+                    rc = ca.intra_scatter_radix_batch(send, count, cdt, dst, comm, k, b)
+                ref = po.phase_collective(mode, allx, dtype, "sum", k, b, count, inplace=inplace)[rank]
+            elif mode == "ag":
                 rc = ca.allgather_radix_batch(send, count, cdt, dst, comm, k, b)
                 ref = np.concatenate(allx)
             elif mode in ("ar", "rs"):
@@ -160,6 +170,11 @@ ALLGATHER_W4 = [("ag", 2, 2, 1 << 16, "f32", False, 0), ("ag", 3, 4, 1001, "bf16
 ALLGATHER_W8 = [("ag", 4, 4, 1 << 16, "f32", False, 0), ("ag", 8, 2, 4097, "i32", False, 0)]
 # the reference's own messages end to end (bcast + left-over k-Bruck at C4; k-nomial scatter for
 # reduce-scatter)
+# CHiArA's phases as stand-alone collectives (intra_reduce_scatter_radix_batch: stages, leftover stage,
+# step-1 folds, in place; inter_reduce_linear; intra_scatter_radix_batch), device and host buffers
+PHASES_W8 = [("irs", 2, 2, 4097, "f32", False, 0), ("irs", 3, 4, 1001, "bf16", False, 0),
+             ("irs", 2, 2, 999, "f32", False, 0, 2, True, True), ("ilr", 0, 2, 5000, "f32", False, 0),
+             ("ilr", 0, 4, 2000, "f32", True, 0), ("isc", 2, 4, 3001, "i32", False, 0), ("isc", 3, 8, 777, "f32", True, 0)]
 EXACT_W8 = [("ar", 4, 4, 1 << 18, "f32", False, 0, 3, True), ("ar", 2, 8, 8 * 1001, "bf16", False, 0, 3, True),
             ("ar", 2, 2, 1 << 16, "f32", True, 0, 3, False), ("rs", 4, 8, 1 << 14, "f32", False, 0, 3, True),
             ("rs", 2, 4, 999, "f32", False, 0, 3, True)]
@@ -167,9 +182,9 @@ EXACT_W8 = [("ar", 4, 4, 1 << 18, "f32", False, 0, 3, True), ("ar", 2, 8, 8 * 10
 
 def test_rccl_world8_geometries_baselines_allgather_exact():
     """8 ranks over RCCL, one session: C4/C5 geometries, the MPICH allreduce and reduce-scatter
-    baselines, allgather_radix_batch, and the exact schedule (the reference's messages): bit-exact
-    vs the oracle."""
-    _run(8, W8_GEOMETRIES + MPICH_W8 + RS_MPICH_W8 + ALLGATHER_W8 + EXACT_W8, timeout=800)
+    baselines, allgather_radix_batch, the exact schedule (the reference's messages) and CHiArA's
+    stand-alone phases: bit-exact vs the oracle."""
+    _run(8, W8_GEOMETRIES + MPICH_W8 + RS_MPICH_W8 + ALLGATHER_W8 + EXACT_W8 + PHASES_W8, timeout=800)
 
 
 def test_rccl_world5_mpich_baselines():
