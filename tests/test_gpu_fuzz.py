@@ -1,4 +1,4 @@
-"""Randomised parity on the GPU: every collective family, geometry, schedule, pipeline depth, dtype,
+"""Randomised parity on the GPU: every collective family (CHiArA's stand-alone phases included), geometry, schedule, pipeline depth, dtype,
 op and in-place combination drawn from a seeded generator, each checked bit for bit against the
 oracle (LocalGroup: the RCCL path's plans and kernels with device copies as messages).
 
@@ -45,13 +45,16 @@ rng = np.random.default_rng({seed})
 groups = {{}}
 bad, done = [], 0
 for case in range({ncases}):
-    fam = rng.choice(["ar", "ar", "rs", "rs", "ag", "mpich", "mpich_rs"])
+    fam = rng.choice(["ar", "ar", "rs", "rs", "ag", "mpich", "mpich_rs", "phase"])
     n = int(rng.integers(1, 13))
     divs = [d for d in range(1, n + 1) if n % d == 0]
     b = int(rng.choice(divs))
     k = int(rng.integers(2, 10))
     dtype, op = PAIRS[int(rng.integers(len(PAIRS)))]
     if fam == "ag":
+        op = "sum"
+    algo = str(rng.choice(["irs", "ilr", "isc"])) if fam == "phase" else None
+    if algo == "isc":
         op = "sum"
     rc_ = int(rng.choice([1, 3, 17, 255, 256, 1000, 4097, 12345, 40000]))
     inplace = bool(rng.integers(2))
@@ -94,6 +97,21 @@ for case in range({ncases}):
                 rc = g.reduce_scatter_mpich(MPICH_RS[algo], d_sendp, d_recv, rc_, DT[dtype], OP[op], k)
                 want = po.mpich_reduce_scatter(algo, sends, dtype, op, k=k, inplace=inplace)
             outc = rc_
+        elif fam == "phase":  # CHiArA's stand-alone phases (in place: intra_reduce_scatter only)
+            tag["algo"] = algo
+            inplace = inplace and algo == "irs"
+            tag["inplace"] = inplace
+            in_n, outc = po.phase_sizes(algo, n, b, rc_)
+            sends = [po.fill(in_n, dtype, pat, seed, r) for r in range(n)]
+            if inplace:
+                d_recv = [gu.to_dev(s_) for s_ in sends]
+                d_sendp = [ca.IN_PLACE] * n
+            else:
+                d_recv = [gu.to_dev(np.zeros(max(outc, 1), dtype=npdt)) for _ in range(n)]
+                d_sendp = [gu.to_dev(s_) for s_ in sends]
+            mode = {"irs": ca.MODE_INTRA_REDUCE_SCATTER, "ilr": ca.MODE_INTER_REDUCE_LINEAR, "isc": ca.MODE_INTRA_SCATTER}[algo]
+            rc = g.phase_collective(mode, d_sendp, d_recv, rc_, DT[dtype], OP[op], k, b)
+            want = po.phase_collective(algo, sends, dtype, op, k, b, rc_, inplace=inplace)
         else:
             sends = [po.fill(rc_, dtype, pat, seed, r) for r in range(n)]
             d_recv = [gu.empty_dev(rc_ * n * es) for _ in range(n)]
