@@ -109,7 +109,8 @@ for case in range({ncases}):
             else:
                 d_recv = [gu.to_dev(np.zeros(max(outc, 1), dtype=npdt)) for _ in range(n)]
                 d_sendp = [gu.to_dev(s_) for s_ in sends]
-            mode = {"irs": ca.MODE_INTRA_REDUCE_SCATTER, "ilr": ca.MODE_INTER_REDUCE_LINEAR, "isc": ca.MODE_INTRA_SCATTER}[algo]
+            mode = {{"irs": ca.MODE_INTRA_REDUCE_SCATTER, "ilr": ca.MODE_INTER_REDUCE_LINEAR,
+                    "isc": ca.MODE_INTRA_SCATTER}}[algo]
             rc = g.phase_collective(mode, d_sendp, d_recv, rc_, DT[dtype], OP[op], k, b)
             want = po.phase_collective(algo, sends, dtype, op, k, b, rc_, inplace=inplace)
         else:
