@@ -118,6 +118,18 @@ def test_reference_allgather_harness_on_mi355x(tmp_path):
     _plots(tmp_path, "allgather")
 
 
+@pytest.mark.parametrize("harness,algo", [("all_reduce", "all_reduce_radix_batch"),
+                                          ("reduce_scatter", "reduce_scatter_radix_batch"),
+                                          ("all_gather", "allgather_radix_batch")])
+def test_reference_work_dir_harnesses_on_mi355x(tmp_path, harness, algo):
+    """The development copies of the harnesses (testing/custom_implementations/work_dir/{all_reduce,
+    reduce_scatter,all_gather}/main.cpp, 50 repetitions per size, their own CSV names), unchanged on the
+    shim: every row is_correct, 4 ranks."""
+    rows = _run(f"ref_harness_wd_{harness}", ["1", "--overwrite", "b=4", "base=64"], 4, tmp_path)
+    assert any(r["algorithm_name"] == algo for r in rows)
+    assert all(r["is_correct"] == "1" for r in rows)
+
+
 BIN = ("configurable-hierarchical-allreduce-algorithms_amd", "bin")
 
 
