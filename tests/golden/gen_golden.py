@@ -298,6 +298,13 @@ def phases_cases_for(n):
         add("ilr", 0, b, 16, "bf16", "sum", pyoracle.PAT_UNIFORM, 0)
         add("isc", 2, b, 16, "f64", "sum", pyoracle.PAT_UNIFORM, 0)
         add("isc", 5, b, 33, "u8", "sum", pyoracle.PAT_UNIFORM, 0)
+        # MPI's pair types (MAXLOC / MINLOC, ties) and C complex types whose MPI_Type_size is their extent
+        # (the reference strides its buffers by MPI_Type_size, intra_reduce_scatter_radix.cpp:238)
+        add("irs", 2, b, 5, "fi", "maxloc", pyoracle.PAT_TIES, 0)
+        add("irs", 3, b, 5, "cf", "sum", pyoracle.PAT_UNIFORM, 0)
+        add("ilr", 0, b, 5, "2i", "minloc", pyoracle.PAT_TIES, 0)
+        add("ilr", 0, b, 4, "cd", "prod", pyoracle.PAT_UNIFORM, 0)
+        add("isc", 2, b, 3, "cd", "sum", pyoracle.PAT_UNIFORM, 0)
     if n % 4 == 0:
         add("irs", 2, 4, 1, "i32", "sum", pyoracle.PAT_SEQ, 0)  # intra_reduce_scatter_radix.cpp:564-566
     if n % 2 == 0:
