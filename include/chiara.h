@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define CHR_ABI_VERSION 7
+#define CHR_ABI_VERSION 8  /* 8: the stand-alone phase collectives (chr_intra_reduce_scatter_radix_batch, ...) */
 
 /* Element types.  The reference is generic over MPI_Datatype (all_reduce_radix_batch.cpp:202-204,
  * sizes from MPI_Type_size at :234-277); these are the MPI predefined types MPICH's
