@@ -41,3 +41,22 @@ def test_normalize_masks_times_only():
                                              "Test PASSED: All 10 values match"]
     assert selftest_util.normalize_csv("algorithm_name,time,is_correct\nx,0.5,1\n") == [
         "algorithm_name,time,is_correct", "x,<t>,1"]
+
+
+def test_build_recipe_and_gpu_runs_match_the_goldens():
+    """oracle/selftests.sh builds every main the goldens hold, and every run the GPU test starts has a golden."""
+    import re
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    with open(os.path.join(os.path.dirname(here), "oracle", "selftests.sh")) as f:
+        specs = re.search(r"<<'SPECS'\n(.*?)\nSPECS", f.read(), re.S).group(1).split("\n")
+    built = {ln.split()[0] for ln in specs if ln.strip()}
+    runs = _runs()
+    assert {r["binary"] for r in runs.values()} == built
+    sys.path.insert(0, here)
+    src = open(os.path.join(here, "test_gpu_ref_harness.py")).read()
+    gpu_runs = re.search(r"SELFTEST_RUNS = \((.*?)\)\n", src, re.S).group(1)
+    keys = re.findall(r'"([^"]+)"', gpu_runs)
+    assert keys and all(k in runs for k in keys)
+    assert {runs[k]["binary"] for k in keys} == built  # one GPU run per main
