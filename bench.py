@@ -702,8 +702,8 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
     (testing/mpich_implementations/all_reduce/allreduce_ring.cpp) run on libchiara's executor and
     (3) the metric's own schedule with the reductions on the transfer stream (no overlap),
     (4) its arithmetic under the balanced, reference-route and exact (the reference's messages
-    end to end) schedules, (5) the flat schedule at pipeline depths 1, 2 and 8 and (6) the other
-    multi-GPU BASELINE configs, C3 and C5 (baseline_configs)."""
+    end to end) schedules, (5) the flat schedule at pipeline depths 1, 2 and 8, (6) CHiArA's phases as
+    stand-alone collectives and (7) the other multi-GPU BASELINE configs, C3 and C5 (baseline_configs)."""
     steps, warm = max(1, min(args.steps, 20)), 2
     S = count * (4 if dt == ca.FLOAT32 else 2)
     out = {"steps": steps}
@@ -770,6 +770,19 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
                 comm.set_slices(0)
     finally:
         comm.set_schedule(restore)
+    # CHiArA's phases as stand-alone collectives (testing/custom_implementations/work_dir/reduce_scatter/), on
+    # the same buffers, each reading the whole S-byte send buffer per rank: phase 1 (b = 2, k = 2), phase 2
+    # (b = 2) and the reduce-scatter's k-nomial scatter (one group of all ranks, k = 2)
+    if world % 2 == 0:
+        nn = world // 2
+        niters = nn // 2 + (1 if nn % 2 else 0)
+        rc_irs, rc_ilr, rc_isc = count // world, count // (niters * 2), count // world
+        timed("phase_intra_reduce_scatter_k2_b2",
+              lambda: ca.check(ca.intra_reduce_scatter_radix_batch(send, recv, rc_irs, dt, ca.SUM, comm, 2, 2)))
+        timed("phase_inter_reduce_linear_b2",
+              lambda: ca.check(ca.inter_reduce_linear(send, recv, rc_ilr, dt, ca.SUM, comm, 2)))
+        timed(f"phase_intra_scatter_k2_b{world}",
+              lambda: ca.check(ca.intra_scatter_radix_batch(send, rc_isc, dt, recv, comm, 2, world)))
     if out.get("aborted"):
         return out
     out["small_messages"] = small_messages(ca, torch, dist, comm, dt, k, b, world, dev, restore)
