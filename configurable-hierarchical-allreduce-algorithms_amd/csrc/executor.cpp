@@ -973,7 +973,7 @@ int run_collective(chr_comm* c, int sched, int slices, int mode, const void* sen
     const Plan& p = c->plan(mode, k, b, count, chr::dtype_size(dtype), sched, slices);
     if (p.error) return p.error;
     if (p.g.total == 0) return CHR_SUCCESS;
-    if (!recv) return CHR_ERR_INVALID_ARG;
+    if (!recv && p.recv_elems) return CHR_ERR_INVALID_ARG;  // a rank whose plan writes no output may pass NULL
     const size_t es = chr::dtype_size(dtype);
     const bool inplace = send == CHR_IN_PLACE;
     if (inplace && (mode == chr::MODE_INTER_LINEAR || mode == chr::MODE_INTRA_SCATTER)) return CHR_ERR_INVALID_ARG;
@@ -1193,7 +1193,7 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
     if (e != hipSuccess) return hip_code(e);
     std::vector<Bufs> B(n);
     for (int r = 0; r < n; ++r) {
-        if (!recvs[r]) return CHR_ERR_INVALID_ARG;
+        if (!recvs[r] && P[r].recv_elems) return CHR_ERR_INVALID_ARG;
         if ((e = g->acc[r].reserve(P[r].acc_elems * es, g->stream)) != hipSuccess) return hip_code(e);
         if ((e = g->stage[r].reserve(P[r].stage_elems * es, g->stream)) != hipSuccess) return hip_code(e);
         if (sends[r] == CHR_IN_PLACE && (mode == chr::MODE_INTER_LINEAR || mode == chr::MODE_INTRA_SCATTER))
@@ -1201,7 +1201,8 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
         const void* in = sends[r] != CHR_IN_PLACE ? sends[r]
                          : mode == chr::MODE_ALLGATHER ? (const void*)((char*)recvs[r] + (size_t)r * count * es)
                                                        : (const void*)recvs[r];
-        if ((P[r].send_elems && (!in || !is_device_ptr(in))) || !is_device_ptr(recvs[r])) return CHR_ERR_INVALID_ARG;
+        if ((P[r].send_elems && (!in || !is_device_ptr(in))) || (P[r].recv_elems && !is_device_ptr(recvs[r])))
+            return CHR_ERR_INVALID_ARG;
         B[r] = Bufs{(const char*)in, (char*)recvs[r], (char*)g->acc[r].p, (char*)g->stage[r].p, es};
     }
     int rc;

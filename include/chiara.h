@@ -417,7 +417,8 @@ int chr_intra_reduce_scatter_radix_batch(const void* send, void* recv, size_t re
  *             MPI_Datatype, MPI_Op, MPI_Comm, int b)   (inter_linear_reduce.cpp:11-73; phase 2).
  * send: niters chunks of IRC; for iteration i the lane's root node is i * b + lane (if < nnodes):
  * recv[0, IRC) = own chunk i reduced with the other nodes' chunk i in ascending node order.  Ranks
- * that are nobody's root leave recv untouched.  send may not be CHR_IN_PLACE (nor in the reference). */
+ * that are nobody's root leave recv untouched and may pass NULL (the reference never touches it there).
+ * send may not be CHR_IN_PLACE (nor in the reference). */
 int chr_inter_reduce_linear(const void* send, void* recv, size_t recvcount, chr_dtype dtype, chr_op op,
                             chr_comm* comm, int b);
 /* Replaces  int intra_scatter_radix_batch(char* sendbuf, int recvcount, MPI_Datatype,

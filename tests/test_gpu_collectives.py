@@ -599,7 +599,14 @@ def _run_phase(gu, group, mode, sends, k, b, rc, dtype, op, inplace=False, null_
         d_sendp = [gu.to_dev(s) for s in sends]
         if null_unread and mode == "isc":  # only node roots read their send buffer
             d_sendp = [d if (r % b) == (r // b) % b else None for r, d in enumerate(d_sendp)]
-    rc_ = group.phase_collective(PHASE_MODE[mode], d_sendp, d_recv, rc, DT[dtype], OP[op], k, b)
+    d_recvp = list(d_recv)
+    if null_unread and mode == "ilr" and not inplace:  # only the iterations' roots write recv
+        nnodes = n // b
+        for r in range(n):
+            node, lane = divmod(r, b)
+            if not any(i * b + lane == node for i in range(nnodes // b + (1 if nnodes % b else 0))):
+                d_recvp[r] = None
+    rc_ = group.phase_collective(PHASE_MODE[mode], d_sendp, d_recvp, rc, DT[dtype], OP[op], k, b)
     assert rc_ == 0, f"rc={rc_}"
     return [gu.from_dev(d, npdt, out_n) for d in d_recv]
 
