@@ -180,3 +180,22 @@ def test_reference_selftest_outputs_agree_with_the_oracle():
             want = po.phase_collective("irs", sends, "i32", "sum", k, b, rc)
             for r in range(n):
                 assert ints(lines[str(r)][-1]) == want[r].tolist(), (key, r)
+
+
+def test_buffers_each_rank_touches():
+    """What each rank's plan reads and writes (chr_plan_describe header): the scatter reads `send` on node
+    roots only and the linear reduce writes `recv` on iteration roots only -- the other ranks may pass NULL,
+    as the reference's own callers do (intra_scatter_radix_batch.cpp:213) or could (inter_linear_reduce.cpp
+    never touches recvbuf off the roots).  Phase 1 writes the leftover stage's chunk on lanes < nu only."""
+    n, b, rc = 12, 2, 5  # nnodes 6, nstages 3, nu 0; niters 3
+    for r in range(n):
+        h = ca.parse_plan(ca.describe_plan(ca.MODE_INTRA_SCATTER, n, r, 2, b, rc))["header"]
+        node, lane = divmod(r, b)
+        assert (h["send"], h["recv"]) == ((b * rc if lane == node % b else 0), rc)
+        h = ca.parse_plan(ca.describe_plan(ca.MODE_INTER_REDUCE_LINEAR, n, r, 2, b, rc))["header"]
+        root = any(i * b + lane == node for i in range(3))
+        assert (h["send"], h["recv"]) == (3 * rc * b, rc * b if root else 0)
+    n, b = 12, 4  # nnodes 3 < b: only a leftover stage, nu = 3
+    for r in range(n):
+        h = ca.parse_plan(ca.describe_plan(ca.MODE_INTRA_REDUCE_SCATTER, n, r, 2, b, rc))["header"]
+        assert (h["send"], h["recv"]) == (rc * n, rc * b if r % b < 3 else 0)
