@@ -111,7 +111,7 @@ def test_reference_mpich_reduce_scatter_harness_on_mi355x(tmp_path):
 
 def test_reference_allgather_harness_on_mi355x(tmp_path):
     """Fugaku_experiments/Allgather/main.cpp unchanged: k = 2..b-1, check_correctness vs MPI_Allgather."""
-    rows = _run("ref_harness_allgather", ["2", "--overwrite", "b=4", "base=16"], 8, tmp_path)
+    rows = _run("ref_harness_allgather", ["1", "--overwrite", "b=4", "base=16"], 8, tmp_path)
     ours = [r for r in rows if r["algorithm_name"] == "allgather_radix_batch"]
     assert ours and {r["k"] for r in ours} == {"2", "3"}
     assert all(r["is_correct"] == "1" for r in rows)
