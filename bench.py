@@ -8,9 +8,14 @@ Inputs are resident in HBM before the timed region; NSETS distinct (acc, in) pai
 cycled so the 2 GiB working set streams from HBM and not from the 256 MiB Infinity
 Cache.  value = algorithmic bytes (3 x 64 MiB per call) / wall time per step.
 
-N>1 (torchrun, one rank per GPU): the whole hierarchical allreduce over RCCL/xGMI
-(C4 geometry: fp32, 1 GiB per rank, k=4, b=4 at N=8; k=b=min(4,N) otherwise).
-value = aggregate input bytes reduced per second (N x 1 GiB per step / time).
+N>1 (one rank per GPU): the whole hierarchical allreduce over RCCL/xGMI (C4 geometry: fp32,
+1 GiB per rank, k=4, b=4 at N=8; k=b=min(4,N) otherwise).  value = aggregate input bytes
+reduced per second (N x 1 GiB per step / time).  `python bench.py --gpus N` starts its own N
+rank processes (torch.distributed.run as a child process, before anything touches the GPU),
+as the reference's run target starts its own ranks (testing/Makefile:83-87, `mpirun -np`);
+under an external launcher (WORLD_SIZE set) each process is one rank.  The whole N>1 line runs
+against a deadline (CHR_BENCH_DEADLINE_S, default 420 s from the launch): context entries that
+would start after it are recorded as {"skipped": "deadline"}, never the metric.
 
 Prints ONE JSON line on rank 0.
 """
@@ -38,7 +43,7 @@ SEED = 0xC41A5EED
 CPU_THREADS = 16             # the GPU box's CPU share per GPU (nproc shows the whole machine)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
@@ -50,6 +55,9 @@ def parse():
     p.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
     p.add_argument("--no-compare", action="store_true",
                    help="N>1: skip the same-run context lines (RCCL allreduce, MPICH ring on libchiara)")
+    p.add_argument("--phases", action="store_true",
+                   help="N>1: add CHiArA's stand-alone phases (phase 1, phase 2, the k-nomial scatter) to the "
+                        "context lines")
     p.add_argument("--e2e", action="store_true",
                    help="N=1: host-memory (PCIe-inclusive) staging cost of the reference's host-buffer contract")
     p.add_argument("--collective-kernels", action="store_true",
@@ -58,7 +66,7 @@ def parse():
     p.add_argument("--collective-kernels-small", action="store_true",
                    help="N=1: the same for the N=2 / N=4 lines' allreduces (1 GiB per rank) and C3's reduce-scatter "
                         "(2 ranks, 256 MiB send): the 2- and 4-leaf trees")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
 # ---- CPU baseline (rank 0, N=1 only; runs BEFORE the GPU is touched) ------------------------
@@ -522,6 +530,90 @@ def replay_rank_trees(ca, torch, dev, cdt, es, count, n, k, b, slices, recv_copi
             "achieved_GBps": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4)}
 
 
+# ---- N > 1: launching the ranks ----------------------------------------------------------------
+
+DEFAULT_DEADLINE_S = 420.0   # the whole N>1 line, from the launch (CHR_BENCH_DEADLINE_S overrides)
+KILL_GRACE_S = 300.0         # the launcher kills the rank group this long after the deadline
+
+
+def launch_command(argv, nproc, port):
+    """The child command that starts `nproc` rank processes of this script, one per GPU."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def plan_launch(args, argv, env, device_count, port=0):
+    """None when this process is the bench itself (one rank of an external launcher, or --gpus 1);
+    otherwise the command that starts --gpus rank processes.  More ranks than visible devices is an
+    error (never a silent fall-back to the one-GPU line), unless CHR_BENCH_VIRTUAL_HOSTS=1 rehearses
+    the N>1 path with ranks sharing a device."""
+    if "WORLD_SIZE" in env or args.gpus <= 1:
+        return None
+    if args.gpus > device_count and env.get("CHR_BENCH_VIRTUAL_HOSTS") != "1":
+        raise ValueError(f"--gpus {args.gpus}: only {device_count} GPU(s) visible; one rank per GPU "
+                         f"(CHR_BENCH_VIRTUAL_HOSTS=1 rehearses ranks sharing a GPU)")
+    return launch_command(argv, args.gpus, port)
+
+
+def free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def deadline_s(env=os.environ):
+    return float(env.get("CHR_BENCH_DEADLINE_S", DEFAULT_DEADLINE_S))
+
+
+def run_launcher(cmd):
+    """Run the rank group as a child (never exec: this process may not replace itself), forward rank
+    0's one JSON line to stdout, everything else to stderr, and return the group's exit status.  The
+    group gets the launch time, so every rank measures the deadline from the same instant."""
+    import signal
+
+    env = dict(os.environ, CHR_BENCH_T0=repr(time.time()))
+    limit = deadline_s(env) + KILL_GRACE_S
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, start_new_session=True)
+    try:
+        out, _ = proc.communicate(timeout=limit)
+    except subprocess.TimeoutExpired:
+        os.killpg(proc.pid, signal.SIGKILL)
+        out, _ = proc.communicate()
+        print(f"bench.py: rank group killed {limit:.0f} s after launch", file=sys.stderr)
+        return 124
+    lines = []
+    for ln in out.splitlines():
+        try:
+            obj = json.loads(ln)
+        except ValueError:
+            obj = None
+        if isinstance(obj, dict) and "metric" in obj:
+            lines.append(ln)
+        elif ln.strip():
+            print(ln, file=sys.stderr)
+    if lines:
+        emit(json.loads(lines[-1]))
+    return proc.returncode if proc.returncode is not None else 1
+
+
+class Deadline:
+    """The N>1 line's wall-clock budget.  Rank 0 decides and broadcasts, so every rank skips the same
+    context entries (a collective one rank skips and another runs would hang)."""
+
+    def __init__(self, dist, env=os.environ):
+        self.dist = dist
+        self.t_end = float(env.get("CHR_BENCH_T0", time.time())) + deadline_s(env)
+
+    def passed(self):
+        import torch
+
+        t = torch.tensor([1.0 if time.time() > self.t_end else 0.0], dtype=torch.float64)
+        self.dist.broadcast(t, 0)
+        return bool(t.item())
+
+
 # ---- N > 1: hierarchical allreduce over RCCL ---------------------------------------------------
 
 def bench_allreduce(args):
@@ -541,6 +633,7 @@ def bench_allreduce(args):
 
     # a rank that dies must not leave the others in a gloo barrier for gloo's default 30 minutes
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=900))
+    deadline = Deadline(dist)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     comm = ca.Comm.from_torch_distributed(device=local)
@@ -614,7 +707,10 @@ def bench_allreduce(args):
                     "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
                     "kernel": "chr::k_reduce_tree / k_reduce_vec (fused reductions inside the collective, busiest rank)",
                     "algorithmic_bytes_per_call": float(busiest[1]), "launches_per_call": int(busiest[2]),
-                    "kernel_ms_per_call": round(float(busiest[0]), 4)}
+                    "kernel_ms_per_call": round(float(busiest[0]), 4),
+                    # one GPU's own grids (one rank per GPU): the fixed per-grid cost shows directly
+                    "grids_per_call": int(busiest[2]),
+                    "avg_grid_us": round(float(busiest[0]) * 1e3 / max(1, int(busiest[2])), 2)}
     # bytes on the busiest directed link of this schedule (max over ranks; slicing only splits messages)
     if tuned is not None:
         sched = tuned[0]
@@ -629,14 +725,15 @@ def bench_allreduce(args):
     lb = torch.tensor([float(max(per_peer.values()) if per_peer else 0)], dtype=torch.float64)
     dist.all_reduce(lb, op=dist.ReduceOp.MAX)
     link_bytes = int(lb.item())
-    compare = None if args.no_compare else compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b,
-                                                         world, dev, metric_sched)
-    # the reference CPU+MPI path on this box's host cores, after every GPU timing (rank 0 runs
-    # it; the other ranks wait at the barrier)
+    # the reference CPU+MPI path on this box's host cores, after the metric's GPU timing and before
+    # the context entries, so the deadline can only cost context (rank 0 runs it; the other ranks
+    # wait at the barrier)
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline_collective(world, k, b, count, es)
     dist.barrier()
+    compare = None if args.no_compare else compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b,
+                                                         world, dev, metric_sched, deadline)
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(world * S * args.steps / el / 1e9, 2), "unit": "GB/s",
@@ -696,14 +793,17 @@ def _timed_max(torch, dist, fn, steps, warmup, comm=None):
     return float(t.item())
 
 
-def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, world, dev, metric_sched=None):
+def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, world, dev, metric_sched=None,
+                  deadline=None):
     """Context, not the metric: on the same buffers and ranks, (1) RCCL's own ncclAllReduce
     (torch.distributed nccl group), (2) the reference's MPICH ring baseline
     (testing/mpich_implementations/all_reduce/allreduce_ring.cpp) run on libchiara's executor and
     (3) the metric's own schedule with the reductions on the transfer stream (no overlap),
     (4) its arithmetic under the balanced, reference-route and exact (the reference's messages
-    end to end) schedules, (5) the flat schedule at pipeline depths 1, 2 and 8, (6) CHiArA's phases as
-    stand-alone collectives and (7) the other multi-GPU BASELINE configs, C3 and C5 (baseline_configs)."""
+    end to end) schedules, (5) the flat schedule at pipeline depths 1, 2 and 8, (6) with --phases, CHiArA's
+    phases as stand-alone collectives and (7) the other multi-GPU BASELINE configs, C3 and C5
+    (baseline_configs).  An entry that would start after the deadline is recorded as skipped."""
+    late = (lambda: False) if deadline is None else deadline.passed
     steps, warm = max(1, min(args.steps, 20)), 2
     S = count * (4 if dt == ca.FLOAT32 else 2)
     out = {"steps": steps}
@@ -714,11 +814,15 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
                 "ms_per_call": round(el / steps * 1e3, 4)}
 
     try:
+        if late():
+            raise TimeoutError("deadline")
         g = dist.new_group(backend="nccl")
         x = torch.empty(count, dtype=torch.float32 if dt == ca.FLOAT32 else torch.bfloat16, device=dev)
         x.view(torch.uint8).copy_(send)
         out["rccl_allreduce"] = entry(_timed_max(torch, dist, lambda: dist.all_reduce(x, group=g), steps, warm))
         dist.destroy_process_group(g)
+    except TimeoutError:
+        out["rccl_allreduce"] = {"skipped": "deadline"}
     except Exception as e:  # context only: never fail the metric line for it
         out["rccl_allreduce"] = {"error": str(e)[:200]}
 
@@ -726,6 +830,9 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
         """One context entry on libchiara; a failure (e.g. a timeout that aborted the communicator)
         is recorded in the line instead of failing the metric, and skips the entries after it."""
         if out.get("aborted"):
+            return
+        if late():
+            out[name] = {"skipped": "deadline"}
             return
         try:
             out[name] = entry(_timed_max(torch, dist, fn, steps, warm, comm))
@@ -773,7 +880,7 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
     # CHiArA's phases as stand-alone collectives (testing/custom_implementations/work_dir/reduce_scatter/), on
     # the same buffers, each reading the whole S-byte send buffer per rank: phase 1 (b = 2, k = 2), phase 2
     # (b = 2) and the reduce-scatter's k-nomial scatter (one group of all ranks, k = 2)
-    if world % 2 == 0:
+    if args.phases and world % 2 == 0:
         nn = world // 2
         niters = nn // 2 + (1 if nn % 2 else 0)
         rc_irs, rc_ilr, rc_isc = count // world, count // (niters * 2), count // world
@@ -785,8 +892,9 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
               lambda: ca.check(ca.intra_scatter_radix_batch(send, rc_isc, dt, recv, comm, 2, world)))
     if out.get("aborted"):
         return out
-    out["small_messages"] = small_messages(ca, torch, dist, comm, dt, k, b, world, dev, restore)
-    out.update(baseline_configs(args, ca, torch, dist, comm, world, dev, steps, warm))
+    out["small_messages"] = ({"skipped": "deadline"} if late() else
+                             small_messages(ca, torch, dist, comm, dt, k, b, world, dev, restore))
+    out.update(baseline_configs(args, ca, torch, dist, comm, world, dev, steps, warm, late))
     return out
 
 
@@ -827,7 +935,7 @@ def small_messages(ca, torch, dist, comm, dt, k, b, world, dev, current):
     return res
 
 
-def baseline_configs(args, ca, torch, dist, comm, world, dev, steps, warm):
+def baseline_configs(args, ca, torch, dist, comm, world, dev, steps, warm, late=lambda: False):
     """The other multi-GPU BASELINE configs at this world size, default schedule, same run:
     C3 (fp32 reduce-scatter, radix 2, 256 MiB send buffer; b = 1 and 2; next to it the four MPICH
     reduce-scatter baselines on the same buffers) and C5 (bf16 allreduce, b = 4 ("4x2": 4 ranks per
@@ -840,6 +948,10 @@ def baseline_configs(args, ca, torch, dist, comm, world, dev, steps, warm):
         r_rs = torch.empty(rc * 4, dtype=torch.uint8, device=dev)
         ca.check(ca.fill(s_rs, rc * world, ca.FLOAT32, 0, SEED, int(os.environ["RANK"]), stream=comm.stream))
         for b in sorted({1, 2} & {d for d in range(1, world + 1) if world % d == 0}):
+            if late():
+                out[f"c3_reduce_scatter_fp32_k2_b{b}_256MiB"] = {"skipped": "deadline"}
+                continue
+
             def rs():
                 ca.check(ca.reduce_scatter_radix_batch(s_rs, r_rs, rc, ca.FLOAT32, ca.SUM, comm, 2, b, async_op=True))
             el = _timed_max(torch, dist, rs, steps, warm, comm)
@@ -857,13 +969,18 @@ def baseline_configs(args, ca, torch, dist, comm, world, dev, steps, warm):
                                                                                        ca.SUM, comm, async_op=True)),
                          ("pairwise", lambda: ca.MPICH_reduce_scatter_pairwise(s_rs, r_rs, rc, ca.FLOAT32, ca.SUM, comm,
                                                                                async_op=True))):
+            if late():
+                out[f"c3_mpich_reduce_scatter_{name}_256MiB"] = {"skipped": "deadline"}
+                continue
             el = _timed_max(torch, dist, lambda: ca.check(fn()), steps, warm, comm)
             algbw = rc * world * 4 * steps / el / 1e9
             out[f"c3_mpich_reduce_scatter_{name}_256MiB"] = {
                 "algbw_GBps": round(algbw, 2), "busbw_GBps": round(algbw * (world - 1) / world, 2),
                 "ms_per_call": round(el / steps * 1e3, 4)}
         del s_rs, r_rs
-        if world == 8:
+        if world == 8 and late():
+            out["c5_allreduce_bf16_k4_b4_1GiB"] = {"skipped": "deadline"}
+        elif world == 8:
             cnt = (1 << 30) // 2
             s5 = torch.empty(cnt * 2, dtype=torch.uint8, device=dev)
             r5 = torch.empty(cnt * 2, dtype=torch.uint8, device=dev)
@@ -918,11 +1035,23 @@ def emit(line):
 def main():
     global OUT
     with _StdoutToStderr() as OUT:
-        _main()
+        rc = _main()
+    return rc or 0
 
 
 def _main():
-    args = parse()
+    argv = sys.argv[1:]
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # start the N rank processes before anything here touches the GPU (counting devices does not)
+        import torch
+
+        try:
+            cmd = plan_launch(args, argv, os.environ, torch.cuda.device_count(), free_port())
+        except ValueError as e:
+            print(f"bench.py: {e}", file=sys.stderr)
+            return 2
+        return run_launcher(cmd)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
         bench_allreduce(args)
@@ -941,4 +1070,4 @@ def _main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

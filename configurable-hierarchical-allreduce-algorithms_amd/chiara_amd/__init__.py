@@ -8,7 +8,7 @@ import os as _os
 
 # Multi-process RCCL on this driver needs dmabuf IPC (HSA_ENABLE_IPC_MODE_LEGACY=0).  Set the default
 # before torch (imported by _lib) or the HIP runtime load; a value the caller set is kept.
-# libchiara.so sets the same default from an ELF constructor for C callers (csrc/api.cpp).
+# C callers: the MPI shim and the harness mains set it themselves (csrc/api.cpp).
 _os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 from ._lib import EXPORTED, ChiaraError, lib  # noqa: F401  (fails loudly without libchiara.so)

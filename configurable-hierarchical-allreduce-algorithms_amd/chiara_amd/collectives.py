@@ -509,7 +509,7 @@ def parse_plan(text):
             wait = int(tok[3].split("=")[1]) if len(tok) > 3 and tok[3].startswith("wait=") else -1
             kv = dict(t.split("=", 1) for t in tok[4:] if "=" in t)
             deps = lambda v: [] if v in (None, "-") else [int(x) for x in v.split(",")]  # noqa: E731
-            cur = {"label": tok[2], "wait": wait, "deps": deps(kv.get("deps")), "ldeps": deps(kv.get("ldeps")),
+            cur = {"label": tok[2], "wait": wait, "deps": deps(kv.get("deps")),
                    "sends": [], "recvs": [], "allgathers": [], "post": []}
             plan["steps"].append(cur)
         elif tok[0] in ("send", "recv"):

@@ -9,15 +9,11 @@
 #include "chr_internal.hpp"
 #include "schedule.hpp"
 
-// Multi-process GPU work on this driver needs dmabuf IPC: without HSA_ENABLE_IPC_MODE_LEGACY=0,
-// RCCL's P2P/IPC transport between the processes of one node (and any CUDA-style tensor sharing)
-// fails with "hipIpcGetMemHandle: invalid argument".  The reference's harnesses reach this library
-// through the MPI shim with whatever environment mpiexec gives them (Fugaku_experiments/Allreduce/
-// main.cpp:111-113 is where control first arrives), so the library sets the default itself, from an
-// ELF constructor that runs at load time -- before any HIP call, since the HIP runtime initialises
-// lazily on the first one.  A value the caller set is kept (overwrite = 0); chr_comm_init_rank warns
-// under CHR_DEBUG if it is anything else.
-__attribute__((constructor)) static void chr_default_ipc_mode() { setenv("HSA_ENABLE_IPC_MODE_LEGACY", "0", 0); }
+// The library leaves the process environment alone.  Multi-process GPU work on this driver needs
+// dmabuf IPC (HSA_ENABLE_IPC_MODE_LEGACY=0); the entry paths that start ranks set that default
+// before any HIP call -- the MPI shim (csrc/shim/chiara_mpi_shim.cpp, for the reference's
+// harnesses), this package's own harness mains, the Python package and bench.py -- and
+// chr_comm_init_rank warns when a multi-rank communicator starts without it.
 
 extern "C" {
 

@@ -318,20 +318,6 @@ int default_overlap() {
     return v;
 }
 
-// CHR_DUAL_COMPUTE=1: local ops spread over two compute streams; default 0 (one).  Measured on the
-// local group's C4/C5 calls (whole-phase spans, 2 alternating rounds, profiles/r03/ab_dual/): one
-// stream 0.747-0.751 (C4) / 0.727-0.728 (C5) of the HBM peak, two streams 0.646-0.663 / 0.665-0.672:
-// two tree launches streaming 18 operands at once lose more HBM efficiency than the overlapped
-// ramp-up and drain win back, while back-to-back launches on one stream already overlap their
-// tails (no event between them).
-int default_dual() {
-    static const int v = [] {
-        const char* e = std::getenv("CHR_DUAL_COMPUTE");
-        return e ? (std::atoi(e) != 0) : 0;
-    }();
-    return v;
-}
-
 // CHR_LG_BATCH=0: a local group launches each virtual rank's trees separately; default 1
 int default_lg_batch() {
     static const int v = [] {
@@ -436,19 +422,6 @@ struct chr_comm {
     ncclComm_t nccl = nullptr;
     hipStream_t stream = nullptr;   // RCCL transfers; the call completes on this stream
     hipStream_t cstream = nullptr;  // local ops (reductions, copies) when overlapping
-    // A second compute stream (CHR_DUAL_COMPUTE=1, default off; created on first use): consecutive
-    // steps' local ops alternate between cstream and cstream2, so when two slices' evaluations are
-    // ready at once one launch's ramp-up could overlap the other's drain (measured a loss on one GPU:
-    // default_dual).  Not used by the pipelined host
-    // windows, which already run four streams (transfers, compute, copy-in, copy-out: the box's
-    // GPU_MAX_HW_QUEUES is 4, and a fifth stream would share a hardware queue with one of them), nor
-    // inside captured graphs (launch_graph).
-    hipStream_t cstream2 = nullptr;
-    int dual = default_dual();
-    hipError_t compute2() {
-        if (cstream2) return hipSuccess;
-        return hipStreamCreateWithFlags(&cstream2, hipStreamDefault);
-    }
     std::vector<hipEvent_t> events;  // pool: 2 per step
     hipEvent_t event(size_t i) {
         while (events.size() <= i) {
@@ -546,11 +519,6 @@ struct chr_local_group {
     // chr_local_group_profile: the fused reductions of every rank, timed as whole phases (from the
     // end of a step's copies to the join of its reductions) with HIP events on the group's stream
     ReduceProfile prof;
-    // The virtual ranks' local ops of one step are independent (each rank's own buffers): with
-    // CHR_DUAL_COMPUTE=1 they alternate between two compute streams, joined back into `stream` before
-    // the next step's copies; by default they run on `stream` (default_dual).
-    hipStream_t cs[2] = {nullptr, nullptr};
-    hipEvent_t ev_copy = nullptr, ev_done[2] = {nullptr, nullptr};
     int slices = 0;  // 0 = auto
     // chr_local_group_set_batching: the virtual ranks' tree evaluations of one step share launches
     // (CHR_LG_BATCH=0 turns it off; default on)
@@ -563,56 +531,38 @@ struct chr_local_group {
 
 namespace {
 
-int enqueue_plan(chr_comm* c, const Plan& p, const void* send, void* recv, int dtype, int op, bool* posted,
-                 bool allow_dual);
+int enqueue_plan(chr_comm* c, const Plan& p, const void* send, void* recv, int dtype, int op, bool* posted);
 
 // Enqueues a whole plan.  A failure after the first RCCL operation was posted aborts the
 // communicator: peers may already be waiting on this rank's messages.
-int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int dtype, int op, bool allow_dual = true) {
+int enqueue_rccl(chr_comm* c, const Plan& p, const void* send, void* recv, int dtype, int op) {
     if (c->failed) return CHR_ERR_ABORTED;
     bool posted = false;
-    const int rc = enqueue_plan(c, p, send, recv, dtype, op, &posted, allow_dual);
+    const int rc = enqueue_plan(c, p, send, recv, dtype, op, &posted);
     if (rc && posted) c->abort_comm();
     return rc;
 }
 
-int enqueue_plan(chr_comm* c, const Plan& p, const void* send, void* recv, int dtype, int op, bool* posted,
-                 bool allow_dual) {
+int enqueue_plan(chr_comm* c, const Plan& p, const void* send, void* recv, int dtype, int op, bool* posted) {
     const size_t es = chr::dtype_size(dtype);
     hipError_t e = c->reserve_scratch(p.acc_elems * es, p.stage_elems * es);
     if (e != hipSuccess) return hip_code(e);
     Bufs B{(const char*)send, (char*)recv, (char*)c->acc.p, (char*)c->stage.p, es};
     int rc;
     if ((rc = run_locals(p.pre, B, dtype, op, c->stream, &c->prof))) return rc;
-    // Transfers on c->stream, local ops on c->cstream (and c->cstream2: consecutive local steps
-    // alternate).  A step's transfers wait for the local ops of its comm_deps, a step's local ops for
-    // its own transfers and its local_deps (schedule.cpp analyze_deps): per compute stream, only the
-    // latest such step on it needs an event wait, since each stream runs in order.  The call ends
-    // with c->stream waiting for the last ops of each compute stream.
+    // Transfers on c->stream, local ops on c->cstream.  A step's transfers wait for the local ops of
+    // its comm_deps (schedule.cpp analyze_deps), a step's local ops for its own transfers.  The
+    // compute stream runs in order, so one wait on the latest dependency (comm_wait) covers every
+    // earlier one, and local ops never need to wait for each other.  The call ends with c->stream
+    // waiting for the last local ops.
     const bool two = c->overlap && c->cstream;
-    hipStream_t cs[2] = {c->cstream, nullptr};
-    if (two && allow_dual && c->dual && c->nranks > 1) {
-        if (hipError_t e2 = c->compute2(); e2 != hipSuccess) return hip_code(e2);
-        cs[1] = c->cstream2;
-    }
-    const int ncs = cs[1] ? 2 : 1;
-    std::vector<int8_t> on(p.steps.size(), -1);  // compute stream that ran each step's local ops
-    int xfer_waited[2] = {-1, -1}, last_on[2] = {-1, -1}, nlocal = 0;
-    std::vector<std::array<int, 2>> local_waited(ncs, std::array<int, 2>{-1, -1});
-    auto latest_on = [&](const std::vector<int>& deps, int k) {
-        for (size_t i = deps.size(); i-- > 0;)
-            if (on[(size_t)deps[i]] == k) return deps[i];
-        return -1;
-    };
+    int xfer_waited = -1, last_local = -1;
     for (size_t t = 0; t < p.steps.size(); ++t) {
         const chr::Step& s = p.steps[t];
-        for (int k = 0; two && k < ncs; ++k) {
-            const int d = latest_on(s.comm_deps, k);
-            if (d > xfer_waited[k]) {
-                hipEvent_t e = c->event(2 * (size_t)d + 1);
-                if (!e || (rc = hip_code(hipStreamWaitEvent(c->stream, e, 0)))) return e ? rc : CHR_ERR_HIP;
-                xfer_waited[k] = d;
-            }
+        if (two && s.comm_wait > xfer_waited) {
+            hipEvent_t ew = c->event(2 * (size_t)s.comm_wait + 1);
+            if (!ew || (rc = hip_code(hipStreamWaitEvent(c->stream, ew, 0)))) return ew ? rc : CHR_ERR_HIP;
+            xfer_waited = s.comm_wait;
         }
         const bool xfers = !s.sends.empty() || !s.recvs.empty() || !s.allgathers.empty();
         const bool timed = c->prof.on && xfers;
@@ -659,33 +609,20 @@ int enqueue_plan(chr_comm* c, const Plan& p, const void* send, void* recv, int d
         }
         hipEvent_t ec = c->event(2 * t), ed = c->event(2 * t + 1);
         if (!ec || !ed) return CHR_ERR_HIP;
-        const int k = nlocal++ % ncs;
-        hipStream_t cst = cs[k];
-        if ((rc = hip_code(hipEventRecord(ec, c->stream))) || (rc = hip_code(hipStreamWaitEvent(cst, ec, 0))))
+        if ((rc = hip_code(hipEventRecord(ec, c->stream))) || (rc = hip_code(hipStreamWaitEvent(c->cstream, ec, 0))))
             return rc;
-        for (int k2 = 0; k2 < ncs; ++k2) {  // the other compute stream's conflicting local ops
-            if (k2 == k) continue;
-            const int d = latest_on(s.local_deps, k2);
-            if (d > local_waited[k][k2]) {
-                hipEvent_t e = c->event(2 * (size_t)d + 1);
-                if (!e || (rc = hip_code(hipStreamWaitEvent(cst, e, 0)))) return e ? rc : CHR_ERR_HIP;
-                local_waited[k][k2] = d;
-            }
-        }
         {
             // RCCL's kernels run beside these launches: streaming reductions leave them room on every
             // CU (reduce_common.hpp kCoresidentWgPerCu)
             chr::CoresidentScope beside_rccl(c->nranks > 1);
-            if ((rc = run_locals(s.post, B, dtype, op, cst, &c->prof))) return rc;
+            if ((rc = run_locals(s.post, B, dtype, op, c->cstream, &c->prof))) return rc;
         }
-        if ((rc = hip_code(hipEventRecord(ed, cst)))) return rc;
-        on[t] = (int8_t)k;
-        last_on[k] = (int)t;
+        if ((rc = hip_code(hipEventRecord(ed, c->cstream)))) return rc;
+        last_local = (int)t;
     }
-    for (int k = 0; two && k < ncs; ++k)
-        if (last_on[k] > xfer_waited[k] &&
-            (rc = hip_code(hipStreamWaitEvent(c->stream, c->event(2 * (size_t)last_on[k] + 1), 0))))
-            return rc;
+    if (two && last_local > xfer_waited &&
+        (rc = hip_code(hipStreamWaitEvent(c->stream, c->event(2 * (size_t)last_local + 1), 0))))
+        return rc;
     return CHR_SUCCESS;
 }
 
@@ -704,9 +641,7 @@ int launch_graph(chr_comm* c, const Plan& p, const void* send, void* recv, int d
     if (it == c->gexec.end()) {
         if (!c->event(2 * p.steps.size() + 1)) return CHR_ERR_HIP;  // the event pool, created outside the capture
         if ((e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal)) != hipSuccess) return hip_code(e);
-        // one compute stream in a graph: graphs serve small, latency-bound calls, and a replay of a
-        // capture forked over two compute streams hung on the test box (4 RCCL ranks sharing one GPU)
-        const int rc = enqueue_rccl(c, p, send, recv, dtype, op, /*allow_dual=*/false);
+        const int rc = enqueue_rccl(c, p, send, recv, dtype, op);
         hipGraph_t g = nullptr;
         e = hipStreamEndCapture(c->stream, &g);
         if (rc || e != hipSuccess) {
@@ -759,7 +694,6 @@ int wait_call(chr_comm* c) {
             c->abort_comm();  // RCCL kernels poll the abort flag and exit
             (void)hipStreamSynchronize(c->stream);
             (void)hipStreamSynchronize(c->cstream);
-            if (c->cstream2) (void)hipStreamSynchronize(c->cstream2);
             return CHR_ERR_TIMEOUT;
         }
         if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
@@ -928,7 +862,7 @@ int run_host_windows(chr_comm* c, int sched, int slices, int mode, const void* i
             }
             const Plan& p = c->plan(mode, k, b, mode == chr::MODE_ALLREDUCE ? n * wj : wj, es, sched, slices);
             if (p.error) return p.error;
-            int r = enqueue_rccl(c, p, c->wsend[i].p, c->wrecv[i].p, dtype, op, /*allow_dual=*/false);
+            int r = enqueue_rccl(c, p, c->wsend[i].p, c->wrecv[i].p, dtype, op);
             if (r) return r;
             if ((e = hipEventRecord(c->ev_coll[i], c->stream)) != hipSuccess) return hip_code(e);
             if (!threaded) {  // this thread copies window j out itself
@@ -1206,9 +1140,8 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
         B[r] = Bufs{(const char*)in, (char*)recvs[r], (char*)g->acc[r].p, (char*)g->stage[r].p, es};
     }
     int rc;
-    // One phase of local ops of all ranks: on the two compute streams when the group has them, joined
-    // back into the group's stream; while profiling, bracketed by events on the group's stream.
-    const bool dual = g->cs[0] && g->cs[1];
+    // One phase of local ops of all ranks, on the group's stream; while profiling, bracketed by events
+    // on that stream.
     auto phase = [&](auto&& ops_of) -> int {
         bool any = false, reduces = false;
         for (int r = 0; r < n; ++r) {
@@ -1223,46 +1156,34 @@ int local_collective(chr_local_group* g, int mode, const void* const* sends, voi
             ev = g->prof.take();
             if ((rc = hip_code(hipEventRecord(ev.first, g->stream)))) return rc;
         }
-        if (!dual) {
-            // The virtual ranks' local ops of one step touch only their own buffers.  When every rank's
-            // ops are one batchable run of trees (the flat schedules' slice evaluations), all ranks'
-            // trees go to one launch_reduce_tree_multi call: one grid per 8 trees instead of one per
-            // rank, so the step pays the fixed cost of a launch -- ~4.5 us between back-to-back grids
-            // on one stream plus ~3-4 us of fill and drain (tools/reduce_microbench focus22/23,
-            // profiles/r03/launch_timeline/) -- once per 8 trees.  A real node has one rank per GPU
-            // and so one launch per rank per slice; rows measured there are the rank-alone replays of
-            // bench.py --collective-kernels.
-            std::vector<chr::TreeJob> jobs;
-            double bytes = 0;
-            bool merged = g->batch_ranks && n > 1;
-            for (int r = 0; r < n && merged; ++r) {
-                const std::vector<chr::LocalOp>& ops = ops_of(r);
-                if (!one_tree_run(ops, B[r])) {
-                    merged = false;
-                    break;
-                }
-                const size_t j0 = jobs.size();
-                bytes += tree_jobs(ops, 0, ops.size(), B[r], &jobs);
-                for (size_t x = 0; x < j0 && merged; ++x)  // earlier ranks' trees vs this rank's
-                    for (size_t y = j0; y < jobs.size() && merged; ++y)
-                        merged = !job_conflict(jobs[x], jobs[y], es) && !job_conflict(jobs[y], jobs[x], es);
+        // The virtual ranks' local ops of one step touch only their own buffers.  When every rank's
+        // ops are one batchable run of trees (the flat schedules' slice evaluations), all ranks'
+        // trees go to one launch_reduce_tree_multi call: one grid per 8 trees instead of one per
+        // rank, so the step pays the fixed cost of a launch -- ~4.5 us between back-to-back grids
+        // on one stream plus ~3-4 us of fill and drain (tools/reduce_microbench focus22/23,
+        // profiles/r03/launch_timeline/) -- once per 8 trees.  A real node has one rank per GPU
+        // and so one launch per rank per slice; rows measured there are the rank-alone replays of
+        // bench.py --collective-kernels.
+        std::vector<chr::TreeJob> jobs;
+        double bytes = 0;
+        bool merged = g->batch_ranks && n > 1;
+        for (int r = 0; r < n && merged; ++r) {
+            const std::vector<chr::LocalOp>& ops = ops_of(r);
+            if (!one_tree_run(ops, B[r])) {
+                merged = false;
+                break;
             }
-            if (merged) {
-                if ((rc = launch_tree_jobs(jobs, bytes, dtype, op, g->stream, &g->prof))) return rc;
-            } else {
-                for (int r = 0; r < n; ++r)
-                    if ((rc = run_locals(ops_of(r), B[r], dtype, op, g->stream, &g->prof))) return rc;
-            }
+            const size_t j0 = jobs.size();
+            bytes += tree_jobs(ops, 0, ops.size(), B[r], &jobs);
+            for (size_t x = 0; x < j0 && merged; ++x)  // earlier ranks' trees vs this rank's
+                for (size_t y = j0; y < jobs.size() && merged; ++y)
+                    merged = !job_conflict(jobs[x], jobs[y], es) && !job_conflict(jobs[y], jobs[x], es);
+        }
+        if (merged) {
+            if ((rc = launch_tree_jobs(jobs, bytes, dtype, op, g->stream, &g->prof))) return rc;
         } else {
-            if ((rc = hip_code(hipEventRecord(g->ev_copy, g->stream)))) return rc;
-            for (int k = 0; k < 2; ++k)
-                if ((rc = hip_code(hipStreamWaitEvent(g->cs[k], g->ev_copy, 0)))) return rc;
             for (int r = 0; r < n; ++r)
-                if ((rc = run_locals(ops_of(r), B[r], dtype, op, g->cs[r & 1], &g->prof))) return rc;
-            for (int k = 0; k < 2; ++k)
-                if ((rc = hip_code(hipEventRecord(g->ev_done[k], g->cs[k]))) ||
-                    (rc = hip_code(hipStreamWaitEvent(g->stream, g->ev_done[k], 0))))
-                    return rc;
+                if ((rc = run_locals(ops_of(r), B[r], dtype, op, g->stream, &g->prof))) return rc;
         }
         if (span) {
             if ((rc = hip_code(hipEventRecord(ev.second, g->stream)))) return rc;
@@ -1331,7 +1252,7 @@ int chr_get_unique_id(chr_unique_id* id) {
 
 int chr_comm_init_rank(chr_comm** out, int nranks, const chr_unique_id* id, int rank, int device) {
     if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks) return CHR_ERR_INVALID_ARG;
-    if (std::getenv("CHR_DEBUG")) {  // the library defaults it to 0 at load (api.cpp chr_default_ipc_mode)
+    {  // the entry paths set the default (api.cpp); a multi-rank communicator without it is worth a warning
         static bool warned = false;
         const char* ipc = std::getenv("HSA_ENABLE_IPC_MODE_LEGACY");
         if (!warned && nranks > 1 && (!ipc || std::strcmp(ipc, "0") != 0)) {
@@ -1378,10 +1299,8 @@ int chr_comm_destroy(chr_comm* c) {
     c->hrecv.release();
     c->host_pipeline_release();
     if (c->cstream) (void)hipStreamSynchronize(c->cstream);
-    if (c->cstream2) (void)hipStreamSynchronize(c->cstream2);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
-    if (c->cstream2) (void)hipStreamDestroy(c->cstream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return CHR_SUCCESS;
@@ -1411,7 +1330,6 @@ int chr_comm_abort(chr_comm* c) {
     c->abort_comm();
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->cstream) (void)hipStreamSynchronize(c->cstream);
-    if (c->cstream2) (void)hipStreamSynchronize(c->cstream2);
     return CHR_SUCCESS;
 }
 
@@ -1566,13 +1484,6 @@ int chr_local_group_create(chr_local_group** out, int nranks, int device) {
     g->prof.span = true;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&g->stream, hipStreamDefault);
-    if (e == hipSuccess && default_dual()) {
-        for (int k = 0; k < 2 && e == hipSuccess; ++k) {
-            e = hipStreamCreateWithFlags(&g->cs[k], hipStreamNonBlocking);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&g->ev_done[k], hipEventDisableTiming);
-        }
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&g->ev_copy, hipEventDisableTiming);
-    }
     if (e != hipSuccess) {
         chr_local_group_destroy(g.release());
         return hip_code(e);
@@ -1607,16 +1518,9 @@ int chr_local_group_destroy(chr_local_group* g) {
     if (!g) return CHR_SUCCESS;
     (void)hipSetDevice(g->device);
     if (g->stream) (void)hipStreamSynchronize(g->stream);
-    for (int k = 0; k < 2; ++k)
-        if (g->cs[k]) (void)hipStreamSynchronize(g->cs[k]);
     g->prof.release();
     for (auto& d : g->acc) d.release();
     for (auto& d : g->stage) d.release();
-    for (int k = 0; k < 2; ++k) {
-        if (g->ev_done[k]) (void)hipEventDestroy(g->ev_done[k]);
-        if (g->cs[k]) (void)hipStreamDestroy(g->cs[k]);
-    }
-    if (g->ev_copy) (void)hipEventDestroy(g->ev_copy);
     if (g->stream) (void)hipStreamDestroy(g->stream);
     delete g;
     return CHR_SUCCESS;

@@ -81,6 +81,7 @@ static void run_standard(const Options& o, Ctx& c, std::ofstream& csv, int count
 }
 
 int main(int argc, char** argv) {
+    setenv("HSA_ENABLE_IPC_MODE_LEGACY", "0", 0);  // dmabuf IPC for RCCL, before any HIP call (api.cpp)
     MPI_Init(&argc, &argv);
     Options o;
     Ctx c;

@@ -16,6 +16,8 @@
 // Prints one JSON line; exit status 0 = all agree.
 #include <mpi.h>
 
+#include <cstdlib>
+
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -117,6 +119,7 @@ bool same(const std::vector<char>& a, const std::vector<char>& b, const TypeCase
 }  // namespace
 
 int main(int argc, char** argv) {
+    setenv("HSA_ENABLE_IPC_MODE_LEGACY", "0", 0);  // dmabuf IPC for RCCL, before any HIP call (api.cpp)
     MPI_Init(&argc, &argv);
     MPI_Comm_set_errhandler(MPI_COMM_WORLD, MPI_ERRORS_RETURN);
     int rank, n;

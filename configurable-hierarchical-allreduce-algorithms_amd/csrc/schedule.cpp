@@ -716,11 +716,9 @@ static void analyze_deps(Plan& p) {
         }
         Step& st = p.steps[t];
         st.comm_deps.clear();
-        st.local_deps.clear();
         for (size_t u = 0; u < t; ++u) {
             if (pwr[u].empty() && prd[u].empty()) continue;
             if (conflict(pwr[u], prd[u], crd, cwr)) st.comm_deps.push_back((int)u);
-            if (conflict(pwr[u], prd[u], prd[t], pwr[t])) st.local_deps.push_back((int)u);
         }
         st.comm_wait = st.comm_deps.empty() ? -1 : st.comm_deps.back();
     }
@@ -975,11 +973,9 @@ std::string describe(const Plan& p) {
     for (size_t i = 0; i < p.steps.size(); ++i) {
         const Step& s = p.steps[i];
         o << "step " << i << " " << (s.label.empty() ? "-" : s.label) << " wait=" << s.comm_wait;
-        for (const auto* v : {&s.comm_deps, &s.local_deps}) {
-            o << (v == &s.comm_deps ? " deps=" : " ldeps=");
-            for (size_t j = 0; j < v->size(); ++j) o << (j ? "," : "") << (*v)[j];
-            if (v->empty()) o << "-";
-        }
+        o << " deps=";
+        for (size_t j = 0; j < s.comm_deps.size(); ++j) o << (j ? "," : "") << s.comm_deps[j];
+        if (s.comm_deps.empty()) o << "-";
         o << "\n";
         for (const Xfer& x : s.sends)
             o << "send " << x.peer << " " << buf_name(x.ref.buf) << " " << x.ref.off << " " << x.count << "\n";
@@ -1824,13 +1820,16 @@ void build_intra_rs(Plan& p, int n, int me, int k_in, int b, uint64_t rc) {
 void build_inter_linear(Plan& p, int n, int me, int b, uint64_t rc) {
     const int node = me / b, lane = me % b, nnodes = n / b, niters = nnodes / b + (nnodes % b ? 1 : 0);
     const uint64_t irc = rc * (uint64_t)b;
-    p.send_elems = (uint64_t)niters * irc;
+    // the send buffer this rank reads: up to the last chunk it sends or folds (0 for a lane that is
+    // the root of no iteration, :48, whose send buffer may be NULL)
+    p.send_elems = 0;
     Step& s = p.steps.emplace_back();
     s.label = "ilr";
     for (int i = 0; i < niters; ++i) {
         const int root_node = i * b + lane;
         if (root_node >= nnodes) continue;  // :48
         const Ref chunk{BUF_SEND, (uint64_t)i * irc};
+        p.send_elems = (uint64_t)(i + 1) * irc;
         if (node != root_node) {
             s.sends.push_back({root_node * b + lane, chunk, irc});
             continue;

@@ -73,12 +73,10 @@ struct Step {
     // `comm_wait` (the latest earlier step whose ops touch what these transfers read or
     // write); -1 = none.  Local ops always wait for their own step's transfers.
     int comm_wait = -1;
-    // Every earlier step whose local ops conflict (RAW / WAR / WAW) with this step's transfers
-    // (comm_deps; comm_wait is the last of them) or with this step's local ops (local_deps),
-    // ascending.  With local ops spread over two compute streams, stream order no longer implies
-    // that an earlier conflicting step has finished, so the executor waits for the latest of these
-    // on each stream.
-    std::vector<int> comm_deps, local_deps;
+    // Every earlier step whose local ops conflict (RAW / WAR / WAW) with this step's transfers,
+    // ascending; comm_wait is the last of them.  Local ops run in order on one compute stream, so
+    // they need no dependency list of their own.
+    std::vector<int> comm_deps;
 };
 
 enum Mode : int {

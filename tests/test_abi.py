@@ -4,6 +4,8 @@ import os
 import re
 import subprocess
 
+import pytest
+
 import chiara_amd as ca
 from chiara_amd import _lib
 
@@ -64,7 +66,7 @@ def test_reduce_tree_rejects_bad_args_without_device():
 
 def _ipc_env_after_dlopen(preset):
     """Loads libchiara.so into a fresh process (no torch, no chiara_amd) and reads the C-level
-    environment afterwards: the library's ELF constructor sets the dmabuf-IPC default."""
+    environment afterwards."""
     code = (
         "import ctypes, sys\n"
         f"ctypes.CDLL({_lib.LIB_PATH!r})\n"
@@ -79,9 +81,37 @@ def _ipc_env_after_dlopen(preset):
     return subprocess.check_output(["python3", "-c", code], env=env).decode().strip()
 
 
-def test_library_defaults_ipc_mode_at_load():
-    assert _ipc_env_after_dlopen(None) == "0"
-    assert _ipc_env_after_dlopen("1") == "1"  # the caller's value is kept
+def test_library_leaves_the_environment_alone():
+    """loading the library changes no process-wide setting (the entry paths set it)."""
+    assert _ipc_env_after_dlopen(None) == "UNSET"
+    assert _ipc_env_after_dlopen("1") == "1"
+
+
+def test_shim_entry_path_defaults_ipc_mode(tmp_path):
+    """The MPI shim, linked into a reference harness executable, sets the dmabuf-IPC default at program
+    load (before main, MPI_Init and any HIP call); a caller's value is kept.  Built here from the shim
+    and a two-line main, with the package Makefile's harness flags."""
+    import shutil
+
+    mpi_home = "/opt/conda"
+    if not os.path.exists(os.path.join(mpi_home, "include", "mpi.h")) or not shutil.which("g++"):
+        pytest.skip("MPICH headers or g++ absent")
+    pkg = _lib.PKG_ROOT
+    src = tmp_path / "probe.cpp"
+    src.write_text('#include <cstdio>\n#include <cstdlib>\nint main() { const char* v = '
+                   'std::getenv("HSA_ENABLE_IPC_MODE_LEGACY"); std::printf("%s\\n", v ? v : "UNSET"); }\n')
+    exe = tmp_path / "probe"
+    subprocess.check_call(["g++", "-O1", "-std=c++17", f"-I{REPO}/include", "-I/opt/rocm/include",
+                           f"-I{mpi_home}/include", "-D__HIP_PLATFORM_AMD__", "-o", str(exe), str(src),
+                           os.path.join(pkg, "csrc", "shim", "chiara_mpi_shim.cpp"),
+                           f"-L{os.path.dirname(_lib.LIB_PATH)}", "-lchiara", "-L/opt/rocm/lib", "-lamdhip64",
+                           f"{mpi_home}/lib/libmpi.so", f"-Wl,-rpath,{os.path.dirname(_lib.LIB_PATH)}",
+                           "-Wl,-rpath,/usr/lib/x86_64-linux-gnu", "-Wl,-rpath,/opt/rocm/lib",
+                           f"-Wl,-rpath,{mpi_home}/lib"])
+    env = {k: v for k, v in os.environ.items() if k != "HSA_ENABLE_IPC_MODE_LEGACY"}
+    assert subprocess.check_output([str(exe)], env=env).decode().strip() == "0"
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "1"
+    assert subprocess.check_output([str(exe)], env=env).decode().strip() == "1"
 
 
 def test_package_defaults_ipc_mode_before_torch():

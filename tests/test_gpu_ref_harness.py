@@ -221,17 +221,26 @@ def test_reference_selftests_on_mi355x(tmp_path, name, run):
     if not os.path.exists(exe) or not os.path.exists(MPIEXEC):
         pytest.skip("self-test binary or MPICH not present")
     n = run["nranks"]
-    cmd = [MPIEXEC, "-outfile-pattern", "out.%r"]
+    fn = selftest_util.shim_functions()[run["binary"]]
+    cmd = [MPIEXEC, "-outfile-pattern", "out.%r", "-errfile-pattern", "err.%r"]
     for r in range(n):
         if r:
             cmd.append(":")
         cmd += ["-n", "1", "-env", "NCCL_HOSTID", f"chiara-selftest-{r}", "-env", "NCCL_SOCKET_IFNAME", "lo",
-                "-env", "NCCL_IB_DISABLE", "1", exe] + run["args"]
+                "-env", "NCCL_IB_DISABLE", "1", "-env", "CHR_SHIM_TRACE", "1", exe] + run["args"]
     out = subprocess.run(cmd, cwd=tmp_path, capture_output=True, text=True, timeout=300)
-    assert out.returncode == 0, out.stderr[-3000:]
+    errs = {r: (tmp_path / f"err.{r}").read_text(encoding="utf-8") if (tmp_path / f"err.{r}").exists() else ""
+            for r in range(n)}
+    assert out.returncode == 0, out.stderr[-3000:] + "".join(errs.values())[-3000:]
     for r in range(n):
-        path = tmp_path / f"out.{r}"
-        got = selftest_util.normalize(path.read_text(encoding="utf-8") if path.exists() else "")
+        # the positive marker: this rank's calls went through the shim's definition of the function
+        # (CHR_SHIM_TRACE), not through the reference file's own, which the build only weakened
+        calls = selftest_util.shim_calls(errs[r])
+        assert calls is not None and calls[0] == r and calls[1].get(fn, 0) >= 1, (r, fn, errs[r][-2000:])
+        raw = (tmp_path / f"out.{r}").read_text(encoding="utf-8") if (tmp_path / f"out.{r}").exists() else ""
+        # the reference function's own DEBUG_MODE phase timers must be absent (they would mean its body ran)
+        assert not selftest_util.reference_phase_lines(raw), (r, selftest_util.reference_phase_lines(raw)[:3])
+        got = selftest_util.normalize(raw)
         assert got == run["lines"][str(r)], (r, got, run["lines"][str(r)])
     for fname, want in run.get("files", {}).items():
         text = (tmp_path / fname).read_text(encoding="utf-8")

@@ -422,22 +422,68 @@ def test_plans_match_pair_and_complex_goldens(golden_pairtypes, schedule):
 
 def test_plan_dependency_lists():
     """Every step lists all earlier steps whose local ops conflict with its transfers (comm_deps, the
-    last of which is comm_wait) or with its own local ops (local_deps): what the executor needs to
-    spread local ops over two compute streams.  Checked here on the flat C4 plan: the evaluation of
-    slice s reads only slice s's receives, so no local step depends on another, and allgather s
-    depends on exactly the evaluation of slice s."""
+    last of which is comm_wait): the executor's transfer stream waits on the latest of them, and the
+    one compute stream runs local ops in order.  Checked here on the flat C4 plan: the evaluation of
+    slice s reads only slice s's receives, and allgather s depends on exactly the evaluation of slice s."""
     p = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 8, 0, 4, 4, 1 << 24, 4))
     assert [st["wait"] for st in p["steps"]] == [-1, -1, 0, 1, 2, 3]
     assert [st["deps"] for st in p["steps"]] == [[], [], [0], [1], [2], [3]]
-    assert all(st["ldeps"] == [] for st in p["steps"])
     for sched in (ca.SCHEDULE_REFERENCE, ca.SCHEDULE_EXACT):
         for mode, count in ((ca.MODE_ALLREDUCE, 1 << 20), (ca.MODE_REDUCE_SCATTER, 1 << 17)):
             for rank in range(8):
                 q = ca.parse_plan(ca.describe_plan(mode, 8, rank, 4, 4, count, 2, sched))
                 for t, st in enumerate(q["steps"]):
-                    assert st["deps"] == sorted(st["deps"]) and all(d < t for d in st["deps"] + st["ldeps"])
+                    assert st["deps"] == sorted(st["deps"]) and all(d < t for d in st["deps"])
                     assert st["wait"] == (st["deps"][-1] if st["deps"] else -1)
-                    assert all(q["steps"][d]["post"] for d in st["deps"] + st["ldeps"])
-    # the reference route's recexch phases fold into the same region step after step: local chains
-    r = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, 16, 0, 2, 16, 1 << 16, 1, ca.SCHEDULE_REFERENCE))
-    assert any(st["ldeps"] for st in r["steps"])
+                    assert all(q["steps"][d]["post"] for d in st["deps"])
+
+
+def _regions(op):
+    """(buffer space, lo, hi) read and written by one parsed local op; SEND and RECV share a space
+    (MPI_IN_PLACE makes them the same memory)."""
+    sp = lambda b: "RECV" if b == "SEND" else b  # noqa: E731
+    kind = op[0]
+    cnt = op[3]
+    if kind == "copy2d":
+        rows, dp, spp = op[4]
+        return ([(sp(op[2][0]), op[2][1] + r * spp, op[2][1] + r * spp + cnt) for r in range(rows)],
+                [(sp(op[1][0]), op[1][1] + r * dp, op[1][1] + r * dp + cnt) for r in range(rows)])
+    rd = [(sp(op[2][0]), op[2][1], op[2][1] + cnt)] + [(sp(x[0]), x[1], x[1] + cnt) for x in op[4]] \
+        if kind in ("reduce", "reduce_sw", "tree") else [(sp(op[2][0]), op[2][1], op[2][1] + cnt)]
+    wr = [(sp(op[1][0]), op[1][1], op[1][1] + cnt)]
+    return rd, wr
+
+
+def test_plan_dependencies_cover_in_place_aliasing():
+    """under CHR_IN_PLACE the SEND and RECV regions are one buffer.  For every schedule and
+    a spread of geometries, a step's transfers must list (in deps) every earlier step whose local ops
+    write memory those transfers read or write, or read memory they write -- with SEND and RECV
+    compared in one address space.  Missing one would let the transfer stream race the compute stream."""
+    bad = []
+    for sched in (ca.SCHEDULE_REFERENCE, ca.SCHEDULE_BALANCED, ca.SCHEDULE_FLAT, ca.SCHEDULE_EXACT,
+                  ca.SCHEDULE_FLAT_AG, ca.SCHEDULE_FLAT_SEQ):
+        for mode, count in ((ca.MODE_ALLREDUCE, 3 << 12), (ca.MODE_REDUCE_SCATTER, 3 << 9)):
+            for n, k, b in ((8, 4, 4), (8, 2, 2), (6, 3, 3), (4, 2, 4)):
+                for rank in range(n):
+                    q = ca.parse_plan(ca.describe_plan(mode, n, rank, k, b, count - count % n, 2, sched))
+                    steps = q["steps"]
+                    rw = []
+                    for st in steps:
+                        rd, wr = [], []
+                        for op in st["post"]:
+                            r_, w_ = _regions(op)
+                            rd += r_
+                            wr += w_
+                        rw.append((rd, wr))
+                    sp = lambda b_: "RECV" if b_ == "SEND" else b_  # noqa: E731
+                    for t, st in enumerate(steps):
+                        crd = [(sp(x[1][0]), x[1][1], x[1][1] + x[2]) for x in st["sends"]]
+                        cwr = [(sp(x[1][0]), x[1][1], x[1][1] + x[2]) for x in st["recvs"]]
+                        for u in range(t):
+                            rd, wr = rw[u]
+                            hit = any(a[0] == c[0] and a[1] < c[2] and c[1] < a[2]
+                                      for a in wr for c in crd + cwr) or \
+                                any(a[0] == c[0] and a[1] < c[2] and c[1] < a[2] for a in rd for c in cwr)
+                            if hit and u not in st["deps"]:
+                                bad.append((sched, mode, n, k, b, rank, t, u))
+    assert not bad, bad[:5]

@@ -60,3 +60,72 @@ def test_build_recipe_and_gpu_runs_match_the_goldens():
     keys = re.findall(r'"([^"]+)"', gpu_runs)
     assert keys and all(k in runs for k in keys)
     assert {runs[k]["binary"] for k in keys} == built  # one GPU run per main
+
+
+# ---- the shim-linked self-test binaries really bind to the shim -------------------
+
+import re  # noqa: E402
+import shutil  # noqa: E402
+import subprocess  # noqa: E402
+
+import pytest  # noqa: E402
+
+REF_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref")
+_CALL = re.compile(r"\bcall\s+[0-9a-f]+\s+<([^>]+)>")
+
+
+def _defined(exe, fn):
+    """Defined text symbols of `exe` for the C++ function `fn` (mangled prefix _Z<len><fn>)."""
+    out = subprocess.run(["nm", exe], capture_output=True, text=True, check=True).stdout
+    pre = f"_Z{len(fn)}{fn}"
+    return [f[2] for f in (ln.split() for ln in out.splitlines()) if len(f) == 3 and f[1] in "TtWw"
+            and f[2].startswith(pre)]
+
+
+def _calls(exe, sym):
+    out = subprocess.run(["objdump", "-d", "--no-show-raw-insn", f"--disassemble={sym}", exe], capture_output=True,
+                         text=True, check=True).stdout
+    return _CALL.findall(out)
+
+
+def _reaches_libchiara(exe, sym, depth=2):
+    """True when `sym`'s body -- or a function it calls directly inside the binary, to `depth` levels --
+    calls one of libchiara's chr_* entry points through the PLT."""
+    calls = _calls(exe, sym)
+    if any(c.startswith("chr_") and c.endswith("@plt") for c in calls):
+        return True
+    return depth > 0 and any(_reaches_libchiara(exe, c, depth - 1) for c in calls
+                             if "@plt" not in c and "+" not in c)
+
+
+def _binding(exe, fn):
+    syms = _defined(exe, fn)
+    strong = [s for s in syms if s in _strong_text(exe)]
+    return strong, bool(strong) and len(strong) == 1 and _reaches_libchiara(exe, strong[0])
+
+
+def _strong_text(exe):
+    out = subprocess.run(["nm", exe], capture_output=True, text=True, check=True).stdout
+    return {f[2] for f in (ln.split() for ln in out.splitlines()) if len(f) == 3 and f[1] == "T"}
+
+
+def _need_tools():
+    if not (shutil.which("nm") and shutil.which("objdump")):
+        pytest.skip("binutils absent")
+
+
+@pytest.mark.parametrize("name", sorted(selftest_util.shim_functions()))
+def test_selftest_binary_binds_function_to_shim(name):
+    """Each oracle/_ref/selftest_<name> defines the replaced function exactly once, as a global text symbol,
+    and that definition calls into libchiara (chr_*@plt) -- so its main, whose call is a relocation against
+    the symbol (-fno-inline), runs the shim.  The reference-only build (selftest_<name>_mpi, the negative
+    control) defines it too, and never reaches libchiara: the check can fail."""
+    _need_tools()
+    fn = selftest_util.shim_functions()[name]
+    exe, ctl = os.path.join(REF_DIR, f"selftest_{name}"), os.path.join(REF_DIR, f"selftest_{name}_mpi")
+    if not os.path.exists(exe) or not os.path.exists(ctl):
+        pytest.skip("self-test binaries not built (oracle/selftests.sh, container-only)")
+    strong, ok = _binding(exe, fn)
+    assert ok, (name, fn, strong)
+    strong_ctl, ok_ctl = _binding(ctl, fn)
+    assert len(strong_ctl) == 1 and not ok_ctl, (name, strong_ctl)

@@ -18,6 +18,8 @@
 #   sweep      bench.py --sweep: 1 KiB .. 1 GiB buckets, m = 1/3/7, fp32 + bf16 (table in sweep.json.err)
 #   probe      tools/mstream_probe.py $PROBE_ARGS               -> mstream_probe.jsonl
 #   tree       tools/tree_bench.py $TREE_ARGS                   -> tree_bench.json
+#   launch     bench.py --gpus ${N:-2} with no external launcher (bench.py starts its own ranks;
+#              virtual hosts: ranks share the one GPU, socket transport) -> bench_launch_n${N}.json
 #   rehearse   the N>1 bench line with ${N:-4} ranks sharing the one GPU (socket transport;
 #              exercises the code path, its GB/s mean nothing)  -> bench_n${N}_rehearsal.json
 # Everything lands under gpurun_out/.
@@ -62,6 +64,10 @@ for step in "$@"; do
   e2e) run 300 e2e.json python bench.py --e2e --no-cpu-baseline ;;
   probe) run 400 mstream_probe.jsonl python tools/mstream_probe.py ${PROBE_ARGS:-} ;;
   tree) run 400 tree_bench.json python tools/tree_bench.py ${TREE_ARGS:-} ;;
+  launch)
+    n=${N:-2}
+    CHR_BENCH_VIRTUAL_HOSTS=1 CHR_BENCH_DEADLINE_S=${DEADLINE:-240} run 600 "bench_launch_n${n}.json" \
+      python bench.py --gpus "$n" --steps 3 --warmup 1 --count $((1 << 21)) ;;
   rehearse)
     n=${N:-4}
     CHR_BENCH_VIRTUAL_HOSTS=1 run 600 "bench_n${n}_rehearsal.json" python -m torch.distributed.run --nnodes=1 \
