@@ -14,7 +14,7 @@ reduced per second (N x 1 GiB per step / time).  `python bench.py --gpus N` star
 rank processes (torch.distributed.run as a child process, before anything touches the GPU),
 as the reference's run target starts its own ranks (testing/Makefile:83-87, `mpirun -np`);
 under an external launcher (WORLD_SIZE set) each process is one rank.  The whole N>1 line runs
-against a deadline (CHR_BENCH_DEADLINE_S, default 420 s from the launch): context entries that
+against a deadline (CHR_BENCH_DEADLINE_S, default 240 s from the launch): context entries that
 would start after it are recorded as {"skipped": "deadline"}, never the metric.
 
 Prints ONE JSON line on rank 0.
@@ -532,8 +532,8 @@ def replay_rank_trees(ca, torch, dev, cdt, es, count, n, k, b, slices, recv_copi
 
 # ---- N > 1: launching the ranks ----------------------------------------------------------------
 
-DEFAULT_DEADLINE_S = 420.0   # the whole N>1 line, from the launch (CHR_BENCH_DEADLINE_S overrides)
-KILL_GRACE_S = 300.0         # the launcher kills the rank group this long after the deadline
+DEFAULT_DEADLINE_S = 240.0   # the whole N>1 line, from the launch (CHR_BENCH_DEADLINE_S overrides)
+KILL_GRACE_S = 180.0         # the launcher kills the rank group this long after the deadline
 
 
 def launch_command(argv, nproc, port):

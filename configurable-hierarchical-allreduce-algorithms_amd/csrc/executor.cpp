@@ -431,7 +431,7 @@ struct chr_comm {
         }
         return events[i];
     }
-    DevBuf acc, stage, hsend, hrecv;
+    DevBuf acc, stage, hsend, hrecv, flag;  // flag: agree_min's 4-byte exchange
     ReduceProfile prof;
     std::map<PlanKey, std::unique_ptr<Plan>> plans;
 
@@ -758,15 +758,37 @@ int wait_event_poll(hipEvent_t ev, int timeout_ms) {
 // wait on ev_coll), the copy-out thread "window j's D2H is enqueued" (a later collective may then
 // wait on ev_out before overwriting that window's device buffer).  Returns -1 when the call is
 // not split (one window would cover it).
-int run_host_windows(chr_comm* c, int sched, int slices, int mode, const void* input, void* recv, size_t count,
-                     int dtype, int op, int k, int b) {
-    if (c->host_window_mib <= 0 || (mode != chr::MODE_ALLREDUCE && mode != chr::MODE_REDUCE_SCATTER)) return -1;
-    const size_t es = chr::dtype_size(dtype), n = (size_t)c->nranks;
+// One int per rank, the minimum over the ranks, on the communicator stream (blocking, under the
+// timeout).  A failure aborts the communicator: the peers are inside the same collective.
+int agree_min(chr_comm* c, int mine, int* all) {
+    int rc = hip_code(c->flag.reserve(sizeof(int), c->stream));
+    int* d = (int*)c->flag.p;
+    if (!rc) rc = hip_code(hipMemcpyAsync(d, &mine, sizeof(int), hipMemcpyHostToDevice, c->stream));
+    if (!rc) rc = nccl_code(ncclAllReduce(d, d, 1, ncclInt32, ncclMin, c->nccl, c->stream));
+    if (!rc) rc = hip_code(hipMemcpyAsync(all, d, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    if (!rc) rc = wait_call(c);
+    else c->abort_comm();
+    return rc;
+}
+
+// Elements per block of one host window, or 0 when the call is not split (one window would cover
+// it, or windows are off): a function of the communicator's setting and the arguments only.
+size_t host_window_elems(const chr_comm* c, int mode, size_t count, size_t es) {
+    if (c->host_window_mib <= 0 || (mode != chr::MODE_ALLREDUCE && mode != chr::MODE_REDUCE_SCATTER)) return 0;
+    const size_t n = (size_t)c->nranks;
     const size_t block = mode == chr::MODE_ALLREDUCE ? count / n : count;  // recvcount
-    if (mode == chr::MODE_ALLREDUCE && block * n != count) return -1;      // the plan reports the error
+    if (mode == chr::MODE_ALLREDUCE && block * n != count) return 0;       // the plan reports the error
     size_t w = ((size_t)c->host_window_mib << 20) / (n * es);
     w -= w % 64;  // windows start 256 B-aligned within each block when the block is
-    if (w == 0 || w >= block) return -1;
+    return w == 0 || w >= block ? 0 : w;
+}
+
+int run_host_windows(chr_comm* c, int sched, int slices, int mode, const void* input, void* recv, size_t count,
+                     int dtype, int op, int k, int b) {
+    const size_t es = chr::dtype_size(dtype), n = (size_t)c->nranks;
+    const size_t w = host_window_elems(c, mode, count, es);
+    if (w == 0) return -1;
+    const size_t block = mode == chr::MODE_ALLREDUCE ? count / n : count;  // recvcount
     hipError_t e = c->host_pipeline_init();
     if (e != hipSuccess) return hip_code(e);
     int rc;
@@ -918,13 +940,20 @@ int run_collective(chr_comm* c, int sched, int slices, int mode, const void* sen
     hipError_t e = hipSetDevice(c->device);
     if (e != hipSuccess) return hip_code(e);
     const bool dev_out = is_device_ptr(recv), dev_in = p.send_elems ? is_device_ptr(input) : dev_out;
-    // Pipelined staging splits a call into window collectives.  Whether it does is a function of the
-    // communicator's setting and the call's arguments only -- never of where this rank's buffers
-    // live -- so every rank issues the same number of RCCL collectives even when one passes host
-    // memory and another device memory (device buffers are then staged device to device).
-    if (sync) {
-        const int rc = run_host_windows(c, sched, slices, mode, input, recv, count, dtype, op, k, b);
-        if (rc >= 0) return rc;
+    // Pipelined staging splits a call into window collectives.  Every rank must issue the same
+    // collectives, so whether a call is split cannot depend on where this rank's buffers live alone:
+    // a call large enough to split (host_window_elems) first agrees with one 4-byte
+    // ncclAllReduce(min) whether every rank is device-resident.  If so, no rank windows (the direct,
+    // graph-capable path, which the AUTO tuner also times); otherwise every rank does, a device
+    // buffer then being staged device to device.  The exchange costs one small collective on calls of
+    // at least one window (32 MiB per rank by default).
+    if (sync && host_window_elems(c, mode, count, es)) {
+        if (c->failed) return CHR_ERR_ABORTED;
+        int all_dev = 0;
+        int rc = agree_min(c, dev_in && dev_out, &all_dev);
+        if (rc) return rc;
+        if (!all_dev && (rc = run_host_windows(c, sched, slices, mode, input, recv, count, dtype, op, k, b)) >= 0)
+            return rc;
     }
     if (dev_in && dev_out) {
         int rc = c->graphs && !c->prof.on ? launch_graph(c, p, input, recv, dtype, op)
@@ -977,18 +1006,6 @@ int run_collective(chr_comm* c, int sched, int slices, int mode, const void* sen
 // RCCL operations aborts the communicator (enqueue_rccl); peers with a timeout (chr_comm_set_timeout)
 // then return an error instead of waiting.
 constexpr int TUNE_REPS = 3;
-
-int agree_min(chr_comm* c, int mine, int* all) {
-    int* d = nullptr;
-    int rc = hip_code(hipMalloc(&d, sizeof(int)));
-    if (!rc) rc = hip_code(hipMemcpyAsync(d, &mine, sizeof(int), hipMemcpyHostToDevice, c->stream));
-    if (!rc) rc = nccl_code(ncclAllReduce(d, d, 1, ncclInt32, ncclMin, c->nccl, c->stream));
-    if (!rc) rc = hip_code(hipMemcpyAsync(all, d, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    if (!rc) rc = wait_call(c);
-    else c->abort_comm();
-    (void)hipFree(d);
-    return rc;
-}
 
 int tune_schedule(chr_comm* c, int mode, const void* send, void* recv, size_t count, int dtype, int op, int k, int b,
                   int* sched_out, int* slices_out) {
@@ -1297,6 +1314,7 @@ int chr_comm_destroy(chr_comm* c) {
     c->stage.release();
     c->hsend.release();
     c->hrecv.release();
+    c->flag.release();
     c->host_pipeline_release();
     if (c->cstream) (void)hipStreamSynchronize(c->cstream);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);

@@ -88,3 +88,34 @@ def test_deadline_agreed_over_ranks(monkeypatch):
         assert d.passed()
     finally:
         dist.destroy_process_group()
+
+
+def _deadline_worker(rank, world, port, q):
+    import time
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # rank 0 is past its deadline, rank 1 is not: both must take rank 0's decision
+        t0 = time.time() - (100 if rank == 0 else 0)
+        d = bench.Deadline(dist, {"CHR_BENCH_T0": repr(t0), "CHR_BENCH_DEADLINE_S": "50"})
+        q.put((rank, d.passed()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_deadline_decision_is_rank0s_world2():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = bench.free_port()
+    procs = [ctx.Process(target=_deadline_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}

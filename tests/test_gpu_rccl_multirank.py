@@ -655,13 +655,33 @@ def _host_pipeline_worker(rank, world, port, q):
                                                   ("rs", "f32", 70000, True, ca.SCHEDULE_EXACT),
                                                   ("ar", "i32", 65536 * 3, False, ca.SCHEDULE_FLAT_SEQ),
                                                   ("ar", "f32", 131075 * 2, "pinned", ca.SCHEDULE_FLAT),
-                                                  ("rs", "f32", 300007, "pinned", ca.SCHEDULE_FLAT)):
+                                                  ("rs", "f32", 300007, "pinned", ca.SCHEDULE_FLAT),
+                                                  # the ranks agree on residency before windowing --
+                                                  # rank 0 device-resident, the others host (all window), and
+                                                  # every rank device-resident (none windows: the direct path)
+                                                  ("ar", "f32", 300001, "dev0", ca.SCHEDULE_FLAT),
+                                                  ("rs", "f32", 250001, "devall", ca.SCHEDULE_FLAT),
+                                                  ("ar", "f32", 300001, "devall", ca.SCHEDULE_FLAT)):
             comm.set_schedule(sched)
             cdt = {"f32": ca.FLOAT32, "bf16": ca.BFLOAT16, "i32": ca.INT32}[dtype]
             npdt = po.NP_DTYPES[dtype]
             n_in = rc_ * world
             allx = [po.fill(n_in, dtype, 0, 555, r) for r in range(world)]
             x = allx[rank].copy()
+            dev = inplace == "devall" or (inplace == "dev0" and rank == 0)
+            if inplace in ("dev0", "devall"):
+                inplace = False
+            if dev:  # device-resident buffers on this rank
+                dx = torch.from_numpy(x).cuda()
+                dout = torch.zeros(n_in if mode == "ar" else rc_, dtype=dx.dtype, device=dx.device)
+                fn = ca.all_reduce_radix_batch if mode == "ar" else ca.reduce_scatter_radix_batch
+                rc = fn(dx, dout, n_in if mode == "ar" else rc_, cdt, ca.SUM, comm, 2, 2)
+                want = (po.allreduce_radix_batch if mode == "ar" else po.reduce_scatter_radix_batch)(
+                    allx, 2, 2, dtype, "sum")[rank]
+                got = dout.cpu().numpy()[:want.size]
+                if rc != 0 or got.tobytes() != want.tobytes():
+                    bad.append((mode, dtype, rc_, "device", rc))
+                continue
             if inplace == "pinned":  # page-locked buffers (the D2H thread then overlaps async copies)
                 inplace = False
                 x = torch.from_numpy(x).pin_memory().numpy()
