@@ -1649,10 +1649,178 @@ static void focus19_vec(size_t bytes, int sets) {
     free_sets(S);
 }
 
+
+// ---- focus24: the C2 launch's timeline, and a persistent variant that balances the XCDs -------
+// The product's C2 body (k_reduce_vec<f32, SUM, 1, 4, nt, ACC0, 64>, 12 per CU, 256 KiB XCD runs)
+// with each workgroup's start and end stamped (as focus22).  The hardware hands every XCD exactly
+// 1/8 of a grid's workgroups, so an XCD that streams slower finishes last and the others idle: the
+// tail.  PERSIST: a grid of resident workgroups that take runs of R trips from a per-launch counter
+// (one vector atomic per run, the next run's index fetched while the current run streams), so the
+// XCDs share the work until it runs out.  Counters are one per launch, zeroed once up front.
+template <bool PERSIST, int R>
+__global__ __launch_bounds__(64) void k_c2_stamped(chr::VecArgs a, unsigned* ctr, unsigned long long* st) {
+    constexpr int U = 4, BL = 64;
+    const unsigned long long t0 = wall_clock64();
+    chr::u32x4* const out = a.out;
+    const chr::u32x4* const accp = a.acc;
+    const chr::u32x4* const in0 = a.ins[0];
+    const size_t nvec = a.nvec;
+    const uint32_t ntrips = (uint32_t)(nvec / (BL * U));
+    auto body = [&](size_t trip) {
+        const size_t base = trip * BL * U + threadIdx.x;
+        chr::u32x4 acc[U], x[U];
+        acc[0] = chr::ld<false>(&accp[base]);
+#pragma unroll
+        for (int u = 1; u < U; ++u) acc[u] = chr::ld<true>(&accp[base + (size_t)u * BL]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = chr::ld<true>(&in0[base + (size_t)u * BL]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] = chr::apply_vec<CHR_FLOAT32, CHR_SUM>(x[u], acc[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) chr::st<true>(&out[base + (size_t)u * BL], acc[u]);
+    };
+    if constexpr (!PERSIST) {
+        chr::pin_sgpr(out, accp, nvec, a.xrun, a.xfull);
+        chr::pin_sgpr(in0);
+        const size_t trip = chr::xcd_trip(blockIdx.x, a.xfull, a.xrun);
+        if ((trip + 1) * BL * U <= nvec) body(trip);
+    } else {
+        const uint32_t nruns = (ntrips + R - 1) / R;
+        auto grab = [&]() -> uint32_t {
+            uint32_t v = 0;
+            if (threadIdx.x == 0) v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+        };
+        uint32_t run = grab();
+        while (run < nruns) {
+            const uint32_t next = grab();
+            for (int r = 0; r < R; ++r) {
+                const uint32_t trip = run * R + r;
+                if (trip < ntrips) body(trip);
+            }
+            run = next;
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long t1 = wall_clock64();
+    if (threadIdx.x == 0) {
+        st[3 * (size_t)blockIdx.x] = t0;
+        st[3 * (size_t)blockIdx.x + 1] = t1;
+        st[3 * (size_t)blockIdx.x + 2] = __smid();
+    }
+}
+
+template <bool PERSIST, int R>
+static void focus24_one(Sets& S, size_t nvec, int sets, int cap, unsigned pgrid, int nlaunch, const char* label) {
+    constexpr int U = 4, BL = 64;
+    const unsigned trips = (unsigned)(nvec / (BL * U));
+    const unsigned grid = PERSIST ? pgrid : trips;
+    uint32_t cs = 0;
+    while (((size_t)2 << cs) * (BL * U * 16) <= (size_t)256 * 1024 && cs < 16) ++cs;
+    unsigned long long* st = nullptr;
+    unsigned* ctr = nullptr;
+    const int total = nlaunch + 4;
+    CK(hipMalloc(&st, 3 * (size_t)grid * total * sizeof(unsigned long long)));
+    CK(hipMalloc(&ctr, total * sizeof(unsigned)));
+    CK(hipMemset(ctr, 0, total * sizeof(unsigned)));
+    int khz = 0;
+    CK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0));
+    const double us_per_tick = 1e3 / khz;
+    const unsigned lds = lds_for_cap(cap);
+    auto launch = [&](int i) {
+        auto& b = S.bufs[i % sets];
+        chr::VecArgs v{};
+        v.out = (chr::u32x4*)b[0];
+        v.acc = (const chr::u32x4*)b[0];
+        v.ins[0] = (const chr::u32x4*)b[1];
+        v.nvec = nvec;
+        v.xrun = cs;
+        v.xfull = chr::xcd_full(trips, cs);
+        hipLaunchKernelGGL((k_c2_stamped<PERSIST, R>), dim3(grid), dim3(BL), lds, 0, v, ctr + i,
+                           st + 3 * (size_t)grid * i);
+    };
+    for (int i = 0; i < 4; ++i) launch(i);
+    CK(hipDeviceSynchronize());
+    std::vector<hipEvent_t> ev(nlaunch + 1);
+    for (auto& e : ev) CK(hipEventCreate(&e));
+    CK(hipEventRecord(ev[0], 0));
+    for (int i = 0; i < nlaunch; ++i) {
+        launch(4 + i);
+        CK(hipEventRecord(ev[i + 1], 0));
+    }
+    CK(hipDeviceSynchronize());
+    std::vector<unsigned long long> h(3 * (size_t)grid * total);
+    CK(hipMemcpy(h.data(), st, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    const double bytes = 3.0 * nvec * 16;
+    double sum_ms = 0;
+    unsigned long long prev_end = 0;
+    for (int i = 0; i < nlaunch; ++i) {
+        const unsigned long long* p = h.data() + 3 * (size_t)grid * (4 + i);
+        unsigned long long tmin = ~0ull, tmax = 0, smin = ~0ull, xend[16] = {};
+        std::vector<unsigned long long> ends(grid);
+        for (size_t w = 0; w < grid; ++w) {
+            const unsigned long long t0 = p[3 * w], t1 = p[3 * w + 1];
+            const unsigned xcc = (unsigned)(p[3 * w + 2] >> 6) & 15u;
+            tmin = std::min(tmin, t0);
+            tmax = std::max(tmax, t1);
+            smin = std::min(smin, t1);
+            ends[w] = t1;
+            xend[xcc] = std::max(xend[xcc], t1);
+        }
+        std::sort(ends.begin(), ends.end());
+        auto at = [&](double f) { return (ends[(size_t)std::min<double>(grid - 1, f * grid)] - tmin) * us_per_tick; };
+        double xe_min = 1e30, xe_max = 0;
+        for (int x = 0; x < 16; ++x) {
+            if (!xend[x]) continue;
+            xe_min = std::min(xe_min, (xend[x] - tmin) * us_per_tick);
+            xe_max = std::max(xe_max, (xend[x] - tmin) * us_per_tick);
+        }
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+        sum_ms += ms;
+        const double span = (tmax - tmin) * us_per_tick;
+        std::printf("{\"focus24\": \"%s\", \"cap\": %d, \"grid\": %u, \"launch\": %d, \"event_us\": %.2f, \"span_us\": %.2f, "
+                    "\"gap_from_prev_us\": %.2f, \"first_end_us\": %.2f, \"t50\": %.2f, \"t95\": %.2f, \"t99\": %.2f, "
+                    "\"xcd_end_min_us\": %.2f, \"xcd_end_max_us\": %.2f, \"frac_event\": %.4f, \"frac_span\": %.4f}\n",
+                    label, cap, grid, i, ms * 1e3, span, prev_end ? (tmin - prev_end) * us_per_tick : -1.0,
+                    (smin - tmin) * us_per_tick, at(0.5), at(0.95), at(0.99), xe_min, xe_max,
+                    bytes / (ms * 1e-3) / 8e12, bytes / (span * 1e-6) / 8e12);
+        prev_end = tmax;
+    }
+    std::printf("{\"focus24_summary\": \"%s\", \"cap\": %d, \"grid\": %u, \"mean_event_us\": %.2f, \"frac\": %.4f}\n",
+                label, cap, grid, sum_ms * 1e3 / nlaunch, bytes / (sum_ms / nlaunch * 1e-3) / 8e12);
+    std::fflush(stdout);
+    for (auto& e : ev) CK(hipEventDestroy(e));
+    CK(hipFree(st));
+    CK(hipFree(ctr));
+}
+
+static void focus24(int rounds) {
+    const size_t nvec = (64u << 20) / 16;
+    const int sets = 16;
+    Sets S = make_sets(1, nvec, sets);
+    int ncu = 0;
+    CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+    for (int r = 0; r < rounds; ++r) {
+        focus24_one<false, 1>(S, nvec, sets, 12, 0, 16, "product_shape");
+        // resident grid: 11 per CU at cap 12 (census), runs of R trips (4 KiB per operand per trip)
+        focus24_one<true, 4>(S, nvec, sets, 12, (unsigned)ncu * 11, 16, "persist_r4_grid11pcu");
+        focus24_one<true, 16>(S, nvec, sets, 12, (unsigned)ncu * 11, 16, "persist_r16_grid11pcu");
+        focus24_one<true, 4>(S, nvec, sets, 0, (unsigned)ncu * 16, 16, "persist_r4_uncapped_grid16pcu");
+        focus24_one<true, 1>(S, nvec, sets, 12, (unsigned)ncu * 11, 16, "persist_r1_grid11pcu");
+    }
+    free_sets(S);
+}
+
 int main(int argc, char** argv) {
     check();
     if (argc > 1 && std::string(argv[1]) == "layout") {
         layout_mode();
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus24") {  // C2 timeline: the XCD tail; persistent balancing
+        focus24(argc > 2 ? std::atoi(argv[2]) : 2);
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus23") {  // what the ~4 us between back-to-back launches is
