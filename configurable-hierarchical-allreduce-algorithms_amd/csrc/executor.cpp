@@ -760,14 +760,21 @@ int wait_event_poll(hipEvent_t ev, int timeout_ms) {
 // not split (one window would cover it).
 // One int per rank, the minimum over the ranks, on the communicator stream (blocking, under the
 // timeout).  A failure aborts the communicator: the peers are inside the same collective.
+// No pageable copy is issued while the exchange may still be pending: such a copy returns only
+// once HIP has staged it, i.e. it would wait for the collective inside HIP, past the timeout, if a
+// peer never arrives.  The value goes in by a device memset and comes out after wait_call.
 int agree_min(chr_comm* c, int mine, int* all) {
     int rc = hip_code(c->flag.reserve(sizeof(int), c->stream));
     int* d = (int*)c->flag.p;
-    if (!rc) rc = hip_code(hipMemcpyAsync(d, &mine, sizeof(int), hipMemcpyHostToDevice, c->stream));
+    if (!rc) rc = hip_code(hipMemsetD32Async((hipDeviceptr_t)d, mine, 1, c->stream));
     if (!rc) rc = nccl_code(ncclAllReduce(d, d, 1, ncclInt32, ncclMin, c->nccl, c->stream));
-    if (!rc) rc = hip_code(hipMemcpyAsync(all, d, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    if (!rc) rc = wait_call(c);
-    else c->abort_comm();
+    if (rc) {
+        c->abort_comm();
+        return rc;
+    }
+    if ((rc = wait_call(c))) return rc;  // under the timeout; aborts the communicator itself
+    rc = hip_code(hipMemcpyAsync(all, d, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    if (!rc) rc = hip_code(hipStreamSynchronize(c->stream));
     return rc;
 }
 
