@@ -65,6 +65,7 @@ struct ReduceTuning {
     size_t tree_nt_min_bytes;  // tree launches
     int wg_per_cu_vec;   // -1: policy
     int wg_per_cu_tree;  // -1: policy
+    int xcd_hand_shift;  // -1: policy (xcd_hand in reduce_common.hpp); 0: off
     unsigned lds_per_cu; // bytes of LDS per CU (device attribute; 160 KiB on gfx950)
     unsigned lds_per_block;  // bytes of LDS one workgroup may allocate (device attribute)
 };

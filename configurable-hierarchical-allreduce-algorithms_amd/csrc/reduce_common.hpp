@@ -257,6 +257,36 @@ __host__ __device__ __forceinline__ size_t xcd_trip(uint32_t b, uint32_t full, u
     return ((((size_t)(i >> cs)) * 8u + x) << cs) | (i & ((1u << cs) - 1u));
 }
 
+// Odd XCDs stream slower.  Stamped C2 launches (tools/reduce_microbench focus25-28,
+// profiles/r04/c2_timeline/) have XCDs 1, 3, 5, 7 finishing 2.5-3 % after XCDs 0, 2, 4, 6, on every
+// box measured, under every trip map (identity, 256 KiB / 1 MiB runs, runs shifted to the neighbour
+// XCD), and in proportion to the launch size (16 MiB: 0.1 us, 64 MiB: 0.9 us, 256 MiB: 2.9 us):
+// a rate, which follows the XCD and not the addresses.  Since every XCD gets exactly 1/8 of a
+// grid's workgroups, the launch ends when the odd ones do.  xcd_trip_w rebalances statically: each
+// odd XCD hands the last `hand` trips of its share to the even XCD below it (the even XCD runs them
+// after its own; the odd XCD's last 2 x hand workgroups exit at once).  hand = per-XCD trips >> 6
+// (1.6 %) balanced the end times at 64 MiB: span 30.68 -> 29.86 us (focus27, h = 16 / 32 / 48).
+// The weighted region is blocks [0, full + 8 x hand), over trips [0, full); later blocks keep the
+// identity (trip = block - 8 x hand).  kIdleTrip: a workgroup with nothing to do.
+constexpr size_t kIdleTrip = ~(size_t)0;
+inline uint32_t xcd_hand(uint32_t full, int env) {
+    const int shift = env >= 0 ? env : 6;
+    return shift <= 0 ? 0u : (full >> 3) >> shift;
+}
+__host__ __device__ __forceinline__ size_t xcd_own(uint32_t x, uint32_t i, uint32_t cs) {
+    return ((((size_t)(i >> cs)) * 8u + x) << cs) | (i & ((1u << cs) - 1u));
+}
+__host__ __device__ __forceinline__ size_t xcd_trip_w(uint32_t b, uint32_t full, uint32_t cs, uint32_t hand) {
+    if (hand == 0) return xcd_trip(b, full, cs);
+    if (b >= full + 8u * hand) return (size_t)(b - 8u * hand);
+    const uint32_t x = b & 7u, i = b >> 3, q = full >> 3;
+    if ((x & 1u) == 0) {
+        if (i < q) return xcd_own(x, i, cs);
+        return xcd_own(x + 1u, q - hand + (i - q), cs);  // i < q + hand in this region
+    }
+    return i < q - hand ? xcd_own(x, i, cs) : kIdleTrip;
+}
+
 // log2 of the trips in one XCD run for a launch of `trip_bytes` per operand per workgroup:
 // CHR_XCD_RUN_KIB if set, else `policy_kib` (0 = identity map).
 inline uint32_t xcd_run_shift(size_t policy_kib, size_t trip_bytes) {

@@ -136,6 +136,8 @@ ReduceTuning& reduce_tuning() {
         r.wg_per_cu_vec = s ? std::max(0, std::atoi(s)) : -1;
         s = std::getenv("CHR_WG_PER_CU_TREE");
         r.wg_per_cu_tree = s ? std::max(0, std::atoi(s)) : -1;
+        s = std::getenv("CHR_XCD_HAND_SHIFT");
+        r.xcd_hand_shift = s ? std::max(0, std::atoi(s)) : -1;
         int dev = 0, lds = 0, blk = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess ||

@@ -19,6 +19,7 @@ struct VecArgs {
     size_t nvec;
     uint32_t xrun;   // log2 of the trips per XCD run (xcd_trip); set by the launcher
     uint32_t xfull;  // blocks [0, xfull) are remapped (xcd_full of the grid); set per launch
+    uint32_t hand;   // trips each odd XCD hands to the even one below (xcd_trip_w); 0 = none
 };
 
 // U vectors (16 B each) per lane per trip; all M+1 operands of the trip are loaded
@@ -51,11 +52,13 @@ __global__ __launch_bounds__(BL) void k_reduce_vec(VecArgs a) {
 #pragma unroll
     for (int j = 0; j < M; ++j) ins[j] = a.ins[j];
     const size_t nvec = a.nvec;
-    const uint32_t xrun = a.xrun, xfull = a.xfull;
+    const uint32_t xrun = a.xrun, xfull = a.xfull, hand = a.hand;
     pin_sgpr(out, accp, nvec, xrun, xfull);
+    pin_sgpr_u32(hand, hand);
 #pragma unroll
     for (int j = 0; j < M; ++j) pin_sgpr(ins[j]);
-    const size_t trip = xcd_trip(blockIdx.x, xfull, xrun);
+    const size_t trip = xcd_trip_w(blockIdx.x, xfull, xrun, hand);
+    if (trip == kIdleTrip) return;
     const size_t base = trip * BL * U + threadIdx.x;
     if ((trip + 1) * BL * U <= nvec) {
         u32x4 acc[U], x[M][U];
@@ -159,8 +162,9 @@ constexpr int vec_u_dt() {
 }
 
 // A grid holds at most 2^31 threads here; larger calls (> 32 GiB per operand at BL = 64, U = 2)
-// run as consecutive launches over consecutive pieces.
-template <int BL, int U, typename L>
+// run as consecutive launches over consecutive pieces.  WEIGHTED: the odd-XCD handover
+// (xcd_trip_w) adds 8 x hand workgroups to the grid.
+template <int BL, int U, bool WEIGHTED = false, typename L>
 inline hipError_t for_each_launch_piece(VecArgs a, L launch) {
     const size_t cap = reduce_tuning().max_launch_vec;
     const size_t max_vec = cap ? cap : ((size_t)1 << 31) / BL * BL * U;
@@ -170,9 +174,10 @@ inline hipError_t for_each_launch_piece(VecArgs a, L launch) {
         p.acc = a.acc + off;
         for (int j = 0; j < kMaxFanIn; ++j) p.ins[j] = a.ins[j] ? a.ins[j] + off : nullptr;
         p.nvec = a.nvec - off < max_vec ? a.nvec - off : max_vec;
-        const unsigned grid = (unsigned)((p.nvec + (size_t)BL * U - 1) / ((size_t)BL * U));
-        p.xfull = xcd_full(grid, p.xrun);
-        launch(p, grid);
+        const unsigned trips = (unsigned)((p.nvec + (size_t)BL * U - 1) / ((size_t)BL * U));
+        p.xfull = xcd_full(trips, p.xrun);
+        p.hand = WEIGHTED ? xcd_hand(p.xfull, reduce_tuning().xcd_hand_shift) : 0u;
+        launch(p, trips + 8u * p.hand);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -189,7 +194,8 @@ inline hipError_t launch_vec_mb_one(VecArgs a, hipStream_t s) {
     constexpr int U = vec_u_dt<DT, OP, M, NT>();
     a.xrun = NT ? xcd_run_shift(vec_xcd_run_kib<M>(), (size_t)BL * U * 16) : 0;
     const unsigned lds = NT ? nt_lds_bytes(reduce_tuning().wg_per_cu_vec, vec_wg_per_cu<M>()) : 0;
-    return for_each_launch_piece<BL, U>(a, [&](const VecArgs& p, unsigned grid) {
+    // the odd-XCD handover applies where the kernel streams from HBM (nt launches)
+    return for_each_launch_piece<BL, U, NT>(a, [&](const VecArgs& p, unsigned grid) {
         hipLaunchKernelGGL((k_reduce_vec<DT, OP, M, U, NT, ACC0, BL>), dim3(grid), dim3(BL), lds, s, p);
     });
 }

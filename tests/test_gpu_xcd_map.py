@@ -1,4 +1,4 @@
-"""The XCD-run workgroup map (reduce_common.hpp xcd_trip) must cover every trip exactly once.
+"""The XCD-run workgroup map (reduce_common.hpp xcd_trip, xcd_trip_w) must cover every trip exactly once.
 
 Streaming (nt) launches place each workgroup's trip by xcd_trip: runs of 2^cs consecutive trips per
 XCD, identity for the blocks past the last whole 8 * 2^cs group.  A wrong map shows up as elements
@@ -64,14 +64,19 @@ print(json.dumps({{"bad": [str(b) for b in bad]}}))
 """
 
 
-@pytest.mark.parametrize("run_kib,max_vec", [(4, 0), (8, 0), (64, 0), (8, 3000)])
-def test_xcd_run_map_covers_every_trip(run_kib, max_vec):
+@pytest.mark.parametrize("run_kib,max_vec,hand_shift", [(4, 0, -1), (8, 0, -1), (64, 0, -1), (8, 3000, -1),
+                                                     (8, 0, 1), (0, 0, 2), (4, 3000, 3)])
+def test_xcd_run_map_covers_every_trip(run_kib, max_vec, hand_shift):
     """max_vec > 0 also caps the vectors per launch / tree segment (CHR_REDUCE_MAX_LAUNCH_VEC), so the
     paths that split > 32 GiB buckets into several launches and > 1 GiB trees into several segments
-    (and several flushes of 8 segments) run at these sizes, with partial trips inside a call."""
+    (and several flushes of 8 segments) run at these sizes, with partial trips inside a call.
+    hand_shift: the odd-XCD handover (xcd_trip_w) -- the policy's shift 6 engages at the 2^21-element
+    bucket here; shifts 1-3 hand up to half of every odd XCD's share over, on run and identity maps."""
     code = CHILD.format(here=HERE, oracle=os.path.join(REPO, "oracle"),
                         pkg=os.path.join(REPO, "configurable-hierarchical-allreduce-algorithms_amd"))
     env = dict(os.environ, CHR_REDUCE_NT="1", CHR_XCD_RUN_KIB=str(run_kib), CHR_REDUCE_MAX_LAUNCH_VEC=str(max_vec))
+    if hand_shift >= 0:
+        env["CHR_XCD_HAND_SHIFT"] = str(hand_shift)
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     res = json.loads(out.stdout.strip().splitlines()[-1])

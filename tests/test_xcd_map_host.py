@@ -1,4 +1,4 @@
-"""CPU check of the XCD-run workgroup map (reduce_common.hpp xcd_trip): the kernels' own
+"""CPU check of the XCD-run workgroup map (reduce_common.hpp xcd_trip, xcd_trip_w): the kernels' own
 __host__ __device__ functions, host-compiled with hipcc, must form a bijection on every grid size
 and send every remapped block into a run of its own XCD.  The GPU side
 (tests/test_gpu_xcd_map.py) checks the kernels element by element."""

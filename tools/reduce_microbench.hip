@@ -1657,7 +1657,7 @@ static void focus19_vec(size_t bytes, int sets) {
 // tail.  PERSIST: a grid of resident workgroups that take runs of R trips from a per-launch counter
 // (one vector atomic per run, the next run's index fetched while the current run streams), so the
 // XCDs share the work until it runs out.  Counters are one per launch, zeroed once up front.
-template <bool PERSIST, int R>
+template <bool PERSIST, int R, int MAPV = 0>
 __global__ __launch_bounds__(64) void k_c2_stamped(chr::VecArgs a, unsigned* ctr, unsigned long long* st) {
     constexpr int U = 4, BL = 64;
     const unsigned long long t0 = wall_clock64();
@@ -1683,8 +1683,32 @@ __global__ __launch_bounds__(64) void k_c2_stamped(chr::VecArgs a, unsigned* ctr
     if constexpr (!PERSIST) {
         chr::pin_sgpr(out, accp, nvec, a.xrun, a.xfull);
         chr::pin_sgpr(in0);
-        const size_t trip = chr::xcd_trip(blockIdx.x, a.xfull, a.xrun);
-        if ((trip + 1) * BL * U <= nvec) body(trip);
+        if constexpr (MAPV == 3) {
+            // weighted runs: in the last round of runs each odd XCD hands the last h trips of its run to
+            // the even XCD below it (grid = 8 x (runs_per_xcd x C + h); only whole-run grids)
+            const uint32_t h = *ctr, cs = a.xrun, C = 1u << cs, x = blockIdx.x & 7u, i = blockIdx.x >> 3;
+            const uint32_t RPX = ntrips >> (cs + 3), L = (RPX - 1) << cs;
+            size_t trip;
+            if (i < L) {
+                trip = ((((size_t)(i >> cs)) * 8u + x) << cs) | (i & (C - 1u));
+            } else {
+                const uint32_t t = i - L;
+                const size_t g0 = (size_t)(RPX - 1) * 8u + x;
+                if ((x & 1u) == 0) {
+                    if (t < C) trip = (g0 << cs) | t;
+                    else if (t < C + h) trip = ((g0 + 1) << cs) | (C - h + (t - C));
+                    else trip = ~(size_t)0;
+                } else {
+                    trip = t < C - h ? (g0 << cs) | t : ~(size_t)0;
+                }
+            }
+            if (trip != ~(size_t)0) body(trip);
+        } else {
+            // MAPV 2: each XCD takes its neighbour's runs (block b does block b ^ 1's trip)
+            const uint32_t bb = MAPV == 2 ? (blockIdx.x ^ 1u) : blockIdx.x;
+            const size_t trip = chr::xcd_trip(bb, a.xfull, a.xrun);
+            if ((trip + 1) * BL * U <= nvec) body(trip);
+        }
     } else {
         const uint32_t nruns = (ntrips + R - 1) / R;
         auto grab = [&]() -> uint32_t {
@@ -1711,19 +1735,25 @@ __global__ __launch_bounds__(64) void k_c2_stamped(chr::VecArgs a, unsigned* ctr
     }
 }
 
-template <bool PERSIST, int R>
-static void focus24_one(Sets& S, size_t nvec, int sets, int cap, unsigned pgrid, int nlaunch, const char* label) {
+template <bool PERSIST, int R, int MAPV = 0>
+static void focus24_one(Sets& S, size_t nvec, int sets, int cap, unsigned pgrid, int nlaunch, const char* label,
+                        int run_kib = 256) {
     constexpr int U = 4, BL = 64;
     const unsigned trips = (unsigned)(nvec / (BL * U));
-    const unsigned grid = PERSIST ? pgrid : trips;
     uint32_t cs = 0;
-    while (((size_t)2 << cs) * (BL * U * 16) <= (size_t)256 * 1024 && cs < 16) ++cs;
+    while (((size_t)2 << cs) * (BL * U * 16) <= (size_t)run_kib * 1024 && cs < 16) ++cs;
+    // MAPV 3: pgrid carries h, the trips each odd XCD hands over in the last round
+    const unsigned grid = PERSIST ? pgrid : MAPV == 3 ? trips + 8u * pgrid : trips;
     unsigned long long* st = nullptr;
     unsigned* ctr = nullptr;
     const int total = nlaunch + 4;
     CK(hipMalloc(&st, 3 * (size_t)grid * total * sizeof(unsigned long long)));
     CK(hipMalloc(&ctr, total * sizeof(unsigned)));
     CK(hipMemset(ctr, 0, total * sizeof(unsigned)));
+    if (MAPV == 3) {
+        std::vector<unsigned> hv(total, pgrid);
+        CK(hipMemcpy(ctr, hv.data(), total * sizeof(unsigned), hipMemcpyHostToDevice));
+    }
     int khz = 0;
     CK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0));
     const double us_per_tick = 1e3 / khz;
@@ -1737,7 +1767,7 @@ static void focus24_one(Sets& S, size_t nvec, int sets, int cap, unsigned pgrid,
         v.nvec = nvec;
         v.xrun = cs;
         v.xfull = chr::xcd_full(trips, cs);
-        hipLaunchKernelGGL((k_c2_stamped<PERSIST, R>), dim3(grid), dim3(BL), lds, 0, v, ctr + i,
+        hipLaunchKernelGGL((k_c2_stamped<PERSIST, R, MAPV>), dim3(grid), dim3(BL), lds, 0, v, ctr + i,
                            st + 3 * (size_t)grid * i);
     };
     for (int i = 0; i < 4; ++i) launch(i);
@@ -1780,11 +1810,16 @@ static void focus24_one(Sets& S, size_t nvec, int sets, int cap, unsigned pgrid,
         CK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
         sum_ms += ms;
         const double span = (tmax - tmin) * us_per_tick;
+        char xe[256];
+        int o = 0;
+        for (int x = 0; x < 8; ++x)
+            o += std::snprintf(xe + o, sizeof xe - o, "%s%.2f", x ? ", " : "", xend[x] ? (xend[x] - tmin) * us_per_tick : -1.0);
         std::printf("{\"focus24\": \"%s\", \"cap\": %d, \"grid\": %u, \"launch\": %d, \"event_us\": %.2f, \"span_us\": %.2f, "
                     "\"gap_from_prev_us\": %.2f, \"first_end_us\": %.2f, \"t50\": %.2f, \"t95\": %.2f, \"t99\": %.2f, "
-                    "\"xcd_end_min_us\": %.2f, \"xcd_end_max_us\": %.2f, \"frac_event\": %.4f, \"frac_span\": %.4f}\n",
+                    "\"xcd_end_min_us\": %.2f, \"xcd_end_max_us\": %.2f, \"xcd_end_us\": [%s], \"frac_event\": %.4f, "
+                    "\"frac_span\": %.4f}\n",
                     label, cap, grid, i, ms * 1e3, span, prev_end ? (tmin - prev_end) * us_per_tick : -1.0,
-                    (smin - tmin) * us_per_tick, at(0.5), at(0.95), at(0.99), xe_min, xe_max,
+                    (smin - tmin) * us_per_tick, at(0.5), at(0.95), at(0.99), xe_min, xe_max, xe,
                     bytes / (ms * 1e-3) / 8e12, bytes / (span * 1e-6) / 8e12);
         prev_end = tmax;
     }
@@ -1821,6 +1856,51 @@ int main(int argc, char** argv) {
     }
     if (argc > 1 && std::string(argv[1]) == "focus24") {  // C2 timeline: the XCD tail; persistent balancing
         focus24(argc > 2 ? std::atoi(argv[2]) : 2);
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus26") {  // does the late XCD set follow the XCD or the addresses?
+        const size_t nvec = (64u << 20) / 16;
+        Sets S = make_sets(1, nvec, 16);
+        for (int r = 0; r < (argc > 2 ? std::atoi(argv[2]) : 2); ++r) {
+            focus24_one<false, 1, 0>(S, nvec, 16, 12, 0, 32, "runs256");
+            focus24_one<false, 1, 2>(S, nvec, 16, 12, 0, 32, "runs256_neighbour");
+            focus24_one<false, 1, 0>(S, nvec, 16, 12, 0, 32, "identity", 0);
+            focus24_one<false, 1, 0>(S, nvec, 16, 12, 0, 32, "runs1024", 1024);
+        }
+        free_sets(S);
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus27") {  // weighted last round: odd XCDs hand h trips to even ones
+        const size_t nvec = (64u << 20) / 16;
+        Sets S = make_sets(1, nvec, 16);
+        for (int r = 0; r < (argc > 2 ? std::atoi(argv[2]) : 2); ++r) {
+            focus24_one<false, 1, 0>(S, nvec, 16, 12, 0, 32, "runs256");
+            for (unsigned h : {16u, 32u, 48u}) {
+                char lab[64];
+                std::snprintf(lab, sizeof lab, "runs256_odd_hand_%u", h);
+                focus24_one<false, 1, 3>(S, nvec, 16, 12, h, 32, lab);
+            }
+        }
+        free_sets(S);
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus28") {  // is the odd XCDs' lag a fixed delay or a rate?
+        for (size_t mib : {16, 64, 256}) {
+            const size_t nvec = (mib << 20) / 16;
+            const int sets = (int)std::max<size_t>(2, (2048 / (2 * mib)));
+            Sets S = make_sets(1, nvec, sets);
+            char lab[64];
+            std::snprintf(lab, sizeof lab, "runs256_%zuMiB", mib);
+            focus24_one<false, 1, 0>(S, nvec, sets, 12, 0, 24, lab);
+            free_sets(S);
+        }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus25") {  // C2 timeline only: which XCD finishes last, launch after launch
+        const size_t nvec = (64u << 20) / 16;
+        Sets S = make_sets(1, nvec, 16);
+        for (int r = 0; r < (argc > 2 ? std::atoi(argv[2]) : 2); ++r) focus24_one<false, 1>(S, nvec, 16, 12, 0, 32, "product_shape");
+        free_sets(S);
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus23") {  // what the ~4 us between back-to-back launches is
