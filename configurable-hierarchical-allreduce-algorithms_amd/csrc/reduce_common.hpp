@@ -269,8 +269,9 @@ __host__ __device__ __forceinline__ size_t xcd_trip(uint32_t b, uint32_t full, u
 // The weighted region is blocks [0, full + 8 x hand), over trips [0, full); later blocks keep the
 // identity (trip = block - 8 x hand).  kIdleTrip: a workgroup with nothing to do.
 constexpr size_t kIdleTrip = ~(size_t)0;
+constexpr int kXcdHandShift = 6;
 inline uint32_t xcd_hand(uint32_t full, int env) {
-    const int shift = env >= 0 ? env : 6;
+    const int shift = env >= 0 ? env : kXcdHandShift;
     return shift <= 0 ? 0u : (full >> 3) >> shift;
 }
 __host__ __device__ __forceinline__ size_t xcd_own(uint32_t x, uint32_t i, uint32_t cs) {

@@ -52,7 +52,8 @@ struct TreeArgs {
     TreeSeg seg[kMaxTreeSegs];
     int nseg;
     int nl;
-    uint32_t xrun;  // log2 of the trips per XCD run within a segment (xcd_trip); set by the launcher
+    uint32_t xrun;    // log2 of the trips per XCD run within a segment (xcd_trip); set by the launcher
+    uint32_t hshift;  // odd-XCD handover per segment, hand = (xfull / 8) >> hshift (xcd_trip_w); 0 = none
 };
 
 // A segment's vector body is at most this many 16-B vectors (1 GiB per operand); longer trees are
@@ -157,7 +158,8 @@ __global__ __launch_bounds__(BL) void k_reduce_tree(TreeArgs a) {
         xfs[j] = a.xfull[j];
         pin_sgpr_u32(b0s[j], xfs[j]);
     }
-    pin_sgpr_u32(xrun, xrun);
+    const uint32_t hshift = a.hshift;
+    pin_sgpr_u32(xrun, hshift);
     int s = 0;
     uint32_t b0 = 0, xfull = xfs[0];
 #pragma unroll
@@ -177,7 +179,11 @@ __global__ __launch_bounds__(BL) void k_reduce_tree(TreeArgs a) {
     pin_sgpr(out, leaves[0], nvec, comb, swaps);
 #pragma unroll
     for (int j = 1; j < NL; ++j) pin_sgpr(leaves[j]);
-    const size_t trip = xcd_trip(b - b0, xfull, xrun);
+    // segments start on a multiple of 8 blocks when hshift is set, so a local block's XCD parity is
+    // its global one
+    const uint32_t hand = hshift ? (xfull >> 3) >> hshift : 0u;
+    const size_t trip = xcd_trip_w(b - b0, xfull, xrun, hand);
+    if (trip == kIdleTrip) return;
     const size_t base = trip * BL * U + threadIdx.x;
     if ((trip + 1) * BL * U <= nvec) {
         u32x4 x[NL][U];
@@ -267,6 +273,9 @@ inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
     constexpr int U = is_complex_dt<DT>() && OP == CHR_PROD ? 1 : tree_u<NL, NT>();  // see vec_u_dt
     TreeArgs a = a_in;
     a.xrun = NT ? xcd_run_shift(tree_xcd_run_kib<NL>(), (size_t)BL * U * 16) : 0;
+    // the odd-XCD handover of streaming launches (xcd_hand / xcd_trip_w in reduce_common.hpp), per segment
+    const int henv = reduce_tuning().xcd_hand_shift;
+    a.hshift = NT ? (uint32_t)(henv >= 0 ? henv : kXcdHandShift) : 0u;
     size_t grid = 0;
     for (int j = 0; j < kMaxTreeSegs; ++j) {
         if (j >= a.nseg) {
@@ -276,9 +285,10 @@ inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
         }
         if (a.seg[j].nvec > kMaxSegVec) return hipErrorInvalidValue;  // launch_reduce_tree_multi cuts them
         const size_t trips = (a.seg[j].nvec + (size_t)BL * U - 1) / ((size_t)BL * U);
+        if (a.hshift) grid = (grid + 7) & ~(size_t)7;  // the segment starts on XCD 0 (its padding blocks idle)
         a.block0[j] = (uint32_t)grid;
         a.xfull[j] = xcd_full((uint32_t)trips, a.xrun);
-        grid += trips;
+        grid += trips + (a.hshift ? 8u * ((a.xfull[j] >> 3) >> a.hshift) : 0u);
     }
     if (grid == 0) return hipSuccess;
     const unsigned lds = NT ? nt_lds_bytes(reduce_tuning().wg_per_cu_tree, tree_wg_per_cu<NL>()) : 0;

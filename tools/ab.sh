@@ -2,7 +2,8 @@
 # Product-API A/B runs behind the occupancy-cap and XCD-run policy, on the GPU box:
 #   gpurun -- bash tools/ab.sh cap    C2 / mstream m=3,7 / collective-kernel rows vs CHR_WG_PER_CU_{VEC,TREE}
 #   gpurun -- bash tools/ab.sh runs   C2 with the policy XCD map vs 256 KiB runs, 3 alternating rounds
-#   gpurun -- bash tools/ab.sh hand   C2 / mstream with the odd-XCD handover off / at shifts 5-7
+#   gpurun -- bash tools/ab.sh hand   C2 / mstream with the odd-XCD handover off / at shifts 5-6
+#   gpurun -- bash tools/ab.sh handtree   the in-collective tree rows with the handover off / on
 # Results land under gpurun_out/cap/ or gpurun_out/ab_runs/ (copied to profiles/r02/occupancy_cap/, ab_runs/).
 set -u -o pipefail
 cd "$(dirname "$0")/.."
@@ -41,7 +42,7 @@ runs)
 hand)  # the odd-XCD handover (xcd_trip_w): off (shift 0) / policy (6) / 5 / 7, C2 at 20 and 200 steps, mstream m=3,7
   mkdir -p gpurun_out/ab_hand
   for r in 1 2 3; do
-    for v in 0 6 5 7; do
+    for v in 0 6 5; do
       CHR_XCD_HAND_SHIFT=$v timeout -k 10 120 python bench.py --steps 200 --warmup 20 --no-cpu-baseline \
         > gpurun_out/ab_hand/c2_shift${v}_r${r}.json 2>/dev/null || exit 1
       CHR_XCD_HAND_SHIFT=$v timeout -k 10 120 python bench.py --steps 20 --warmup 5 --no-cpu-baseline \
@@ -53,6 +54,15 @@ hand)  # the odd-XCD handover (xcd_trip_w): off (shift 0) / policy (6) / 5 / 7, 
     CHR_XCD_HAND_SHIFT=$v timeout -k 10 300 python tools/mstream_probe.py --ms 3,7 --mib 256 --layouts sep --sets 1,8 \
       > gpurun_out/ab_hand/mstream_shift${v}.jsonl 2>/dev/null || exit 1
     echo "mstream shift=$v"; cut -c1-300 gpurun_out/ab_hand/mstream_shift${v}.jsonl
+  done ;;
+handtree)  # the odd-XCD handover on the tree kernel: in-collective rows (rank-alone replays = one GPU's grids)
+  mkdir -p gpurun_out/ab_hand
+  for r in 1 2; do
+    for v in 0 6; do
+      CHR_XCD_HAND_SHIFT=$v timeout -k 10 400 python bench.py --collective-kernels \
+        > gpurun_out/ab_hand/ck_shift${v}_r${r}.json 2>/dev/null || exit 1
+      echo "tree shift=$v r=$r $(python -c "import json;d=json.load(open('gpurun_out/ab_hand/ck_shift${v}_r${r}.json'))['collective_kernels']['rows'];print({k: v['frac'] for k, v in d.items()})")"
+    done
   done ;;
 tree)  # the tree shape: policy vs the previous one (16 per CU, 512 KiB runs), collective-kernel rows, alternating
   mkdir -p gpurun_out/ab_tree
