@@ -20,6 +20,7 @@
 #   tree       tools/tree_bench.py $TREE_ARGS                   -> tree_bench.json
 #   launch     bench.py --gpus ${N:-2} with no external launcher (bench.py starts its own ranks;
 #              virtual hosts: ranks share the one GPU, socket transport) -> bench_launch_n${N}.json
+#   launch8    bench.py --gpus 8 at 1 GiB per rank, launcher + deadline, ranks sharing the GPU -> bench_launch_n8_1gib.json
 #   rehearse   the N>1 bench line with ${N:-4} ranks sharing the one GPU (socket transport;
 #              exercises the code path, its GB/s mean nothing)  -> bench_n${N}_rehearsal.json
 # Everything lands under gpurun_out/.
@@ -68,6 +69,15 @@ for step in "$@"; do
     n=${N:-2}
     CHR_BENCH_VIRTUAL_HOSTS=1 CHR_BENCH_DEADLINE_S=${DEADLINE:-240} run 600 "bench_launch_n${n}.json" \
       python bench.py --gpus "$n" --steps 3 --warmup 1 --count $((1 << 21)) ;;
+  launch8)  # the N=8 line at its real size (1 GiB per rank), 8 ranks sharing the one GPU over sockets: the
+            # launcher and the deadline end to end (FLAT: AUTO's tuning over sockets would take minutes; a
+            # heartbeat file keeps the call visibly alive while the socket-bound steps run)
+    ( while sleep 50; do date +%T >> "$OUT/heartbeat_launch8.txt"; done ) &
+    hb=$!
+    trap 'kill $hb 2>/dev/null' EXIT
+    CHR_BENCH_VIRTUAL_HOSTS=1 CHR_BENCH_DEADLINE_S=${DEADLINE:-150} CHR_SCHEDULE=flat run 700 bench_launch_n8_1gib.json \
+      python bench.py --gpus 8 --steps 2 --warmup 1
+    kill $hb ;;
   rehearse)
     n=${N:-4}
     CHR_BENCH_VIRTUAL_HOSTS=1 run 600 "bench_n${n}_rehearsal.json" python -m torch.distributed.run --nnodes=1 \
