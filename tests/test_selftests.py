@@ -129,3 +129,30 @@ def test_selftest_binary_binds_function_to_shim(name):
     assert ok, (name, fn, strong)
     strong_ctl, ok_ctl = _binding(ctl, fn)
     assert len(strong_ctl) == 1 and not ok_ctl, (name, strong_ctl)
+
+
+def test_gpu_selftest_checks_reject_the_reference_only_build(tmp_path):
+    """Negative control for test_gpu_ref_harness.py::test_reference_selftests_on_mi355x, on CPU: the
+    reference-only build of all_reduce_radix_batch.cpp's DEBUG main (selftest_*_mpi: its own function, no
+    shim), run exactly as the GPU test runs the shim build (CHR_SHIM_TRACE=1, one output file per rank),
+    fails both of that test's binding checks -- no shim marker on stderr, and the function's own
+    `Phase N time:` lines in the output -- while its normalised lines still equal the golden ones (which is
+    why the normaliser alone could not tell the builds apart)."""
+    mpiexec = "/opt/conda/bin/mpiexec"
+    exe = os.path.join(REF_DIR, "selftest_all_reduce_radix_batch_mpi")
+    if not (os.path.exists(exe) and os.path.exists(mpiexec)):
+        pytest.skip("reference self-test build or MPICH absent (container-built)")
+    run = _runs()["all_reduce_radix_batch_n6_3_b2"]
+    n = run["nranks"]
+    out = subprocess.run([mpiexec, "-outfile-pattern", "out.%r", "-errfile-pattern", "err.%r", "-n", str(n),
+                          "-env", "CHR_SHIM_TRACE", "1", exe] + run["args"], cwd=tmp_path, capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    phases = []
+    for r in range(n):
+        err = (tmp_path / f"err.{r}").read_text() if (tmp_path / f"err.{r}").exists() else ""
+        raw = (tmp_path / f"out.{r}").read_text() if (tmp_path / f"out.{r}").exists() else ""
+        assert selftest_util.shim_calls(err) is None
+        assert selftest_util.normalize(raw) == run["lines"][str(r)]
+        phases.append(bool(selftest_util.reference_phase_lines(raw)))
+    assert phases[0], "rank 0 prints the reference function's phase timers"
