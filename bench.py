@@ -41,6 +41,7 @@ C2_ELEMS = 16 << 20          # 64 MiB fp32 per bucket
 NSETS = 16                   # 16 x 128 MiB distinct = 2 GiB working set: 8x the 256 MiB Infinity Cache
 SEED = 0xC41A5EED
 CPU_THREADS = 16             # the GPU box's CPU share per GPU (nproc shows the whole machine)
+GATE_CYCLES = 1_000_000      # torch.cuda._sleep before the timed region: ~0.4 ms at the shader clock
 
 
 def parse(argv=None):
@@ -201,10 +202,17 @@ def bench_bucket(args, cpu):
     torch.cuda.synchronize()
     # Timed region: HIP events on the launch stream around K back-to-back launches of the
     # one kernel; the average launch duration is the region time / K (inter-launch gaps
-    # included, so it can only under-state the kernel's own rate).
+    # included, so it can only under-state the kernel's own rate).  After the synchronize, an
+    # untimed gate kernel (torch.cuda._sleep, ~0.4 ms of spinning) holds the stream while the host
+    # enqueues the start event and the K launches: otherwise the start event fires at once on the
+    # idle GPU and the first launch's host-side latency (~5-10 us from Python) is booked into the
+    # region, 1-2 % of a 20-step line.  CHR_BENCH_GATE=0 leaves it out.
+    gate = os.environ.get("CHR_BENCH_GATE", "1") != "0"
     t_start, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     wall0 = time.perf_counter()
+    if gate:
+        torch.cuda._sleep(GATE_CYCLES)
     t_start.record(stream)
     for i in range(args.steps):
         rc = step(i)
@@ -225,7 +233,8 @@ def bench_bucket(args, cpu):
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": "C2 bucket reduction: k=2 (m=1 incoming bucket), 64 MiB fp32 per bucket, "
                                "device-resident, MPI_Reduce_local semantics", "bucket_bytes": 4 * n, "m": 1,
-                   "buffer_sets": NSETS, "untimed_launches": touch, "parallelism": "replicas"},
+                   "buffer_sets": NSETS, "untimed_launches": touch, "parallelism": "replicas",
+                   "gate": "untimed spin kernel ahead of the start event" if gate else None},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "kernel": C2_KERNEL_SYMBOL, "algorithmic_bytes_per_launch": bytes_per_step,

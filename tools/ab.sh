@@ -55,6 +55,17 @@ hand)  # the odd-XCD handover (xcd_trip_w): off (shift 0) / policy (6) / 5 / 7, 
       > gpurun_out/ab_hand/mstream_shift${v}.jsonl 2>/dev/null || exit 1
     echo "mstream shift=$v"; cut -c1-300 gpurun_out/ab_hand/mstream_shift${v}.jsonl
   done ;;
+gate)  # bench.py's untimed gate kernel ahead of the C2 timed region: off / on at the driver's 20 / 5 and at 200 / 20
+  mkdir -p gpurun_out/ab_gate
+  for r in 1 2 3 4; do
+    for v in 0 1; do
+      CHR_BENCH_GATE=$v timeout -k 10 120 python bench.py --steps 20 --warmup 5 --no-cpu-baseline \
+        > gpurun_out/ab_gate/c2s20_gate${v}_r${r}.json 2>/dev/null || exit 1
+      CHR_BENCH_GATE=$v timeout -k 10 120 python bench.py --steps 200 --warmup 20 --no-cpu-baseline \
+        > gpurun_out/ab_gate/c2s200_gate${v}_r${r}.json 2>/dev/null || exit 1
+      echo "c2 gate=$v r=$r s20 $(frac gpurun_out/ab_gate/c2s20_gate${v}_r${r}.json)  s200 $(frac gpurun_out/ab_gate/c2s200_gate${v}_r${r}.json)"
+    done
+  done ;;
 handtree)  # the odd-XCD handover on the tree kernel: in-collective rows (rank-alone replays = one GPU's grids)
   mkdir -p gpurun_out/ab_hand
   for r in 1 2; do
