@@ -841,10 +841,10 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
     def timed(name, fn):
         """One context entry on libchiara; a failure (e.g. a timeout that aborted the communicator)
         is recorded in the line instead of failing the metric, and skips the entries after it."""
-        if out.get("aborted"):
-            return
-        if late():
+        if late():  # first: a collective every rank reaches, whatever its communicator's state
             out[name] = {"skipped": "deadline"}
+            return
+        if out.get("aborted"):
             return
         try:
             out[name] = entry(_timed_max(torch, dist, fn, steps, warm, comm))
