@@ -902,7 +902,11 @@ def compare_lines(args, ca, torch, dist, comm, send, recv, count, dt, k, b, worl
               lambda: ca.check(ca.inter_reduce_linear(send, recv, rc_ilr, dt, ca.SUM, comm, 2)))
         timed(f"phase_intra_scatter_k2_b{world}",
               lambda: ca.check(ca.intra_scatter_radix_batch(send, rc_isc, dt, recv, comm, 2, world)))
-    if out.get("aborted"):
+    # whether any rank's communicator aborted, agreed over gloo: the entries below are collectives
+    ab = torch.tensor([1.0 if out.get("aborted") else 0.0], dtype=torch.float64)
+    dist.all_reduce(ab, op=dist.ReduceOp.MAX)
+    if ab.item():
+        out.setdefault("aborted", "on another rank")
         return out
     out["small_messages"] = ({"skipped": "deadline"} if late() else
                              small_messages(ca, torch, dist, comm, dt, k, b, world, dev, restore))
