@@ -55,7 +55,8 @@ __attribute__((constructor)) void shim_default_ipc_mode() { setenv("HSA_ENABLE_I
 int g_keyval = MPI_KEYVAL_INVALID;
 
 // Call counts for CHR_SHIM_TRACE (plain arrays: read by an atexit handler, after which no static
-// destructor may have run first).
+// destructor may have run first).  Not synchronised: the reference's harnesses call the collectives
+// from one thread per rank (MPI_Init, not MPI_Init_thread).
 constexpr int kMaxTraced = 32;
 const char* g_trace_name[kMaxTraced];
 long g_trace_count[kMaxTraced];
