@@ -232,6 +232,18 @@ __global__ __launch_bounds__(kBlock) void k_reduce_tree_scalar(TreeScalarArgs a)
     }
 }
 
+// The odd-XCD handover for streaming tree launches (xcd_trip_w): each odd XCD hands 1/2^shift of its
+// share of a segment to the even XCD below.  The odd XCDs lag only when the leaves stream from HBM.
+// Same-box A/Bs (profiles/r04/ab_hand/, 2 alternating rounds each):
+//  * HBM-cold leaves -- whole C4 calls on 8 virtual ranks, one grid per rank and slice
+//    (bench.py --collective-kernels): shift 7 0.754, 6 0.756-0.759, 5 0.760, 4 0.759-0.765, 3 0.745-0.749,
+//    off 0.749; tree_bench's cold batched slices: 6 and 4 +0.5-1.3 % over off;
+//  * leaves just rewritten (tree_bench's warm batched slices, 7 of 8 leaves copied in first, as RCCL's
+//    receives leave them on a node): off 0.759 / 0.756 at 16 MiB pieces, 6 0.752 / 0.757, 4 0.715 / 0.721.
+// On a node 7 of a tree's 8 leaves arrive over xGMI just before the launch, so the mild shift 6 is kept:
+// it gains on cold leaves and costs at most ~1 % on warm ones, where 4 costs 5 %.
+constexpr int kTreeXcdHandShift = 6;
+
 // XCD runs for streaming (nt) tree launches (profiles/r02/xcd_runs/ab_tree_*.json, C4 slice of 2
 // batched 8-leaf trees, HBM-cold, identity -> 512 KiB): 8 MiB pieces 0.571 -> 0.634, 16 MiB
 // 0.668 -> 0.700, 32 MiB 0.719 -> 0.750; fused reductions of a whole C4 call 0.676 -> 0.719.
@@ -275,7 +287,7 @@ inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
     a.xrun = NT ? xcd_run_shift(tree_xcd_run_kib<NL>(), (size_t)BL * U * 16) : 0;
     // the odd-XCD handover of streaming launches (xcd_hand / xcd_trip_w in reduce_common.hpp), per segment
     const int henv = reduce_tuning().xcd_hand_shift;
-    a.hshift = NT ? (uint32_t)(henv >= 0 ? henv : kXcdHandShift) : 0u;
+    a.hshift = NT ? (uint32_t)(henv >= 0 ? henv : kTreeXcdHandShift) : 0u;
     size_t grid = 0;
     for (int j = 0; j < kMaxTreeSegs; ++j) {
         if (j >= a.nseg) {

@@ -69,10 +69,24 @@ gate)  # bench.py's untimed gate kernel ahead of the C2 timed region: off / on a
 handtree)  # the odd-XCD handover on the tree kernel: in-collective rows (rank-alone replays = one GPU's grids)
   mkdir -p gpurun_out/ab_hand
   for r in 1 2; do
-    for v in 0 6; do
-      CHR_XCD_HAND_SHIFT=$v timeout -k 10 400 python bench.py --collective-kernels \
+    for v in ${SHIFTS:-0 6}; do  # "def": the library default (no env)
+      if [ "$v" = def ]; then unset CHR_XCD_HAND_SHIFT; else export CHR_XCD_HAND_SHIFT=$v; fi
+      timeout -k 10 400 python bench.py --collective-kernels \
         > gpurun_out/ab_hand/ck_shift${v}_r${r}.json 2>/dev/null || exit 1
       echo "tree shift=$v r=$r $(python -c "import json;d=json.load(open('gpurun_out/ab_hand/ck_shift${v}_r${r}.json'))['collective_kernels']['rows'];print({k: v['frac'] for k, v in d.items()})")"
+    done
+  done ;;
+handtreebench)  # the tree handover on tools/tree_bench.py (one tree at 8 / 64 / 128 MiB pieces, batched C4 slices)
+  mkdir -p gpurun_out/ab_hand
+  for r in 1 2; do
+    for v in ${SHIFTS:-def 6 0}; do
+      if [ "$v" = def ]; then unset CHR_XCD_HAND_SHIFT; else export CHR_XCD_HAND_SHIFT=$v; fi
+      timeout -k 10 300 python tools/tree_bench.py > gpurun_out/ab_hand/tb_shift${v}_r${r}.json 2>/dev/null || exit 1
+      echo "tree_bench shift=$v r=$r $(python -c "
+import json; d = json.load(open('gpurun_out/ab_hand/tb_shift${v}_r${r}.json'))
+a = {k: round(v['tree']['alg_GBps'] / 8000, 4) for k, v in d['tree_vs_folds_c4']['f32'].items()}
+b = {k: (v['batched_cold']['frac'], v['batched_warm']['frac']) for k, v in d['slice_batched_c4']['f32'].items()}
+print(a, b)")"
     done
   done ;;
 tree)  # the tree shape: policy vs the previous one (16 per CU, 512 KiB runs), collective-kernel rows, alternating
