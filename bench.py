@@ -754,7 +754,9 @@ def bench_allreduce(args):
                                    f"xGMI, device-resident", "k": k, "b": b, "count": count,
                        "schedule": (f"auto -> {sched_names.get(tuned[0], tuned[0])}, {tuned[1]} slices" if tuned
                                     else sched_env or "flat"),
-                       "parallelism": f"collective x{world}"},
+                       "parallelism": f"collective x{world}",
+                       # who started the ranks: bench.py itself (--gpus N) or an external launcher
+                       "launcher": "bench.py" if "CHR_BENCH_T0" in os.environ else "external"},
             "algbw_GBps": round(algbw, 2), "busbw_GBps": round(busbw, 2),
             # rank 0's host enqueue time per call: close to ms_per_step would mean host-bound
             "host_enqueue_ms_per_call": round(t_enq / args.steps * 1e3, 4),
