@@ -75,7 +75,7 @@ for step in "$@"; do
     ( while sleep 50; do date +%T >> "$OUT/heartbeat_launch8.txt"; done ) &
     hb=$!
     trap 'kill $hb 2>/dev/null' EXIT
-    CHR_BENCH_VIRTUAL_HOSTS=1 CHR_BENCH_DEADLINE_S=${DEADLINE:-150} CHR_SCHEDULE=flat run 700 bench_launch_n8_1gib.json \
+    CHR_BENCH_VIRTUAL_HOSTS=1 CHR_BENCH_DEADLINE_S=${DEADLINE:-150} CHR_SCHEDULE=${SCHED:-flat} run 700 "bench_launch_n8_1gib${SCHED:+_$SCHED}.json" \
       python bench.py --gpus 8 --steps 2 --warmup 1
     kill $hb ;;
   rehearse)
