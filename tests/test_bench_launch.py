@@ -119,3 +119,15 @@ def test_deadline_decision_is_rank0s_world2():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def test_launcher_kills_a_rank_group_past_its_limit(monkeypatch):
+    """A rank group still running at deadline + grace is killed as a process group (exit 124), so a
+    hung N>1 line cannot hold the node."""
+    import time
+
+    monkeypatch.setattr(bench, "KILL_GRACE_S", 1.0)
+    monkeypatch.setenv("CHR_BENCH_DEADLINE_S", "0.5")
+    t0 = time.time()
+    rc = bench.run_launcher([sys.executable, "-c", "import time; time.sleep(60)"])
+    assert rc == 124 and time.time() - t0 < 30
