@@ -233,15 +233,17 @@ __global__ __launch_bounds__(kBlock) void k_reduce_tree_scalar(TreeScalarArgs a)
 }
 
 // The odd-XCD handover for streaming tree launches (xcd_trip_w): each odd XCD hands 1/2^shift of its
-// share of a segment to the even XCD below.  The odd XCDs lag only when the leaves stream from HBM.
-// Same-box A/Bs (profiles/r04/ab_hand/, 2 alternating rounds each):
+// share of a segment to the even XCD below.  Same-box A/Bs (profiles/r04/ab_hand/, 2 alternating rounds
+// each):
 //  * HBM-cold leaves -- whole C4 calls on 8 virtual ranks, one grid per rank and slice
 //    (bench.py --collective-kernels): shift 7 0.754, 6 0.756-0.759, 5 0.760, 4 0.759-0.765, 3 0.745-0.749,
 //    off 0.749; tree_bench's cold batched slices: 6 and 4 +0.5-1.3 % over off;
 //  * leaves just rewritten (tree_bench's warm batched slices, 7 of 8 leaves copied in first, as RCCL's
 //    receives leave them on a node): off 0.759 / 0.756 at 16 MiB pieces, 6 0.752 / 0.757, 4 0.715 / 0.721.
-// On a node 7 of a tree's 8 leaves arrive over xGMI just before the launch, so the mild shift 6 is kept:
-// it gains on cold leaves and costs at most ~1 % on warm ones, where 4 costs 5 %.
+// (The bucket kernel's odd XCDs still lag on cache-resident operands, 2.2 % against 3 % cold: reduce_microbench
+// focus29; what the warm tree rows respond to is not pinned down.)  On a node 7 of a tree's 8 leaves arrive
+// over xGMI just before the launch, so the mild shift 6 is kept: it gains on cold leaves and costs at most
+// ~1 % on warm ones, where 4 costs 5 %.
 constexpr int kTreeXcdHandShift = 6;
 
 // XCD runs for streaming (nt) tree launches (profiles/r02/xcd_runs/ab_tree_*.json, C4 slice of 2

@@ -1896,6 +1896,17 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
+    if (argc > 1 && std::string(argv[1]) == "focus29") {  // the odd-XCD lag with cache-resident (warm) operands
+        for (int sets : {16, 1}) {  // 2 GiB rotation (HBM-cold) vs one 128 MiB set (Infinity Cache)
+            const size_t nvec = (64u << 20) / 16;
+            Sets S = make_sets(1, nvec, sets);
+            char lab[64];
+            std::snprintf(lab, sizeof lab, "runs256_sets%d", sets);
+            for (int r = 0; r < 2; ++r) focus24_one<false, 1, 0>(S, nvec, sets, 12, 0, 24, lab);
+            free_sets(S);
+        }
+        return 0;
+    }
     if (argc > 1 && std::string(argv[1]) == "focus25") {  // C2 timeline only: which XCD finishes last, launch after launch
         const size_t nvec = (64u << 20) / 16;
         Sets S = make_sets(1, nvec, 16);
