@@ -48,6 +48,7 @@ def _load():
         "chr_comm_destroy": ([vp], i),
         "chr_comm_rank": ([vp, ctypes.POINTER(i)], i),
         "chr_comm_size": ([vp, ctypes.POINTER(i)], i),
+        "chr_comm_info": ([vp, ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(i), ctypes.c_char_p, i], i),
         "chr_comm_stream": ([vp, pp], i),
         "chr_allreduce_radix_batch": ([vp, vp, sz, i, i, vp, i, i], i),
         "chr_reduce_scatter_radix_batch": ([vp, vp, sz, i, i, vp, i, i], i),
@@ -129,5 +130,5 @@ EXPORTED = [
     "chr_local_group_profile_read", "chr_reduce_scatter_mpich", "chr_reduce_scatter_mpich_async",
     "chr_local_reduce_scatter_mpich", "chr_local_group_set_batching",
     "chr_intra_reduce_scatter_radix_batch", "chr_inter_reduce_linear", "chr_intra_scatter_radix_batch",
-    "chr_local_phase_collective",
+    "chr_local_phase_collective", "chr_comm_info",
 ]

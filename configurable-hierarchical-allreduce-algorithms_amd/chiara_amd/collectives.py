@@ -126,6 +126,17 @@ def get_unique_id():
     return ctypes.string_at(ctypes.addressof(uid), ctypes.sizeof(uid))  # all 128 bytes (NULs included)
 
 
+def _env_overlap():
+    """The executor's default_overlap(): CHR_OVERLAP read with atoi, on when unset."""
+    import re
+
+    e = os.environ.get("CHR_OVERLAP")
+    if e is None:
+        return True
+    m = re.match(r"\s*[+-]?\d+", e)
+    return bool(m) and int(m.group(0)) != 0
+
+
 class Comm:
     """RCCL-backed communicator (one rank per process, one MI355X per rank)."""
 
@@ -138,6 +149,7 @@ class Comm:
               "chr_comm_init_rank")
         self._h = h
         self.rank, self.nranks, self.device = rank, nranks, device
+        self._overlap = _env_overlap()
 
     @classmethod
     def from_torch_distributed(cls, group=None, device=None):
@@ -159,6 +171,15 @@ class Comm:
     def handle(self):
         return self._h
 
+    def info(self):
+        """What RCCL's communicator reports (chr_comm_info): {"nranks": ncclCommCount, "rank":
+        ncclCommUserRank, "device": ncclCommCuDevice, "pci_bus_id": hipDeviceGetPCIBusId}."""
+        n, r, d = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        bus = ctypes.create_string_buffer(64)
+        check(lib().chr_comm_info(self._h, ctypes.byref(n), ctypes.byref(r), ctypes.byref(d), bus, len(bus)),
+              "chr_comm_info")
+        return {"nranks": n.value, "rank": r.value, "device": d.value, "pci_bus_id": bus.value.decode()}
+
     def set_slices(self, slices):
         """Pipeline depth (0 = automatic); results are bit-identical for every depth."""
         check(lib().chr_comm_set_slices(self._h, slices))
@@ -166,6 +187,12 @@ class Comm:
     def set_overlap(self, enable):
         """Reductions on a second stream, overlapped with the RCCL transfers (default on)."""
         check(lib().chr_comm_set_overlap(self._h, int(bool(enable))))
+        self._overlap = bool(enable)
+
+    @property
+    def overlap(self):
+        """Whether local reductions run on the compute stream beside the transfers (set_overlap)."""
+        return self._overlap
 
     def set_schedule(self, schedule):
         """SCHEDULE_REFERENCE / SCHEDULE_BALANCED / SCHEDULE_FLAT / SCHEDULE_EXACT / SCHEDULE_FLAT_AG /

@@ -1343,6 +1343,24 @@ int chr_comm_size(const chr_comm* c, int* n) {
     return CHR_SUCCESS;
 }
 
+int chr_comm_info(const chr_comm* c, int* rccl_nranks, int* rccl_rank, int* rccl_device, char* pci_bus_id,
+                  int len) {
+    if (!c || !rccl_nranks || !rccl_rank || !rccl_device || (!pci_bus_id && len > 0) || len < 0)
+        return CHR_ERR_INVALID_ARG;
+    if (c->failed || !c->nccl) return CHR_ERR_ABORTED;
+    // what RCCL's communicator itself holds, not this struct's copy of the init arguments
+    int rc = nccl_code(ncclCommCount(c->nccl, rccl_nranks));
+    if (!rc) rc = nccl_code(ncclCommUserRank(c->nccl, rccl_rank));
+    if (!rc) rc = nccl_code(ncclCommCuDevice(c->nccl, rccl_device));
+    if (rc) return rc;
+    if (len > 0) {
+        pci_bus_id[0] = '\0';
+        const hipError_t e = hipDeviceGetPCIBusId(pci_bus_id, len, *rccl_device);
+        if (e != hipSuccess) return hip_code(e);
+    }
+    return CHR_SUCCESS;
+}
+
 int chr_comm_set_timeout(chr_comm* c, int timeout_ms) {
     if (!c || timeout_ms < 0) return CHR_ERR_INVALID_ARG;
     c->timeout_ms = timeout_ms;

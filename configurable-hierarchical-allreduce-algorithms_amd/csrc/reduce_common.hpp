@@ -270,9 +270,10 @@ __host__ __device__ __forceinline__ size_t xcd_trip(uint32_t b, uint32_t full, u
 // identity (trip = block - 8 x hand).  kIdleTrip: a workgroup with nothing to do.
 constexpr size_t kIdleTrip = ~(size_t)0;
 constexpr int kXcdHandShift = 6;
+// `env` < 0: the policy shift; 0: off; shifts past 31 hand nothing (a 32-bit shift by >= 32 is undefined)
 inline uint32_t xcd_hand(uint32_t full, int env) {
     const int shift = env >= 0 ? env : kXcdHandShift;
-    return shift <= 0 ? 0u : (full >> 3) >> shift;
+    return shift <= 0 || shift > 31 ? 0u : (full >> 3) >> shift;
 }
 __host__ __device__ __forceinline__ size_t xcd_own(uint32_t x, uint32_t i, uint32_t cs) {
     return ((((size_t)(i >> cs)) * 8u + x) << cs) | (i & ((1u << cs) - 1u));

@@ -137,7 +137,7 @@ ReduceTuning& reduce_tuning() {
         s = std::getenv("CHR_WG_PER_CU_TREE");
         r.wg_per_cu_tree = s ? std::max(0, std::atoi(s)) : -1;
         s = std::getenv("CHR_XCD_HAND_SHIFT");
-        r.xcd_hand_shift = s ? std::max(0, std::atoi(s)) : -1;
+        r.xcd_hand_shift = s ? std::min(31, std::max(0, std::atoi(s))) : -1;  // [0, 31]; 31 hands nothing
         int dev = 0, lds = 0, blk = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess ||

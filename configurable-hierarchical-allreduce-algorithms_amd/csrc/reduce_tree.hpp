@@ -52,8 +52,9 @@ struct TreeArgs {
     TreeSeg seg[kMaxTreeSegs];
     int nseg;
     int nl;
+    uint32_t hand[kMaxTreeSegs];   // each segment's odd-XCD handover in trips (xcd_trip_w); 0 = none.  Computed
+                                   // once, by the launcher, which also sizes the grid from it
     uint32_t xrun;    // log2 of the trips per XCD run within a segment (xcd_trip); set by the launcher
-    uint32_t hshift;  // odd-XCD handover per segment, hand = (xfull / 8) >> hshift (xcd_trip_w); 0 = none
 };
 
 // A segment's vector body is at most this many 16-B vectors (1 GiB per operand); longer trees are
@@ -151,23 +152,24 @@ __global__ __launch_bounds__(BL) void k_reduce_tree(TreeArgs a) {
     // this workgroup's segment: one pass over the block0 table (scalar compares, no loop-carried
     // loads), then the segment's pointers pinned into SGPRs before the first vector load
     const uint32_t b = blockIdx.x, xrun = a.xrun;
-    uint32_t b0s[kMaxTreeSegs], xfs[kMaxTreeSegs];
+    uint32_t b0s[kMaxTreeSegs], xfs[kMaxTreeSegs], hds[kMaxTreeSegs];
 #pragma unroll
     for (int j = 0; j < kMaxTreeSegs; ++j) {
         b0s[j] = a.block0[j];
         xfs[j] = a.xfull[j];
+        hds[j] = a.hand[j];
         pin_sgpr_u32(b0s[j], xfs[j]);
+        pin_sgpr_u32(hds[j], xrun);
     }
-    const uint32_t hshift = a.hshift;
-    pin_sgpr_u32(xrun, hshift);
     int s = 0;
-    uint32_t b0 = 0, xfull = xfs[0];
+    uint32_t b0 = 0, xfull = xfs[0], hand = hds[0];
 #pragma unroll
     for (int j = 1; j < kMaxTreeSegs; ++j)
         if (b >= b0s[j]) {
             s = j;
             b0 = b0s[j];
             xfull = xfs[j];
+            hand = hds[j];
         }
     const TreeSeg& g = a.seg[s];
     u32x4* const out = g.out;
@@ -179,9 +181,8 @@ __global__ __launch_bounds__(BL) void k_reduce_tree(TreeArgs a) {
     pin_sgpr(out, leaves[0], nvec, comb, swaps);
 #pragma unroll
     for (int j = 1; j < NL; ++j) pin_sgpr(leaves[j]);
-    // segments start on a multiple of 8 blocks when hshift is set, so a local block's XCD parity is
+    // segments start on a multiple of 8 blocks when a handover is set, so a local block's XCD parity is
     // its global one
-    const uint32_t hand = hshift ? (xfull >> 3) >> hshift : 0u;
     const size_t trip = xcd_trip_w(b - b0, xfull, xrun, hand);
     if (trip == kIdleTrip) return;
     const size_t base = trip * BL * U + threadIdx.x;
@@ -289,20 +290,22 @@ inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
     a.xrun = NT ? xcd_run_shift(tree_xcd_run_kib<NL>(), (size_t)BL * U * 16) : 0;
     // the odd-XCD handover of streaming launches (xcd_hand / xcd_trip_w in reduce_common.hpp), per segment
     const int henv = reduce_tuning().xcd_hand_shift;
-    a.hshift = NT ? (uint32_t)(henv >= 0 ? henv : kTreeXcdHandShift) : 0u;
+    const int hshift = NT ? (henv >= 0 ? henv : kTreeXcdHandShift) : 0;
     size_t grid = 0;
     for (int j = 0; j < kMaxTreeSegs; ++j) {
         if (j >= a.nseg) {
             a.block0[j] = ~0u;
             a.xfull[j] = 0;
+            a.hand[j] = 0;
             continue;
         }
         if (a.seg[j].nvec > kMaxSegVec) return hipErrorInvalidValue;  // launch_reduce_tree_multi cuts them
         const size_t trips = (a.seg[j].nvec + (size_t)BL * U - 1) / ((size_t)BL * U);
-        if (a.hshift) grid = (grid + 7) & ~(size_t)7;  // the segment starts on XCD 0 (its padding blocks idle)
+        if (hshift) grid = (grid + 7) & ~(size_t)7;  // the segment starts on XCD 0 (its padding blocks idle)
         a.block0[j] = (uint32_t)grid;
         a.xfull[j] = xcd_full((uint32_t)trips, a.xrun);
-        grid += trips + (a.hshift ? 8u * ((a.xfull[j] >> 3) >> a.hshift) : 0u);
+        a.hand[j] = xcd_hand(a.xfull[j], hshift);  // the kernel maps with exactly the hand the grid is sized for
+        grid += trips + 8u * (size_t)a.hand[j];
     }
     if (grid == 0) return hipSuccess;
     const unsigned lds = NT ? nt_lds_bytes(reduce_tuning().wg_per_cu_tree, tree_wg_per_cu<NL>()) : 0;

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define CHR_ABI_VERSION 8  /* 8: the stand-alone phase collectives (chr_intra_reduce_scatter_radix_batch, ...) */
+#define CHR_ABI_VERSION 9  /* 9: chr_comm_info; 8: the stand-alone phase collectives (chr_intra_reduce_scatter_radix_batch, ...) */
 
 /* Element types.  The reference is generic over MPI_Datatype (all_reduce_radix_batch.cpp:202-204,
  * sizes from MPI_Type_size at :234-277); these are the MPI predefined types MPICH's
@@ -158,6 +158,13 @@ int chr_comm_synchronize(chr_comm* comm);
 int chr_comm_is_aborted(const chr_comm* comm);
 int chr_comm_rank(const chr_comm* comm, int* rank);
 int chr_comm_size(const chr_comm* comm, int* nranks);
+/* What RCCL's communicator itself reports -- ncclCommCount, ncclCommUserRank, ncclCommCuDevice --
+ * and that device's PCI bus id (hipDeviceGetPCIBusId, "dddd:bb:dd.f", NUL-terminated in `len` bytes;
+ * len 0 skips it).  The record of which GPUs a multi-GPU run's ranks were on (bench.py's N>1 line):
+ * the reference's ranks are MPI processes (MPI_Comm_rank / MPI_Comm_size,
+ * Fugaku_experiments/Allreduce/main.cpp:116-117).  CHR_ERR_ABORTED on an aborted communicator. */
+int chr_comm_info(const chr_comm* comm, int* rccl_nranks, int* rccl_rank, int* rccl_device, char* pci_bus_id,
+                  int len);
 /* The stream all of this communicator's collective work is enqueued on.  It is a blocking
  * stream: it orders after work on the legacy NULL stream (hipMemset, default-stream kernels),
  * as an MPI caller expects.  Work that produces `send` on another non-blocking stream must be

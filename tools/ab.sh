@@ -99,6 +99,69 @@ tree)  # the tree shape: policy vs the previous one (16 per CU, 512 KiB runs), c
     done
   done
   unset CHR_WG_PER_CU_TREE CHR_XCD_RUN_KIB ;;
-*) echo "usage: tools/ab.sh cap|runs|tree"; exit 2 ;;
+mid)  # mid-size buckets: streaming shape (nt, one wave) vs plain 256-thread at 4-64 MiB,
+      # m = 1 and 3, the sweep's rotation (16 sets) and an HBM-cold one (>= 2 GiB), gated, 3 alternating rounds
+  mkdir -p gpurun_out/ab_mid
+  for r in 1 2 3; do
+    for v in 0 1; do
+      for rot in "--sets 16" "--ws-mib 2048"; do
+        tag="nt${v}_$(echo $rot | tr -d ' -')_r${r}"
+        CHR_REDUCE_NT=$v timeout -k 10 200 python tools/mstream_probe.py --ms 1,3 --mib 4,8,16,32,64 --layouts sep \
+          $rot --reps 200 --gate --tag "$tag" >> gpurun_out/ab_mid/mid.jsonl 2>>gpurun_out/ab_mid/mid.err || exit 1
+        echo "mid $tag done"
+      done
+    done
+  done ;;
+mid2)  # follow-ups of `mid`: the cache-resident case (1-2 sets), the streaming shape's cap / XCD runs / hand at
+       # 8-32 MiB, and the HIP runtime's kernel fence options (what the inter-launch gap is made of)
+  mkdir -p gpurun_out/ab_mid
+  P="python tools/mstream_probe.py --layouts sep --reps 200 --gate"
+  for r in 1 2; do
+    for v in 0 1; do
+      CHR_REDUCE_NT=$v timeout -k 10 200 $P --ms 1,3 --mib 4,8,16,32,64 --sets 1,2 --tag "warm_nt${v}_r${r}" \
+        >> gpurun_out/ab_mid/mid2.jsonl 2>>gpurun_out/ab_mid/mid2.err || exit 1
+    done
+    for c in 0 12 16 24; do
+      CHR_REDUCE_NT=1 CHR_WG_PER_CU_VEC=$c timeout -k 10 200 $P --ms 1,3 --mib 8,16,32 --ws-mib 2048 --tag "cap${c}_r${r}" \
+        >> gpurun_out/ab_mid/mid2.jsonl 2>>gpurun_out/ab_mid/mid2.err || exit 1
+    done
+    for x in 0 256 1024; do
+      CHR_REDUCE_NT=1 CHR_XCD_RUN_KIB=$x timeout -k 10 200 $P --ms 1,3 --mib 8,16,32 --ws-mib 2048 --tag "xrun${x}_r${r}" \
+        >> gpurun_out/ab_mid/mid2.jsonl 2>>gpurun_out/ab_mid/mid2.err || exit 1
+    done
+    for h in 0 4; do
+      CHR_REDUCE_NT=1 CHR_XCD_HAND_SHIFT=$h timeout -k 10 200 $P --ms 1,3 --mib 8,16,32 --ws-mib 2048 --tag "hand${h}_r${r}" \
+        >> gpurun_out/ab_mid/mid2.jsonl 2>>gpurun_out/ab_mid/mid2.err || exit 1
+    done
+    for f in "AMD_OPT_FLUSH=0" "AMD_OPT_FLUSH=1" "DEBUG_CLR_SKIP_RELEASE_SCOPE=1"; do
+      env CHR_REDUCE_NT=1 $f timeout -k 10 200 $P --ms 1 --mib 1,4,16,64 --ws-mib 2048 --tag "${f}_r${r}" \
+        >> gpurun_out/ab_mid/mid2.jsonl 2>>gpurun_out/ab_mid/mid2.err || exit 1
+    done
+    echo "mid2 r=$r done"
+  done ;;
+xrun)  # the translation cliff: XCD run length vs working sets past the translation
+       # caches' reach -- m = 1/3/7 at 1 GiB buckets (one set: every call walks 3-9 GiB) and 256 MiB rotated
+       # over ~5 GiB; 512 KiB (policy for m >= 3), 2/4/8 MiB runs (each 2 MiB fragment on one XCD), identity
+  mkdir -p gpurun_out/ab_xrun
+  P="python tools/mstream_probe.py --layouts sep --reps 12 --gate"
+  for r in 1 2; do
+    for x in ${XRUNS:-512 2048 4096 8192 0}; do
+      CHR_XCD_RUN_KIB=$x timeout -k 10 300 $P --ms 1,3,7 --mib 1024 --sets 1 --tag "xrun${x}_1g_r${r}" \
+        >> gpurun_out/ab_xrun/xrun.jsonl 2>>gpurun_out/ab_xrun/xrun.err || exit 1
+      CHR_XCD_RUN_KIB=$x timeout -k 10 300 $P --ms 3,7 --mib 256 --ws-mib 5120 --tag "xrun${x}_256m_ws5g_r${r}" \
+        >> gpurun_out/ab_xrun/xrun.jsonl 2>>gpurun_out/ab_xrun/xrun.err || exit 1
+      echo "xrun $x r=$r done"
+    done
+  done ;;
+xrunpmc)  # translation counters beside the rates above: m = 3, 1 GiB, one set, policy vs 2 MiB runs
+  mkdir -p gpurun_out/ab_xrun
+  for x in 512 ${XRUN_PMC:-2048}; do
+    CHR_XCD_RUN_KIB=$x timeout -s KILL 120 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum \
+      GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE --output-format csv -d "$PWD/gpurun_out/ab_xrun/pmc_x$x" -o run \
+      -- python3 tools/mstream_probe.py --layouts sep --reps 6 --ms 3 --mib 1024 --sets 1 \
+      > gpurun_out/ab_xrun/pmc_x$x.txt 2>&1 || exit 1
+    echo "xrunpmc $x done"
+  done ;;
+*) echo "usage: tools/ab.sh cap|runs|tree|mid|mid2|xrun|xrunpmc"; exit 2 ;;
 esac
 echo AB_DONE

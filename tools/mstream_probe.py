@@ -60,6 +60,13 @@ def main():
     ap.add_argument("--layouts", default="sep,slab,slab+4k,slab+64k,slab+2m4k")
     ap.add_argument("--reps", type=int, default=12)
     ap.add_argument("--sets", default="", help="buffer sets to rotate over (comma list; default: >= 2 GiB)")
+    ap.add_argument("--ws-mib", default="",
+                    help="working sets to rotate over, in MiB (comma list): sets = max(1, ws / ((m + 1) * bucket)), "
+                         "at most 64; overrides --sets")
+    ap.add_argument("--gate", action="store_true",
+                    help="an untimed spin kernel ahead of the start event (bench.py's gate): the host enqueues "
+                         "the timed launches while the GPU is busy, so small buckets are not host-bound")
+    ap.add_argument("--tag", default="", help="copied into every line (e.g. the A/B arm)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     s = torch.cuda.current_stream(dev)
@@ -68,7 +75,11 @@ def main():
             nbytes = mib << 20
             n = nbytes // 4
             auto = max(1, min(4, (2048 << 20) // ((m + 1) * nbytes)))
-            for lay, sets in [(x, int(y)) for x in a.layouts.split(",") for y in (a.sets.split(",") if a.sets else [auto])]:
+            if a.ws_mib:
+                set_list = [max(1, min(64, (int(w) << 20) // ((m + 1) * nbytes))) for w in a.ws_mib.split(",")]
+            else:
+                set_list = [int(y) for y in a.sets.split(",")] if a.sets else [auto]
+            for lay, sets in [(x, y) for x in a.layouts.split(",") for y in set_list]:
                 bufs, keep = [], []
                 for si in range(sets):
                     if lay.split("/")[0] == "contig":
@@ -103,8 +114,12 @@ def main():
 
                 for i in range(2):
                     ca.check(go(i))
+                for i in range(sets):  # every set streamed once before timing
+                    ca.check(go(i))
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 torch.cuda.synchronize()
+                if a.gate:
+                    torch.cuda._sleep(1_000_000)
                 e0.record(s)
                 for i in range(a.reps):
                     go(i)
@@ -112,7 +127,9 @@ def main():
                 torch.cuda.synchronize()
                 us = e0.elapsed_time(e1) / a.reps * 1e3
                 gbps = (m + 2) * nbytes / (us * 1e-6) / 1e9
-                print(json.dumps({"m": m, "bucket_MiB": mib, "layout": lay, "sets": sets, "us": round(us, 2),
+                print(json.dumps({"m": m, "bucket_MiB": mib, "layout": lay, "sets": sets,
+                                  "working_set_MiB": sets * (m + 1) * mib, "tag": a.tag,
+                                  "nt": os.environ.get("CHR_REDUCE_NT", "policy"), "reps": a.reps, "us": round(us, 2),
                                   "GBps": round(gbps, 1), "frac": round(gbps / 8000, 4)}), flush=True)
                 del bufs, keep
                 torch.cuda.synchronize()
