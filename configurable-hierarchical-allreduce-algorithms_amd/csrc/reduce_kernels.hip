@@ -14,7 +14,7 @@
 //    U independent vectors per lane in flight (ILP) with every operand's loads issued
 //    before the first add, one trip per workgroup (the full grid measured faster than a
 //    capped grid-stride grid on large buckets);
-//  * non-temporal loads and stores for calls that stream >= 128 MiB (HBM-cold buckets
+//  * non-temporal loads and stores for calls that stream >= 40 MiB (HBM-cold buckets
 //    +15-40 % over plain accesses; plain stays faster on small, cache-warm calls);
 //  * workgroup size by regime: one wave (64 threads) for the streaming (nt) calls, +3 % on
 //    the 64 MiB m=1 bucket and up to +5 % for m >= 3 (profiles/r01/block_ab_*); 256 threads
@@ -126,7 +126,15 @@ ReduceTuning& reduce_tuning() {
         s = std::getenv("CHR_REDUCE_NT");     // 0 / 1 / unset = by size
         r.nt_mode = s ? std::atoi(s) : -1;
         s = std::getenv("CHR_REDUCE_NT_MIN_BYTES");
-        r.nt_min_bytes = s ? (size_t)std::atoll(s) : (size_t)128 << 20;
+        // bucket launches stream from 40 MiB per call (profiles/r05/ab_mid/, 2-3 alternating
+        // rounds, gated back-to-back launches): the streaming shape (nt, one wave, U / cap / XCD runs per fan-in)
+        // against plain 256-thread workgroups -- m = 1 at 16 MiB (48 MiB per call) 0.624-0.626 vs 0.583-0.585 on
+        // a 2 GiB rotation and 0.644-0.647 vs 0.586-0.589 on the sweep's 16 sets, 32 MiB 0.72-0.75 vs 0.65, m = 3
+        // at 8 MiB (40 MiB) 0.61-0.64 vs 0.56-0.57; below, plain wins where the rotation stays cache-resident
+        // (m = 1 at 8 MiB over 16 sets 0.604 vs 0.535, m = 3 at 4 MiB 0.565 vs 0.508).  One set reused call
+        // after call (fully cache-resident) prefers plain up to 48 MiB per call too (m = 1 16 MiB 1.26 vs
+        // 0.87 of 8 TB/s): a just-reduced region reduced again; the collectives' trees keep their own threshold.
+        r.nt_min_bytes = s ? (size_t)std::atoll(s) : (size_t)40 << 20;
         // trees stream 3-9 operands at once: from 64 MiB per launch the nt shapes win on HBM-cold
         // leaves and tie on cache-warm ones (C4 slice, 4 MiB pieces = 72 MiB: nt 0.591-0.602 vs
         // plain 0.572-0.577 cold, 0.651-0.657 vs 0.599-0.666 warm; 2 MiB pieces tie;
@@ -138,6 +146,17 @@ ReduceTuning& reduce_tuning() {
         r.wg_per_cu_tree = s ? std::max(0, std::atoi(s)) : -1;
         s = std::getenv("CHR_XCD_HAND_SHIFT");
         r.xcd_hand_shift = s ? std::min(31, std::max(0, std::atoi(s))) : -1;  // [0, 31]; 31 hands nothing
+        s = std::getenv("CHR_TLB_PF_TRIPS");  // multiple of 8 (same XCD); 0 / unset = off
+        r.tlb_pf_trips = s ? (unsigned)std::max(0, std::atoi(s)) & ~7u : 0u;
+        s = std::getenv("CHR_TREE_BL");
+        r.tree_bl = s && std::atoi(s) == 128 ? 128 : 64;
+        s = std::getenv("CHR_TLB_PF_PAGE_KIB");
+        {
+            const unsigned kib = s ? (unsigned)std::max(4, std::atoi(s)) : 2048u;
+            unsigned lg = 12;
+            while ((1u << (lg + 1)) <= kib * 1024u && lg < 30) ++lg;
+            r.tlb_pf_page_log2 = lg;
+        }
         int dev = 0, lds = 0, blk = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess ||

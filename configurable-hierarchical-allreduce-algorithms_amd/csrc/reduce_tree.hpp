@@ -308,7 +308,8 @@ inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
         grid += trips + 8u * (size_t)a.hand[j];
     }
     if (grid == 0) return hipSuccess;
-    const unsigned lds = NT ? nt_lds_bytes(reduce_tuning().wg_per_cu_tree, tree_wg_per_cu<NL>()) : 0;
+    // the policy's resident waves per CU, whatever the workgroup size (BL / 64 waves each)
+    const unsigned lds = NT ? nt_lds_bytes(reduce_tuning().wg_per_cu_tree, tree_wg_per_cu<NL>() / (BL / 64)) : 0;
     hipLaunchKernelGGL((k_reduce_tree<DT, OP, NL, U, NT, BL>), dim3((unsigned)grid), dim3(BL), lds, s, a);
     return hipGetLastError();
 }
@@ -347,7 +348,11 @@ inline hipError_t launch_tree_nl(const TreeArgs& a, const TreeScalarArgs* sa, hi
     const size_t call_bytes = (size_t)(a.nl + 1) * nvec * 16;
     const bool nt = t.nt_mode == 1 || (t.nt_mode < 0 && call_bytes >= t.tree_nt_min_bytes);
     if constexpr (is_pair_dt<DT>() || is_complex_dt<DT>()) return launch_tree_vec<DT, OP, NL, 256, false>(a, s);  // as launch_vec_m
-    else return nt ? launch_tree_vec<DT, OP, NL, 64, true>(a, s) : launch_tree_vec<DT, OP, NL, 256, false>(a, s);
+    else if constexpr (NL >= 5) {
+        // A/B knob (CHR_TREE_BL=128): two-wave workgroups at the same waves per CU (tree_wg_per_cu halved)
+        if (nt && t.tree_bl == 128) return launch_tree_vec<DT, OP, NL, 128, true>(a, s);
+        return nt ? launch_tree_vec<DT, OP, NL, 64, true>(a, s) : launch_tree_vec<DT, OP, NL, 256, false>(a, s);
+    } else return nt ? launch_tree_vec<DT, OP, NL, 64, true>(a, s) : launch_tree_vec<DT, OP, NL, 256, false>(a, s);
 }
 
 template <int DT, int OP>

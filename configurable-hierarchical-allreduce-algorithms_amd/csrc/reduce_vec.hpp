@@ -20,6 +20,8 @@ struct VecArgs {
     uint32_t xrun;   // log2 of the trips per XCD run (xcd_trip); set by the launcher
     uint32_t xfull;  // blocks [0, xfull) are remapped (xcd_full of the grid); set per launch
     uint32_t hand;   // trips each odd XCD hands to the even one below (xcd_trip_w); 0 = none
+    uint32_t pf;     // translation prefetch: workgroups ahead (multiple of 8), 0 = off (tlb_pf_one)
+    uint32_t pf_page_log2;
 };
 
 // U vectors (16 B each) per lane per trip; all M+1 operands of the trip are loaded
@@ -69,6 +71,17 @@ __global__ __launch_bounds__(BL) void k_reduce_vec(VecArgs a) {
         for (int j = 0; j < M; ++j)
 #pragma unroll
             for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&ins[j][base + (size_t)u * BL]);
+        // translation prefetch (after the trip's own loads, so waiting for those never waits for it)
+        uint32_t pfv[M + 2];
+        const bool pf_now = a.pf && tlb_pf_due(blockIdx.x, a.pf, xfull, xrun, (size_t)BL * U * 16, a.pf_page_log2,
+                                               nvec / ((size_t)BL * U));
+        if (pf_now) {
+            const size_t t2 = xcd_trip(blockIdx.x + a.pf, xfull, xrun) * BL * U;
+            pfv[0] = tlb_touch(&accp[t2]);
+            pfv[1] = tlb_touch(&out[t2]);
+#pragma unroll
+            for (int j = 0; j < M; ++j) pfv[2 + j] = tlb_touch(&ins[j][t2]);
+        }
         // Keep every load of the trip ahead of the first add: without this the
         // scheduler interleaves the first add (and its vmcnt(0)) between the loads.
         __builtin_amdgcn_sched_barrier(0);
@@ -78,6 +91,7 @@ __global__ __launch_bounds__(BL) void k_reduce_vec(VecArgs a) {
             for (int u = 0; u < U; ++u) acc[u] = apply_vec<DT, OP>(x[j][u], acc[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) st<NT>(&out[base + (size_t)u * BL], acc[u]);
+        if (pf_now) tlb_retire<M + 2>(pfv);
     } else {
         for (int u = 0; u < U; ++u) {
             const size_t i = base + (size_t)u * BL;
@@ -177,6 +191,8 @@ inline hipError_t for_each_launch_piece(VecArgs a, L launch) {
         const unsigned trips = (unsigned)((p.nvec + (size_t)BL * U - 1) / ((size_t)BL * U));
         p.xfull = xcd_full(trips, p.xrun);
         p.hand = WEIGHTED ? xcd_hand(p.xfull, reduce_tuning().xcd_hand_shift) : 0u;
+        p.pf = WEIGHTED ? reduce_tuning().tlb_pf_trips : 0u;  // streaming launches only
+        p.pf_page_log2 = reduce_tuning().tlb_pf_page_log2;
         launch(p, trips + 8u * p.hand);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
@@ -184,9 +200,9 @@ inline hipError_t for_each_launch_piece(VecArgs a, L launch) {
     return hipSuccess;
 }
 
-// Policy (profiles/r01/block_ab_*): calls that stream >= 128 MiB run non-temporal with
-// one-wave workgroups and the first accumulator slot temporal (ACC0); smaller, cache-warm
-// calls keep plain accesses and 256-thread workgroups.  Only these two shapes are compiled into
+// Policy (profiles/r01/block_ab_*, profiles/r05/ab_mid/): calls that stream >= 40 MiB (nt_min_bytes)
+// run non-temporal with one-wave workgroups and the first accumulator slot temporal (ACC0); smaller,
+// cache-warm calls keep plain accesses and 256-thread workgroups.  Only these two shapes are compiled into
 // the library; the design-space variants (other workgroup sizes, all-nt accumulators) live in
 // tools/reduce_microbench.hip, which instantiates the kernel templates directly.
 template <int DT, int OP, int M, int BL, bool NT, bool ACC0>

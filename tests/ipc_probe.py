@@ -10,12 +10,18 @@ with dmabuf IPC (HSA_ENABLE_IPC_MODE_LEGACY=0, which bench.py and chiara_amd set
                               print OK
 
 Plain ctypes over torch's libamdhip64 (the same HIP runtime the product links); no torch.cuda call, so
-nothing but these HIP calls touches the GPU.  Used by tests/test_gpu_rccl_multirank.py."""
+nothing but these HIP calls touches the GPU.  Used by tests/test_gpu_ipc.py."""
 import ctypes
 import os
 import sys
 
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+
+class IpcHandle(ctypes.Structure):
+    """hipIpcMemHandle_t: 64 opaque bytes, passed BY VALUE to hipIpcOpenMemHandle (a ctypes array argtype
+    would be passed as a pointer)."""
+    _fields_ = [("reserved", ctypes.c_char * 64)]
 
 
 def hip():
@@ -27,7 +33,7 @@ def hip():
     lib.hipFree.argtypes = [vp]
     lib.hipMemcpy.argtypes = [vp, vp, sz, ctypes.c_int]
     lib.hipIpcGetMemHandle.argtypes = [ctypes.c_char_p, vp]
-    lib.hipIpcOpenMemHandle.argtypes = [ctypes.POINTER(vp), ctypes.c_char * 64, ctypes.c_uint]
+    lib.hipIpcOpenMemHandle.argtypes = [ctypes.POINTER(vp), IpcHandle, ctypes.c_uint]
     lib.hipIpcCloseMemHandle.argtypes = [vp]
     lib.hipSetDevice.argtypes = [ctypes.c_int]
     return lib
@@ -71,7 +77,7 @@ def main():
     else:
         hx, nbytes = sys.argv[2], int(sys.argv[3])
         n = nbytes // 4
-        h = (ctypes.c_char * 64).from_buffer_copy(bytes.fromhex(hx))
+        h = IpcHandle.from_buffer_copy(bytes.fromhex(hx))
         p = ctypes.c_void_p()
         ck(lib.hipIpcOpenMemHandle(ctypes.byref(p), h, 1), "hipIpcOpenMemHandle")  # hipIpcMemLazyEnablePeerAccess
         got = words(n, lambda i: 0)

@@ -21,7 +21,7 @@ def _env():
     return env
 
 
-@pytest.mark.parametrize("nbytes", [4096, 64 << 20])
+@pytest.mark.parametrize("nbytes", [4096, 8 << 20])
 def test_hip_ipc_handle_between_two_processes(nbytes):
     owner = subprocess.Popen([sys.executable, PROBE, "owner", str(nbytes)], stdin=subprocess.PIPE,
                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=_env())

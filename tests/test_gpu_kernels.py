@@ -113,7 +113,7 @@ def test_float_logical_ops(gu, dtype, op, m):
 
 @pytest.mark.parametrize("dtype", ["u8", "i16", "i64", "u64"])
 def test_integer_types_streaming_path(gu, dtype):
-    """>= 128 MiB calls switch to the non-temporal one-wave instantiation."""
+    """>= 40 MiB calls switch to the non-temporal one-wave instantiation."""
     n = (48 << 20) // np.dtype(po.NP_DTYPES[dtype]).itemsize
     _check_multi(gu, dtype, "sum", 1, n)
     _check_multi(gu, dtype, "max", 3, n // 2 + 7)
@@ -183,7 +183,7 @@ def test_bucket_sizes_1k_to_1g(gu, nbytes):
                                                     ("f64", "sum", 7, 16 << 20, 3), ("i32", "prod", 2, 48 << 20, 2),
                                                     ("bf16", "sum", 1, 64 << 20, 5)])
 def test_streaming_path_ragged(gu, dtype, op, m, nbytes, off):
-    """Calls that stream >= 128 MiB take the nt / one-wave / ACC0 instantiation: ragged counts and
+    """Calls that stream >= 40 MiB take the nt / one-wave / ACC0 instantiation: ragged counts and
     misaligned heads there too (scalar head and tail around the vector body)."""
     es = np.dtype(po.NP_DTYPES[dtype]).itemsize
     _check_multi(gu, dtype, op, m, nbytes // es + 12345, off, seed=21)

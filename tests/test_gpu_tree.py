@@ -103,7 +103,7 @@ def test_out_aliases_leaf(gu):
 
 
 def test_large_nt_path(gu):
-    """>= 128 MiB streamed per call takes the non-temporal instantiation."""
+    """>= 64 MiB streamed per call takes the non-temporal instantiation."""
     _run(gu, "f32", "sum", *C4_TREE, (16 << 20) + 7)
 
 

@@ -2,7 +2,7 @@
 
 Streaming (nt) launches place each workgroup's trip by xcd_trip: runs of 2^cs consecutive trips per
 XCD, identity for the blocks past the last whole 8 * 2^cs group.  A wrong map shows up as elements
-never written or written twice.  The policy only engages on >= 128 MiB calls, so these tests run in
+never written or written twice.  The policy only engages on >= 40 MiB calls (bucket) / 64 MiB (trees), so these tests run in
 a child process with CHR_REDUCE_NT=1 (nt at any size) and small runs (CHR_XCD_RUN_KIB) so that
 ragged trip counts, partial groups and the tail trip all occur at oracle-sized inputs.  Bit-exact
 against the oracle, for the bucket kernel (m = 1, 3, 7) and for batched trees (segments whose first

@@ -162,6 +162,58 @@ xrunpmc)  # translation counters beside the rates above: m = 3, 1 GiB, one set, 
       > gpurun_out/ab_xrun/pmc_x$x.txt 2>&1 || exit 1
     echo "xrunpmc $x done"
   done ;;
-*) echo "usage: tools/ab.sh cap|runs|tree|mid|mid2|xrun|xrunpmc"; exit 2 ;;
+tlbpf)  # translation prefetch (CHR_TLB_PF_TRIPS: workgroups ahead; CHR_TLB_PF_PAGE_KIB: granule) past the
+        # translation caches' reach, and C2 with it off (the policy) to check the code costs nothing there
+  mkdir -p gpurun_out/ab_tlbpf
+  P="python tools/mstream_probe.py --layouts sep --reps 12 --gate"
+  for r in 1 2; do
+    for v in ${PFS:-0 2816 5632 11264 2816/512 2816/64}; do
+      pf=${v%%/*}; pg=2048; [ "$v" != "$pf" ] && pg=${v##*/}
+      CHR_TLB_PF_TRIPS=$pf CHR_TLB_PF_PAGE_KIB=$pg timeout -k 10 300 $P --ms 1,3,7 --mib 1024 --sets 1 \
+        --tag "pf${pf}_pg${pg}_1g_r${r}" >> gpurun_out/ab_tlbpf/pf.jsonl 2>>gpurun_out/ab_tlbpf/pf.err || exit 1
+      CHR_TLB_PF_TRIPS=$pf CHR_TLB_PF_PAGE_KIB=$pg timeout -k 10 300 $P --ms 3 --mib 256 --ws-mib 5120 \
+        --tag "pf${pf}_pg${pg}_256m_ws5g_r${r}" >> gpurun_out/ab_tlbpf/pf.jsonl 2>>gpurun_out/ab_tlbpf/pf.err || exit 1
+      echo "tlbpf $v r=$r done"
+    done
+    timeout -k 10 120 python bench.py --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/ab_tlbpf/c2_r${r}.json \
+      2>/dev/null || exit 1
+    echo "c2 r=$r $(frac gpurun_out/ab_tlbpf/c2_r${r}.json)"
+  done ;;
+treebl)  # two-wave tree workgroups (CHR_TREE_BL=128, same waves per CU) and the
+         # tree handover off, on the in-collective rows (rank-alone rows: one GPU's own grids, whole-call spans)
+  mkdir -p gpurun_out/ab_treebl
+  for r in 1 2; do
+    for v in ${ARMS:-64_def 128_def 64_0 128_0}; do
+      bl=${v%%_*}; h=${v##*_}
+      if [ "$h" = def ]; then unset CHR_XCD_HAND_SHIFT; else export CHR_XCD_HAND_SHIFT=$h; fi
+      CHR_TREE_BL=$bl timeout -k 10 400 python bench.py --collective-kernels > gpurun_out/ab_treebl/ck_${v}_r${r}.json \
+        2>/dev/null || exit 1
+      echo "treebl $v r=$r $(python -c "import json;d=json.load(open('gpurun_out/ab_treebl/ck_${v}_r${r}.json'))['collective_kernels']['rows'];print({k: (v['frac'], v.get('graph_replay', {}).get('eager', {}).get('frac')) for k, v in d.items() if 'rank0' in k})")"
+    done
+  done
+  unset CHR_XCD_HAND_SHIFT ;;
+xrun3)  # XCD runs for m = 2, 3 at mid sizes: 256 KiB vs the 512 KiB policy (m = 3) / identity (m = 2), 2 GiB rotation
+  mkdir -p gpurun_out/ab_xrun
+  P="python tools/mstream_probe.py --layouts sep --reps 100 --gate"
+  for r in 1 2 3; do
+    for x in 256 512 0; do
+      CHR_XCD_RUN_KIB=$x timeout -k 10 300 $P --ms 2,3 --mib 16,32,64,128,256 --ws-mib 2048 --tag "x${x}_r${r}" \
+        >> gpurun_out/ab_xrun/xrun3.jsonl 2>>gpurun_out/ab_xrun/xrun3.err || exit 1
+    done
+    echo "xrun3 r=$r done"
+  done ;;
+wspmc)  # the working-set cliff's counters: m = 3 at 256 MiB over 1 set (1.25 GiB) vs 4 sets (5 GiB), two passes
+  mkdir -p gpurun_out/ab_wspmc
+  for sets in 1 4; do
+    for pass in "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE" \
+                "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_STALL_sum"; do
+      tag=$(echo $pass | cut -d' ' -f1 | cut -d_ -f1)
+      timeout -s KILL 120 rocprofv3 --pmc $pass --output-format csv -d "$PWD/gpurun_out/ab_wspmc/s${sets}_$tag" -o run \
+        -- python3 tools/mstream_probe.py --layouts sep --reps 8 --ms 3 --mib 256 --sets $sets \
+        > gpurun_out/ab_wspmc/s${sets}_$tag.txt 2>&1 || exit 1
+      echo "wspmc sets=$sets $tag done"
+    done
+  done ;;
+*) echo "usage: tools/ab.sh cap|runs|tree|mid|mid2|xrun|xrunpmc|tlbpf|treebl|xrun3|wspmc"; exit 2 ;;
 esac
 echo AB_DONE

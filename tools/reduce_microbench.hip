@@ -1376,6 +1376,34 @@ static void focus19(size_t piece, int sets) {
     free_sets(S);
 }
 
+// ---- focus30: fewer, fatter workgroups for the in-collective 8-leaf trees -------
+// C4's slice at 8 and 16 MiB pieces (2 trees x 9 operands), back to back: the product shape (one wave,
+// U = 1, 16 per CU) against U = 2 and 128 / 256-thread workgroups with the cap scaled to the same waves
+// per CU, all with 512 KiB XCD runs.  A fatter workgroup means fewer dispatches per grid and a shorter
+// ramp if the dispatcher, not memory latency, paces the start of a grid.
+template <int U, int BL>
+static void focus30_shape(Sets& S, size_t nvec, int sets, int waves_per_cu, size_t piece) {
+    uint32_t cs = 0;
+    while (((size_t)2 << cs) * ((size_t)BL * U * 16) <= (size_t)512 * 1024 && cs < 16) ++cs;
+    const int cap = waves_per_cu / (BL / 64);
+    char name[160];
+    std::snprintf(name, sizeof name, "tree8x2 nt U=%d BL=%d cap=%d (%d waves/CU) piece=%zuMiB sets=%d", U, BL, cap,
+                  waves_per_cu, piece >> 20, sets);
+    report_moved(name, 2.0 * 9 * piece, tree8x2_time<U, true, BL>(S, nvec, sets, lds_for_cap(cap), cs));
+}
+
+static void focus30(size_t piece, int sets) {
+    const size_t nvec = piece / 16;
+    Sets S = make_sets(17, nvec, sets);
+    focus30_shape<1, 64>(S, nvec, sets, 16, piece);
+    focus30_shape<2, 64>(S, nvec, sets, 16, piece);
+    focus30_shape<1, 128>(S, nvec, sets, 16, piece);
+    focus30_shape<1, 256>(S, nvec, sets, 16, piece);
+    focus30_shape<2, 256>(S, nvec, sets, 16, piece);
+    focus30_shape<1, 256>(S, nvec, sets, 32, piece);
+    free_sets(S);
+}
+
 // ---- focus21: back-to-back tree launches with the AQL barrier bit cleared ----------------------
 // hipExtAnyOrderLaunch lets the packet processor start launch i+1 while launch i drains; the flat
 // plan's consecutive slice evaluations touch disjoint memory, so only the ramp/drain gap is at stake.
@@ -1951,6 +1979,16 @@ int main(int argc, char** argv) {
                     }
                     free_sets(S);
                 }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus30") {  // fatter workgroups for the 8-leaf trees
+        for (int r = 0; r < 2; ++r) {
+            for (size_t mib : {8, 16}) {
+                focus30(mib << 20, 16);  // cold: 2.25 / 4.5 GiB rotation
+                focus30(mib << 20, 2);   // warm: 288 / 576 MiB
+            }
+            std::printf("--\n");
+        }
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus20") {  // XCD run length for the U = 1 tree shape
