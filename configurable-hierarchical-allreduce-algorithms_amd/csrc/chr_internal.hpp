@@ -54,8 +54,6 @@ hipError_t launch_fill(void* buf, size_t n, int dtype, int pattern, uint64_t see
 //   CHR_REDUCE_NT            0 / 1 forces plain / non-temporal loads+stores; unset = by size
 //   CHR_REDUCE_NT_MIN_BYTES  bytes streamed by one call from which NT is used (40 MiB for
 //                            bucket launches, 64 MiB for tree launches; the variable sets both)
-//   CHR_TLB_PF_TRIPS         experimental translation prefetch distance in workgroups (0 / unset: off;
-//   CHR_TLB_PF_PAGE_KIB      measured without effect) and its granule (default 2048)
 //   CHR_WG_PER_CU_VEC        streaming (NT) bucket launches: at most this many workgroups resident
 //   CHR_WG_PER_CU_TREE       per CU, capped through dynamic LDS (0 = uncapped); unset = policy
 //                            (nt_lds_bytes in reduce_common.hpp); likewise for the tree kernel
@@ -68,9 +66,6 @@ struct ReduceTuning {
     int wg_per_cu_vec;   // -1: policy
     int wg_per_cu_tree;  // -1: policy
     int xcd_hand_shift;  // -1: policy (xcd_hand in reduce_common.hpp); 0: off
-    unsigned tlb_pf_trips;     // translation prefetch distance in workgroups (tlb_pf in reduce_common.hpp); 0: off
-    unsigned tlb_pf_page_log2; // the prefetch granule (log2 bytes)
-    int tree_bl;               // threads per workgroup of streaming trees of 5+ leaves (64 or 128; CHR_TREE_BL)
     unsigned lds_per_cu; // bytes of LDS per CU (device attribute; 160 KiB on gfx950)
     unsigned lds_per_block;  // bytes of LDS one workgroup may allocate (device attribute)
 };

@@ -289,30 +289,6 @@ __host__ __device__ __forceinline__ size_t xcd_trip_w(uint32_t b, uint32_t full,
     return i < q - hand ? xcd_own(x, i, cs) : kIdleTrip;
 }
 
-// Translation prefetch (experimental, off unless CHR_TLB_PF_TRIPS is set).  Past the translation caches'
-// reach (~2.5 GiB of distinct memory per rotation) every page of every call is walked when the
-// stream first reaches it.  A workgroup whose block runs `pf` blocks ahead of a page's first trip (same XCD:
-// pf is a multiple of 8) touches one dword of that page in every operand after issuing its own loads, so
-// the walk overlaps the stream instead of stalling it.  tlb_pf_due: block b + pf maps to the first trip of
-// a 2^page_log2-byte granule of the operand (relative to the operand's base).
-__device__ __forceinline__ bool tlb_pf_due(uint32_t b, uint32_t pf, uint32_t full, uint32_t cs, size_t trip_bytes,
-                                           uint32_t page_log2, size_t ntrips) {
-    const size_t t2 = xcd_trip(b + pf, full, cs);
-    if (t2 >= ntrips) return false;
-    const size_t off = t2 * trip_bytes;
-    return (off & (((size_t)1 << page_log2) - 1)) < trip_bytes;
-}
-__device__ __forceinline__ uint32_t tlb_touch(const void* p) {
-    return __builtin_nontemporal_load((const uint32_t*)p);
-}
-// Keep the touches alive until after the trip's stores (a use at the very end: the wait for them lands
-// there, not in front of the adds).
-template <int N>
-__device__ __forceinline__ void tlb_retire(const uint32_t (&v)[N]) {
-#pragma unroll
-    for (int i = 0; i < N; ++i) asm volatile("" ::"v"(v[i]) : "memory");
-}
-
 // log2 of the trips in one XCD run for a launch of `trip_bytes` per operand per workgroup:
 // CHR_XCD_RUN_KIB if set, else `policy_kib` (0 = identity map).
 inline uint32_t xcd_run_shift(size_t policy_kib, size_t trip_bytes) {

@@ -146,17 +146,6 @@ ReduceTuning& reduce_tuning() {
         r.wg_per_cu_tree = s ? std::max(0, std::atoi(s)) : -1;
         s = std::getenv("CHR_XCD_HAND_SHIFT");
         r.xcd_hand_shift = s ? std::min(31, std::max(0, std::atoi(s))) : -1;  // [0, 31]; 31 hands nothing
-        s = std::getenv("CHR_TLB_PF_TRIPS");  // multiple of 8 (same XCD); 0 / unset = off
-        r.tlb_pf_trips = s ? (unsigned)std::max(0, std::atoi(s)) & ~7u : 0u;
-        s = std::getenv("CHR_TREE_BL");
-        r.tree_bl = s && std::atoi(s) == 128 ? 128 : 64;
-        s = std::getenv("CHR_TLB_PF_PAGE_KIB");
-        {
-            const unsigned kib = s ? (unsigned)std::max(4, std::atoi(s)) : 2048u;
-            unsigned lg = 12;
-            while ((1u << (lg + 1)) <= kib * 1024u && lg < 30) ++lg;
-            r.tlb_pf_page_log2 = lg;
-        }
         int dev = 0, lds = 0, blk = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess ||

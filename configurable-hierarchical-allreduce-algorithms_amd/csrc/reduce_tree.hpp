@@ -257,6 +257,11 @@ constexpr size_t tree_xcd_run_kib() {
     return NL <= 2 ? 0 : 512;
 }
 
+// Two-wave workgroups at the same 16 waves per CU (fewer dispatches per grid): the
+// microbench put them 1-2 % ahead on C4's slice at 8 / 16 MiB pieces (tools/reduce_microbench focus30,
+// profiles/r05/microbench_focus30_tree_bl.txt: 0.771-0.780 vs 0.754-0.764 cold at 16 MiB); through the product
+// (a CHR_TREE_BL knob, profiles/r05/ab_treebl/, 2 alternating rounds) the rank-alone C4 / C5 rows moved within
+// their +-3 % noise, so the one-wave shape stays.  U = 2 and 256-thread shapes lost 1-4 % in the microbench.
 // Vectors per lane per trip and resident workgroups per CU (nt_lds_bytes; 0 = uncapped) of
 // streaming tree launches.  At U = 2, 8-12 per CU moved the C4/C5 collective rows by -2..+1 %
 // (profiles/r02/occupancy_cap/); U = 1 with 16 per CU measured 0.751-0.763 against U = 2
@@ -308,8 +313,7 @@ inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
         grid += trips + 8u * (size_t)a.hand[j];
     }
     if (grid == 0) return hipSuccess;
-    // the policy's resident waves per CU, whatever the workgroup size (BL / 64 waves each)
-    const unsigned lds = NT ? nt_lds_bytes(reduce_tuning().wg_per_cu_tree, tree_wg_per_cu<NL>() / (BL / 64)) : 0;
+    const unsigned lds = NT ? nt_lds_bytes(reduce_tuning().wg_per_cu_tree, tree_wg_per_cu<NL>()) : 0;
     hipLaunchKernelGGL((k_reduce_tree<DT, OP, NL, U, NT, BL>), dim3((unsigned)grid), dim3(BL), lds, s, a);
     return hipGetLastError();
 }
@@ -348,11 +352,7 @@ inline hipError_t launch_tree_nl(const TreeArgs& a, const TreeScalarArgs* sa, hi
     const size_t call_bytes = (size_t)(a.nl + 1) * nvec * 16;
     const bool nt = t.nt_mode == 1 || (t.nt_mode < 0 && call_bytes >= t.tree_nt_min_bytes);
     if constexpr (is_pair_dt<DT>() || is_complex_dt<DT>()) return launch_tree_vec<DT, OP, NL, 256, false>(a, s);  // as launch_vec_m
-    else if constexpr (NL >= 5) {
-        // A/B knob (CHR_TREE_BL=128): two-wave workgroups at the same waves per CU (tree_wg_per_cu halved)
-        if (nt && t.tree_bl == 128) return launch_tree_vec<DT, OP, NL, 128, true>(a, s);
-        return nt ? launch_tree_vec<DT, OP, NL, 64, true>(a, s) : launch_tree_vec<DT, OP, NL, 256, false>(a, s);
-    } else return nt ? launch_tree_vec<DT, OP, NL, 64, true>(a, s) : launch_tree_vec<DT, OP, NL, 256, false>(a, s);
+    else return nt ? launch_tree_vec<DT, OP, NL, 64, true>(a, s) : launch_tree_vec<DT, OP, NL, 256, false>(a, s);
 }
 
 template <int DT, int OP>

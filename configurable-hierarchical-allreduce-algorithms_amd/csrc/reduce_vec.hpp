@@ -20,8 +20,6 @@ struct VecArgs {
     uint32_t xrun;   // log2 of the trips per XCD run (xcd_trip); set by the launcher
     uint32_t xfull;  // blocks [0, xfull) are remapped (xcd_full of the grid); set per launch
     uint32_t hand;   // trips each odd XCD hands to the even one below (xcd_trip_w); 0 = none
-    uint32_t pf;     // translation prefetch: workgroups ahead (multiple of 8), 0 = off (tlb_pf_one)
-    uint32_t pf_page_log2;
 };
 
 // U vectors (16 B each) per lane per trip; all M+1 operands of the trip are loaded
@@ -71,17 +69,6 @@ __global__ __launch_bounds__(BL) void k_reduce_vec(VecArgs a) {
         for (int j = 0; j < M; ++j)
 #pragma unroll
             for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&ins[j][base + (size_t)u * BL]);
-        // translation prefetch (after the trip's own loads, so waiting for those never waits for it)
-        uint32_t pfv[M + 2];
-        const bool pf_now = a.pf && tlb_pf_due(blockIdx.x, a.pf, xfull, xrun, (size_t)BL * U * 16, a.pf_page_log2,
-                                               nvec / ((size_t)BL * U));
-        if (pf_now) {
-            const size_t t2 = xcd_trip(blockIdx.x + a.pf, xfull, xrun) * BL * U;
-            pfv[0] = tlb_touch(&accp[t2]);
-            pfv[1] = tlb_touch(&out[t2]);
-#pragma unroll
-            for (int j = 0; j < M; ++j) pfv[2 + j] = tlb_touch(&ins[j][t2]);
-        }
         // Keep every load of the trip ahead of the first add: without this the
         // scheduler interleaves the first add (and its vmcnt(0)) between the loads.
         __builtin_amdgcn_sched_barrier(0);
@@ -91,7 +78,6 @@ __global__ __launch_bounds__(BL) void k_reduce_vec(VecArgs a) {
             for (int u = 0; u < U; ++u) acc[u] = apply_vec<DT, OP>(x[j][u], acc[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) st<NT>(&out[base + (size_t)u * BL], acc[u]);
-        if (pf_now) tlb_retire<M + 2>(pfv);
     } else {
         for (int u = 0; u < U; ++u) {
             const size_t i = base + (size_t)u * BL;
@@ -130,11 +116,16 @@ __global__ __launch_bounds__(kBlock) void k_reduce_scalar(ScalarArgs a) {
 // set) and 0.784 -> 0.795 (10 GiB); m = 7 0.811 -> 0.833 / 0.747 -> 0.751.  m = 1: uncapped, the C2
 // bucket measured 0.806 identity, 0.803 at 256 KiB, 0.792 at 512 KiB; under the 12-per-CU cap
 // (vec_wg_per_cu) 256 KiB runs win instead, 0.829-0.831 -> 0.833 over three alternating rounds
-// (profiles/r02/ab_runs/; microbench focus13: 0.814-0.822 -> 0.828).  m = 2 keeps the identity
-// (not measured under the cap).  Cache-warm (plain) calls keep the identity map too.
+// (profiles/r02/ab_runs/; microbench focus13: 0.814-0.822 -> 0.828).  m = 2 kept the identity
+// until round 5 (below).  Cache-warm (plain) calls keep the identity map too.
+//
+// Round 5 (profiles/r05/ab_xrun/xrun3.jsonl, 3 alternating rounds, 2 GiB rotation, 16-256 MiB buckets): m = 2
+// and m = 3 prefer 256 KiB -- m = 2 against the identity 0.687 vs 0.624 at 16 MiB, 0.735 vs 0.687 at 32, 0.770
+// vs 0.746 at 64, 0.914 vs 0.902 at 256; m = 3 against 512 KiB 0.820 vs 0.801 at 32 MiB, 0.865 vs 0.852 at 64,
+// ties at 128 / 256 (0.887 / 0.904 vs 0.887 / 0.901).  Wider fan-in keeps 512 KiB (256 not measured there).
 template <int M>
 constexpr size_t vec_xcd_run_kib() {
-    return M == 1 ? 256 : M == 2 ? 0 : 512;
+    return M <= 3 ? 256 : 512;
 }
 
 // Resident workgroups per CU for streaming launches (nt_lds_bytes; 0 = uncapped).  Uncapped, a CU
@@ -191,8 +182,6 @@ inline hipError_t for_each_launch_piece(VecArgs a, L launch) {
         const unsigned trips = (unsigned)((p.nvec + (size_t)BL * U - 1) / ((size_t)BL * U));
         p.xfull = xcd_full(trips, p.xrun);
         p.hand = WEIGHTED ? xcd_hand(p.xfull, reduce_tuning().xcd_hand_shift) : 0u;
-        p.pf = WEIGHTED ? reduce_tuning().tlb_pf_trips : 0u;  // streaming launches only
-        p.pf_page_log2 = reduce_tuning().tlb_pf_page_log2;
         launch(p, trips + 8u * p.hand);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
