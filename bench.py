@@ -940,7 +940,7 @@ def bench_allreduce(args):
     if metric_sched is not None:
         comm.set_schedule(metric_sched)
     ca.check(ca.all_reduce_radix_batch(send, recv, count, dt, ca.SUM, comm, k, b))
-    tuned = comm.tuned_schedule(ca.MODE_ALLREDUCE, count, dt, k, b) if metric_sched is not None else None
+    tuned = comm.tuned_schedule(ca.MODE_ALLREDUCE, count, dt, k, b)  # AUTO's choice, or the fixed schedule's depth
     sched_names = {0: "reference", 1: "balanced", 2: "flat", 3: "exact", 4: "flat_ag", 5: "flat_seq", 7: "flat_1shot"}
     # which ranks and GPUs RCCL's communicator holds, and which wire each peer pair got: the setup call
     # above has connected every pair the schedule uses (ncclSend/ncclRecv connect lazily)
@@ -1046,7 +1046,8 @@ def bench_allreduce(args):
             "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
             "config": {"workload": f"all_reduce_radix_batch, {S >> 20} MiB per rank, k={k}, b={b}, RCCL p2p over "
                                    f"xGMI, device-resident", "k": k, "b": b, "count": count,
-                       "schedule": (f"auto -> {sched_names.get(tuned[0], tuned[0])}, {tuned[1]} slices" if tuned
+                       "schedule": (f"{'auto -> ' if metric_sched is not None else ''}"
+                                    f"{sched_names.get(tuned[0], tuned[0])}, {tuned[1]} slices" if tuned
                                     else sched_env or "flat"),
                        "slices": tuned[1] if tuned else None,
                        # the metric's calls run with the communicator's compute stream beside the transfers;
@@ -1356,7 +1357,7 @@ def c5_overlap_record(ca, comm, count, world):
     tuned = comm.tuned_schedule(ca.MODE_ALLREDUCE, count, ca.BFLOAT16, 4, 4)
     overlap_on = comm.overlap
     if tuned is None:
-        return {"schedule": "not AUTO (CHR_SCHEDULE)", "schedule_code": None, "slices": None, "overlap": None}
+        return {"schedule": "unknown", "schedule_code": None, "slices": None, "overlap": None}
     sched, slices = tuned
     return {"schedule": SCHED_NAMES.get(sched, str(sched)), "schedule_code": sched, "slices": slices,
             "overlap": bool(overlap_on and slices >= 2)}

@@ -229,7 +229,7 @@ class Comm:
 
     def tuned_schedule(self, mode, count, datatype, k, b):
         """(schedule, slices) SCHEDULE_AUTO kept for a collective already called with these arguments,
-        or None."""
+        or None; under a fixed schedule, that schedule and the depth such a call runs at."""
         sc, sl = ctypes.c_int(), ctypes.c_int()
         rc = lib().chr_comm_tuned_schedule(self._h, mode, count, datatype, k, b, ctypes.byref(sc), ctypes.byref(sl))
         return (sc.value, sl.value) if rc == SUCCESS else None

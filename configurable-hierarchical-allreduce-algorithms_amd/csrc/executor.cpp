@@ -1462,6 +1462,11 @@ int chr_comm_set_graphs(chr_comm* c, int enable) {
 int chr_comm_tuned_schedule(const chr_comm* c, int mode, size_t count, chr_dtype dtype, int k, int b, int* schedule,
                             int* slices) {
     if (!c || !schedule || !slices || !chr::dtype_size(dtype)) return CHR_ERR_INVALID_ARG;
+    if (c->sched != CHR_SCHEDULE_AUTO) {  // a fixed schedule: it, at the depth such a call runs
+        *schedule = c->sched;
+        *slices = pick_slices(c->slices, (uint64_t)count, mode, c->nranks, b, chr::dtype_size(dtype), c->sched);
+        return CHR_SUCCESS;
+    }
     auto it = c->tuned.find(std::make_tuple(mode, (uint64_t)count, (int)chr::dtype_size(dtype), k, b, c->slices,
                                             c->overlap));
     if (it == c->tuned.end()) return CHR_ERR_INVALID_ARG;

@@ -220,7 +220,9 @@ int chr_comm_set_slices(chr_comm* comm, int slices);
 #define CHR_SCHEDULE_FLAT_1SHOT 7
 int chr_comm_set_schedule(chr_comm* comm, int schedule);
 /* What CHR_SCHEDULE_AUTO chose for a collective already called with these arguments
- * (mode: 0 allreduce_radix_batch, 1 reduce_scatter_radix_batch; count as passed). */
+ * (mode: 0 allreduce_radix_batch, 1 reduce_scatter_radix_batch; count as passed); CHR_ERR_INVALID_ARG
+ * under AUTO before such a call.  Under any other schedule: that schedule and the pipeline depth a
+ * device-resident call with these arguments runs at. */
 int chr_comm_tuned_schedule(const chr_comm* comm, int mode, size_t count, chr_dtype dtype, int k, int b, int* schedule,
                             int* slices);
 /* Compute/xGMI overlap (default on; env CHR_OVERLAP=0): local reductions run on a second HIP
