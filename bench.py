@@ -195,8 +195,8 @@ def line_problems(line):
     if probs:
         return probs
 
-    def close(a, b, rel=2e-3):
-        return abs(a - b) <= rel * max(abs(a), abs(b), 1e-12)
+    def close(a, b, rel=2e-3):  # the line rounds GB/s to 0.01: allow that on either side
+        return abs(a - b) <= rel * max(abs(a), abs(b), 1e-12) + 0.011
 
     n, ms, rf = line["n_gpus"], line["ms_per_step"], line["roofline"]
     if "workload" not in line["config"]:
@@ -1044,8 +1044,9 @@ def bench_allreduce(args):
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
-            "config": {"workload": f"all_reduce_radix_batch, {S >> 20} MiB per rank, k={k}, b={b}, RCCL p2p over "
-                                   f"xGMI, device-resident", "k": k, "b": b, "count": count,
+            "config": {"workload": f"all_reduce_radix_batch, {S >> 20} MiB per rank, k={k}, b={b}, RCCL send/recv "
+                                   f"(the wire each peer pair used: rccl.pairs), device-resident", "k": k, "b": b,
+                       "count": count,
                        "schedule": (f"{'auto -> ' if metric_sched is not None else ''}"
                                     f"{sched_names.get(tuned[0], tuned[0])}, {tuned[1]} slices" if tuned
                                     else sched_env or "flat"),
