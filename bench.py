@@ -69,6 +69,8 @@ def parse(argv=None):
     p.add_argument("--collective-kernels-small", action="store_true",
                    help="N=1: the same for the N=2 / N=4 lines' allreduces (1 GiB per rank) and C3's reduce-scatter "
                         "(2 ranks, 256 MiB send): the 2- and 4-leaf trees")
+    p.add_argument("--rank-trees", action="store_true",
+                   help="N=1: only the rank-alone rows of --collective-kernels (one GPU's own C4 / C5 grids)")
     return p.parse_args(argv)
 
 
@@ -543,6 +545,29 @@ def bench_collective_kernels(args):
                                              "send/recv/STAGE only", "rows": rows}})
 
 
+def bench_rank_trees(args):
+    """Only the rank-alone rows of --collective-kernels (one GPU's own grids of a C4 / C5 call at 4 and
+    8 slices, with and without the receive copies in front): small enough to run under rocprofv3
+    --kernel-trace, whose per-dispatch durations give the grids' own time beside the spans."""
+    import torch
+
+    import chiara_amd as ca
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    rows = {}
+    for dname, cdt, es in (("f32", ca.FLOAT32, 4), ("bf16", ca.BFLOAT16, 2)):
+        for slices in (4, 8):
+            for recv_copies in (False, True):
+                key = f"{'c4' if dname == 'f32' else 'c5'}_{dname}_rank0_alone_slices_{slices}" + \
+                      ("_after_recv_copies" if recv_copies else "")
+                rows[key] = replay_rank_trees(ca, torch, dev, cdt, es, (1 << 30) // es, 8, 4, 4, slices, recv_copies,
+                                              graph=False)
+                torch.cuda.empty_cache()
+    emit({"rank_trees": {"workload": "rank 0's fused reductions of one all_reduce_radix_batch call, 8 ranks, k=4, "
+                                     "b=4, 1 GiB per rank, flat schedule, on its own send/recv/STAGE", "rows": rows}})
+
+
 def bench_collective_kernels_small(args):
     """The fused reductions of the smaller multi-GPU configs, on virtual ranks as above: the N=2 and
     N=4 lines' allreduces (1 GiB fp32 per rank, b = N, k = min(4, N): 2- and 4-leaf trees) and C3
@@ -611,8 +636,12 @@ def replay_rank_trees(ca, torch, dev, cdt, es, count, n, k, b, slices, recv_copi
     under-state the per-GPU case.  The plan is the flat schedule's own (describe_plan), its tree
     ops batched per step as the executor batches them (chr_reduce_tree_batch); leaf data are
     synthetic (timing only, SUM is data-independent).  With recv_copies, every step's receives are
-    first written into STAGE by device copies from SEND (as RCCL's receives would leave them) and
-    only the tree launches are timed."""
+    first written into STAGE by device copies from SEND (as RCCL's receives would leave them).
+
+    `frac` (round 5): one call's grids back to back as ONE gated HIP-event span (the median of `reps`
+    calls), every inter-grid gap included; with recv_copies, the span of copies + grids minus the span
+    of the same copies alone.  `event_pairs_frac`: rounds 3-4's figure, an event pair around every
+    grid, whose extra event packets add ~2-5 us per grid and +-3 % of noise (profiles/r05/ab_treebl/)."""
     plan = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, n, 0, k, b, count, slices, ca.SCHEDULE_FLAT))
     h = plan["header"]
     bufs = {name: torch.empty(max(1, h[name.lower()]) * es, dtype=torch.uint8, device=dev)
@@ -629,42 +658,65 @@ def replay_rank_trees(ca, torch, dev, cdt, es, count, n, k, b, slices, recv_copi
         copies = [(bufs[dst[0]].narrow(0, dst[1] * es, cnt * es), bufs["SEND"].narrow(0, 0, cnt * es))
                   for (_, dst, cnt) in st["recvs"]]
         steps.append((trees, copies))
+    by = sum((len(op[4]) + 2) * op[3] * es for trees, _ in steps for op in trees)
+    grids = sum(1 for trees, _ in steps if trees)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in steps]
-    ms = by = launches = 0
 
-    def call(timed):
-        nonlocal ms, by, launches
+    def call(with_copies, with_trees, pairs=False):
         for (trees, copies), (e0, e1) in zip(steps, evs):
-            if recv_copies:
+            if with_copies:
                 for d, src in copies:
                     d.copy_(src)  # D2D on s
-            if not trees:
+            if not trees or not with_trees:
                 continue
-            e0.record(s)
+            if pairs:
+                e0.record(s)
             ca.check(ca.reduce_tree_batch([ptr(op[1]) for op in trees],
                                           [[ptr(op[2])] + [ptr(x) for x in op[4]] for op in trees],
                                           [op[5][0] for op in trees], [op[5][1] for op in trees],
                                           trees[0][3], cdt, ca.SUM, s))
-            e1.record(s)
-        if timed:
+            if pairs:
+                e1.record(s)
+
+    g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def span(with_copies, with_trees):
+        out = []
+        for _ in range(reps):
             torch.cuda.synchronize()
-            for (trees, _), (e0, e1) in zip(steps, evs):
-                if trees:
-                    ms += e0.elapsed_time(e1)
-                    by += sum((len(op[4]) + 2) * op[3] * es for op in trees)
-                    launches += 1
+            if hasattr(torch.cuda, "_sleep"):  # host enqueue latency out of the span (bench_bucket's gate)
+                torch.cuda._sleep(GATE_CYCLES)
+            g0.record(s)
+            call(with_copies, with_trees)
+            g1.record(s)
+            torch.cuda.synchronize()
+            out.append(g0.elapsed_time(g1))
+        return sorted(out)[len(out) // 2]
 
     for _ in range(2):
-        call(False)
-    for _ in range(reps):
-        call(True)
+        call(recv_copies, True)
+    ms = span(recv_copies, True)
+    row = {}
+    if recv_copies:
+        ms_c = span(True, False)
+        row["copies_ms_per_call"] = round(ms_c, 4)
+        ms -= ms_c
     ach = by / (ms * 1e-3) / 1e9
-    row = {"launches_per_call": launches // reps, "kernel_ms_per_call": round(ms / reps, 4),
-           "algorithmic_bytes_per_call": int(by / reps), "working_set_GiB": round(
-               (h["send"] + h["recv"] + h["stage"] + h["acc"]) * es / 2**30, 2),
-           "achieved_GBps": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4)}
+    # rounds 3-4: an event pair around every grid
+    pm = 0.0
+    for _ in range(reps):
+        call(recv_copies, True, pairs=True)
+        torch.cuda.synchronize()
+        pm += sum(e0.elapsed_time(e1) for (trees, _), (e0, e1) in zip(steps, evs) if trees)
+    pm /= reps
+    row.update({"launches_per_call": grids, "kernel_ms_per_call": round(ms, 4),
+                "algorithmic_bytes_per_call": int(by), "working_set_GiB": round(
+                    (h["send"] + h["recv"] + h["stage"] + h["acc"]) * es / 2**30, 2),
+                "achieved_GBps": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4),
+                "event_pairs_ms_per_call": round(pm, 4),
+                "event_pairs_frac": round(by / (pm * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)})
     if graph and not recv_copies:
-        row["graph_replay"] = trees_span_eager_vs_graph(ca, torch, s, steps, ptr, cdt, by / reps)
+        row["graph_replay"] = trees_span_eager_vs_graph(ca, torch, s, steps, ptr, cdt, by)
     del bufs
     return row
 
@@ -1431,6 +1483,9 @@ def _main():
         return
     if args.collective_kernels_small:
         bench_collective_kernels_small(args)
+        return
+    if args.rank_trees:
+        bench_rank_trees(args)
         return
     cpu = None if args.no_cpu_baseline else cpu_baseline(args.cpu_seconds)
     bench_bucket(args, cpu)

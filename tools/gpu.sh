@@ -13,6 +13,7 @@
 #   prof       rocprofv3 kernel trace + stats of the bench (csv) -> prof/
 #   pmc        FETCH_SIZE and WRITE_SIZE passes of the bench     -> pmc_FETCH_SIZE/, pmc_WRITE_SIZE/
 #   kernels    bench.py --collective-kernels (C4/C5 in-collective kernel rows) -> collective_kernels.json
+#   ranktrees  bench.py --rank-trees, plain and under rocprofv3 --kernel-trace -> rank_trees.json, rank_trees_prof/
 #   treepmc    rocprofv3 stats + FETCH_SIZE / WRITE_SIZE passes of the tree kernel alone (tools/tree_pmc.py)
 #   e2e        bench.py --e2e: host-buffer (PCIe-inclusive) cost of the reference's contract -> e2e.json
 #   sweep      bench.py --sweep: 1 KiB .. 1 GiB buckets, m = 1/3/7, fp32 + bf16 (table in sweep.json.err)
@@ -54,6 +55,10 @@ for step in "$@"; do
         -- python3 bench.py --steps 40 --warmup 5 --no-cpu-baseline
     done ;;
   kernels) run 400 collective_kernels.json python bench.py --collective-kernels ;;
+  ranktrees)  # one GPU's own C4 / C5 grids: spans (JSON) and, under rocprofv3, each grid's kernel duration
+    run 300 rank_trees.json python bench.py --rank-trees
+    run 300 rank_trees_prof.json rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/rank_trees_prof" \
+      -o run -- python3 bench.py --rank-trees ;;
   treepmc)  # the fused tree alone at C4's shape (tools/tree_pmc.py): kernel stats, then FETCH / WRITE passes
     run 300 tree_prof.txt rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/tree_prof" -o run \
       -- python3 tools/tree_pmc.py 40
