@@ -244,7 +244,10 @@ __global__ __launch_bounds__(kBlock) void k_reduce_tree_scalar(TreeScalarArgs a)
 // (The bucket kernel's odd XCDs still lag on cache-resident operands, 2.2 % against 3 % cold: reduce_microbench
 // focus29; what the warm tree rows respond to is not pinned down.)  On a node 7 of a tree's 8 leaves arrive
 // over xGMI just before the launch, so the mild shift 6 is kept: it gains on cold leaves and costs at most
-// ~1 % on warm ones, where 4 costs 5 %.
+// ~1 % on warm ones, where 4 costs 5 %.  Round 5 re-ran it on one GPU's own grids with the receive copies in
+// front (bench.py rank-alone rows, profiles/r05/ab_treebl/, 2 alternating rounds): off 0.671 / 0.673 vs 6 0.657
+// / 0.690 at 4 slices, 0.594 / 0.544 vs 0.540 / 0.603 at 8 -- a tie inside the rows' noise -- and 6 ahead on
+// cold leaves (whole-call spans 0.763 / 0.774 vs 0.736 / 0.747).
 constexpr int kTreeXcdHandShift = 6;
 
 // XCD runs for streaming (nt) tree launches (profiles/r02/xcd_runs/ab_tree_*.json, C4 slice of 2

@@ -214,6 +214,30 @@ wspmc)  # the working-set cliff's counters: m = 3 at 256 MiB over 1 set (1.25 Gi
       echo "wspmc sets=$sets $tag done"
     done
   done ;;
-*) echo "usage: tools/ab.sh cap|runs|tree|mid|mid2|xrun|xrunpmc|tlbpf|treebl|xrun3|wspmc"; exit 2 ;;
+treerun)  # XCD runs of the 8-leaf trees (policy 512 KiB) on one GPU's own C4 / C5 grids, by rocprof kernel
+          # duration (tools/rank_trees_summary.py), 2 alternating rounds
+  mkdir -p gpurun_out/ab_treerun
+  for r in 1 2; do
+    for x in ${XRUNS:-512 256 1024}; do
+      d="$PWD/gpurun_out/ab_treerun/x${x}_r${r}"
+      CHR_XCD_RUN_KIB=$x timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$d" -o run \
+        -- python3 bench.py --rank-trees > "$d.json" 2>/dev/null || exit 1
+      echo "treerun $x r=$r $(python tools/rank_trees_summary.py "$d.json" "$d" | python -c "
+import json, sys; d = json.load(sys.stdin)['rank_trees_rocprof']; print({k.replace('_rank0_alone', ''): v['frac_avg'] for k, v in d.items()})")"
+    done
+  done ;;
+xrun4)  # XCD runs for wide fan-in (m = 4..7) and m = 3 at 1 GiB: 128 / 256 KiB vs the 512 KiB policy, 2 GiB rotation
+  mkdir -p gpurun_out/ab_xrun
+  P="python tools/mstream_probe.py --layouts sep --reps 40 --gate"
+  for r in 1 2; do
+    for x in 256 512 128; do
+      CHR_XCD_RUN_KIB=$x timeout -k 10 300 $P --ms 4,5,7 --mib 32,128,256 --ws-mib 2048 --tag "x${x}_r${r}" \
+        >> gpurun_out/ab_xrun/xrun4.jsonl 2>>gpurun_out/ab_xrun/xrun4.err || exit 1
+      CHR_XCD_RUN_KIB=$x timeout -k 10 300 $P --ms 3 --mib 1024 --sets 1 --reps 12 --tag "x${x}_1g_r${r}" \
+        >> gpurun_out/ab_xrun/xrun4.jsonl 2>>gpurun_out/ab_xrun/xrun4.err || exit 1
+    done
+    echo "xrun4 r=$r done"
+  done ;;
+*) echo "usage: tools/ab.sh cap|runs|tree|mid|mid2|xrun|xrunpmc|tlbpf|treebl|xrun3|wspmc|treerun|xrun4"; exit 2 ;;
 esac
 echo AB_DONE
