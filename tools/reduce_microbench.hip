@@ -1404,6 +1404,92 @@ static void focus30(size_t piece, int sets) {
     free_sets(S);
 }
 
+// ---- focus31: page-local streaming past the translation reach (second attempt) -------
+// The product's one-trip grid hands consecutive trips of a run to every CU of an XCD, so every CU touches every
+// 2 MiB page of its XCD's share: (pages x CUs) first-level translations per launch.  Here a resident grid of
+// G one-wave workgroups walks chunks of C consecutive trips (chunk c -> workgroup c mod G), so a page is
+// touched by 2 MiB / (C x trip bytes) workgroups: C = 1 is the old grid-stride form, C x 2 KiB = 2 MiB gives
+// each page to one workgroup (one CU).  Same loads, adds and nt / ACC0 policy as k_reduce_vec's trip.
+template <int M, int U>
+__global__ __launch_bounds__(64) void k_span(chr::VecArgs a, unsigned chunk, unsigned G) {
+    using chr::u32x4;
+    u32x4* const out = a.out;
+    const u32x4* const accp = a.acc;
+    const u32x4* ins[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) ins[j] = a.ins[j];
+    const size_t nvec = a.nvec;
+    const size_t trips = nvec / (64 * U);  // whole trips only (focus31 sizes are multiples)
+    for (size_t c = blockIdx.x;; c += G) {
+        const size_t t0 = c * chunk;
+        if (t0 >= trips) break;
+        const size_t t1 = t0 + chunk < trips ? t0 + chunk : trips;
+        for (size_t t = t0; t < t1; ++t) {
+            const size_t base = t * 64 * U + threadIdx.x;
+            u32x4 acc[U], x[M][U];
+            acc[0] = chr::ld<false>(&accp[base]);
+#pragma unroll
+            for (int u = 1; u < U; ++u) acc[u] = chr::ld<true>(&accp[base + (size_t)u * 64]);
+#pragma unroll
+            for (int j = 0; j < M; ++j)
+#pragma unroll
+                for (int u = 0; u < U; ++u) x[j][u] = chr::ld<true>(&ins[j][base + (size_t)u * 64]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < M; ++j)
+#pragma unroll
+                for (int u = 0; u < U; ++u) acc[u] = chr::apply_vec<CHR_FLOAT32, CHR_SUM>(x[j][u], acc[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) chr::st<true>(&out[base + (size_t)u * 64], acc[u]);
+        }
+    }
+}
+
+template <int M, int U>
+static void focus31_m(size_t bytes, int sets, int ncu) {
+    const size_t nvec = bytes / 16;
+    const unsigned trips = (unsigned)(nvec / (64 * U));
+    Sets S = make_sets(M, nvec, sets);
+    uint32_t cs = 0;  // the product's runs (vec_xcd_run_kib)
+    const size_t run_kib = M <= 3 ? 256 : 512;
+    while (((size_t)2 << cs) * (64 * U * 16) <= run_kib * 1024 && cs < 16) ++cs;
+    const unsigned lds = lds_for_cap(12);
+    char tag[64];
+    std::snprintf(tag, sizeof tag, " sets=%d ws=%zuMiB", sets, (size_t)sets * (M + 1) * (bytes >> 20));
+    auto vargs = [&](int i) {
+        auto& b = S.bufs[i % sets];
+        chr::VecArgs v{};
+        v.out = (chr::u32x4*)b[0];
+        v.acc = (const chr::u32x4*)b[0];
+        for (int j = 0; j < M; ++j) v.ins[j] = (const chr::u32x4*)b[j + 1];
+        v.nvec = nvec;
+        return v;
+    };
+    const int reps = std::max(6, (int)std::min<size_t>(60, (16ull << 30) / ((M + 1) * bytes)));
+    double t = time_launches([&](int i) {
+        chr::VecArgs v = vargs(i);
+        v.xrun = cs;
+        v.xfull = chr::xcd_full(trips, cs);
+        hipLaunchKernelGGL((chr::k_reduce_vec<CHR_FLOAT32, CHR_SUM, M, U, true, true, 64>), dim3(trips), dim3(64), lds,
+                           0, v);
+    }, reps);
+    char name[128];
+    std::snprintf(name, sizeof name, "product one-trip runs%zuK%s", run_kib, tag);
+    report(name, M, bytes, t);
+    for (unsigned per_cu : {11u, 8u}) {
+        const unsigned G = (unsigned)ncu * per_cu;
+        for (unsigned chunk : {1u, 16u, 128u, 1024u, (trips + G - 1) / G}) {
+            t = time_launches([&](int i) {
+                hipLaunchKernelGGL((k_span<M, U>), dim3(G), dim3(64), lds, 0, vargs(i), chunk, G);
+            }, reps);
+            std::snprintf(name, sizeof name, "span G=%u/CU chunk=%u trips (%u KiB)%s", per_cu, chunk,
+                          chunk * 64u * U * 16u >> 10, tag);
+            report(name, M, bytes, t);
+        }
+    }
+    free_sets(S);
+}
+
 // ---- focus21: back-to-back tree launches with the AQL barrier bit cleared ----------------------
 // hipExtAnyOrderLaunch lets the packet processor start launch i+1 while launch i drains; the flat
 // plan's consecutive slice evaluations touch disjoint memory, so only the ramp/drain gap is at stake.
@@ -1979,6 +2065,19 @@ int main(int argc, char** argv) {
                     }
                     free_sets(S);
                 }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus31") {  // page-local chunks past the translation reach
+        int ncu = 0;
+        CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+        for (int r = 0; r < 2; ++r) {
+            focus31_m<3, 2>(1024ull << 20, 1, ncu);  // 4 GiB per launch: the cliff
+            focus31_m<3, 2>(256ull << 20, 4, ncu);   // 4 GiB rotation
+            focus31_m<3, 2>(256ull << 20, 1, ncu);   // 1 GiB: inside the reach (control)
+            focus31_m<7, 1>(256ull << 20, 2, ncu);   // 4 GiB rotation, 8 streams
+            focus31_m<1, 4>(1024ull << 20, 1, ncu);  // 2 GiB per launch
+            std::printf("--\n");
+        }
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus30") {  // fatter workgroups for the 8-leaf trees
