@@ -185,7 +185,9 @@ LINE_DEFINITIONS_NN = {
     "xgmi_roofline.frac": "the compiled plan's busiest directed GPU pair's bytes / 76.8 GB/s (one direction of one "
                           "xGMI link) / t",
     "cpu_baseline.value": "N x S / t of the reference all_reduce_radix_batch on N host cores (same definition as value)",
-    "rccl.xgmi": "RCCL holds N ranks on N distinct PCI devices and every logged connection is P2P"}
+    "rccl.xgmi": "RCCL holds N ranks on N distinct PCI devices and every logged connection is P2P",
+    "result_check": "the metric's output on every rank and element: ranks bit-identical (position-weighted int64 "
+                    "checksums of the raw words) and |x - fp64 sum of the N inputs| <= (N-1) ulp sum|x_i| (DESIGN §7)"}
 
 def line_problems(line):
     """What in a bench line disagrees with LINE_DEFINITIONS_N1 / _NN (empty list: none).  Checked by
@@ -244,6 +246,11 @@ def line_problems(line):
             probs.append("rccl.xgmi true with reasons against it")
         if r.get("xgmi") is False and not r.get("not_xgmi_because"):
             probs.append("rccl.xgmi false without a reason")
+        rc = line.get("result_check")
+        if not isinstance(rc, dict):
+            probs.append("result_check missing")
+        elif not (rc.get("ranks_bit_identical") and rc.get("within_tolerance")):
+            probs.append(f"result_check failed: {rc}"[:300])
         if rf is not None and rf.get("traffic") is None and not rf.get("traffic_stale"):
             probs.append("roofline.traffic null without traffic_stale")
         c5 = (line.get("compare") or {}).get("c5_allreduce_bf16_k4_b4_1GiB")
@@ -1036,6 +1043,16 @@ def bench_allreduce(args):
     red_ms, red_bytes, red_n = comm.profile_read()
     phases = comm.profile_phases()  # transfer ms per plan phase (DEBUG_MODE phase timers' analogue)
     comm.profile(False)
+    # the metric's output on every rank: bit-identical across ranks and within the stated tolerance of
+    # the fp64 sum (recv holds the last call's result; every call computes the same bits)
+    try:
+        def fill_rank(r, buf):
+            ca.check(ca.fill(buf, count, dt, 0, SEED, r, stream=stream))
+            torch.cuda.synchronize()
+        check = result_check(torch, dist, recv, count, es, world, fill_rank)
+    except Exception as e:  # recorded, never hidden: line_problems() flags a line without a passing check
+        check = {"error": str(e)[:200]}
+    torch.cuda.empty_cache()
     allph = [None] * world
     dist.all_gather_object(allph, phases)
     phases_ms = {}
@@ -1133,6 +1150,7 @@ def bench_allreduce(args):
             "phase_transfer_ms": phases_ms,
             # RCCL's own view: ranks, GPUs and the transport of every connected pair (xgmi: all P2P)
             "rccl": rccl,
+            "result_check": check,
         }
         if cpu:
             line["gpu_vs_cpu"] = round(line["value"] / cpu["value"], 1)
@@ -1141,6 +1159,67 @@ def bench_allreduce(args):
         emit(line)
     comm.destroy()
     dist.destroy_process_group()
+
+
+RESULT_TOL_ULP = {"f32": 2.0 ** -23, "bf16": 2.0 ** -8}  # (n-1) x ulp x sum|x_i| per element
+
+
+def result_check(torch, dist, recv, count, es, world, fill_rank, window=1 << 26):
+    """The metric's output, checked on every rank without the oracle (which only the CPU-baseline leg may
+    touch): (1) the ranks' recv buffers are bit-identical (each chunk is reduced once, at one root, then
+    copied: all_reduce_radix_batch.cpp:529-756), by two position-weighted int64 checksums of the raw words;
+    (2) every element is within DESIGN §7's stated tolerance of the fp64 sum of the N inputs, regenerated here
+    with the same device generator: |x - sum| <= (N - 1) ulp sum|x_i| + 2^-126 (f32) / + 2^-133 (bf16),
+    so a transport that delivered stale or misplaced bytes shows up in the node's own record.
+    fill_rank(r, buf) writes rank r's input (count elements) into the byte buffer buf.  Windows of `window`
+    elements bound the fp64 temporaries."""
+    tdt = torch.float32 if es == 4 else torch.bfloat16
+    words = recv[:count * es].view(torch.int32 if es == 4 else torch.int16)
+    out = recv[:count * es].view(tdt)
+    h1 = h2 = 0
+    tmp = torch.empty(count * es, dtype=torch.uint8, device=recv.device)
+    tol_ulp = RESULT_TOL_ULP["f32" if es == 4 else "bf16"]
+    bad, worst, maxerr = 0, 0.0, 0.0
+    for w0 in range(0, count, window):
+        w1 = min(count, w0 + window)
+        v = words[w0:w1].to(torch.int64)
+        h1 += int(v.sum())
+        idx = torch.arange(w0, w1, device=recv.device, dtype=torch.int64) % 1000003 + 1
+        h2 += int((v * idx).sum())
+    h1 &= (1 << 63) - 1
+    h2 &= (1 << 63) - 1
+    ref = torch.zeros(count, dtype=torch.float64, device=recv.device)
+    mag = torch.zeros(count, dtype=torch.float64, device=recv.device)
+    for r in range(world):
+        fill_rank(r, tmp)
+        x = tmp.view(tdt)
+        for w0 in range(0, count, window):
+            w1 = min(count, w0 + window)
+            xd = x[w0:w1].double()
+            ref[w0:w1] += xd
+            mag[w0:w1] += xd.abs()
+    floor = 2.0 ** -126 if es == 4 else 2.0 ** -133
+    for w0 in range(0, count, window):
+        w1 = min(count, w0 + window)
+        err = (out[w0:w1].double() - ref[w0:w1]).abs()
+        bound = (world - 1) * tol_ulp * mag[w0:w1] + floor
+        bad += int((err > bound).sum())
+        worst = max(worst, float((err / bound).max()))
+        maxerr = max(maxerr, float(err.max()))
+    del ref, mag, tmp
+    mine = torch.tensor([float(h1), float(h2), float(bad), worst, maxerr], dtype=torch.float64)
+    hs = [None] * world
+    dist.all_gather_object(hs, (h1, h2))
+    allv = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allv, mine)
+    return {"ranks_bit_identical": len(set(hs)) == 1,
+            "within_tolerance": all(int(t[2]) == 0 for t in allv),
+            "elements_checked_per_rank": count,
+            "violations": int(sum(int(t[2]) for t in allv)),
+            "max_err_over_bound": round(max(float(t[3]) for t in allv), 6),
+            "max_abs_err": max(float(t[4]) for t in allv),
+            "checksum_rank0": f"{hs[0][0]:016x}:{hs[0][1]:016x}",
+            "tolerance": f"|x - fp64 sum| <= (N-1) x {tol_ulp:.3g} x sum|x_i| (DESIGN §7), every element, every rank"}
 
 
 def _timed_max(torch, dist, fn, steps, warmup, comm=None):

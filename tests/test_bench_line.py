@@ -121,6 +121,7 @@ def _nn_line(n=8):
             "rccl": bench.rccl_record([_info(r, True) for r in range(n)],
                                       [bench.parse_rccl_transports(P2P_8, nranks=8)] * n, n),
             "cpu_baseline": {"value": 3.0, "unit": "GB/s", "cores": n, "kind": "reference", "sample": "s"},
+            "result_check": {"ranks_bit_identical": True, "within_tolerance": True, "violations": 0},
             "compare": {"c5_allreduce_bf16_k4_b4_1GiB": {"algbw_GBps": 1, "schedule": "flat", "slices": 4,
                                                          "overlap": True}}}
 

@@ -59,6 +59,10 @@ for step in "$@"; do
     run 300 rank_trees.json python bench.py --rank-trees
     run 300 rank_trees_prof.json rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/rank_trees_prof" \
       -o run -- python3 bench.py --rank-trees ;;
+  ranktrees12)  # the same grids at the in-collective cap: a multi-rank call runs its trees under CoresidentScope,
+                # 12 workgroups per CU beside RCCL (reduce_common.hpp stream_wg_cap)
+    CHR_WG_PER_CU_TREE=12 run 300 rank_trees_cap12_prof.json rocprofv3 --kernel-trace --stats --output-format csv \
+      -d "$PWD/$OUT/rank_trees_cap12_prof" -o run -- python3 bench.py --rank-trees ;;
   treepmc)  # the fused tree alone at C4's shape (tools/tree_pmc.py): kernel stats, then FETCH / WRITE passes
     run 300 tree_prof.txt rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/tree_prof" -o run \
       -- python3 tools/tree_pmc.py 40

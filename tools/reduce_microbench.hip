@@ -1490,6 +1490,59 @@ static void focus31_m(size_t bytes, int sets, int ncu) {
     free_sets(S);
 }
 
+// ---- focus32: the bf16 tree (C5) against the f32 one (C4) at the in-collective shapes ---------------
+// C5's per-GPU grids run 3-6 % below C4's at equal bytes (profiles/r05/rank_trees/).  A bf16 combine widens both
+// operands, adds in f32 and packs with RNE: ~7 VALU per dword against 1 for f32, which stretches a one-trip
+// workgroup's life after its loads land.  More bytes per wave (U = 2) or more waves per CU (cap 16 / 20 /
+// uncapped) keep more loads in flight through that tail; cap 12 is what the collective runs beside RCCL.
+template <int DT, int U>
+static double tree8x2_time_dt(Sets& S, size_t nvec, int sets, unsigned lds, uint32_t cs) {
+    return time_launches([&](int i) {
+        chr::TreeArgs a{};
+        const auto& b = S.bufs[i % sets];
+        a.nseg = 2;
+        a.nl = 8;
+        a.xrun = cs;
+        const uint32_t trips = (uint32_t)((nvec + 64 * U - 1) / (64 * U));
+        for (int j = 0; j < chr::kMaxTreeSegs; ++j) {
+            a.block0[j] = j < 2 ? j * trips : ~0u;
+            a.xfull[j] = j < 2 ? chr::xcd_full(trips, cs) : 0;
+        }
+        const int comb[8] = {0, 1, 1, 1, 0, 1, 1, 2};
+        for (int t2 = 0; t2 < 2; ++t2) {
+            chr::TreeSeg& g = a.seg[t2];
+            for (int l = 0; l < 8; ++l) g.leaves[l] = (const chr::u32x4*)b[9 * t2 + l];
+            g.out = (chr::u32x4*)b[9 * t2 + 8];
+            g.nvec = nvec;
+            g.comb = 0;
+            for (int l = 0; l < 8; ++l) g.comb |= (uint32_t)comb[l] << (2 * l);
+            g.swaps = 0;
+        }
+        hipLaunchKernelGGL((chr::k_reduce_tree<DT, CHR_SUM, 8, U, true, 64>), dim3(2 * trips), dim3(64), lds, 0, a);
+    }, 60);
+}
+
+template <int DT, int U>
+static void focus32_row(Sets& S, size_t nvec, int sets, size_t piece, int cap) {
+    uint32_t cs = 0;  // the product's 512 KiB runs for 5+ leaves
+    while (((size_t)2 << cs) * ((size_t)64 * U * 16) <= (size_t)512 * 1024 && cs < 16) ++cs;
+    char name[160];
+    std::snprintf(name, sizeof name, "tree8x2 %s U=%d cap=%d piece=%zuMiB sets=%d", DT == CHR_FLOAT32 ? "f32 " : "bf16",
+                  U, cap, piece >> 20, sets);
+    report_moved(name, 2.0 * 9 * piece, tree8x2_time_dt<DT, U>(S, nvec, sets, lds_for_cap(cap), cs));
+}
+
+static void focus32(size_t piece, int sets) {
+    const size_t nvec = piece / 16;
+    Sets S = make_sets(17, nvec, sets);
+    for (int cap : {12, 16, 20, 0}) {
+        focus32_row<CHR_FLOAT32, 1>(S, nvec, sets, piece, cap);
+        focus32_row<CHR_BFLOAT16, 1>(S, nvec, sets, piece, cap);
+        focus32_row<CHR_BFLOAT16, 2>(S, nvec, sets, piece, cap);
+    }
+    free_sets(S);
+}
+
 // ---- focus21: back-to-back tree launches with the AQL barrier bit cleared ----------------------
 // hipExtAnyOrderLaunch lets the packet processor start launch i+1 while launch i drains; the flat
 // plan's consecutive slice evaluations touch disjoint memory, so only the ramp/drain gap is at stake.
@@ -2065,6 +2118,16 @@ int main(int argc, char** argv) {
                     }
                     free_sets(S);
                 }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus32") {  // bf16 vs f32 trees: U and waves per CU
+        for (int r = 0; r < 2; ++r) {
+            for (size_t mib : {16, 8}) {
+                focus32(mib << 20, 16);  // cold: 2.25 / 4.5 GiB rotation
+                focus32(mib << 20, 2);   // warm
+            }
+            std::printf("--\n");
+        }
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus31") {  // page-local chunks past the translation reach
