@@ -5,7 +5,6 @@
 
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
 #include <type_traits>
 
 #include "reduce_common.hpp"
@@ -282,6 +281,11 @@ constexpr size_t tree_xcd_run_kib() {
 // 0.703-0.709 (C5) against 0.695-0.697 / 0.688), so 16 / 512 KiB stays -- except beside RCCL
 // (stream_wg_cap), where every tree takes kCoresidentWgPerCu: at 16 or uncapped RCCL's kernel waits
 // for the tree launch to drain (profiles/r03/coresidency/).
+// Beside RCCL (cap 12) U = 2 would keep more bytes in flight -- one GPU's own C4 / C5 grids on just-received leaves
+// +4-7 % (profiles/r05/ab_treeu/, 3 rounds) -- but it needs 82-90 VGPRs per wave against U = 1's 50-58, and then
+// three tree waves on a SIMD leave less than the ~288 VGPRs rcclGenericKernel's waves need: an RCCL-sized kernel
+// was admitted only when the tree launch drained (median 170 us against 4 us) and the real RCCL kernel beside the
+// C4 slice took 164-165 us against 114-120 us (tools/gpu_cores_u.sh, profiles/r05/cores_u/).  U = 1 stays.
 template <int NL, bool NT>
 constexpr int tree_u() {
     if constexpr (!NT) return NL <= 4 ? 4 : 2;  // cache-warm (plain) launches: the round-1 shapes
@@ -292,34 +296,9 @@ constexpr int tree_wg_per_cu() {
     return NL <= 4 ? 0 : 16;
 }
 
-// CHR_TREE_U (A/B hook): 1 or 2 vectors per lane for streaming f32 / bf16 trees of 5+ leaves; unset or 0 = the
-// policy (tree_u_wide).
-inline int tree_u_env() {
-    static const int v = [] {
-        const char* e = std::getenv("CHR_TREE_U");
-        return e ? std::atoi(e) : 0;
-    }();
-    return v;
-}
-
-// Whether a streaming f32 / bf16 tree of 5+ leaves takes U = 2 instead of tree_u's 1, given the resident workgroups
-// per CU it will run at (`cap`, 0 = uncapped).  At the in-collective cap (<= kCoresidentWgPerCu, CoresidentScope
-// beside RCCL) a one-wave U = 1 workgroup set holds too few bytes in flight: one GPU's own C4 / C5 grids
-// (tools/ab.sh treeu, profiles/r05/ab_treeu/, rocprof kernel durations, 3 alternating rounds) gain with U = 2 on
-// leaves just rewritten by the receive copies -- the node's case -- C4 0.691-0.699 -> 0.730-0.737 (4 slices),
-// 0.625-0.628 -> 0.667-0.671 (8), C5 0.687-0.689 -> 0.711-0.726, 0.606-0.612 -> 0.635-0.640 -- and tie or gain
-// 1-2 % on cold leaves; at the standalone cap 16 U = 2 loses 2-4 % on every row, so U = 1 stays there
-// (microbench focus32 agrees: profiles/r05/microbench_focus32_bf16_tree.txt).  CHR_TREE_U forces either shape.
-template <int DT>
-inline bool tree_u_wide(int cap) {
-    const int e = tree_u_env();
-    if (e == 1 || e == 2) return e == 2;
-    return cap > 0 && cap <= kCoresidentWgPerCu;
-}
-
-template <int DT, int OP, int NL, int BL, bool NT, int UF = 0>
+template <int DT, int OP, int NL, int BL, bool NT>
 inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
-    constexpr int U = UF ? UF : is_complex_dt<DT>() && OP == CHR_PROD ? 1 : tree_u<NL, NT>();  // see vec_u_dt
+    constexpr int U = is_complex_dt<DT>() && OP == CHR_PROD ? 1 : tree_u<NL, NT>();  // see vec_u_dt
     TreeArgs a = a_in;
     a.xrun = NT ? xcd_run_shift(tree_xcd_run_kib<NL>(), (size_t)BL * U * 16) : 0;
     // the odd-XCD handover of streaming launches (xcd_hand / xcd_trip_w in reduce_common.hpp), per segment
@@ -381,12 +360,7 @@ inline hipError_t launch_tree_nl(const TreeArgs& a, const TreeScalarArgs* sa, hi
     const size_t call_bytes = (size_t)(a.nl + 1) * nvec * 16;
     const bool nt = t.nt_mode == 1 || (t.nt_mode < 0 && call_bytes >= t.tree_nt_min_bytes);
     if constexpr (is_pair_dt<DT>() || is_complex_dt<DT>()) return launch_tree_vec<DT, OP, NL, 256, false>(a, s);  // as launch_vec_m
-    else {
-        if constexpr (NL > 4 && (DT == CHR_FLOAT32 || DT == CHR_BFLOAT16))
-            if (nt && tree_u_wide<DT>(stream_wg_cap(t.wg_per_cu_tree, tree_wg_per_cu<NL>())))
-                return launch_tree_vec<DT, OP, NL, 64, true, 2>(a, s);
-        return nt ? launch_tree_vec<DT, OP, NL, 64, true>(a, s) : launch_tree_vec<DT, OP, NL, 256, false>(a, s);
-    }
+    else return nt ? launch_tree_vec<DT, OP, NL, 64, true>(a, s) : launch_tree_vec<DT, OP, NL, 256, false>(a, s);
 }
 
 template <int DT, int OP>

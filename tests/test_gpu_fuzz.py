@@ -164,11 +164,3 @@ def test_fuzz_collectives_streaming_kernels_forced():
     assert res["nbad"] == 0, res["bad"]
     assert res["done"] == 400
 
-
-def test_fuzz_collectives_streaming_trees_two_vectors_per_lane():
-    """The U = 2 streaming shape of the 5+-leaf floating trees (CHR_TREE_U=2; reduce_tree.hpp tree_u_wide), every
-    family and dtype class of the fuzz, bit-exact against the oracle like the policy shapes."""
-    res = _run(4242, 300, {"CHR_REDUCE_NT": "1", "CHR_XCD_RUN_KIB": "4", "CHR_REDUCE_MAX_LAUNCH_VEC": "2048",
-                           "CHR_TREE_U": "2"})
-    assert res["nbad"] == 0, res["bad"]
-    assert res["done"] == 300

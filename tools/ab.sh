@@ -226,7 +226,8 @@ treerun)  # XCD runs of the 8-leaf trees (policy 512 KiB) on one GPU's own C4 / 
 import json, sys; d = json.load(sys.stdin)['rank_trees_rocprof']; print({k.replace('_rank0_alone', ''): v['frac_avg'] for k, v in d.items()})")"
     done
   done ;;
-treeu)  # U = 1 vs 2 for the floating 8-leaf trees (CHR_TREE_U) on one GPU's own C4 / C5 grids, at the in-collective
+treeu)  # U = 1 vs 2 for the floating 8-leaf trees (CHR_TREE_U: the knob exists at commit bace861 only) on one GPU's
+        # own C4 / C5 grids, at the in-collective
         # cap 12 (CHR_WG_PER_CU_TREE=12, what CoresidentScope gives them beside RCCL) and at the standalone policy 16,
         # by rocprof kernel duration (tools/rank_trees_summary.py), 3 alternating rounds
   mkdir -p gpurun_out/ab_treeu
