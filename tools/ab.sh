@@ -242,6 +242,19 @@ import json, sys; d = json.load(sys.stdin)['rank_trees_rocprof']; print({k.repla
       done
     done
   done ;;
+treestage)  # the LDS-staged 8-leaf trees (CHR_TREE_STAGE: a round-5 working-tree knob, never committed; the
+            # kernel is tools/reduce_microbench.hip's k_tree_lds) against the one-vector trip on one GPU's own C4 / C5 grids at
+            # the in-collective cap 12, by rocprof kernel duration (tools/rank_trees_summary.py), 3 alternating rounds
+  mkdir -p gpurun_out/ab_treestage
+  for r in 1 2 3; do
+    for v in 0 1; do
+      d="$PWD/gpurun_out/ab_treestage/s${v}_r${r}"
+      CHR_WG_PER_CU_TREE=12 CHR_TREE_STAGE=$v timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$d" \
+        -o run -- python3 bench.py --rank-trees > "$d.json" 2>/dev/null || exit 1
+      echo "treestage stage=$v r=$r $(python tools/rank_trees_summary.py "$d.json" "$d" | python -c "
+import json, sys; d = json.load(sys.stdin)['rank_trees_rocprof']; print({k.replace('_rank0_alone', ''): v['frac_avg'] for k, v in d.items()})")"
+    done
+  done ;;
 xrun4)  # XCD runs for wide fan-in (m = 4..7) and m = 3 at 1 GiB: 128 / 256 KiB vs the 512 KiB policy, 2 GiB rotation
   mkdir -p gpurun_out/ab_xrun
   P="python tools/mstream_probe.py --layouts sep --reps 40 --gate"
@@ -254,6 +267,6 @@ xrun4)  # XCD runs for wide fan-in (m = 4..7) and m = 3 at 1 GiB: 128 / 256 KiB 
     done
     echo "xrun4 r=$r done"
   done ;;
-*) echo "usage: tools/ab.sh cap|runs|tree|mid|mid2|xrun|xrunpmc|tlbpf|treebl|xrun3|wspmc|treerun|xrun4|treeu"; exit 2 ;;
+*) echo "usage: tools/ab.sh cap|runs|tree|mid|mid2|xrun|xrunpmc|tlbpf|treebl|xrun3|wspmc|treerun|xrun4|treeu|treestage"; exit 2 ;;
 esac
 echo AB_DONE

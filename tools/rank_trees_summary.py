@@ -20,7 +20,7 @@ def main():
     calls = int(sys.argv[3]) if len(sys.argv) > 3 else 12
     trace = sorted(glob.glob(os.path.join(sys.argv[2], "**", "*kernel_trace.csv"), recursive=True))[0]
     disp = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
-                   for r in csv.DictReader(open(trace)) if "k_reduce_tree<" in r["Kernel_Name"]))
+                   for r in csv.DictReader(open(trace)) if "k_reduce_tree<" in r["Kernel_Name"] or "k_reduce_tree_staged<" in r["Kernel_Name"]))
     need = sum(calls * v["launches_per_call"] for v in rows.values())
     if len(disp) != need:
         raise SystemExit(f"{len(disp)} tree dispatches in the trace, the rows account for {need}")
@@ -29,8 +29,9 @@ def main():
         n = calls * v["launches_per_call"]
         mine = disp[i:i + n]
         i += n
-        sym = "k_reduce_tree<3," if "bf16" in key else "k_reduce_tree<0,"
-        if not all(sym in name.replace(" ", "") for _, _, name in mine):
+        dt = "<3," if "bf16" in key else "<0,"
+        if not all(("k_reduce_tree" + dt) in name.replace(" ", "") or ("k_reduce_tree_staged" + dt) in name.replace(" ", "")
+                   for _, _, name in mine):
             raise SystemExit(f"row {key}: dispatches of another kernel in its slice of the trace")
         durs = [(e - s) / 1e3 for s, e, _ in mine[2 * v["launches_per_call"]:]]  # past the 2 warm-up calls
         by = v["algorithmic_bytes_per_call"] / v["launches_per_call"]

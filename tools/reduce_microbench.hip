@@ -1543,6 +1543,197 @@ static void focus32(size_t piece, int sets) {
     free_sets(S);
 }
 
+// ---- focus33: the second vector of each leaf through LDS (in-collective cap 12) -----------------------------
+// U = 2 in registers recovers the bytes in flight that cap 12 costs the trees but needs 82-90 VGPRs, which locks
+// RCCL's ~288-VGPR waves out (profiles/r05/cores_u/).  The cap already reserves 13.5 KiB of LDS per workgroup
+// that nothing uses: here the trip is U = 2 vectors per lane, the first held in registers as in k_reduce_tree, the
+// second landed in that LDS by global_load_lds_dwordx4 (1 KiB per leaf per wave; each lane reads back only the
+// 16 B its own DMA wrote, so the wave's own vmcnt orders it).  Half 0 is evaluated while half 1 sits in LDS, so
+// the register peak stays near U = 1's.
+template <int DT, int OP, int NL, bool NT>
+__global__ __launch_bounds__(64) void k_tree_lds(chr::TreeArgs a) {
+    using chr::u32x4;
+    extern __shared__ u32x4 lbuf[];
+    const uint32_t b = blockIdx.x, xrun = a.xrun;
+    uint32_t b0s[chr::kMaxTreeSegs], xfs[chr::kMaxTreeSegs], hds[chr::kMaxTreeSegs];
+#pragma unroll
+    for (int j = 0; j < chr::kMaxTreeSegs; ++j) {
+        b0s[j] = a.block0[j];
+        xfs[j] = a.xfull[j];
+        hds[j] = a.hand[j];
+        chr::pin_sgpr_u32(b0s[j], xfs[j]);
+        chr::pin_sgpr_u32(hds[j], xrun);
+    }
+    int s = 0;
+    uint32_t b0 = 0, xfull = xfs[0], hand = hds[0];
+#pragma unroll
+    for (int j = 1; j < chr::kMaxTreeSegs; ++j)
+        if (b >= b0s[j]) {
+            s = j;
+            b0 = b0s[j];
+            xfull = xfs[j];
+            hand = hds[j];
+        }
+    const chr::TreeSeg& g = a.seg[s];
+    u32x4* const out = g.out;
+    const u32x4* leaves[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) leaves[j] = g.leaves[j];
+    const size_t nvec = g.nvec;
+    const uint32_t comb = g.comb, swaps = g.swaps;
+    chr::pin_sgpr(out, leaves[0], nvec, comb, swaps);
+#pragma unroll
+    for (int j = 1; j < NL; ++j) chr::pin_sgpr(leaves[j]);
+    const size_t trip = chr::xcd_trip_w(b - b0, xfull, xrun, hand);
+    if (trip == chr::kIdleTrip) return;
+    const size_t base = trip * 128 + threadIdx.x;
+    if ((trip + 1) * 128 <= nvec) {
+        u32x4 x[NL][1];
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            x[j][0] = chr::ld<NT>(&leaves[j][base]);
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)&leaves[j][base + 64],
+                                             (__attribute__((address_space(3))) void*)&lbuf[j * 64], 16, 0,
+                                             NT ? 2 : 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        u32x4 r0[1];
+        chr::tree_eval<u32x4, NL, 1, chr::VecOp<DT, OP>>(x, r0, comb, swaps);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        u32x4 y[NL][1];
+#pragma unroll
+        for (int j = 0; j < NL; ++j) y[j][0] = lbuf[j * 64 + threadIdx.x];
+        u32x4 r1[1];
+        chr::tree_eval<u32x4, NL, 1, chr::VecOp<DT, OP>>(y, r1, comb, swaps);
+        chr::st<NT>(&out[base], r0[0]);
+        chr::st<NT>(&out[base + 64], r1[0]);
+    } else {
+        for (int u = 0; u < 2; ++u) {
+            const size_t i = base + (size_t)u * 64;
+            if (i >= nvec) break;
+            u32x4 x[NL][1];
+#pragma unroll
+            for (int j = 0; j < NL; ++j) x[j][0] = leaves[j][i];
+            u32x4 r[1];
+            chr::tree_eval<u32x4, NL, 1, chr::VecOp<DT, OP>>(x, r, comb, swaps);
+            out[i] = r[0];
+        }
+    }
+}
+
+// tree8x2 at the product's 512 KiB runs and the odd-XCD handover (shift 6), kernel chosen by KIND: 0 = product U = 1,
+// 1 = product U = 2, 2 = k_tree_lds
+template <int DT, int KIND>
+static double tree8x2_kind(Sets& S, size_t nvec, int sets, unsigned lds) {
+    constexpr int U = KIND == 0 ? 1 : 2;
+    uint32_t cs = 0;
+    while (((size_t)2 << cs) * ((size_t)64 * U * 16) <= (size_t)512 * 1024 && cs < 16) ++cs;
+    return time_launches([&](int i) {
+        chr::TreeArgs a{};
+        const auto& b = S.bufs[i % sets];
+        a.nseg = 2;
+        a.nl = 8;
+        a.xrun = cs;
+        const uint32_t trips = (uint32_t)((nvec + 64 * U - 1) / (64 * U));
+        size_t grid = 0;
+        for (int j = 0; j < chr::kMaxTreeSegs; ++j) {
+            if (j >= 2) {
+                a.block0[j] = ~0u;
+                continue;
+            }
+            grid = (grid + 7) & ~(size_t)7;
+            a.block0[j] = (uint32_t)grid;
+            a.xfull[j] = chr::xcd_full(trips, cs);
+            a.hand[j] = chr::xcd_hand(a.xfull[j], 6);
+            grid += trips + 8u * (size_t)a.hand[j];
+        }
+        const int comb[8] = {0, 1, 1, 1, 0, 1, 1, 2};
+        for (int t2 = 0; t2 < 2; ++t2) {
+            chr::TreeSeg& g = a.seg[t2];
+            for (int l = 0; l < 8; ++l) g.leaves[l] = (const chr::u32x4*)b[9 * t2 + l];
+            g.out = (chr::u32x4*)b[9 * t2 + 8];
+            g.nvec = nvec;
+            g.comb = 0;
+            for (int l = 0; l < 8; ++l) g.comb |= (uint32_t)comb[l] << (2 * l);
+            g.swaps = 0;
+        }
+        if constexpr (KIND == 2)
+            hipLaunchKernelGGL((k_tree_lds<DT, CHR_SUM, 8, true>), dim3((unsigned)grid), dim3(64), lds, 0, a);
+        else
+            hipLaunchKernelGGL((chr::k_reduce_tree<DT, CHR_SUM, 8, U, true, 64>), dim3((unsigned)grid), dim3(64), lds, 0,
+                               a);
+    }, 60);
+}
+
+static void focus33(size_t piece, int sets) {
+    const size_t nvec = piece / 16;
+    Sets S = make_sets(17, nvec, sets);
+    const char* kinds[3] = {"U=1    ", "U=2    ", "U=1+LDS"};
+    for (int cap : {12, 16}) {
+        const unsigned lds = lds_for_cap(cap);
+        char name[160];
+#define F33(DT, K)                                                                                             \
+    std::snprintf(name, sizeof name, "tree8x2 %s %s cap=%d piece=%zuMiB sets=%d", DT == CHR_FLOAT32 ? "f32 " : "bf16", \
+                  kinds[K], cap, piece >> 20, sets);                                                          \
+    report_moved(name, 2.0 * 9 * piece, tree8x2_kind<DT, K>(S, nvec, sets, lds));
+        F33(CHR_FLOAT32, 0) F33(CHR_FLOAT32, 1) F33(CHR_FLOAT32, 2)
+        F33(CHR_BFLOAT16, 0) F33(CHR_BFLOAT16, 1) F33(CHR_BFLOAT16, 2)
+#undef F33
+    }
+    free_sets(S);
+}
+
+// A correctness check of k_tree_lds against the product U = 1 kernel (bit-identical outputs), run once.
+static bool focus33_check() {
+    const size_t nvec = (size_t)(3 << 20) / 16 + 37;  // a partial trip at the end
+    Sets S = make_sets(17, nvec, 1);
+    chr::u32x4 *o1, *o2;
+    CK(hipMalloc(&o1, nvec * 16));
+    CK(hipMalloc(&o2, nvec * 16));
+    bool ok = true;
+    for (int kind = 0; kind < 2 && ok; ++kind) {
+        chr::TreeArgs a{};
+        auto& b = S.bufs[0];
+        a.nseg = 1;
+        a.nl = 8;
+        a.xrun = 0;
+        const int comb[8] = {0, 1, 0, 1, 1, 0, 2, 2};
+        for (int j = 0; j < chr::kMaxTreeSegs; ++j) a.block0[j] = j ? ~0u : 0;
+        chr::TreeSeg& g = a.seg[0];
+        for (int l = 0; l < 8; ++l) g.leaves[l] = (const chr::u32x4*)b[l];
+        g.nvec = nvec;
+        g.comb = 0;
+        for (int l = 0; l < 8; ++l) g.comb |= (uint32_t)comb[l] << (2 * l);
+        g.swaps = 0x15;
+        const uint32_t t1 = (uint32_t)((nvec + 63) / 64), t2 = (uint32_t)((nvec + 127) / 128);
+        a.xfull[0] = chr::xcd_full(t1, 0);
+        g.out = o1;
+        hipLaunchKernelGGL((chr::k_reduce_tree<CHR_FLOAT32, CHR_MAX, 8, 1, true, 64>), dim3(t1), dim3(64), 0, 0, a);
+        a.xfull[0] = chr::xcd_full(t2, 0);
+        g.out = o2;
+        if (kind == 0)
+            hipLaunchKernelGGL((k_tree_lds<CHR_FLOAT32, CHR_MAX, 8, true>), dim3(t2), dim3(64), lds_for_cap(12), 0, a);
+        else
+            hipLaunchKernelGGL((k_tree_lds<CHR_BFLOAT16, CHR_SUM, 8, true>), dim3(t2), dim3(64), lds_for_cap(16), 0, a);
+        if (kind == 1) {  // compare against the product's bf16 U = 1
+            a.xfull[0] = chr::xcd_full(t1, 0);
+            g.out = o1;
+            hipLaunchKernelGGL((chr::k_reduce_tree<CHR_BFLOAT16, CHR_SUM, 8, 1, true, 64>), dim3(t1), dim3(64), 0, 0, a);
+        }
+        CK(hipDeviceSynchronize());
+        std::vector<uint32_t> h1(nvec * 4), h2(nvec * 4);
+        CK(hipMemcpy(h1.data(), o1, nvec * 16, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(h2.data(), o2, nvec * 16, hipMemcpyDeviceToHost));
+        ok = h1 == h2;
+        std::printf("{\"focus33_check\": %d, \"bit_identical\": %s}\n", kind, ok ? "true" : "false");
+    }
+    CK(hipFree(o1));
+    CK(hipFree(o2));
+    free_sets(S);
+    return ok;
+}
+
 // ---- focus21: back-to-back tree launches with the AQL barrier bit cleared ----------------------
 // hipExtAnyOrderLaunch lets the packet processor start launch i+1 while launch i drains; the flat
 // plan's consecutive slice evaluations touch disjoint memory, so only the ramp/drain gap is at stake.
@@ -2118,6 +2309,17 @@ int main(int argc, char** argv) {
                     }
                     free_sets(S);
                 }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus33") {  // second vector through LDS at the in-collective cap
+        if (!focus33_check()) return 1;
+        for (int r = 0; r < 3; ++r) {
+            for (size_t mib : {16, 8}) {
+                focus33(mib << 20, 16);  // cold
+                focus33(mib << 20, 2);   // warm
+            }
+            std::printf("--\n");
+        }
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus32") {  // bf16 vs f32 trees: U and waves per CU
