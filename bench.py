@@ -258,6 +258,9 @@ def line_problems(line):
             probs += [f"c5.{k} missing" for k in ("schedule", "slices", "overlap") if k not in c5]
             if c5.get("slices") is not None and c5["slices"] < 2 and "overlapped_best_depth_ge2" not in c5:
                 probs.append("c5 ran one slice and no overlapped depth was timed")
+            c5rc = c5.get("result_check")
+            if c5rc is not None and not (c5rc.get("ranks_bit_identical") and c5rc.get("within_tolerance")):
+                probs.append(f"c5 result_check failed: {c5rc}"[:300])
         if line["definitions"] != LINE_DEFINITIONS_NN:
             probs.append("definitions differ from LINE_DEFINITIONS_NN")
     cb = line["cpu_baseline"]
@@ -1452,6 +1455,16 @@ def baseline_configs(args, ca, torch, dist, comm, world, dev, steps, warm, late=
                 "algbw_GBps": round(algbw, 2), "busbw_GBps": round(algbw * 2 * (world - 1) / world, 2),
                 "ms_per_call": round(el / steps * 1e3, 4)}
             row.update(c5_overlap_record(ca, comm, cnt, world))
+            # C5's own output, as the metric's (bf16 tolerance: DESIGN §7)
+            try:
+                def fill5(r, buf):
+                    ca.check(ca.fill(buf, cnt, ca.BFLOAT16, 0, SEED, r, stream=comm.stream))
+                    torch.cuda.synchronize()
+                ca.check(comm.synchronize())
+                row["result_check"] = result_check(torch, dist, r5, cnt, 2, world, fill5)
+            except Exception as e:
+                row["result_check"] = {"error": str(e)[:200]}
+            torch.cuda.empty_cache()
             # C5 names compute/xGMI overlap: with one slice a call has nothing to overlap inside it, so
             # the best depth >= 2 is timed too and both are recorded
             if row.get("slices", 0) < 2 and not late():

@@ -141,6 +141,9 @@ def test_canned_lines_pass():
     (lambda l: l["roofline"].update(traffic=None), "traffic"),
     (lambda l: l["compare"]["c5_allreduce_bf16_k4_b4_1GiB"].pop("overlap"), "c5.overlap"),
     (lambda l: l["compare"]["c5_allreduce_bf16_k4_b4_1GiB"].update(slices=1), "overlapped depth"),
+    (lambda l: l["compare"]["c5_allreduce_bf16_k4_b4_1GiB"].update(
+        result_check={"ranks_bit_identical": False, "within_tolerance": True}), "c5 result_check"),
+    (lambda l: l["result_check"].update(ranks_bit_identical=False), "result_check failed"),
 ])
 def test_nn_line_definitions_are_enforced(mutate, problem):
     line = _nn_line()

@@ -1734,6 +1734,180 @@ static bool focus33_check() {
     return ok;
 }
 
+// ---- focus34: the tree program known at compile time ---------------------------------------------------------
+// k_reduce_tree interprets the post-order program (comb / swap bits) at run time: every push and combine is a scalar
+// branch over the stack depth with u32x4 moves between named slots.  For bf16 each combine also widens, adds and
+// RNE-packs (~6 VALU per dword), so a trip's VALU tail after its loads land is longest there, and at the
+// in-collective cap of 12 workgroups per CU bf16 trees run 3-6 % behind f32 (focus32).  Here the same trip with
+// the program as a template argument (C4 / C5's ((l0 l1 l2 l3)(l4 l5 l6 l7)), no swaps): the branches and slot
+// moves fold away.  Same arithmetic, same order.
+template <int DT, int OP, int NL, uint32_t COMB>
+__device__ __forceinline__ chr::u32x4 tree_eval_static(const chr::u32x4 (&x)[NL]) {
+    chr::u32x4 st[4];
+    int d = 0;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+        st[d++] = x[j];
+#pragma unroll
+        for (int c = (int)((COMB >> (2 * j)) & 3u); c > 0; --c) {
+            st[d - 2] = chr::apply_vec<DT, OP>(st[d - 1], st[d - 2]);
+            --d;
+        }
+    }
+    return st[0];
+}
+
+template <int DT, int OP, int NL, uint32_t COMB>
+__global__ __launch_bounds__(64) void k_tree_static(chr::TreeArgs a) {
+    using chr::u32x4;
+    const uint32_t b = blockIdx.x, xrun = a.xrun;
+    uint32_t b0s[chr::kMaxTreeSegs], xfs[chr::kMaxTreeSegs], hds[chr::kMaxTreeSegs];
+#pragma unroll
+    for (int j = 0; j < chr::kMaxTreeSegs; ++j) {
+        b0s[j] = a.block0[j];
+        xfs[j] = a.xfull[j];
+        hds[j] = a.hand[j];
+        chr::pin_sgpr_u32(b0s[j], xfs[j]);
+        chr::pin_sgpr_u32(hds[j], xrun);
+    }
+    int s = 0;
+    uint32_t b0 = 0, xfull = xfs[0], hand = hds[0];
+#pragma unroll
+    for (int j = 1; j < chr::kMaxTreeSegs; ++j)
+        if (b >= b0s[j]) {
+            s = j;
+            b0 = b0s[j];
+            xfull = xfs[j];
+            hand = hds[j];
+        }
+    const chr::TreeSeg& g = a.seg[s];
+    u32x4* const out = g.out;
+    const u32x4* leaves[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) leaves[j] = g.leaves[j];
+    const size_t nvec = g.nvec;
+    chr::pin_sgpr(out, leaves[0], nvec, 0u, 0u);
+#pragma unroll
+    for (int j = 1; j < NL; ++j) chr::pin_sgpr(leaves[j]);
+    const size_t trip = chr::xcd_trip_w(b - b0, xfull, xrun, hand);
+    if (trip == chr::kIdleTrip) return;
+    const size_t base = trip * 64 + threadIdx.x;
+    if ((trip + 1) * 64 <= nvec) {
+        u32x4 x[NL];
+#pragma unroll
+        for (int j = 0; j < NL; ++j) x[j] = chr::ld<true>(&leaves[j][base]);
+        __builtin_amdgcn_sched_barrier(0);
+        chr::st<true>(&out[base], tree_eval_static<DT, OP, NL, COMB>(x));
+    } else if (base < nvec) {
+        u32x4 x[NL];
+#pragma unroll
+        for (int j = 0; j < NL; ++j) x[j] = leaves[j][base];
+        out[base] = tree_eval_static<DT, OP, NL, COMB>(x);
+    }
+}
+
+constexpr uint32_t kC4Comb = (0u << 0) | (1u << 2) | (1u << 4) | (1u << 6) | (0u << 8) | (1u << 10) | (1u << 12) | (2u << 14);
+
+// tree8x2 at the product's 512 KiB runs and handover shift 6: KIND 0 = product k_reduce_tree U = 1, 1 = k_tree_static
+template <int DT, int KIND>
+static double tree8x2_static(Sets& S, size_t nvec, int sets, unsigned lds) {
+    uint32_t cs = 0;
+    while (((size_t)2 << cs) * ((size_t)64 * 16) <= (size_t)512 * 1024 && cs < 16) ++cs;
+    return time_launches([&](int i) {
+        chr::TreeArgs a{};
+        const auto& b = S.bufs[i % sets];
+        a.nseg = 2;
+        a.nl = 8;
+        a.xrun = cs;
+        const uint32_t trips = (uint32_t)((nvec + 63) / 64);
+        size_t grid = 0;
+        for (int j = 0; j < chr::kMaxTreeSegs; ++j) {
+            if (j >= 2) {
+                a.block0[j] = ~0u;
+                continue;
+            }
+            grid = (grid + 7) & ~(size_t)7;
+            a.block0[j] = (uint32_t)grid;
+            a.xfull[j] = chr::xcd_full(trips, cs);
+            a.hand[j] = chr::xcd_hand(a.xfull[j], 6);
+            grid += trips + 8u * (size_t)a.hand[j];
+        }
+        for (int t2 = 0; t2 < 2; ++t2) {
+            chr::TreeSeg& g = a.seg[t2];
+            for (int l = 0; l < 8; ++l) g.leaves[l] = (const chr::u32x4*)b[9 * t2 + l];
+            g.out = (chr::u32x4*)b[9 * t2 + 8];
+            g.nvec = nvec;
+            g.comb = kC4Comb;
+            g.swaps = 0;
+        }
+        if constexpr (KIND == 1)
+            hipLaunchKernelGGL((k_tree_static<DT, CHR_SUM, 8, kC4Comb>), dim3((unsigned)grid), dim3(64), lds, 0, a);
+        else
+            hipLaunchKernelGGL((chr::k_reduce_tree<DT, CHR_SUM, 8, 1, true, 64>), dim3((unsigned)grid), dim3(64), lds, 0,
+                               a);
+    }, 60);
+}
+
+static void focus34(size_t piece, int sets) {
+    const size_t nvec = piece / 16;
+    Sets S = make_sets(17, nvec, sets);
+    for (int cap : {12, 16}) {
+        const unsigned lds = lds_for_cap(cap);
+        char name[160];
+#define F34(DT, K)                                                                                              \
+    std::snprintf(name, sizeof name, "tree8x2 %s %s cap=%d piece=%zuMiB sets=%d", DT == CHR_FLOAT32 ? "f32 " : "bf16", \
+                  K ? "static " : "runtime", cap, piece >> 20, sets);                                            \
+    report_moved(name, 2.0 * 9 * piece, tree8x2_static<DT, K>(S, nvec, sets, lds));
+        F34(CHR_FLOAT32, 0) F34(CHR_FLOAT32, 1) F34(CHR_BFLOAT16, 0) F34(CHR_BFLOAT16, 1)
+#undef F34
+    }
+    free_sets(S);
+}
+
+// k_tree_static against the product kernel on the same leaves: bit-identical (f32 and bf16 SUM)
+static bool focus34_check() {
+    const size_t nvec = (size_t)(3 << 20) / 16 + 37;
+    Sets S = make_sets(17, nvec, 1);
+    chr::u32x4 *o1, *o2;
+    CK(hipMalloc(&o1, nvec * 16));
+    CK(hipMalloc(&o2, nvec * 16));
+    bool ok = true;
+    for (int kind = 0; kind < 2 && ok; ++kind) {
+        chr::TreeArgs a{};
+        auto& b = S.bufs[0];
+        a.nseg = 1;
+        a.nl = 8;
+        for (int j = 0; j < chr::kMaxTreeSegs; ++j) a.block0[j] = j ? ~0u : 0;
+        chr::TreeSeg& g = a.seg[0];
+        for (int l = 0; l < 8; ++l) g.leaves[l] = (const chr::u32x4*)b[l];
+        g.nvec = nvec;
+        g.comb = kC4Comb;
+        g.swaps = 0;
+        const uint32_t t1 = (uint32_t)((nvec + 63) / 64);
+        a.xfull[0] = chr::xcd_full(t1, 0);
+        g.out = o1;
+        if (kind == 0) {
+            hipLaunchKernelGGL((chr::k_reduce_tree<CHR_FLOAT32, CHR_SUM, 8, 1, true, 64>), dim3(t1), dim3(64), 0, 0, a);
+            g.out = o2;
+            hipLaunchKernelGGL((k_tree_static<CHR_FLOAT32, CHR_SUM, 8, kC4Comb>), dim3(t1), dim3(64), 0, 0, a);
+        } else {
+            hipLaunchKernelGGL((chr::k_reduce_tree<CHR_BFLOAT16, CHR_SUM, 8, 1, true, 64>), dim3(t1), dim3(64), 0, 0, a);
+            g.out = o2;
+            hipLaunchKernelGGL((k_tree_static<CHR_BFLOAT16, CHR_SUM, 8, kC4Comb>), dim3(t1), dim3(64), 0, 0, a);
+        }
+        CK(hipDeviceSynchronize());
+        std::vector<uint32_t> h1(nvec * 4), h2(nvec * 4);
+        CK(hipMemcpy(h1.data(), o1, nvec * 16, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(h2.data(), o2, nvec * 16, hipMemcpyDeviceToHost));
+        ok = h1 == h2;
+        std::printf("{\"focus34_check\": %d, \"bit_identical\": %s}\n", kind, ok ? "true" : "false");
+    }
+    CK(hipFree(o1));
+    CK(hipFree(o2));
+    free_sets(S);
+    return ok;
+}
+
 // ---- focus21: back-to-back tree launches with the AQL barrier bit cleared ----------------------
 // hipExtAnyOrderLaunch lets the packet processor start launch i+1 while launch i drains; the flat
 // plan's consecutive slice evaluations touch disjoint memory, so only the ramp/drain gap is at stake.
@@ -2309,6 +2483,17 @@ int main(int argc, char** argv) {
                     }
                     free_sets(S);
                 }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "focus34") {  // the tree program at compile time
+        if (!focus34_check()) return 1;
+        for (int r = 0; r < 3; ++r) {
+            for (size_t mib : {16, 8}) {
+                focus34(mib << 20, 16);  // cold
+                focus34(mib << 20, 2);   // warm
+            }
+            std::printf("--\n");
+        }
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "focus33") {  // second vector through LDS at the in-collective cap
