@@ -102,6 +102,72 @@ __device__ __forceinline__ void tree_eval(const V (&x)[NL][W], V (&r)[W], uint32
     }
 }
 
+// ---- programs known at compile time ------------------------------------------------------------------------
+// tree_eval interprets the program at run time: every push and combine is a scalar branch over the stack depth,
+// with u32x4 moves between the named slots.  That VALU tail after a trip's loads land stretches the workgroup's
+// life, which costs the most where residency is capped -- beside RCCL, 12 workgroups per CU -- and for bf16, whose
+// combines widen, add and RNE-pack (tools/reduce_microbench focus34, profiles/r05/microbench_focus34_static_tree.txt:
+// C4's tree at cap 12, 16 MiB pieces, cold f32 0.753-0.762 -> 0.782-0.784, bf16 0.723-0.737 -> 0.778-0.793; 8 MiB
+// f32 0.684-0.689 -> 0.721-0.724, bf16 0.646-0.652 -> 0.710-0.715; cap 16 +1-3 %).  The programs the flat
+// schedule emits at 4 and 8 ranks (every k and b; enumerated from chr_plan_describe) are unrolled at compile time
+// and chosen by one scalar compare per workgroup; anything else (other rank counts, swapped combines) keeps the
+// interpreter.  Same combines in the same order: only the instruction stream changes.
+constexpr uint32_t tree_prog(const int (&c)[8], int nl) {
+    uint32_t v = 0;
+    for (int j = 0; j < nl; ++j) v |= (uint32_t)c[j] << (2 * j);
+    return v;
+}
+template <int NL> struct StaticProgs { static constexpr int n = 0; static constexpr uint32_t v[1] = {0}; };
+template <> struct StaticProgs<8> {
+    static constexpr int n = 6;
+    static constexpr uint32_t v[6] = {
+        tree_prog({0, 1, 1, 1, 0, 1, 1, 2}, 8),  // b = 4, k >= 3: C4 / C5
+        tree_prog({0, 1, 0, 2, 0, 2, 0, 2}, 8),  // b = 2, any k
+        tree_prog({0, 1, 0, 2, 0, 1, 0, 3}, 8),  // b = 4 / 8, k = 2
+        tree_prog({0, 1, 1, 0, 1, 2, 0, 2}, 8),  // b = 8, k = 3
+        tree_prog({0, 1, 1, 1, 0, 2, 1, 1}, 8),  // b = 8, k = 4
+        tree_prog({0, 1, 1, 1, 1, 1, 1, 1}, 8)}; // b = 8, k >= 5: a left fold
+};
+template <> struct StaticProgs<4> {
+    static constexpr int n = 2;
+    static constexpr uint32_t v[2] = {tree_prog({0, 1, 0, 2, 0, 0, 0, 0}, 4), tree_prog({0, 1, 1, 1, 0, 0, 0, 0}, 4)};
+};
+
+// One program, unrolled: push leaf j, then its combines, each below = F(in = top, below) (no swapped combines).
+template <typename V, int NL, int W, typename F, uint32_t COMB>
+__device__ __forceinline__ void tree_eval_static(const V (&x)[NL][W], V (&r)[W]) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        V st[kTreeDepth];
+        int d = 0;
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            st[d++] = x[j][w];
+#pragma unroll
+            for (int c = (int)((COMB >> (2 * j)) & 3u); c > 0; --c) {
+                st[d - 2] = F::template ap<false>(st[d - 1], st[d - 2]);
+                --d;
+            }
+        }
+        r[w] = st[0];
+    }
+}
+
+// The unrolled body of `comb` when it is one of StaticProgs<NL> and no combine is swapped, else the interpreter.
+template <typename V, int NL, int W, typename F, int I = 0>
+__device__ __forceinline__ void tree_eval_fast(const V (&x)[NL][W], V (&r)[W], uint32_t comb, uint32_t swaps) {
+    if constexpr (I < StaticProgs<NL>::n) {
+        constexpr uint32_t P = StaticProgs<NL>::v[I];
+        if (swaps == 0 && comb == P) {
+            tree_eval_static<V, NL, W, F, P>(x, r);
+            return;
+        }
+        tree_eval_fast<V, NL, W, F, I + 1>(x, r, comb, swaps);
+    } else {
+        tree_eval<V, NL, W, F>(x, r, comb, swaps);
+    }
+}
+
 template <int DT, int OP>
 struct VecOp {
     template <bool SW>
@@ -194,7 +260,7 @@ __global__ __launch_bounds__(BL) void k_reduce_tree(TreeArgs a) {
             for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&leaves[j][base + (size_t)u * BL]);
         __builtin_amdgcn_sched_barrier(0);
         u32x4 r[U];
-        tree_eval<u32x4, NL, U, VecOp<DT, OP>>(x, r, comb, swaps);
+        tree_eval_fast<u32x4, NL, U, VecOp<DT, OP>>(x, r, comb, swaps);
 #pragma unroll
         for (int u = 0; u < U; ++u) st<NT>(&out[base + (size_t)u * BL], r[u]);
     } else {
