@@ -28,6 +28,39 @@ __device__ __forceinline__ uint32_t f2bf_pk(float lo, float hi) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2));
 }
 
+// a + b and a * b with a's NaN surviving when both are NaN (see kSumSw): the operand order is written into the
+// instruction, which the compiler cannot commute.  Rounding and every non-NaN result are those of the plain op.
+__device__ __forceinline__ float add_keep(float a, float b) {
+    float r;
+    asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float mul_keep(float a, float b) {
+    float r;
+    asm("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double add_keep(double a, double b) {
+    double r;
+    asm("v_add_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double mul_keep(double a, double b) {
+    double r;
+    asm("v_mul_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ f32x2 pk_add_keep(f32x2 a, f32x2 b) {
+    f32x2 r;
+    asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ f32x2 pk_mul_keep(f32x2 a, f32x2 b) {
+    f32x2 r;
+    asm("v_pk_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // MPI's pair types for MAXLOC / MINLOC and the C99 complex types, as element types of the kernels.
 // A pair element is carried as its raw 32-bit words (the C struct {value; int index} MPI defines,
 // padding included): MPICH replaces a whole element when the incoming one wins (padding bytes and
@@ -88,11 +121,17 @@ template <int DT>
 constexpr bool is_float_dt() { return DT == CHR_FLOAT32 || DT == CHR_FLOAT64 || DT == CHR_BFLOAT16; }
 
 // Internal op codes for the running-value-first order of MPICH_do_reduce
-// (allreduce_recexch.cpp:147-186): each step is MPI_Reduce_local(running, next).  SUM and
-// PROD are bitwise commutative (IEEE add/mul, wrapping int, bf16 RNE of a commutative f32
-// op), so only MAX/MIN need their own instantiations (they differ on ties such as -0/+0
-// and on NaN compares).
+// (allreduce_recexch.cpp:147-186): each step is MPI_Reduce_local(running, next).  Integer SUM
+// and PROD are bitwise commutative (wrapping); MAX/MIN differ on ties such as -0/+0 and on NaN
+// compares, so they have their own codes.
 constexpr int kMaxSw = 16, kMinSw = 17;
+// SUM / PROD on the floating types are bitwise commutative except for one thing: when both operands are NaN, IEEE
+// 754 leaves open whose payload survives.  The reference's loop (inout = inout + in, MPICH on x86) keeps inout's;
+// gfx950 keeps the FIRST SOURCE OPERAND's (tools/nan_rule_probe.hip), and the compiler may commute a plain + or *
+// (`a + b` and `b + a` both compiled to a-first there).  So the kernels pin the order in the instruction
+// (add_keep / mul_keep above: the first argument's NaN survives), and the running-value-first order gets its own
+// codes, as MAX / MIN do: kSumSw / kProdSw keep the incoming operand's NaN (tests/test_gpu_nan_payloads.py).
+constexpr int kSumSw = 20, kProdSw = 21;
 // The same for MAXLOC / MINLOC on the pairs with a floating value: a NaN compare keeps inout, and a
 // tie keeps inout's value bits (-0 vs +0), so the operand order shows.
 constexpr int kMaxLocSw = 18, kMinLocSw = 19;
@@ -162,17 +201,19 @@ __device__ __forceinline__ typename DTy<DT>::T apply(typename DTy<DT>::T x, type
             return r;
         }    } else if constexpr (is_complex_dt<DT>()) {
         typename DTy<DT>::T r;
-        if constexpr (OP == CHR_SUM) {
-            r.re = y.re + x.re;
-            r.im = y.im + x.im;
+        if constexpr (OP == CHR_SUM) {  // inout's NaN survives per part, as MPICH's loop on x86 keeps it
+            r.re = add_keep(y.re, x.re);
+            r.im = add_keep(y.im, x.im);
         } else {
             cmul(y.re, y.im, x.re, x.im, &r.re, &r.im);
         }
         return r;
     } else if constexpr (DT == CHR_BFLOAT16) {
         const float fx = bf2f(x), fy = bf2f(y);
-        if constexpr (OP == CHR_SUM) return f2bf(fy + fx);
-        else if constexpr (OP == CHR_PROD) return f2bf(fy * fx);
+        if constexpr (OP == CHR_SUM) return f2bf(add_keep(fy, fx));
+        else if constexpr (OP == CHR_PROD) return f2bf(mul_keep(fy, fx));
+        else if constexpr (OP == kSumSw) return f2bf(add_keep(fx, fy));
+        else if constexpr (OP == kProdSw) return f2bf(mul_keep(fx, fy));
         else if constexpr (OP == CHR_MAX) return fy > fx ? y : x;
         else if constexpr (OP == CHR_MIN) return fy < fx ? y : x;
         else if constexpr (OP == kMaxSw) return fx > fy ? x : y;
@@ -196,8 +237,10 @@ __device__ __forceinline__ typename DTy<DT>::T apply(typename DTy<DT>::T x, type
         else return (T)(y ^ x);
     } else {
         using T = typename DTy<DT>::T;
-        if constexpr (OP == CHR_SUM) return y + x;
-        else if constexpr (OP == CHR_PROD) return y * x;
+        if constexpr (OP == CHR_SUM) return add_keep(y, x);  // inout's NaN survives (kSumSw)
+        else if constexpr (OP == CHR_PROD) return mul_keep(y, x);
+        else if constexpr (OP == kSumSw) return add_keep(x, y);
+        else if constexpr (OP == kProdSw) return mul_keep(x, y);
         else if constexpr (OP == CHR_MAX) return y > x ? y : x;
         else if constexpr (OP == CHR_MIN) return y < x ? y : x;
         else if constexpr (OP == kMaxSw) return x > y ? x : y;
@@ -215,14 +258,31 @@ __device__ __forceinline__ u32x4 apply_vec(u32x4 in, u32x4 acc) {
     if constexpr (OP == CHR_BAND) return acc & in;
     if constexpr (OP == CHR_BOR) return acc | in;
     if constexpr (OP == CHR_BXOR) return acc ^ in;
-    if constexpr (DT == CHR_BFLOAT16 && (OP == CHR_SUM || OP == CHR_PROD)) {
-        // two bf16 per dword: widen by shift / mask, one f32 op each, one packed RNE convert
+    constexpr bool SUMLIKE = OP == CHR_SUM || OP == kSumSw, PRODLIKE = OP == CHR_PROD || OP == kProdSw;
+    constexpr bool SW = OP == kSumSw || OP == kProdSw;  // the incoming operand's NaN survives
+    if constexpr (DT == CHR_BFLOAT16 && (SUMLIKE || PRODLIKE)) {
+        // two bf16 per dword: widen by shift / mask, one packed f32 op (operand order pinned), one packed RNE convert
         u32x4 r;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const float xl = __uint_as_float(in[e] << 16), xh = __uint_as_float(in[e] & 0xFFFF0000u);
-            const float yl = __uint_as_float(acc[e] << 16), yh = __uint_as_float(acc[e] & 0xFFFF0000u);
-            r[e] = OP == CHR_SUM ? f2bf_pk(yl + xl, yh + xh) : f2bf_pk(yl * xl, yh * xh);
+            const f32x2 x2 = {__uint_as_float(in[e] << 16), __uint_as_float(in[e] & 0xFFFF0000u)};
+            const f32x2 y2 = {__uint_as_float(acc[e] << 16), __uint_as_float(acc[e] & 0xFFFF0000u)};
+            const f32x2 o = SUMLIKE ? (SW ? pk_add_keep(x2, y2) : pk_add_keep(y2, x2))
+                                    : (SW ? pk_mul_keep(x2, y2) : pk_mul_keep(y2, x2));
+            r[e] = f2bf_pk(o.x, o.y);
+        }
+        return r;
+    }
+    if constexpr (DT == CHR_FLOAT32 && (SUMLIKE || PRODLIKE)) {
+        u32x4 r;
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+            const f32x2 x2 = {__uint_as_float(in[e]), __uint_as_float(in[e + 1])};
+            const f32x2 y2 = {__uint_as_float(acc[e]), __uint_as_float(acc[e + 1])};
+            const f32x2 o = SUMLIKE ? (SW ? pk_add_keep(x2, y2) : pk_add_keep(y2, x2))
+                                    : (SW ? pk_mul_keep(x2, y2) : pk_mul_keep(y2, x2));
+            r[e] = __float_as_uint(o.x);
+            r[e + 1] = __float_as_uint(o.y);
         }
         return r;
     }

@@ -79,7 +79,8 @@ bool valid_dtype_op(int dtype, int op) {
 // The kernel instantiation that computes (dtype, op).  Signedness only matters to MAX/MIN:
 // wrapping SUM/PROD, the logical and the bitwise ops give the same bits on the unsigned type of
 // the same width (int32's kernels serve uint32 there).  running_first (MPICH_do_reduce order)
-// changes MAX/MIN results only for floating types (ties of -0/+0, NaN compares).
+// changes results only for floating types: MAX/MIN on ties of -0/+0 and NaN compares, SUM/PROD on
+// which NaN survives when two meet (kSumSw / kProdSw).
 void canon_op(int dtype, int op, bool running_first, int* kdt, int* kop) {
     *kop = op;
     if (is_pair_dtype(dtype) || is_complex_dtype(dtype)) {
@@ -91,6 +92,7 @@ void canon_op(int dtype, int op, bool running_first, int* kdt, int* kop) {
     if (is_float_dtype(dtype)) {
         *kdt = dtype;
         if (running_first && (op == CHR_MAX || op == CHR_MIN)) *kop = op == CHR_MAX ? kMaxSw : kMinSw;
+        if (running_first && (op == CHR_SUM || op == CHR_PROD)) *kop = op == CHR_SUM ? kSumSw : kProdSw;  // NaN payloads
         return;
     }
     if (op == CHR_MAX || op == CHR_MIN) {
@@ -108,7 +110,7 @@ void canon_op(int dtype, int op, bool running_first, int* kdt, int* kop) {
 // kernel types compiled in this translation unit; the rest: reduce_int.hip
 static bool in_core_tu(int kdt, int kop) {
     return (is_float_dtype(kdt) || kdt == CHR_INT32) && ((kop >= CHR_SUM && kop <= CHR_MIN) || kop == kMaxSw ||
-                                                         kop == kMinSw);
+                                                         kop == kMinSw || kop == kSumSw || kop == kProdSw);
 }
 
 int& coresident_depth() {
@@ -175,6 +177,12 @@ static hipError_t launch_vec_dt(const VecArgs& a, int m, int op, hipStream_t s) 
     case kMinSw:
         if constexpr (DT == CHR_INT32) return hipErrorInvalidValue;
         else return launch_vec_op<DT, kMinSw>(a, m, s);
+    case kSumSw:
+        if constexpr (DT == CHR_INT32) return hipErrorInvalidValue;
+        else return launch_vec_op<DT, kSumSw>(a, m, s);
+    case kProdSw:
+        if constexpr (DT == CHR_INT32) return hipErrorInvalidValue;
+        else return launch_vec_op<DT, kProdSw>(a, m, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -192,6 +200,12 @@ static hipError_t launch_scalar_dt(const ScalarArgs& a, int op, hipStream_t s) {
     case kMinSw:
         if constexpr (DT == CHR_INT32) return hipErrorInvalidValue;
         else return launch_scalar_op<DT, kMinSw>(a, s);
+    case kSumSw:
+        if constexpr (DT == CHR_INT32) return hipErrorInvalidValue;
+        else return launch_scalar_op<DT, kSumSw>(a, s);
+    case kProdSw:
+        if constexpr (DT == CHR_INT32) return hipErrorInvalidValue;
+        else return launch_scalar_op<DT, kProdSw>(a, s);
     default: return hipErrorInvalidValue;
     }
 }

@@ -63,13 +63,15 @@ constexpr size_t kMaxSegVec = (size_t)1 << 26;
 
 template <int OP>
 constexpr int swapped_op() {
-    return OP == CHR_MAX ? kMaxSw : OP == CHR_MIN ? kMinSw : OP == CHR_MAXLOC ? kMaxLocSw : OP == CHR_MINLOC ? kMinLocSw : OP;
+    return OP == CHR_MAX ? kMaxSw : OP == CHR_MIN ? kMinSw : OP == CHR_MAXLOC ? kMaxLocSw : OP == CHR_MINLOC ? kMinLocSw
+           : OP == CHR_SUM ? kSumSw : OP == CHR_PROD ? kProdSw : OP;
 }
 // Whether MPI_Reduce_local(running, next) can differ bitwise from MPI_Reduce_local(next, running):
-// MAX / MIN on floating types and MAXLOC / MINLOC on floating-valued pairs (ties, -0 / +0, NaN).
+// MAX / MIN on floating types and MAXLOC / MINLOC on floating-valued pairs (ties, -0 / +0, NaN), and SUM / PROD on
+// the floating types when two NaNs meet (whose payload survives: kSumSw in reduce_common.hpp).
 template <int DT, int OP>
 constexpr bool order_sensitive() {
-    return (is_float_dt<DT>() && (OP == CHR_MAX || OP == CHR_MIN)) ||
+    return (is_float_dt<DT>() && (OP == CHR_MAX || OP == CHR_MIN || OP == CHR_SUM || OP == CHR_PROD)) ||
            ((DT == CHR_FLOAT_INT || DT == CHR_DOUBLE_INT) && (OP == CHR_MAXLOC || OP == CHR_MINLOC));
 }
 

@@ -374,11 +374,15 @@ void orc_reduce_local(const void* in, void* inout, size_t n, int dtype, int op) 
     case ORC_BF16:
         /* The reference has no bf16; the golden driver runs it as a user-defined op on
          * MPI_Type_contiguous(2, MPI_BYTE) computing bf16_rne(f32(inout) op f32(in)) with the
-         * same operand order as the predefined float ops. */
+         * same operand order as the predefined float ops.  Two NaNs: inout's survives (quieted), as
+         * MPICH's float and double loops keep it -- written out, since a plain + or * leaves the
+         * payload to whichever operand order the compiler picks (gcc here kept in's). */
         if (op == ORC_SUM)
-            ORC_LOOP(uint16_t, orc_f32_to_bf16(orc_bf16_to_f32(y) + orc_bf16_to_f32(x)));
+            ORC_LOOP(uint16_t, isnan(orc_bf16_to_f32(y)) ? orc_f32_to_bf16(orc_bf16_to_f32(y))
+                                                         : orc_f32_to_bf16(orc_bf16_to_f32(y) + orc_bf16_to_f32(x)));
         else if (op == ORC_PROD)
-            ORC_LOOP(uint16_t, orc_f32_to_bf16(orc_bf16_to_f32(y) * orc_bf16_to_f32(x)));
+            ORC_LOOP(uint16_t, isnan(orc_bf16_to_f32(y)) ? orc_f32_to_bf16(orc_bf16_to_f32(y))
+                                                         : orc_f32_to_bf16(orc_bf16_to_f32(y) * orc_bf16_to_f32(x)));
         else if (op == ORC_MAX)
             ORC_LOOP(uint16_t, orc_bf16_to_f32(y) > orc_bf16_to_f32(x) ? y : x);
         else
