@@ -111,9 +111,11 @@ __device__ __forceinline__ void tree_eval(const V (&x)[NL][W], V (&r)[W], uint32
 // combines widen, add and RNE-pack (tools/reduce_microbench focus34, profiles/r05/microbench_focus34_static_tree.txt:
 // C4's tree at cap 12, 16 MiB pieces, cold f32 0.753-0.762 -> 0.782-0.784, bf16 0.723-0.737 -> 0.778-0.793; 8 MiB
 // f32 0.684-0.689 -> 0.721-0.724, bf16 0.646-0.652 -> 0.710-0.715; cap 16 +1-3 %).  The programs the flat
-// schedule emits at 4 and 8 ranks (every k and b; enumerated from chr_plan_describe) are unrolled at compile time
+// schedule emits at 2, 4 and 8 ranks (every k and b; enumerated from chr_plan_describe) are unrolled at compile time
 // and chosen by one scalar compare per workgroup; anything else (other rank counts, swapped combines) keeps the
-// interpreter.  Same combines in the same order: only the instruction stream changes.
+// interpreter.  Same combines in the same order: only the instruction stream changes.  Through the product: one
+// GPU's own C4 grids at cap 12 0.767 -> 0.798, 0.688 -> 0.752 on just-received leaves, C5 0.705 -> 0.763
+// (profiles/r05/static_tree/).
 constexpr uint32_t tree_prog(const int (&c)[8], int nl) {
     uint32_t v = 0;
     for (int j = 0; j < nl; ++j) v |= (uint32_t)c[j] << (2 * j);
@@ -129,6 +131,10 @@ template <> struct StaticProgs<8> {
         tree_prog({0, 1, 1, 0, 1, 2, 0, 2}, 8),  // b = 8, k = 3
         tree_prog({0, 1, 1, 1, 0, 2, 1, 1}, 8),  // b = 8, k = 4
         tree_prog({0, 1, 1, 1, 1, 1, 1, 1}, 8)}; // b = 8, k >= 5: a left fold
+};
+template <> struct StaticProgs<2> {  // the 2-rank schedules (C3, the N = 2 line)
+    static constexpr int n = 1;
+    static constexpr uint32_t v[1] = {tree_prog({0, 1, 0, 0, 0, 0, 0, 0}, 2)};
 };
 template <> struct StaticProgs<4> {
     static constexpr int n = 2;
