@@ -103,8 +103,9 @@ int chr_reduce_multi(void* out, const void* acc, const void* const* ins, int m, 
 /* chr_reduce_multi with flags.  CHR_REDUCE_RUNNING_FIRST: the running value is the FIRST
  * operand of every step, acc = acc (op) ins[j], i.e. MPI_Reduce_local(acc, ins[j]) chained
  * the way MPICH_do_reduce does it
- * (testing/mpich_implementations/all_reduce/allreduce_recexch.cpp:147-186).  Only MAX/MIN
- * on floating types can differ bitwise from the default order (ties of -0/+0, NaN). */
+ * (testing/mpich_implementations/all_reduce/allreduce_recexch.cpp:147-186).  Only the floating
+ * types can differ bitwise from the default order: MAX/MIN on ties of -0/+0 and NaN compares,
+ * SUM/PROD on which NaN survives when two meet (inout's, as MPICH's loop keeps it). */
 #define CHR_REDUCE_RUNNING_FIRST 1
 int chr_reduce_multi_ex(void* out, const void* acc, const void* const* ins, int m, size_t n,
                         chr_dtype dtype, chr_op op, int flags, hipStream_t stream);
