@@ -61,11 +61,6 @@ struct TreeArgs {
 // cut into several segments, so a grid stays far below 2^31 threads.
 constexpr size_t kMaxSegVec = (size_t)1 << 26;
 
-template <int OP>
-constexpr int swapped_op() {
-    return OP == CHR_MAX ? kMaxSw : OP == CHR_MIN ? kMinSw : OP == CHR_MAXLOC ? kMaxLocSw : OP == CHR_MINLOC ? kMinLocSw
-           : OP == CHR_SUM ? kSumSw : OP == CHR_PROD ? kProdSw : OP;
-}
 // Whether MPI_Reduce_local(running, next) can differ bitwise from MPI_Reduce_local(next, running):
 // MAX / MIN on floating types and MAXLOC / MINLOC on floating-valued pairs (ties, -0 / +0, NaN), and SUM / PROD on
 // the floating types when two NaNs meet (whose payload survives: kSumSw in reduce_common.hpp).
@@ -94,9 +89,19 @@ __device__ __forceinline__ void tree_eval(const V (&x)[NL][W], V (&r)[W], uint32
             ++d;
             for (int c = (int)((comb >> (2 * j)) & 3u); c > 0; --c, ++ci) {
                 const bool sw = (swaps >> ci) & 1u;
-                if (d == 2) s0 = sw ? F::template ap<true>(s1, s0) : F::template ap<false>(s1, s0);
-                else if (d == 3) s1 = sw ? F::template ap<true>(s2, s1) : F::template ap<false>(s2, s1);
-                else s2 = sw ? F::template ap<true>(s3, s2) : F::template ap<false>(s3, s2);
+                if constexpr (F::kOrderSensitive) {
+                    // a swapped combine is the plain one on exchanged operands: select them, combine once.
+                    // Written as `sw ? apply<kSumSw>(in, run) : apply<SUM>(in, run)`, both pinned-order
+                    // combines were computed and one selected, and the bf16 SUM trees held 80 VGPRs instead of
+                    // 61 (RCCL's room beside them)
+                    if (d == 2) s0 = F::ap(sw ? s0 : s1, sw ? s1 : s0);
+                    else if (d == 3) s1 = F::ap(sw ? s1 : s2, sw ? s2 : s1);
+                    else s2 = F::ap(sw ? s2 : s3, sw ? s3 : s2);
+                } else {  // bitwise commutative: the swap bit changes nothing
+                    if (d == 2) s0 = F::ap(s1, s0);
+                    else if (d == 3) s1 = F::ap(s2, s1);
+                    else s2 = F::ap(s3, s2);
+                }
                 --d;
             }
         }
@@ -153,7 +158,7 @@ __device__ __forceinline__ void tree_eval_static(const V (&x)[NL][W], V (&r)[W])
             st[d++] = x[j][w];
 #pragma unroll
             for (int c = (int)((COMB >> (2 * j)) & 3u); c > 0; --c) {
-                st[d - 2] = F::template ap<false>(st[d - 1], st[d - 2]);
+                st[d - 2] = F::ap(st[d - 1], st[d - 2]);
                 --d;
             }
         }
@@ -176,13 +181,13 @@ __device__ __forceinline__ void tree_eval_fast(const V (&x)[NL][W], V (&r)[W], u
     }
 }
 
+// F::ap(in, run) is MPI_Reduce_local(in, inout = run).  A swapped combine -- MPICH_do_reduce's
+// MPI_Reduce_local(run, in) -- is F::ap(run, in): the tree evaluators exchange the operands (the swapped codes
+// kMaxSw ... kProdSw of reduce_common.hpp serve the bucket kernels, whose result lands in the other buffer).
 template <int DT, int OP>
 struct VecOp {
-    template <bool SW>
-    __device__ __forceinline__ static u32x4 ap(u32x4 in, u32x4 run) {
-        if constexpr (SW && order_sensitive<DT, OP>()) return apply_vec<DT, swapped_op<OP>()>(in, run);
-        else return apply_vec<DT, OP>(in, run);
-    }
+    static constexpr bool kOrderSensitive = order_sensitive<DT, OP>();
+    __device__ __forceinline__ static u32x4 ap(u32x4 in, u32x4 run) { return apply_vec<DT, OP>(in, run); }
 };
 
 // The scalar kernel's stack slots: the element type itself, except for the pair and complex
@@ -209,11 +214,10 @@ template <int DT, int OP>
 struct ScalarOp {
     using T = typename DTy<DT>::T;
     using V = slot_t<DT>;
-    template <bool SW>
+    static constexpr bool kOrderSensitive = order_sensitive<DT, OP>();
     __device__ __forceinline__ static V ap(V in, V run) {
-        constexpr int O = SW && order_sensitive<DT, OP>() ? swapped_op<OP>() : OP;
-        if constexpr (std::is_same_v<V, T>) return apply<DT, O>(in, run);
-        else return __builtin_bit_cast(V, apply<DT, O>(__builtin_bit_cast(T, in), __builtin_bit_cast(T, run)));
+        if constexpr (std::is_same_v<V, T>) return apply<DT, OP>(in, run);
+        else return __builtin_bit_cast(V, apply<DT, OP>(__builtin_bit_cast(T, in), __builtin_bit_cast(T, run)));
     }
 };
 
@@ -360,10 +364,16 @@ constexpr size_t tree_xcd_run_kib() {
 // three tree waves on a SIMD leave less than the ~288 VGPRs rcclGenericKernel's waves need: an RCCL-sized kernel
 // was admitted only when the tree launch drained (median 170 us against 4 us) and the real RCCL kernel beside the
 // C4 slice took 164-165 us against 114-120 us (tools/gpu_cores_u.sh, profiles/r05/cores_u/).  U = 1 stays.
+// The same budget (<= 72 VGPRs, tests/test_kernel_resources.py) moved the streaming 3- and 4-leaf trees of the N = 4
+// flat schedule from U = 4 (104 f32 / 112 bf16 VGPRs) to U = 2 (62 / 65): beside 4-leaf f32 trees of 64 MiB
+// pieces at cap 12 an RCCL-sized kernel's median workgroup was admitted after 5.5 / 17.6 us instead of ~90 us
+// (the launch drained first), the real RCCL kernel took 122-123 us instead of 129-133, and the trees ran faster
+// too, 0.770 / 0.780 vs 0.761 / 0.741 at cap 12 and 0.759 vs 0.746 at the stand-alone policy
+// (tools/gpu_cores_ab.sh LEAVES=4, profiles/r05/cores_ab_l4/, 2 alternating rounds of 3).
 template <int NL, bool NT>
 constexpr int tree_u() {
     if constexpr (!NT) return NL <= 4 ? 4 : 2;  // cache-warm (plain) launches: the round-1 shapes
-    return NL <= 4 ? 4 : 1;
+    return NL <= 2 ? 4 : NL <= 4 ? 2 : 1;
 }
 template <int NL>
 constexpr int tree_wg_per_cu() {

@@ -18,6 +18,7 @@
 //
 //   coresidency_probe [--mode rccl|mimic] [--prio 0|1] [--cumask R] [--piece MiB] [--xfer MiB]
 //                     [--launches L] [--reps N] [--nsets S]
+//                     [--dtype f32|bf16]  (C4's f32 trees or C5's bf16 ones)  [--leaves 8|4|2]
 //   --prio 1:   stream B is created with the highest stream priority
 //   --cumask R: stream A runs with R CUs per XCD masked off (hipExtStreamCreateWithCUMask)
 //   --delay-us D: in the concurrent runs the transfer is submitted D us after the trees start (both
@@ -170,6 +171,8 @@ struct Opts {
     int prio = 0, cumask = 0, launches = 4, reps = 5, nsets = 4, mimic_grid = 64, delay_us = 10, census = 0;
     unsigned mimic_lds = kMimicLds;
     size_t piece_mib = 16, xfer_mib = 56;
+    chr_dtype dtype = CHR_FLOAT32;  // --dtype f32|bf16: C4's trees or C5's
+    int leaves = 8;                 // --leaves 8|4|2: C4 / C5's trees, or the N = 4 / N = 2 flat schedules
 };
 
 extern "C" int probe_main(int argc, char** argv) {
@@ -189,12 +192,15 @@ extern "C" int probe_main(int argc, char** argv) {
         else if (k == "--delay-us") o.delay_us = std::atoi(v);
         else if (k == "--census") o.census = std::atoi(v);
         else if (k == "--mimic-lds") o.mimic_lds = (unsigned)std::atoi(v);
+        else if (k == "--dtype") o.dtype = std::string(v) == "bf16" ? CHR_BFLOAT16 : CHR_FLOAT32;
+        else if (k == "--leaves") o.leaves = std::atoi(v);
         else {
             std::fprintf(stderr, "unknown option %s\n", k.c_str());
             return 2;
         }
     }
     if (o.launches < 1 || o.nsets < 1 || o.reps < 1 || o.piece_mib < 1 || o.xfer_mib < 1 || o.launches > 64) return 2;
+    if (o.leaves != 8 && o.leaves != 4 && o.leaves != 2) return 2;
     HIPCHECK(hipSetDevice(0));
     hipDeviceProp_t prop;
     HIPCHECK(hipGetDeviceProperties(&prop, 0));
@@ -224,30 +230,31 @@ extern "C" int probe_main(int argc, char** argv) {
         HIPCHECK(hipStreamCreateWithFlags(&sB, hipStreamNonBlocking));
     }
 
-    // tree leaf sets: nsets x 2 trees x 8 leaves + 2 outputs, `piece` MiB each
-    const size_t n = (o.piece_mib << 20) / 4;
+    // tree leaf sets: nsets x 2 trees x L leaves + 2 outputs, `piece` MiB each
+    const size_t es = o.dtype == CHR_BFLOAT16 ? 2 : 4, n = (o.piece_mib << 20) / es;
     struct Set {
         std::vector<void*> leaves;  // 16 (tree-major)
         void* outs[2];
     };
     std::vector<Set> sets(o.nsets);
     for (int s = 0; s < o.nsets; ++s) {
-        sets[s].leaves.resize(16);
-        for (int j = 0; j < 16; ++j) {
-            HIPCHECK(hipMalloc(&sets[s].leaves[j], n * 4));
-            CHRCHECK(chr_fill(sets[s].leaves[j], n, CHR_FLOAT32, 0, 7, 16 * s + j, 0, sA));
+        sets[s].leaves.resize(2 * o.leaves);
+        for (int j = 0; j < 2 * o.leaves; ++j) {
+            HIPCHECK(hipMalloc(&sets[s].leaves[j], n * es));
+            CHRCHECK(chr_fill(sets[s].leaves[j], n, o.dtype, 0, 7, 16 * s + j, 0, sA));
         }
-        for (int t = 0; t < 2; ++t) HIPCHECK(hipMalloc(&sets[s].outs[t], n * 4));
+        for (int t = 0; t < 2; ++t) HIPCHECK(hipMalloc(&sets[s].outs[t], n * es));
     }
-    // C4's per-chunk tree ((l0 l1 l2 l3)(l4 l5 l6 l7)), both trees
-    const unsigned char comb1[8] = {0, 1, 1, 1, 0, 1, 1, 2};
+    // C4's per-chunk tree ((l0 l1 l2 l3)(l4 l5 l6 l7)), both trees; the 4-rank flat schedule's ((l0 l1)(l2 l3)); 2
+    const unsigned char c8[8] = {0, 1, 1, 1, 0, 1, 1, 2}, c4[4] = {0, 1, 0, 2}, c2[2] = {0, 1};
+    const unsigned char* comb1 = o.leaves == 8 ? c8 : o.leaves == 4 ? c4 : c2;
     unsigned char comb[16];
-    std::memcpy(comb, comb1, 8);
-    std::memcpy(comb + 8, comb1, 8);
+    std::memcpy(comb, comb1, o.leaves);
+    std::memcpy(comb + o.leaves, comb1, o.leaves);
     auto trees = [&](int launch) {
         Set& st = sets[launch % o.nsets];
-        CHRCHECK(chr_reduce_tree_batch(st.outs, (const void* const*)st.leaves.data(), 2, 8, comb, nullptr, n,
-                                       CHR_FLOAT32, CHR_SUM, sA));
+        CHRCHECK(chr_reduce_tree_batch(st.outs, (const void* const*)st.leaves.data(), 2, o.leaves, comb, nullptr, n,
+                                       o.dtype, CHR_SUM, sA));
     };
 
     // transfer buffers
@@ -300,11 +307,13 @@ extern "C" int probe_main(int argc, char** argv) {
     xfer();
     HIPCHECK(hipDeviceSynchronize());
 
-    const double tree_bytes = 2.0 * 9.0 * (double)n * 4.0 * o.launches;
+    const double tree_bytes = 2.0 * (o.leaves + 1.0) * (double)n * (double)es * o.launches;
     std::printf("{\"config\": {\"mode\": \"%s\", \"prio\": %d, \"cumask_per_xcd\": %d, \"piece_mib\": %zu, "
-                "\"xfer_mib\": %zu, \"launches\": %d, \"nsets\": %d, \"wg_per_cu_tree_env\": \"%s\", \"cus\": %d}}\n",
+                "\"xfer_mib\": %zu, \"launches\": %d, \"nsets\": %d, \"wg_per_cu_tree_env\": \"%s\", \"cus\": %d, "
+                "\"dtype\": \"%s\", \"leaves\": %d}}\n",
                 o.mode.c_str(), o.prio, o.cumask, o.piece_mib, o.xfer_mib, o.launches, o.nsets,
-                std::getenv("CHR_WG_PER_CU_TREE") ? std::getenv("CHR_WG_PER_CU_TREE") : "policy", ncu);
+                std::getenv("CHR_WG_PER_CU_TREE") ? std::getenv("CHR_WG_PER_CU_TREE") : "policy", ncu,
+                o.dtype == CHR_BFLOAT16 ? "bf16" : "f32", o.leaves);
     int launch = 0;
     for (int r = 0; r < o.reps; ++r) {
         // alone: trees, then the transfer
