@@ -11,6 +11,8 @@
 namespace chr {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kBlock = 256;
 
@@ -270,6 +272,49 @@ __device__ __forceinline__ u32x4 apply_vec(u32x4 in, u32x4 acc) {
             const f32x2 o = SUMLIKE ? (SW ? pk_add_keep(x2, y2) : pk_add_keep(y2, x2))
                                     : (SW ? pk_mul_keep(x2, y2) : pk_mul_keep(y2, x2));
             r[e] = f2bf_pk(o.x, o.y);
+        }
+        return r;
+    }
+    if constexpr (DT == CHR_INT8 || DT == CHR_UINT8) {
+        // four bytes per dword, worked on in place (SIMD within a register): per-element code on sixteen byte lanes
+        // per vector held the streaming kernels at 88-152 VGPRs, above the 72 RCCL's waves leave room for
+        // (tests/test_kernel_resources.py).  Every result is MPICH's C loop's, bit for bit (integers: wrapping
+        // SUM / PROD, ties bitwise equal, so the swapped MAX / MIN codes are the same op).
+        constexpr uint32_t LO7 = 0x7F7F7F7Fu, HI = 0x80808080u, EVEN = 0x00FF00FFu;
+        u32x4 r;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t x = in[e], y = acc[e];
+            if constexpr (OP == CHR_SUM) {
+                r[e] = ((x & LO7) + (y & LO7)) ^ ((x ^ y) & HI);  // carries stay inside each byte
+            } else if constexpr (OP == CHR_PROD) {
+                // the low byte of a 16-bit product depends only on the operands' low bytes
+                const uint32_t pe = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, x) * __builtin_bit_cast(u16x2, y));
+                const uint32_t po = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, x >> 8) * __builtin_bit_cast(u16x2, y >> 8));
+                r[e] = (pe & EVEN) | ((po << 8) & ~EVEN);
+            } else if constexpr (OP == CHR_LAND || OP == CHR_LOR || OP == CHR_LXOR) {
+                const uint32_t nx = (((x & LO7) + LO7) | x) & HI, ny = (((y & LO7) + LO7) | y) & HI;  // bit 7: byte != 0
+                const uint32_t t = OP == CHR_LAND ? (nx & ny) : OP == CHR_LOR ? (nx | ny) : (nx ^ ny);
+                r[e] = t >> 7;
+            } else {
+                // MAX / MIN: even and odd bytes as two 16-bit pairs, sign- or zero-extended in place, one packed
+                // 16-bit max / min each, re-packed
+                constexpr bool MX = OP == CHR_MAX || OP == kMaxSw;
+                static_assert(OP == CHR_MAX || OP == CHR_MIN || OP == kMaxSw || OP == kMinSw);
+                if constexpr (DT == CHR_INT8) {
+                    const i16x2 xe = __builtin_bit_cast(i16x2, x << 8) >> 8, xo = __builtin_bit_cast(i16x2, x) >> 8;
+                    const i16x2 ye = __builtin_bit_cast(i16x2, y << 8) >> 8, yo = __builtin_bit_cast(i16x2, y) >> 8;
+                    const i16x2 re = MX ? __builtin_elementwise_max(ye, xe) : __builtin_elementwise_min(ye, xe);
+                    const i16x2 ro = MX ? __builtin_elementwise_max(yo, xo) : __builtin_elementwise_min(yo, xo);
+                    r[e] = (__builtin_bit_cast(uint32_t, re) & EVEN) | ((__builtin_bit_cast(uint32_t, ro) << 8) & ~EVEN);
+                } else {
+                    const u16x2 xe = __builtin_bit_cast(u16x2, x & EVEN), xo = __builtin_bit_cast(u16x2, (x >> 8) & EVEN);
+                    const u16x2 ye = __builtin_bit_cast(u16x2, y & EVEN), yo = __builtin_bit_cast(u16x2, (y >> 8) & EVEN);
+                    const u16x2 re = MX ? __builtin_elementwise_max(ye, xe) : __builtin_elementwise_min(ye, xe);
+                    const u16x2 ro = MX ? __builtin_elementwise_max(yo, xo) : __builtin_elementwise_min(yo, xo);
+                    r[e] = __builtin_bit_cast(uint32_t, re) | (__builtin_bit_cast(uint32_t, ro) << 8);
+                }
+            }
         }
         return r;
     }

@@ -23,12 +23,8 @@ DT = ["f32", "f64", "i32", "bf16", "i8", "u8", "i16", "u16", "u32", "i64", "u64"
       "cf", "cd"]
 OP = ["sum", "prod", "max", "min", "land", "lor", "lxor", "band", "bor", "bxor", "maxloc", "minloc"]
 RCCL_ROOM_VGPRS = 72
-# 8-bit MAX / MIN (and u8 on two-leaf trees) unpack sixteen lanes per vector; MPI_CHAR / MPI_BYTE maxima are not
-# what the collectives are for, and these stay above the budget.  A new entry here is a regression.
-KNOWN_OVER = {("tree", "i8", "max"), ("tree", "i8", "min"), ("tree", "u8", "max"), ("tree", "u8", "min"),
-              ("tree", "u8", "sum"), ("tree", "u8", "prod"), ("tree", "u8", "land"), ("tree", "u8", "lor"),
-              ("tree", "u8", "lxor"), ("vec", "i8", "max"), ("vec", "i8", "min"), ("vec", "u8", "max"),
-              ("vec", "u8", "min")}
+# Until round 5's SWAR 8-bit code (reduce_common.hpp apply_vec) the int8 / uint8 MAX / MIN kernels held 88-152
+# and the u8 two-leaf trees 96: no exception is left.
 
 
 @pytest.fixture(scope="module")
@@ -61,23 +57,25 @@ def test_every_kernel_found_and_none_uses_scratch(res):
 def test_streaming_kernels_leave_rccl_its_registers(res):
     s = _streaming(res)
     assert len(s) > 500
-    over = {(k[0], k[1], k[2]): v for k, v in s.items() if v > RCCL_ROOM_VGPRS}
-    new = sorted(set(over) - KNOWN_OVER)
-    assert not new, f"streaming kernels above {RCCL_ROOM_VGPRS} VGPRs: {[(k, over[k]) for k in new]}"
+    over = sorted((k, v) for k, v in s.items() if v > RCCL_ROOM_VGPRS)
+    assert not over, f"streaming kernels above {RCCL_ROOM_VGPRS} VGPRs: {over[:8]}"
 
 
-@pytest.mark.parametrize("dt", ["f32", "bf16", "f64", "i32"])
+@pytest.mark.parametrize("dt", ["f32", "bf16", "f64", "i32", "i8", "u8"])
 def test_the_configs_kernels_in_budget(res, dt):
     """C4 / C5's 8-leaf trees, the N = 4 / N = 2 lines' 4- and 2-leaf trees and every fold width, per dtype the
-    reference's harnesses use (and bf16)."""
+    reference's harnesses use (and bf16), and the 8-bit types whose per-lane code used to be the outliers."""
     s = _streaming(res)
-    for nl, u in ((8, 1), (4, 2), (2, 4)):
-        for op in ("sum", "prod", "max", "min"):
-            assert s[("tree", dt, op, (nl, u))] <= RCCL_ROOM_VGPRS, (dt, op, nl, s[("tree", dt, op, (nl, u))])
-    for key, v in s.items():
-        if key[0] == "vec" and key[1] == dt:
-            assert v <= RCCL_ROOM_VGPRS, (key, v)
-    assert s[("tree", dt, "sum", (8, 1))] <= 64
+    mine = {k: v for k, v in s.items() if k[1] == dt}
+    assert {k[0] for k in mine} == {"tree", "vec"}
+    if dt in ("f32", "bf16", "f64", "i32"):
+        for nl, u in ((8, 1), (4, 2), (2, 4)):
+            for op in ("sum", "prod", "max", "min"):
+                assert ("tree", dt, op, (nl, u)) in mine
+    for key, v in mine.items():
+        assert v <= RCCL_ROOM_VGPRS, (key, v)
+    if dt in ("f32", "bf16"):  # C4 / C5 themselves: 58 / 61 in round 5
+        assert s[("tree", dt, "sum", (8, 1))] <= 64
 
 
 def test_alloc_granule():
