@@ -273,6 +273,11 @@ C2_KERNEL_SYMBOL = "void chr::k_reduce_vec<0, 0, 1, 4, true, true, 64>(chr::VecA
 
 
 TREE8_KERNEL_SYMBOL = "void chr::k_reduce_tree<0, 0, 8, 1, true, 64>(chr::TreeArgs)"
+# the flat schedule's per-chunk tree at 8 / 4 / 2 ranks (b = N): its PMC entry (tools/tree_pmc.py --leaves L) and the
+# streaming instantiation a 1 GiB call launches (reduce_tree.hpp tree_u: U = 1 / 2 / 4)
+TREE_PMC = {8: ("tree_f32_sum_8leaves_64MiB", TREE8_KERNEL_SYMBOL),
+            4: ("tree_f32_sum_4leaves_64MiB", "void chr::k_reduce_tree<0, 0, 4, 2, true, 64>(chr::TreeArgs)"),
+            2: ("tree_f32_sum_2leaves_64MiB", "void chr::k_reduce_tree<0, 0, 2, 4, true, 64>(chr::TreeArgs)")}
 
 
 def pmc_ratio(kernel_key, symbol, root=REPO):
@@ -1070,8 +1075,10 @@ def bench_allreduce(args):
     if float(busiest[0]) > 0:
         ach = float(busiest[1]) / (float(busiest[0]) * 1e-3) / 1e9
         traffic, stale = None, None
-        if world == 8 and args.dtype == "f32":  # C4's trees have 8 leaves: the PMC entry's kernel
-            ratio, stale = pmc_ratio("tree_f32_sum_8leaves_64MiB", TREE8_KERNEL_SYMBOL)
+        pmc_key = None
+        if world in TREE_PMC and args.dtype == "f32":  # the flat schedule's world-leaf trees: the PMC entry's kernel
+            pmc_key, sym = TREE_PMC[world]
+            ratio, stale = pmc_ratio(pmc_key, sym)
             traffic = None if ratio is None else round(float(busiest[1]) * ratio)
         else:
             stale = f"no PMC entry for the {world}-rank {args.dtype} trees"
@@ -1086,7 +1093,7 @@ def bench_allreduce(args):
         if stale:
             roofline["traffic_stale"] = stale
         else:
-            roofline["traffic_source"] = "profiles/pmc_latest.json tree_f32_sum_8leaves_64MiB ratio x algorithmic bytes"
+            roofline["traffic_source"] = f"profiles/pmc_latest.json {pmc_key} ratio x algorithmic bytes"
     # bytes on the busiest directed link of this schedule (max over ranks; slicing only splits messages)
     if tuned is not None:
         sched = tuned[0]

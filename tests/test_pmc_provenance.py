@@ -56,3 +56,14 @@ def test_bench_reads_through_provenance(tmp_path):
     src.write_bytes(src.read_bytes() + b" ")
     traffic, why = bench.pmc_traffic(KEY, bench.C2_KERNEL_SYMBOL, str(root))
     assert traffic is None and why
+
+
+def test_every_n_line_has_its_tree_entry():
+    """The N = 8 / 4 / 2 lines each read the PMC entry of the flat schedule's tree at that width (bench.TREE_PMC):
+    the key has sources registered, and the symbol is the streaming instantiation reduce_tree.hpp's tree_u ships
+    (U = 1 / 2 / 4).  Whether the committed figures are current is the bench line's own `traffic_stale`."""
+    import bench
+
+    for world, (key, sym) in bench.TREE_PMC.items():
+        assert key in pp.KERNEL_SOURCES
+        assert f"k_reduce_tree<0, 0, {world}, {dict([(8, 1), (4, 2), (2, 4)])[world]}, true, 64>" in sym

@@ -15,6 +15,7 @@
 #   kernels    bench.py --collective-kernels (C4/C5 in-collective kernel rows) -> collective_kernels.json
 #   ranktrees  bench.py --rank-trees, plain and under rocprofv3 --kernel-trace -> rank_trees.json, rank_trees_prof/
 #   treepmc    rocprofv3 stats + FETCH_SIZE / WRITE_SIZE passes of the tree kernel alone (tools/tree_pmc.py)
+#   treepmc42  the same for the 4- and 2-leaf trees of the N = 4 / N = 2 lines
 #   e2e        bench.py --e2e: host-buffer (PCIe-inclusive) cost of the reference's contract -> e2e.json
 #   sweep      bench.py --sweep: 1 KiB .. 1 GiB buckets, m = 1/3/7, fp32 + bf16 (table in sweep.json.err)
 #   probe      tools/mstream_probe.py $PROBE_ARGS               -> mstream_probe.jsonl
@@ -69,6 +70,15 @@ for step in "$@"; do
     for ctr in FETCH_SIZE WRITE_SIZE; do
       run 300 "tree_pmc_$ctr.txt" rocprofv3 --pmc $ctr --output-format csv -d "$PWD/$OUT/tree_pmc_$ctr" -o run \
         -- python3 tools/tree_pmc.py 40
+    done ;;
+  treepmc42)  # the N = 4 / N = 2 lines' 4- and 2-leaf trees the same way -> tree{4,2}_prof/, tree{4,2}_pmc_*/
+    for nl in 4 2; do
+      run 300 "tree${nl}_prof.txt" rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/tree${nl}_prof" \
+        -o run -- python3 tools/tree_pmc.py 40 --leaves $nl
+      for ctr in FETCH_SIZE WRITE_SIZE; do
+        run 300 "tree${nl}_pmc_$ctr.txt" rocprofv3 --pmc $ctr --output-format csv -d "$PWD/$OUT/tree${nl}_pmc_$ctr" \
+          -o run -- python3 tools/tree_pmc.py 40 --leaves $nl
+      done
     done ;;
   sweep) run 600 sweep.json python bench.py --sweep --no-cpu-baseline ;;
   e2e) run 300 e2e.json python bench.py --e2e --no-cpu-baseline ;;

@@ -19,6 +19,9 @@ KERNEL_SOURCES = {
     "tree_f32_sum_8leaves_64MiB": [f"{CSRC}/reduce_tree.hpp", f"{CSRC}/reduce_common.hpp", f"{CSRC}/reduce_tree.hip",
                                    f"{CSRC}/chr_internal.hpp"],
 }
+# the 4- and 2-leaf trees of the N = 4 / N = 2 lines come from the same sources
+KERNEL_SOURCES["tree_f32_sum_4leaves_64MiB"] = KERNEL_SOURCES["tree_f32_sum_8leaves_64MiB"]
+KERNEL_SOURCES["tree_f32_sum_2leaves_64MiB"] = KERNEL_SOURCES["tree_f32_sum_8leaves_64MiB"]
 
 
 def sources_hash(key, root=REPO):

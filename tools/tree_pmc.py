@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Launches only the fused tree kernel at C4's shape (f32, 8 leaves, 64 MiB pieces, 8 rotating
 leaf sets = 4.5 GiB, HBM-cold) for rocprofv3 --pmc passes: HBM bytes per launch vs the
-algorithmic 9 x 64 MiB (tools/pmc_summary.py ... k_reduce_tree)."""
+algorithmic 9 x 64 MiB (tools/pmc_summary.py ... k_reduce_tree).  `--leaves 4|2`: the N = 4 / N = 2
+lines' trees instead ((L + 1) x 64 MiB).
+
+    python3 tools/tree_pmc.py [launches] [--leaves L]"""
+import argparse
 import os
 import sys
 
@@ -12,22 +16,27 @@ import torch  # noqa: E402
 
 import chiara_amd as ca  # noqa: E402
 
-COMB = [0, 1, 1, 1, 0, 1, 1, 2]
+COMBS = {8: [0, 1, 1, 1, 0, 1, 1, 2], 4: [0, 1, 0, 2], 2: [0, 1]}  # the flat schedule's programs at b = 8 / 4 / 2
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("launches", type=int, nargs="?", default=40)
+    ap.add_argument("--leaves", type=int, default=8, choices=sorted(COMBS))
+    a = ap.parse_args()
+    nl, comb = a.leaves, COMBS[a.leaves]
     dev = torch.device("cuda:0")
     s = torch.cuda.current_stream(dev)
     n = (64 << 20) // 4
     sets = []
-    for si in range(8):
-        leaves = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(8)]
+    for si in range(max(8, 64 // (nl + 1))):  # >= 4.5 GiB of distinct operands per rotation
+        leaves = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(nl)]
         for j, t in enumerate(leaves):
             ca.check(ca.fill(t, n, ca.FLOAT32, 0, 3, 8 * si + j, stream=s))
         sets.append((leaves, torch.empty(n, dtype=torch.float32, device=dev)))
-    for i in range(int(sys.argv[1]) if len(sys.argv) > 1 else 40):
+    for i in range(a.launches):
         lv, o = sets[i % len(sets)]
-        ca.check(ca.reduce_tree(o, lv, COMB, [0] * 7, n, ca.FLOAT32, ca.SUM, s))
+        ca.check(ca.reduce_tree(o, lv, comb, [0] * (nl - 1), n, ca.FLOAT32, ca.SUM, s))
     torch.cuda.synchronize()
     print("tree launches done")
 
