@@ -331,11 +331,16 @@ constexpr int kTreeXcdHandShift = 6;
 // XCD runs for streaming (nt) tree launches (profiles/r02/xcd_runs/ab_tree_*.json, C4 slice of 2
 // batched 8-leaf trees, HBM-cold, identity -> 512 KiB): 8 MiB pieces 0.571 -> 0.634, 16 MiB
 // 0.668 -> 0.700, 32 MiB 0.719 -> 0.750; fused reductions of a whole C4 call 0.676 -> 0.719.
-// Two leaves move the m = 1 bucket's traffic (2 reads + 1 write) and keep the identity (focus18's
-// microbench lead for 256 KiB runs under a cap is not product-verified; see tree_u below).
+// Two leaves move the m = 1 bucket's traffic (2 reads + 1 write) and kept the identity until focus18's
+// microbench lead for 256 KiB runs under a cap was product-verified:
+// Round 5, the product A/B focus18 asked for (tools/gpu_small_tree_ab.sh, profiles/r05/small_tree_ab/, 2
+// alternating rounds, HBM-cold, f32): the 2- and 4-leaf trees of the N = 2 / N = 4 lines take 256 KiB runs and 12
+// per CU (tree_wg_per_cu) -- alone 0.745-0.747 -> 0.765-0.766 (2 leaves, 64 MiB pieces), 0.677-0.690 -> 0.707 (two
+// trees of 16 MiB), 0.778-0.784 -> 0.791-0.800 (4 leaves, 64 MiB), 0.744-0.745 -> 0.750-0.757 (2 x 16 MiB); at
+// the in-collective cap 12 the runs add 0-1.4 %.
 template <int NL>
 constexpr size_t tree_xcd_run_kib() {
-    return NL <= 2 ? 0 : 512;
+    return NL <= 4 ? 256 : 512;
 }
 
 // Two-wave workgroups at the same 16 waves per CU (fewer dispatches per grid): the
@@ -351,8 +356,9 @@ constexpr size_t tree_xcd_run_kib() {
 // trees of the N = 2 / N = 4 flat schedules (focus18, microbench_focus18_small_trees.txt, 2 rounds,
 // 6 HBM-cold sets) showed 2 leaves at 128 MiB U = 4 uncapped 0.774-0.783 -> 0.801-0.804 with 12 per
 // CU and 256 KiB runs, and 4 leaves at 64 MiB 0.741-0.750 -> 0.774-0.781 at U = 2 with 12 per CU,
-// but the microbench over-predicted the 8-leaf change below, and no product A/B of the 2- and
-// 4-leaf shapes exists yet, so trees of <= 4 leaves keep the round-1 shapes (U = 4, uncapped).
+// but the microbench over-predicted the 8-leaf change below, so trees of <= 4 leaves kept the round-1
+// shapes (U = 4, uncapped) until round 5's product A/Bs: U = 2 for 3-4 leaves (below), 12 per CU and 256 KiB
+// runs for 2-4 (tree_xcd_run_kib).
 // For the U = 1 8-leaf tree the microbench preferred 12 per CU with 1-2 MiB
 // XCD runs (focus20: 0.760 -> 0.772-0.782 on the C4 slice), but the same-box product A/B over the
 // whole C4/C5 calls reversed it (profiles/r02/ab_tree/: 16 per CU / 512 KiB 0.7245-0.7255 (C4),
@@ -377,7 +383,7 @@ constexpr int tree_u() {
 }
 template <int NL>
 constexpr int tree_wg_per_cu() {
-    return NL <= 4 ? 0 : 16;
+    return NL <= 4 ? 12 : 16;
 }
 
 template <int DT, int OP, int NL, int BL, bool NT>
