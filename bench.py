@@ -189,9 +189,10 @@ LINE_DEFINITIONS_NN = {
     "result_check": "the metric's output on every rank and element: ranks bit-identical (position-weighted int64 "
                     "checksums of the raw words) and |x - fp64 sum of the N inputs| <= (N-1) ulp sum|x_i| (DESIGN §7)"}
 
-def line_problems(line):
+def line_problems(line, rccl_library=True):
     """What in a bench line disagrees with LINE_DEFINITIONS_N1 / _NN (empty list: none).  Checked by
-    tests/test_bench_line.py on canned lines and on the lines GPU runs committed under profiles/."""
+    tests/test_bench_line.py on canned lines and on the lines GPU runs committed under profiles/.
+    rccl_library: an N>1 line must name its librccl and version (round 6 on; round-5 lines predate it)."""
     probs = []
     need = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
             "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "definitions")
@@ -242,6 +243,8 @@ def line_problems(line):
         for k in ("nranks", "user_ranks", "pci_bus_ids", "transports", "pairs", "xgmi", "not_xgmi_because"):
             if k not in r:
                 probs.append(f"rccl.{k} missing")
+        if rccl_library:
+            probs += [f"rccl.{k} missing" for k in ("library", "version", "same_on_all_ranks") if not r.get(k)]
         if r.get("xgmi") and r.get("not_xgmi_because"):
             probs.append("rccl.xgmi true with reasons against it")
         if r.get("xgmi") is False and not r.get("not_xgmi_because"):
@@ -906,7 +909,38 @@ def transport_family(tr):
     return head if head in ("P2P", "SHM", "NET", "COLLNET") else "?"
 
 
-def rccl_record(infos, pair_sets, world):
+def rccl_library():
+    """Which librccl this process runs and its version: the path from /proc/self/maps (the copy torch loaded, which
+    libchiara.so resolves to) and ncclGetVersion() of that copy (RTLD_NOLOAD: never a second one).  The co-residency
+    cap was tuned against two RCCL builds with different LDS footprints, so the node record names it."""
+    import ctypes
+
+    path = None
+    try:
+        with open("/proc/self/maps") as f:
+            for ln in f:
+                p = ln.split()[-1] if len(ln.split()) >= 6 else ""
+                if os.path.basename(p).startswith("librccl"):
+                    path = p
+                    break
+    except OSError:
+        pass
+    rec = {"library": path, "version": None, "version_code": None}
+    if path:
+        try:
+            lib = ctypes.CDLL(path, mode=os.RTLD_NOLOAD | os.RTLD_LAZY)
+            v = ctypes.c_int(0)
+            if lib.ncclGetVersion(ctypes.byref(v)) == 0:
+                code = v.value
+                rec["version_code"] = code
+                rec["version"] = (f"{code // 10000}.{code % 10000 // 100}.{code % 100}" if code >= 10000 else
+                                  f"{code // 1000}.{code % 1000 // 100}.{code % 100}")
+        except (OSError, AttributeError) as e:
+            rec["version"] = f"error: {e}"[:80]
+    return rec
+
+
+def rccl_record(infos, pair_sets, world, libs=None):
     """The N>1 line's `rccl` object from every rank's chr_comm_info() and parsed pairs (rank order).
     xgmi is true only when RCCL's communicator holds `world` ranks with distinct user ranks, the ranks
     sit on `world` distinct PCI devices, at least one connection was logged, and every logged connection
@@ -931,7 +965,12 @@ def rccl_record(infos, pair_sets, world):
                              f"non-P2P transports: {sorted(f for f in fams if f != 'P2P')}")) if bad]
     ok = not why
     why = why or None
-    return {"nranks": sorted(nr)[0] if len(nr) == 1 else sorted(nr), "user_ranks": ranks, "devices": [i["device"] for i in infos],
+    lib = {}
+    if libs is not None:  # rank 0's library, and whether every rank runs the same one
+        lib = dict(libs[0])
+        lib["same_on_all_ranks"] = all(x == libs[0] for x in libs)
+    return {**lib, "nranks": sorted(nr)[0] if len(nr) == 1 else sorted(nr), "user_ranks": ranks,
+            "devices": [i["device"] for i in infos],
             "pci_bus_ids": buses, "transports": dict(sorted(counts.items())),
             "pairs": {f"{a}->{b}": "+".join(sorted(v)) for (a, b), v in sorted(merged.items())},
             "pairs_logged": len(merged), "xgmi": ok, "not_xgmi_because": why,
@@ -939,10 +978,13 @@ def rccl_record(infos, pair_sets, world):
                       "transports from each rank's NCCL_DEBUG_FILE (NCCL_DEBUG=INFO, NCCL_DEBUG_SUBSYS=INIT)"}
 
 
-def read_rccl_logs(root, rank):
+def read_rccl_logs(root, rank, pid=None):
+    """This rank's RCCL log lines under root; with `pid`, only the file that process wrote (NCCL_DEBUG_FILE's %p),
+    so a file another run left behind is never parsed into the record."""
     out = []
     try:
-        names = sorted(f for f in os.listdir(root) if f.startswith(f"rccl.rank{rank}."))
+        names = sorted(f for f in os.listdir(root) if f.startswith(f"rccl.rank{rank}.")
+                       and (pid is None or f == f"rccl.rank{rank}.{pid}.log"))
     except OSError:
         return out
     for f in names:
@@ -974,12 +1016,17 @@ def bench_allreduce(args):
     # a rank that dies must not leave the others in a gloo barrier for gloo's default 30 minutes
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=900))
     deadline = Deadline(dist)
-    # RCCL's connection log, one file per rank (rccl_log_env), set before this process's first RCCL call
+    # RCCL's connection log, one file per rank (rccl_log_env), set before this process's first RCCL call, in a
+    # directory named by a token rank 0 draws for this run (and read back by this process's pid only)
     log_root = None
     if os.environ.get("CHR_BENCH_RCCL_LOG", "1") != "0":
         import tempfile
+        import uuid
 
-        log_root = os.path.join(tempfile.gettempdir(), f"chiara_bench_rccl_{os.environ.get('MASTER_PORT', '0')}")
+        token = [uuid.uuid4().hex[:12] if rank == 0 else None]
+        dist.broadcast_object_list(token, 0)
+        log_root = os.path.join(tempfile.gettempdir(),
+                                f"chiara_bench_rccl_{os.environ.get('MASTER_PORT', '0')}_{token[0]}")
         os.environ.update(rccl_log_env(rank, log_root))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -1016,11 +1063,12 @@ def bench_allreduce(args):
         info = comm.info()
     except Exception as e:
         info = {"nranks": -1, "rank": -1, "device": -1, "pci_bus_id": f"error: {e}"[:80]}
-    pairs = parse_rccl_transports(read_rccl_logs(log_root, rank), nranks=world) if log_root else {}
-    allinfo, allpairs = [None] * world, [None] * world
+    pairs = parse_rccl_transports(read_rccl_logs(log_root, rank, os.getpid()), nranks=world) if log_root else {}
+    allinfo, allpairs, alllibs = [None] * world, [None] * world, [None] * world
     dist.all_gather_object(allinfo, info)
     dist.all_gather_object(allpairs, pairs)
-    rccl = rccl_record(allinfo, allpairs, world)
+    dist.all_gather_object(alllibs, rccl_library())
+    rccl = rccl_record(allinfo, allpairs, world, alllibs)
     if not log_root:
         rccl["not_xgmi_because"] = "CHR_BENCH_RCCL_LOG=0: transports not logged"
     for _ in range(args.warmup):

@@ -126,17 +126,6 @@ def get_unique_id():
     return ctypes.string_at(ctypes.addressof(uid), ctypes.sizeof(uid))  # all 128 bytes (NULs included)
 
 
-def _env_overlap():
-    """The executor's default_overlap(): CHR_OVERLAP read with atoi, on when unset."""
-    import re
-
-    e = os.environ.get("CHR_OVERLAP")
-    if e is None:
-        return True
-    m = re.match(r"\s*[+-]?\d+", e)
-    return bool(m) and int(m.group(0)) != 0
-
-
 class Comm:
     """RCCL-backed communicator (one rank per process, one MI355X per rank)."""
 
@@ -149,7 +138,6 @@ class Comm:
               "chr_comm_init_rank")
         self._h = h
         self.rank, self.nranks, self.device = rank, nranks, device
-        self._overlap = _env_overlap()
 
     @classmethod
     def from_torch_distributed(cls, group=None, device=None):
@@ -187,12 +175,14 @@ class Comm:
     def set_overlap(self, enable):
         """Reductions on a second stream, overlapped with the RCCL transfers (default on)."""
         check(lib().chr_comm_set_overlap(self._h, int(bool(enable))))
-        self._overlap = bool(enable)
 
     @property
     def overlap(self):
-        """Whether local reductions run on the compute stream beside the transfers (set_overlap)."""
-        return self._overlap
+        """Whether local reductions run on the compute stream beside the transfers: the library's own setting
+        (chr_comm_get_overlap), so a record reports what runs."""
+        v = ctypes.c_int(0)
+        check(lib().chr_comm_get_overlap(self._h, ctypes.byref(v)), "chr_comm_get_overlap")
+        return bool(v.value)
 
     def set_schedule(self, schedule):
         """SCHEDULE_REFERENCE / SCHEDULE_BALANCED / SCHEDULE_FLAT / SCHEDULE_EXACT / SCHEDULE_FLAT_AG /

@@ -1437,6 +1437,12 @@ int chr_comm_set_overlap(chr_comm* c, int enable) {
     return CHR_SUCCESS;
 }
 
+int chr_comm_get_overlap(const chr_comm* c, int* enable) {
+    if (!c || !enable) return CHR_ERR_INVALID_ARG;
+    *enable = c->overlap ? 1 : 0;
+    return CHR_SUCCESS;
+}
+
 int chr_comm_set_schedule(chr_comm* c, int schedule) {
     if (!c || !(chr::plan_schedule(schedule) || schedule == CHR_SCHEDULE_AUTO)) return CHR_ERR_INVALID_ARG;
     c->sched = schedule;
@@ -1462,9 +1468,15 @@ int chr_comm_set_graphs(chr_comm* c, int enable) {
 int chr_comm_tuned_schedule(const chr_comm* c, int mode, size_t count, chr_dtype dtype, int k, int b, int* schedule,
                             int* slices) {
     if (!c || !schedule || !slices || !chr::dtype_size(dtype)) return CHR_ERR_INVALID_ARG;
+    if (mode != chr::MODE_ALLREDUCE && mode != chr::MODE_REDUCE_SCATTER) return CHR_ERR_INVALID_ARG;
+    if (c->failed) return CHR_ERR_ABORTED;
     if (c->sched != CHR_SCHEDULE_AUTO) {  // a fixed schedule: it, at the depth such a call runs
+        const int P = pick_slices(c->slices, (uint64_t)count, mode, c->nranks, b, chr::dtype_size(dtype), c->sched);
+        // the arguments a call would reject (k < 2, nranks % b, count % nranks) are rejected here too
+        const chr::Plan p = chr::build_plan((chr::Mode)mode, c->nranks, c->rank, k, b, (uint64_t)count, P, c->sched);
+        if (p.error) return p.error;
         *schedule = c->sched;
-        *slices = pick_slices(c->slices, (uint64_t)count, mode, c->nranks, b, chr::dtype_size(dtype), c->sched);
+        *slices = P;
         return CHR_SUCCESS;
     }
     auto it = c->tuned.find(std::make_tuple(mode, (uint64_t)count, (int)chr::dtype_size(dtype), k, b, c->slices,

@@ -138,15 +138,43 @@ constexpr int kSumSw = 20, kProdSw = 21;
 // tie keeps inout's value bits (-0 vs +0), so the operand order shows.
 constexpr int kMaxLocSw = 18, kMinLocSw = 19;
 
-// C99 Annex G complex multiplication (libgcc's __mulsc3 / __muldc3, what MPICH's `a = a * b` on
-// `float _Complex` compiles to): (a + bi)(c + di), products rounded one by one (the library is
-// built with -ffp-contract=off), and the infinity recovery when both parts come out NaN.  The
-// result is the same with the operands exchanged (every term is a commuting product or sum).
+// x86 SSE arithmetic with its NaN rules written out, for the complex types (the oracle's orc_x86f / orc_x86d):
+// two NaNs -> the FIRST operand's, quieted; one NaN -> that NaN, quieted (sign and payload kept); an invalid
+// operation on numbers (inf - inf, 0 * inf) -> x86's default NaN, sign set.  gfx950 also keeps the first
+// source's NaN, but its invalid operations give the positive canonical NaN, so the rules are spelled out as selects
+// rather than left to the instruction.  The complex kernels are not on a BASELINE path; the f32 / f64 / bf16
+// reductions keep their one-instruction combines (add_keep / mul_keep).
+enum { kXAdd, kXSub, kXMul };
+__device__ __forceinline__ float quiet_nan(float v) { return __uint_as_float(__float_as_uint(v) | 0x00400000u); }
+__device__ __forceinline__ double quiet_nan(double v) {
+    return __longlong_as_double(__double_as_longlong(v) | 0x0008000000000000ll);
+}
+__device__ __forceinline__ float x86_default_nan(float) { return __uint_as_float(0xFFC00000u); }
+__device__ __forceinline__ double x86_default_nan(double) { return __longlong_as_double((long long)0xFFF8000000000000ull); }
+template <int XOP, typename F>
+__device__ __forceinline__ F x86op(F p, F q) {
+    const F r = XOP == kXAdd ? p + q : XOP == kXSub ? p - q : p * q;
+    return __builtin_isnan(p) ? quiet_nan(p)
+           : __builtin_isnan(q) ? quiet_nan(q)
+           : __builtin_isnan(r) ? x86_default_nan(r)
+                                : r;
+}
+
+// C99 Annex G complex multiplication as MPICH's `a = a * b` on `float _Complex` compiles (gcc, x86): the plain
+// formula inline and, when both parts come out NaN, libgcc's __mulsc3 / __muldc3, which computes the products
+// again (rounded one by one; the library is built with -ffp-contract=off) and, if both parts are still NaN, recovers
+// the infinities (C11 G.5.1).  (a + bi) = inout, (c + di) = in.  Every input NaN makes both inline parts NaN, so the
+// NaN that survives follows __mulsc3's operand order, which MPICH's own outputs pin (tests/golden/
+// gen_nan_payloads.py, all orders searched: a*c, b*d, a*d, c*b, (ac) - (bd), (ad) + (bc), first operand first);
+// the inline formula and the recalculation see numbers only, so they can only yield the default NaN.
 template <typename F>
 __device__ __forceinline__ void cmul(F a, F b, F c, F d, F* re, F* im) {
-    const F ac = a * c, bd = b * d, ad = a * d, bc = b * c;
-    F x = ac - bd, y = ad + bc;
-    if (__builtin_isnan(x) && __builtin_isnan(y)) {
+    F x = x86op<kXSub>(x86op<kXMul>(a, c), x86op<kXMul>(b, d));
+    F y = x86op<kXAdd>(x86op<kXMul>(a, d), x86op<kXMul>(b, c));
+    if (__builtin_isnan(x) && __builtin_isnan(y)) {  // __mulsc3
+        const F ac = x86op<kXMul>(a, c), bd = x86op<kXMul>(b, d), ad = x86op<kXMul>(a, d), bc = x86op<kXMul>(c, b);
+        x = x86op<kXSub>(ac, bd);
+        y = x86op<kXAdd>(ad, bc);
         bool recalc = false;
         if (__builtin_isinf(a) || __builtin_isinf(b)) {
             a = __builtin_copysign(__builtin_isinf(a) ? (F)1 : (F)0, a);
@@ -170,8 +198,9 @@ __device__ __forceinline__ void cmul(F a, F b, F c, F d, F* re, F* im) {
             recalc = true;
         }
         if (recalc) {
-            x = __builtin_inf() * (a * c - b * d);
-            y = __builtin_inf() * (a * d + b * c);
+            const F inf = (F)__builtin_inf();
+            x = x86op<kXMul>(inf, x86op<kXSub>(x86op<kXMul>(a, c), x86op<kXMul>(b, d)));
+            y = x86op<kXMul>(inf, x86op<kXAdd>(x86op<kXMul>(a, d), x86op<kXMul>(b, c)));
         }
     }
     *re = x;
@@ -202,12 +231,21 @@ __device__ __forceinline__ typename DTy<DT>::T apply(typename DTy<DT>::T x, type
             }
             return r;
         }    } else if constexpr (is_complex_dt<DT>()) {
+        // MPICH's complex SUM keeps in's NaN in each part (its compiled loop adds in + inout; tests/golden/
+        // nan_reduce_local.npz), where MPI_FLOAT's keeps inout's.  kSumSw / kProdSw (the running value is `in`, the
+        // result lands in the incoming buffer) are the plain ops on exchanged operands.
         typename DTy<DT>::T r;
-        if constexpr (OP == CHR_SUM) {  // inout's NaN survives per part, as MPICH's loop on x86 keeps it
-            r.re = add_keep(y.re, x.re);
-            r.im = add_keep(y.im, x.im);
-        } else {
+        if constexpr (OP == CHR_SUM) {
+            r.re = x86op<kXAdd>(x.re, y.re);
+            r.im = x86op<kXAdd>(x.im, y.im);
+        } else if constexpr (OP == kSumSw) {
+            r.re = x86op<kXAdd>(y.re, x.re);
+            r.im = x86op<kXAdd>(y.im, x.im);
+        } else if constexpr (OP == CHR_PROD) {
             cmul(y.re, y.im, x.re, x.im, &r.re, &r.im);
+        } else {
+            static_assert(OP == kProdSw);
+            cmul(x.re, x.im, y.re, y.im, &r.re, &r.im);
         }
         return r;
     } else if constexpr (DT == CHR_BFLOAT16) {

@@ -87,6 +87,8 @@ void canon_op(int dtype, int op, bool running_first, int* kdt, int* kop) {
         *kdt = dtype;
         if (running_first && (dtype == CHR_FLOAT_INT || dtype == CHR_DOUBLE_INT))  // ties of -0/+0, NaN
             *kop = op == CHR_MAXLOC ? kMaxLocSw : op == CHR_MINLOC ? kMinLocSw : op;
+        if (running_first && is_complex_dtype(dtype))  // which NaN survives, per part (reduce_common.hpp apply)
+            *kop = op == CHR_SUM ? kSumSw : op == CHR_PROD ? kProdSw : op;
         return;
     }
     if (is_float_dtype(dtype)) {
@@ -148,6 +150,8 @@ ReduceTuning& reduce_tuning() {
         r.wg_per_cu_tree = s ? std::max(0, std::atoi(s)) : -1;
         s = std::getenv("CHR_XCD_HAND_SHIFT");
         r.xcd_hand_shift = s ? std::min(31, std::max(0, std::atoi(s))) : -1;  // [0, 31]; 31 hands nothing
+        s = std::getenv("CHR_TREE_ACC0");
+        r.tree_acc0 = s ? (std::atoi(s) != 0) : -1;
         int dev = 0, lds = 0, blk = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess ||

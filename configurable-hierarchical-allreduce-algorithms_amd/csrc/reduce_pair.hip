@@ -4,7 +4,7 @@
 // MPI_Datatype x MPI_Op (all_reduce_radix_batch.cpp:202-204) and reduces with MPICH's
 // MPI_Reduce_local (:332, :364, :446, :529), which accepts exactly these pairs for these types
 // (tests/golden/pairs_manifest.json).  Element semantics: reduce_common.hpp apply<> (MPICH's loops,
-// pinned by tests/golden/pairs_reduce_local.npz).  Same kernels and policy shapes as reduce_int.hip:
+// pinned by tests/golden/pairs_reduce_local.npz and nan_reduce_local.npz).  Same kernels and policy shapes as reduce_int.hip:
 // an element is 8 or 16 bytes, so one 16-B vector holds two or one of them.
 #include <hip/hip_runtime.h>
 
@@ -31,6 +31,8 @@ template <int DT>
 static hipError_t vec_cplx(const VecArgs& a, int op, int m, hipStream_t s) {
     if (op == CHR_SUM) return launch_vec_op<DT, CHR_SUM>(a, m, s);
     if (op == CHR_PROD) return launch_vec_op<DT, CHR_PROD>(a, m, s);
+    if (op == kSumSw) return launch_vec_op<DT, kSumSw>(a, m, s);
+    if (op == kProdSw) return launch_vec_op<DT, kProdSw>(a, m, s);
     return hipErrorInvalidValue;
 }
 
@@ -66,6 +68,8 @@ template <int DT>
 static hipError_t scalar_cplx(const ScalarArgs& a, int op, hipStream_t s) {
     if (op == CHR_SUM) return launch_scalar_op<DT, CHR_SUM>(a, s);
     if (op == CHR_PROD) return launch_scalar_op<DT, CHR_PROD>(a, s);
+    if (op == kSumSw) return launch_scalar_op<DT, kSumSw>(a, s);
+    if (op == kProdSw) return launch_scalar_op<DT, kProdSw>(a, s);
     return hipErrorInvalidValue;
 }
 

@@ -63,11 +63,12 @@ constexpr size_t kMaxSegVec = (size_t)1 << 26;
 
 // Whether MPI_Reduce_local(running, next) can differ bitwise from MPI_Reduce_local(next, running):
 // MAX / MIN on floating types and MAXLOC / MINLOC on floating-valued pairs (ties, -0 / +0, NaN), and SUM / PROD on
-// the floating types when two NaNs meet (whose payload survives: kSumSw in reduce_common.hpp).
+// the floating and the complex types when two NaNs meet (whose payload survives: kSumSw in reduce_common.hpp).
 template <int DT, int OP>
 constexpr bool order_sensitive() {
     return (is_float_dt<DT>() && (OP == CHR_MAX || OP == CHR_MIN || OP == CHR_SUM || OP == CHR_PROD)) ||
-           ((DT == CHR_FLOAT_INT || DT == CHR_DOUBLE_INT) && (OP == CHR_MAXLOC || OP == CHR_MINLOC));
+           ((DT == CHR_FLOAT_INT || DT == CHR_DOUBLE_INT) && (OP == CHR_MAXLOC || OP == CHR_MINLOC)) ||
+           (is_complex_dt<DT>() && (OP == CHR_SUM || OP == CHR_PROD));
 }
 
 // Generic over the value carried per lane (W values of type V, combined with F).  The stack
@@ -166,12 +167,13 @@ __device__ __forceinline__ void tree_eval_static(const V (&x)[NL][W], V (&r)[W])
     }
 }
 
-// The unrolled body of `comb` when it is one of StaticProgs<NL> and no combine is swapped, else the interpreter.
+// The unrolled body of `comb` when it is one of StaticProgs<NL> and no combine is swapped (or the op is bitwise
+// commutative, so a swap bit changes nothing), else the interpreter.
 template <typename V, int NL, int W, typename F, int I = 0>
 __device__ __forceinline__ void tree_eval_fast(const V (&x)[NL][W], V (&r)[W], uint32_t comb, uint32_t swaps) {
     if constexpr (I < StaticProgs<NL>::n) {
         constexpr uint32_t P = StaticProgs<NL>::v[I];
-        if (swaps == 0 && comb == P) {
+        if ((swaps == 0 || !F::kOrderSensitive) && comb == P) {
             tree_eval_static<V, NL, W, F, P>(x, r);
             return;
         }
@@ -225,7 +227,8 @@ struct ScalarOp {
 // the first combine (NL * U <= 16 loads of 16 B in flight per lane).  One trip per workgroup;
 // within its segment a workgroup's trip is placed by xcd_trip (the segment's first block may sit
 // anywhere in the 8-XCD rotation: blocks of one local residue class still share one XCD).
-template <int DT, int OP, int NL, int U, bool NT, int BL>
+// ACC0 (streaming 2-leaf trees): leaf 0's first vector keeps the default policy, as the bucket kernel's ACC0 slot.
+template <int DT, int OP, int NL, int U, bool NT, int BL, bool ACC0 = false>
 __global__ __launch_bounds__(BL) void k_reduce_tree(TreeArgs a) {
     // this workgroup's segment: one pass over the block0 table (scalar compares, no loop-carried
     // loads), then the segment's pointers pinned into SGPRs before the first vector load
@@ -266,8 +269,11 @@ __global__ __launch_bounds__(BL) void k_reduce_tree(TreeArgs a) {
     const size_t base = trip * BL * U + threadIdx.x;
     if ((trip + 1) * BL * U <= nvec) {
         u32x4 x[NL][U];
+        x[0][0] = ld<NT && !ACC0>(&leaves[0][base]);  // peeled: one instruction per policy (reduce_vec.hpp)
 #pragma unroll
-        for (int j = 0; j < NL; ++j)
+        for (int u = 1; u < U; ++u) x[0][u] = ld<NT>(&leaves[0][base + (size_t)u * BL]);
+#pragma unroll
+        for (int j = 1; j < NL; ++j)
 #pragma unroll
             for (int u = 0; u < U; ++u) x[j][u] = ld<NT>(&leaves[j][base + (size_t)u * BL]);
         __builtin_amdgcn_sched_barrier(0);
@@ -388,7 +394,7 @@ constexpr int tree_wg_per_cu() {
 
 template <int DT, int OP, int NL, int BL, bool NT>
 inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
-    constexpr int U = is_complex_dt<DT>() && OP == CHR_PROD ? 1 : tree_u<NL, NT>();  // see vec_u_dt
+    constexpr int U = is_complex_dt<DT>() && (OP == CHR_PROD || OP == kProdSw) ? 1 : tree_u<NL, NT>();  // vec_u_dt
     TreeArgs a = a_in;
     a.xrun = NT ? xcd_run_shift(tree_xcd_run_kib<NL>(), (size_t)BL * U * 16) : 0;
     // the odd-XCD handover of streaming launches (xcd_hand / xcd_trip_w in reduce_common.hpp), per segment
@@ -412,6 +418,12 @@ inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
     }
     if (grid == 0) return hipSuccess;
     const unsigned lds = NT ? nt_lds_bytes(reduce_tuning().wg_per_cu_tree, tree_wg_per_cu<NL>()) : 0;
+    if constexpr (NL == 2 && NT && !is_pair_dt<DT>() && !is_complex_dt<DT>()) {
+        if (reduce_tuning().tree_acc0 > 0) {
+            hipLaunchKernelGGL((k_reduce_tree<DT, OP, NL, U, NT, BL, true>), dim3((unsigned)grid), dim3(BL), lds, s, a);
+            return hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL((k_reduce_tree<DT, OP, NL, U, NT, BL>), dim3((unsigned)grid), dim3(BL), lds, s, a);
     return hipGetLastError();
 }

@@ -163,7 +163,7 @@ constexpr int vec_u() {
 // Complex PROD (C99 Annex G multiplication per element) keeps one vector per lane per trip.
 template <int DT, int OP, int M, bool NT>
 constexpr int vec_u_dt() {
-    return is_complex_dt<DT>() && OP == CHR_PROD ? 1 : vec_u<M, NT>();
+    return is_complex_dt<DT>() && (OP == CHR_PROD || OP == kProdSw) ? 1 : vec_u<M, NT>();
 }
 
 // A grid holds at most 2^31 threads here; larger calls (> 32 GiB per operand at BL = 64, U = 2)

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define CHR_ABI_VERSION 9  /* 9: chr_comm_info; 8: the stand-alone phase collectives (chr_intra_reduce_scatter_radix_batch, ...) */
+#define CHR_ABI_VERSION 10 /* 10: chr_comm_get_overlap; 9: chr_comm_info; 8: the stand-alone phase collectives (chr_intra_reduce_scatter_radix_batch, ...) */
 
 /* Element types.  The reference is generic over MPI_Datatype (all_reduce_radix_batch.cpp:202-204,
  * sizes from MPI_Type_size at :234-277); these are the MPI predefined types MPICH's
@@ -231,6 +231,9 @@ int chr_comm_tuned_schedule(const chr_comm* comm, int mode, size_t count, chr_dt
  * require it, so e.g. the flat schedule reduces slice s while slice s+1 is being gathered.
  * The call still completes on chr_comm_stream. */
 int chr_comm_set_overlap(chr_comm* comm, int enable);
+/* The overlap setting the communicator runs with (set_overlap, else CHR_OVERLAP as the library read it once per
+ * process), so that a record of a call reports what ran rather than a re-read of the environment. */
+int chr_comm_get_overlap(const chr_comm* comm, int* enable);
 /* HIP graph replay (default off; env CHR_GRAPHS=1): a device-resident collective is captured once
  * per (plan, send, recv, dtype, op) -- its RCCL groups, fused reductions and copies on both streams
  * -- and later calls with the same arguments replay it with one hipGraphLaunch.  Cuts the host

@@ -269,44 +269,98 @@ void orc_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int ra
     if (op == ORC_MAXLOC) ORC_LOC_LOOP(T, ys[i].v < xs[i].v);  \
     else if (op == ORC_MINLOC) ORC_LOC_LOOP(T, ys[i].v > xs[i].v)
 
-/* C99 Annex G complex multiplication, as libgcc's __mulsc3 / __muldc3 restate it (what MPICH's
- * `a = a * b` on `float _Complex` compiles to): products rounded one by one, and when both parts
- * come out NaN, the infinity recovery of C11 G.5.1.  (a + bi) = inout, (c + di) = in. */
-#define ORC_CMUL(F, INF, a_, b_, c_, d_, re_, im_)                                                 \
-    do {                                                                                          \
-        F a = (a_), b = (b_), c = (c_), d = (d_);                                                 \
-        F ac = a * c, bd = b * d, ad = a * d, bc = b * c;                                         \
-        F x = ac - bd, y = ad + bc;                                                               \
-        if (isnan(x) && isnan(y)) {                                                               \
-            int recalc = 0;                                                                       \
-            if (isinf(a) || isinf(b)) {                                                           \
-                a = copysign(isinf(a) ? (F)1 : (F)0, a);                                          \
-                b = copysign(isinf(b) ? (F)1 : (F)0, b);                                          \
-                if (isnan(c)) c = copysign((F)0, c);                                              \
-                if (isnan(d)) d = copysign((F)0, d);                                              \
-                recalc = 1;                                                                       \
-            }                                                                                     \
-            if (isinf(c) || isinf(d)) {                                                           \
-                c = copysign(isinf(c) ? (F)1 : (F)0, c);                                          \
-                d = copysign(isinf(d) ? (F)1 : (F)0, d);                                          \
-                if (isnan(a)) a = copysign((F)0, a);                                              \
-                if (isnan(b)) b = copysign((F)0, b);                                              \
-                recalc = 1;                                                                       \
-            }                                                                                     \
-            if (!recalc && (isinf(ac) || isinf(bd) || isinf(ad) || isinf(bc))) {                  \
-                if (isnan(a)) a = copysign((F)0, a);                                              \
-                if (isnan(b)) b = copysign((F)0, b);                                              \
-                if (isnan(c)) c = copysign((F)0, c);                                              \
-                if (isnan(d)) d = copysign((F)0, d);                                              \
-                recalc = 1;                                                                       \
-            }                                                                                     \
-            if (recalc) {                                                                         \
-                x = (F)(INF) * (a * c - b * d);                                                   \
-                y = (F)(INF) * (a * d + b * c);                                                   \
-            }                                                                                     \
-        }                                                                                         \
-        (re_) = x;                                                                                \
-        (im_) = y;                                                                                \
+/* x86 SSE arithmetic with its NaN rules written out, so that the oracle does not depend on which operand order the
+ * compiler of the oracle picks (the reference's MPICH loops run on x86):
+ *   two NaNs      -> the FIRST operand's, quieted (sign and payload kept);
+ *   one NaN       -> that NaN, quieted;
+ *   invalid operation on numbers (inf - inf, 0 * inf) -> the x86 default NaN, sign set (0xFFC00000 /
+ *                    0xFFF8000000000000).
+ * Which operand of each add / multiply is first in MPICH's compiled loops is what tests/golden/nan_reduce_local.npz
+ * (MPICH 3.3.2's own outputs on two-NaN, one-NaN and invalid operands) pins: inout first for MPI_FLOAT / MPI_DOUBLE
+ * SUM and PROD (opsum.c, opprod.c: `a = a op b`, a = inoutvec); in first for the C complex SUM, both parts. */
+enum { ORC_XADD, ORC_XSUB, ORC_XMUL };
+static float orc_quietf(float v) {
+    uint32_t u;
+    memcpy(&u, &v, 4);
+    u |= 0x00400000u;
+    memcpy(&v, &u, 4);
+    return v;
+}
+static double orc_quietd(double v) {
+    uint64_t u;
+    memcpy(&u, &v, 8);
+    u |= 0x0008000000000000ull;
+    memcpy(&v, &u, 8);
+    return v;
+}
+static float orc_x86f(float p, float q, int op) {
+    float r;
+    if (isnan(p)) return orc_quietf(p);
+    if (isnan(q)) return orc_quietf(q);
+    r = op == ORC_XADD ? p + q : op == ORC_XSUB ? p - q : p * q;
+    if (isnan(r)) {
+        const uint32_t u = 0xFFC00000u;
+        memcpy(&r, &u, 4);
+    }
+    return r;
+}
+static double orc_x86d(double p, double q, int op) {
+    double r;
+    if (isnan(p)) return orc_quietd(p);
+    if (isnan(q)) return orc_quietd(q);
+    r = op == ORC_XADD ? p + q : op == ORC_XSUB ? p - q : p * q;
+    if (isnan(r)) {
+        const uint64_t u = 0xFFF8000000000000ull;
+        memcpy(&r, &u, 8);
+    }
+    return r;
+}
+
+/* C99 Annex G complex multiplication, as MPICH's `a = a * b` on `float _Complex` compiles (gcc): the plain formula
+ * inline, and when both parts come out NaN a call to libgcc's __mulsc3 / __muldc3, which computes the products again
+ * (rounded one by one; the library is built with -ffp-contract=off) and, if both parts are still NaN, recovers the
+ * infinities (C11 G.5.1).  (a + bi) = inout, (c + di) = in.  Every input NaN makes both inline parts NaN, so the NaN
+ * that survives is decided by __mulsc3's operand order, which MPICH's fixture pins (tests/golden/gen_nan_payloads.py,
+ * searched over all orders: a*c, b*d, a*d, c*b, (ac) - (bd), (ad) + (bc), first operand first); the inline order and
+ * the recalc order only ever see numbers, so only the default NaN of an invalid operation can come out of them. */
+#define ORC_CMUL(F, X, INF, a_, b_, c_, d_, re_, im_)                                                               \
+    do {                                                                                                           \
+        F a = (a_), b = (b_), c = (c_), d = (d_);                                                                  \
+        F ac = X(a, c, ORC_XMUL), bd = X(b, d, ORC_XMUL), ad = X(a, d, ORC_XMUL), bc = X(b, c, ORC_XMUL);         \
+        F x = X(ac, bd, ORC_XSUB), y = X(ad, bc, ORC_XADD);                                                        \
+        if (isnan(x) && isnan(y)) { /* __mulsc3 */                                                                 \
+            int recalc = 0;                                                                                       \
+            ac = X(a, c, ORC_XMUL), bd = X(b, d, ORC_XMUL), ad = X(a, d, ORC_XMUL), bc = X(c, b, ORC_XMUL);       \
+            x = X(ac, bd, ORC_XSUB);                                                                               \
+            y = X(ad, bc, ORC_XADD);                                                                               \
+            if (isinf(a) || isinf(b)) {                                                                            \
+                a = copysign(isinf(a) ? (F)1 : (F)0, a);                                                           \
+                b = copysign(isinf(b) ? (F)1 : (F)0, b);                                                           \
+                if (isnan(c)) c = copysign((F)0, c);                                                               \
+                if (isnan(d)) d = copysign((F)0, d);                                                               \
+                recalc = 1;                                                                                        \
+            }                                                                                                      \
+            if (isinf(c) || isinf(d)) {                                                                            \
+                c = copysign(isinf(c) ? (F)1 : (F)0, c);                                                           \
+                d = copysign(isinf(d) ? (F)1 : (F)0, d);                                                           \
+                if (isnan(a)) a = copysign((F)0, a);                                                               \
+                if (isnan(b)) b = copysign((F)0, b);                                                               \
+                recalc = 1;                                                                                        \
+            }                                                                                                      \
+            if (!recalc && (isinf(ac) || isinf(bd) || isinf(ad) || isinf(bc))) {                                   \
+                if (isnan(a)) a = copysign((F)0, a);                                                               \
+                if (isnan(b)) b = copysign((F)0, b);                                                               \
+                if (isnan(c)) c = copysign((F)0, c);                                                               \
+                if (isnan(d)) d = copysign((F)0, d);                                                               \
+                recalc = 1;                                                                                        \
+            }                                                                                                      \
+            if (recalc) {                                                                                          \
+                x = X((F)(INF), X(X(a, c, ORC_XMUL), X(b, d, ORC_XMUL), ORC_XSUB), ORC_XMUL);                      \
+                y = X((F)(INF), X(X(a, d, ORC_XMUL), X(b, c, ORC_XMUL), ORC_XADD), ORC_XMUL);                      \
+            }                                                                                                      \
+        }                                                                                                          \
+        (re_) = x;                                                                                                 \
+        (im_) = y;                                                                                                 \
     } while (0)
 
 void orc_reduce_local(const void* in, void* inout, size_t n, int dtype, int op) {
@@ -321,11 +375,11 @@ void orc_reduce_local(const void* in, void* inout, size_t n, int dtype, int op) 
         orc_cf* ys = (orc_cf*)inout;
         size_t i;
         for (i = 0; i < n; ++i) {
-            if (op == ORC_SUM) {
-                ys[i].re = ys[i].re + xs[i].re;
-                ys[i].im = ys[i].im + xs[i].im;
+            if (op == ORC_SUM) { /* in's NaN survives, each part (MPICH's fixture) */
+                ys[i].re = orc_x86f(xs[i].re, ys[i].re, ORC_XADD);
+                ys[i].im = orc_x86f(xs[i].im, ys[i].im, ORC_XADD);
             } else {
-                ORC_CMUL(float, INFINITY, ys[i].re, ys[i].im, xs[i].re, xs[i].im, ys[i].re, ys[i].im);
+                ORC_CMUL(float, orc_x86f, INFINITY, ys[i].re, ys[i].im, xs[i].re, xs[i].im, ys[i].re, ys[i].im);
             }
         }
         break;
@@ -336,18 +390,18 @@ void orc_reduce_local(const void* in, void* inout, size_t n, int dtype, int op) 
         size_t i;
         for (i = 0; i < n; ++i) {
             if (op == ORC_SUM) {
-                ys[i].re = ys[i].re + xs[i].re;
-                ys[i].im = ys[i].im + xs[i].im;
+                ys[i].re = orc_x86d(xs[i].re, ys[i].re, ORC_XADD);
+                ys[i].im = orc_x86d(xs[i].im, ys[i].im, ORC_XADD);
             } else {
-                ORC_CMUL(double, INFINITY, ys[i].re, ys[i].im, xs[i].re, xs[i].im, ys[i].re, ys[i].im);
+                ORC_CMUL(double, orc_x86d, INFINITY, ys[i].re, ys[i].im, xs[i].re, xs[i].im, ys[i].re, ys[i].im);
             }
         }
         break;
     }
     /* MPICH 3.3.2 also takes LAND/LOR/LXOR on float and double (probed: rc 0), C truth values. */
     case ORC_F32:
-        if (op == ORC_SUM) ORC_LOOP(float, y + x);
-        else if (op == ORC_PROD) ORC_LOOP(float, y * x);
+        if (op == ORC_SUM) ORC_LOOP(float, orc_x86f(y, x, ORC_XADD)); /* inout's NaN survives */
+        else if (op == ORC_PROD) ORC_LOOP(float, orc_x86f(y, x, ORC_XMUL));
         else if (op == ORC_MAX) ORC_LOOP(float, y > x ? y : x);
         else if (op == ORC_MIN) ORC_LOOP(float, y < x ? y : x);
         else if (op == ORC_LAND) ORC_LOOP(float, (float)(y && x));
@@ -355,8 +409,8 @@ void orc_reduce_local(const void* in, void* inout, size_t n, int dtype, int op) 
         else if (op == ORC_LXOR) ORC_LOOP(float, (float)(!y != !x));
         break;
     case ORC_F64:
-        if (op == ORC_SUM) ORC_LOOP(double, y + x);
-        else if (op == ORC_PROD) ORC_LOOP(double, y * x);
+        if (op == ORC_SUM) ORC_LOOP(double, orc_x86d(y, x, ORC_XADD));
+        else if (op == ORC_PROD) ORC_LOOP(double, orc_x86d(y, x, ORC_XMUL));
         else if (op == ORC_MAX) ORC_LOOP(double, y > x ? y : x);
         else if (op == ORC_MIN) ORC_LOOP(double, y < x ? y : x);
         else if (op == ORC_LAND) ORC_LOOP(double, (double)(y && x));
@@ -374,15 +428,11 @@ void orc_reduce_local(const void* in, void* inout, size_t n, int dtype, int op) 
     case ORC_BF16:
         /* The reference has no bf16; the golden driver runs it as a user-defined op on
          * MPI_Type_contiguous(2, MPI_BYTE) computing bf16_rne(f32(inout) op f32(in)) with the
-         * same operand order as the predefined float ops.  Two NaNs: inout's survives (quieted), as
-         * MPICH's float and double loops keep it -- written out, since a plain + or * leaves the
-         * payload to whichever operand order the compiler picks (gcc here kept in's). */
+         * same operand order as the predefined float ops: inout first, with x86's NaN rules (orc_x86f). */
         if (op == ORC_SUM)
-            ORC_LOOP(uint16_t, isnan(orc_bf16_to_f32(y)) ? orc_f32_to_bf16(orc_bf16_to_f32(y))
-                                                         : orc_f32_to_bf16(orc_bf16_to_f32(y) + orc_bf16_to_f32(x)));
+            ORC_LOOP(uint16_t, orc_f32_to_bf16(orc_x86f(orc_bf16_to_f32(y), orc_bf16_to_f32(x), ORC_XADD)));
         else if (op == ORC_PROD)
-            ORC_LOOP(uint16_t, isnan(orc_bf16_to_f32(y)) ? orc_f32_to_bf16(orc_bf16_to_f32(y))
-                                                         : orc_f32_to_bf16(orc_bf16_to_f32(y) * orc_bf16_to_f32(x)));
+            ORC_LOOP(uint16_t, orc_f32_to_bf16(orc_x86f(orc_bf16_to_f32(y), orc_bf16_to_f32(x), ORC_XMUL)));
         else if (op == ORC_MAX)
             ORC_LOOP(uint16_t, orc_bf16_to_f32(y) > orc_bf16_to_f32(x) ? y : x);
         else

@@ -9,7 +9,9 @@
 //   ref_pairs_probe table                      -> JSON: size / extent per type, and which of the
 //                                                 12 predefined ops MPI_Reduce_local accepts for it
 //   ref_pairs_probe reduce TYPE OP N in inout out -> out = MPI_Reduce_local(in, inout) on N elements
-//                                                 (raw bytes at the type's extent)
+//                                                 (raw bytes at the type's extent); TYPE also f32 / f64
+//                                                 (MPI_FLOAT / MPI_DOUBLE, for the NaN-payload fixture,
+//                                                 tests/golden/gen_nan_payloads.py)
 #include <mpi.h>
 
 #include <cstdio>
@@ -65,7 +67,10 @@ int main(int argc, char** argv) {
         std::printf("}\n");
     } else if (cmd == "reduce" && argc == 8) {
         MPI_Datatype t = MPI_DATATYPE_NULL;
-        for (const Named& x : types())
+        std::vector<Named> all = types();
+        all.push_back({"f32", MPI_FLOAT});
+        all.push_back({"f64", MPI_DOUBLE});
+        for (const Named& x : all)
             if (x.name == std::string(argv[2])) t = x.t;
         MPI_Op op = MPI_OP_NULL;
         for (auto& o : ops())

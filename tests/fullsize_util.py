@@ -19,10 +19,12 @@ def windows(recvcount, width):
     return [(off, min(width, recvcount - off)) for off in range(0, recvcount, width)]
 
 
-def check_allreduce(out_window, n, k, b, dtype, count, seed, pattern=po.PAT_UNIFORM, width=1 << 21, threads=8,
-                    ranks=None):
+def check_allreduce(out_window, n, k, b, dtype, count, seed, pattern=po.PAT_UNIFORM, width=1 << 21, threads=16,
+                    ranks=None, part=None):
     """out_window(r, off, w) -> numpy array of rank r's output at block_window(n, count // n, off, w).
-    Returns the list of (rank, off) windows that differ from the oracle (empty = bit-exact)."""
+    Returns the list of (rank, off) windows that differ from the oracle (empty = bit-exact).  part = (i, p): only
+    every p-th window from the i-th (p processes checking one output together).  16 threads: the GPU box's CPU share
+    (one process checking alone)."""
     rc = count // n
     check = list(range(n)) if ranks is None else list(ranks)
 
@@ -38,13 +40,16 @@ def check_allreduce(out_window, n, k, b, dtype, count, seed, pattern=po.PAT_UNIF
                 bad.append((r, off))
         return bad
 
+    wins = windows(rc, width)
+    if part is not None:
+        wins = wins[part[0]::part[1]]
     with ThreadPoolExecutor(threads) as ex:
-        res = list(ex.map(one, windows(rc, width)))
+        res = list(ex.map(one, wins))
     return [x for bad in res for x in bad]
 
 
 def check_reduce_scatter(out_window, n, k, b, dtype, recvcount, seed, pattern=po.PAT_UNIFORM, width=1 << 21,
-                         threads=8):
+                         threads=16):
     """out_window(r, off, w) -> rank r's output elements [off, off + w)."""
     count = recvcount * n
 

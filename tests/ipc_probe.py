@@ -48,10 +48,12 @@ def ck(rc, what):
         sys.exit(3)
 
 
-def words(n, f):
-    import array
+def words(n, kind):
+    """The probe's word patterns as a contiguous uint32 array: "owner" i ^ 0x5A5A0000, "peer" ~i, "zero"."""
+    import numpy as np
 
-    return array.array("I", (f(i) & 0xFFFFFFFF for i in range(n)))
+    i = np.arange(n, dtype=np.uint32)
+    return {"owner": i ^ np.uint32(0x5A5A0000), "peer": ~i, "zero": np.zeros(n, dtype=np.uint32)}[kind]
 
 
 def main():
@@ -63,16 +65,17 @@ def main():
         n = nbytes // 4
         p = ctypes.c_void_p()
         ck(lib.hipMalloc(ctypes.byref(p), nbytes), "hipMalloc")
-        src = words(n, lambda i: i ^ 0x5A5A0000)
-        ck(lib.hipMemcpy(p, src.buffer_info()[0], nbytes, H2D), "hipMemcpy H2D")
+        src = words(n, "owner")
+        ck(lib.hipMemcpy(p, src.ctypes.data, nbytes, H2D), "hipMemcpy H2D")
         h = ctypes.create_string_buffer(64)
         ck(lib.hipIpcGetMemHandle(h, p), "hipIpcGetMemHandle")
         print(h.raw.hex(), flush=True)
         sys.stdin.readline()  # the peer has written
-        back = words(n, lambda i: 0)
-        ck(lib.hipMemcpy(back.buffer_info()[0], p, nbytes, D2H), "hipMemcpy D2H")
-        want = words(n, lambda i: ~i)
-        print("OK" if back == want else f"FAIL owner sees {back[:4].tolist()} want {want[:4].tolist()}", flush=True)
+        back = words(n, "zero")
+        ck(lib.hipMemcpy(back.ctypes.data, p, nbytes, D2H), "hipMemcpy D2H")
+        want = words(n, "peer")
+        ok = bool((back == want).all())
+        print("OK" if ok else f"FAIL owner sees {back[:4].tolist()} want {want[:4].tolist()}", flush=True)
         ck(lib.hipFree(p), "hipFree")
     else:
         hx, nbytes = sys.argv[2], int(sys.argv[3])
@@ -80,13 +83,13 @@ def main():
         h = IpcHandle.from_buffer_copy(bytes.fromhex(hx))
         p = ctypes.c_void_p()
         ck(lib.hipIpcOpenMemHandle(ctypes.byref(p), h, 1), "hipIpcOpenMemHandle")  # hipIpcMemLazyEnablePeerAccess
-        got = words(n, lambda i: 0)
-        ck(lib.hipMemcpy(got.buffer_info()[0], p, nbytes, D2H), "hipMemcpy D2H (peer)")
-        if got != words(n, lambda i: i ^ 0x5A5A0000):
+        got = words(n, "zero")
+        ck(lib.hipMemcpy(got.ctypes.data, p, nbytes, D2H), "hipMemcpy D2H (peer)")
+        if not (got == words(n, "owner")).all():
             print(f"FAIL peer sees {got[:4].tolist()}", flush=True)
             sys.exit(4)
-        new = words(n, lambda i: ~i)
-        ck(lib.hipMemcpy(p, new.buffer_info()[0], nbytes, H2D), "hipMemcpy H2D (peer)")
+        new = words(n, "peer")
+        ck(lib.hipMemcpy(p, new.ctypes.data, nbytes, H2D), "hipMemcpy H2D (peer)")
         ck(lib.hipIpcCloseMemHandle(p), "hipIpcCloseMemHandle")
         print("OK", flush=True)
 

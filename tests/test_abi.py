@@ -34,7 +34,7 @@ def test_library_is_gfx950_code_object():
 
 
 def test_abi_basics():
-    assert ca.lib().chr_abi_version() == 9
+    assert ca.lib().chr_abi_version() == 10
     assert ca.lib().chr_error_string(2).decode().startswith("count")
     assert ca.lib().chr_error_string(0) == b"success"
 

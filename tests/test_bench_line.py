@@ -30,6 +30,9 @@ NOISE = [
 ]
 
 
+LIB = {"library": "/x/torch/lib/librccl.so", "version": "2.22.3", "version_code": 22203}
+
+
 def _info(r, bus, n=8):
     return {"nranks": n, "rank": r, "device": r if bus else 0, "pci_bus_id": f"0000:{(r + 1) if bus else 5:02x}:00.0"}
 
@@ -93,6 +96,33 @@ def test_rccl_log_env_is_per_rank_file(tmp_path):
     assert bench.read_rccl_logs(str(tmp_path / "nowhere"), 3) == []
 
 
+def test_stale_rccl_log_is_ignored(tmp_path):
+    """a file an earlier run left in the log directory (another pid: P2P lines that would make
+    the record claim xGMI) is not read into this run's pairs; only this process's own file is."""
+    logs = tmp_path / "logs"
+    logs.mkdir()
+    (logs / "rccl.rank0.111.log").write_text("\n".join(ln for ln in P2P_8 if "[0] NCCL" in ln))  # stale
+    (logs / "rccl.rank0.222.log").write_text("\n".join(SOCKET_2))                               # this run
+    got = bench.parse_rccl_transports(bench.read_rccl_logs(str(logs), 0, 222), nranks=2)
+    assert got == bench.parse_rccl_transports(SOCKET_2, nranks=2)
+    assert bench.read_rccl_logs(str(logs), 0, 333) == []
+
+
+def test_rccl_library_names_the_loaded_copy():
+    """rccl_library() on this process: the path comes from /proc/self/maps only (None when no librccl is loaded,
+    as in a CPU test that has not imported torch's RCCL), never from a fresh dlopen."""
+    rec = bench.rccl_library()
+    assert set(rec) == {"library", "version", "version_code"}
+    if rec["library"] is not None:
+        assert "librccl" in os.path.basename(rec["library"])
+        assert rec["version_code"] is None or rec["version_code"] > 20000
+    # the record carries rank 0's library and whether every rank agrees
+    recs = [bench.rccl_record([_info(r, True) for r in range(2)], [{}, {}], 2, libs)
+            for libs in ([LIB, LIB], [LIB, dict(LIB, version="2.27.3")])]
+    assert recs[0]["version"] == "2.22.3" and recs[0]["same_on_all_ranks"] is True
+    assert recs[1]["same_on_all_ranks"] is False
+
+
 def _n1_line():
     by, span = 3 * 4 * bench.C2_ELEMS, 0.0302
     ach = by / (span * 1e-3) / 1e9
@@ -119,7 +149,7 @@ def _nn_line(n=8):
             "aggregate_GBps": round(n * algbw, 2), "definitions": bench.LINE_DEFINITIONS_NN,
             "roofline": {"traffic": 123, "traffic_source": "pmc"},
             "rccl": bench.rccl_record([_info(r, True) for r in range(n)],
-                                      [bench.parse_rccl_transports(P2P_8, nranks=8)] * n, n),
+                                      [bench.parse_rccl_transports(P2P_8, nranks=8)] * n, n, [LIB] * n),
             "cpu_baseline": {"value": 3.0, "unit": "GB/s", "cores": n, "kind": "reference", "sample": "s"},
             "result_check": {"ranks_bit_identical": True, "within_tolerance": True, "violations": 0},
             "compare": {"c5_allreduce_bf16_k4_b4_1GiB": {"algbw_GBps": 1, "schedule": "flat", "slices": 4,
@@ -138,6 +168,9 @@ def test_canned_lines_pass():
     (lambda l: l["config"].pop("slices"), "config.slices"),
     (lambda l: l.pop("rccl"), "rccl"),
     (lambda l: l["rccl"].__setitem__("not_xgmi_because", ["x"]), "xgmi true"),
+    (lambda l: l["rccl"].pop("version"), "rccl.version"),
+    (lambda l: l["rccl"].pop("library"), "rccl.library"),
+    (lambda l: l["rccl"].__setitem__("same_on_all_ranks", False), "rccl.same_on_all_ranks"),
     (lambda l: l["roofline"].update(traffic=None), "traffic"),
     (lambda l: l["compare"]["c5_allreduce_bf16_k4_b4_1GiB"].pop("overlap"), "c5.overlap"),
     (lambda l: l["compare"]["c5_allreduce_bf16_k4_b4_1GiB"].update(slices=1), "overlapped depth"),
@@ -173,7 +206,7 @@ def test_committed_round5_lines_meet_the_definitions():
             continue
         if "metric" not in line:
             continue
-        assert bench.line_problems(line) == [], f
+        assert bench.line_problems(line, rccl_library=False) == [], f
         checked += 1
     if not files:
         pytest.skip("no round-5 bench lines committed yet")

@@ -382,6 +382,18 @@ def test_rccl_comm_single_rank(gu):
     np.testing.assert_array_equal(host_out, x)
     assert ca.reduce_scatter_radix_batch(ds, dr, x.size, ca.FLOAT32, ca.SUM, comm, 2, 1) == 0
     np.testing.assert_array_equal(gu.from_dev(dr, np.float32), x)
+    # a fixed schedule's (schedule, depth) for a call with these arguments -- and none for arguments such a call
+    # rejects, or on an aborted communicator; the overlap setting read back from the library
+    comm.set_schedule(ca.SCHEDULE_FLAT)
+    assert comm.tuned_schedule(ca.MODE_ALLREDUCE, x.size, ca.FLOAT32, 2, 1) == (ca.SCHEDULE_FLAT, 1)
+    assert comm.tuned_schedule(ca.MODE_ALLREDUCE, x.size, ca.FLOAT32, 1, 1) is None  # k < 2
+    assert comm.tuned_schedule(ca.MODE_ALLREDUCE, x.size, ca.FLOAT32, 2, 3) is None  # nranks % b
+    assert comm.tuned_schedule(5, x.size, ca.FLOAT32, 2, 1) is None  # not allreduce / reduce-scatter
+    assert comm.overlap is True
+    comm.set_overlap(False)
+    assert comm.overlap is False
+    comm.abort()
+    assert comm.tuned_schedule(ca.MODE_ALLREDUCE, x.size, ca.FLOAT32, 2, 1) is None
     comm.destroy()
     torch.cuda.synchronize()
 

@@ -151,3 +151,90 @@ def test_tree_kernel_nan_payloads(gu, dtype, op, prog, n, mixed):
                           gu.stream()) == 0
     gu.sync()
     np.testing.assert_array_equal(_bits(gu.from_dev(out, npdt)), _bits(tree_ref(leaves, comb, swaps, dtype, op)))
+
+
+# ---- MPICH's own NaN results (tests/golden/nan_reduce_local.npz, tests/golden/gen_nan_payloads.py) ------------------
+# Two-NaN, one-NaN and invalid operations (inf - inf, 0 * inf: x86's default NaN, sign set) on every floating type x
+# op -- MPI_FLOAT / MPI_DOUBLE SUM and PROD, the C complex types' SUM and PROD in both parts (libgcc's __mulsc3
+# included), MPI_FLOAT_INT / MPI_DOUBLE_INT MAXLOC and MINLOC -- as MPICH 3.3.2's MPI_Reduce_local computed them.
+NAN_CASES = [("f32", "sum"), ("f32", "prod"), ("f64", "sum"), ("f64", "prod"), ("cf", "sum"), ("cf", "prod"),
+             ("cd", "sum"), ("cd", "prod"), ("fi", "maxloc"), ("fi", "minloc"), ("di", "maxloc"), ("di", "minloc")]
+NAN_DT = {"f32": ca.FLOAT32, "f64": ca.FLOAT64, "cf": ca.C_FLOAT_COMPLEX, "cd": ca.C_DOUBLE_COMPLEX,
+          "fi": ca.FLOAT_INT, "di": ca.DOUBLE_INT}
+NAN_OP = {"sum": ca.SUM, "prod": ca.PROD, "maxloc": ca.MAXLOC, "minloc": ca.MINLOC}
+
+
+@pytest.fixture(scope="module")
+def nan_fix():
+    import os
+
+    return np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "nan_reduce_local.npz"),
+                   allow_pickle=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype, op", NAN_CASES, ids=[f"{d}_{o}" for d, o in NAN_CASES])
+def test_mpich_nan_fixture_on_device(gu, nan_fix, dtype, op):
+    """MPICH's bytes, element for element, through every kernel shape that can run the (type, op): the scalar kernel
+    (chr_reduce_local), the vector kernel plain and -- for f32 / f64, tiled to 48 / 96 MiB per call -- streaming,
+    MPICH_do_reduce's running-value-first order (chr_reduce_multi_ex with the operands exchanged), and the tree
+    kernel's 2-leaf program, plain and swapped."""
+    key = f"{dtype}_{op}"
+    x, y, want = nan_fix[key + "_in"], nan_fix[key + "_inout"], nan_fix[key + "_out"]
+    ext = po.NP_DTYPES[dtype].itemsize if dtype in ("fi", "di") else np.dtype(po.NP_DTYPES[dtype]).itemsize
+    n = x.size // ext
+    dt, o = NAN_DT[dtype], NAN_OP[op]
+    # scalar kernel: MPI_Reduce_local(in, inout) one element off the 16-B grid
+    d_x, d_y = gu.empty_dev(x.size + ext), gu.empty_dev(y.size + ext)
+    d_x[ext:] = gu.to_dev(x)
+    d_y[ext:] = gu.to_dev(y)
+    assert ca.reduce_local(d_x.data_ptr() + ext, d_y.data_ptr() + ext, n, dt, o, gu.stream()) == 0
+    gu.sync()
+    assert np.array_equal(d_y.cpu().numpy()[ext:], want), "scalar"
+    reps = 1024 if dtype in ("f32", "f64") else 4
+    xs, ys, ws = np.tile(x, reps), np.tile(y, reps), np.tile(want, reps)
+    N = n * reps
+    # vector kernel, m = 1 (plain, or streaming from 40 MiB per call)
+    d_x, d_y, d_o = gu.to_dev(xs), gu.to_dev(ys), gu.empty_dev(ys.size)
+    assert ca.reduce_multi(d_o.data_ptr(), d_y.data_ptr(), [d_x.data_ptr()], N, dt, o, gu.stream()) == 0
+    gu.sync()
+    assert np.array_equal(d_o.cpu().numpy(), ws), "vector"
+    # running-value-first: MPI_Reduce_local(in = running, inout = next), the running value being the accumulator
+    assert ca.reduce_multi_ex(d_o.data_ptr(), d_x.data_ptr(), [d_y.data_ptr()], N, dt, o, ca.REDUCE_RUNNING_FIRST,
+                              gu.stream()) == 0
+    gu.sync()
+    assert np.array_equal(d_o.cpu().numpy(), ws), "running first"
+    # tree kernel, 2 leaves: F(in = leaf 1, inout = leaf 0); swapped: F(in = leaf 0, inout = leaf 1)
+    for leaves, swaps in (([d_y, d_x], [0]), ([d_x, d_y], [1])):
+        assert ca.reduce_tree(d_o.data_ptr(), [t.data_ptr() for t in leaves], [0, 1], swaps, N, dt, o,
+                              gu.stream()) == 0
+        gu.sync()
+        assert np.array_equal(d_o.cpu().numpy(), ws), ("tree", swaps)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype, op", NAN_CASES, ids=[f"{d}_{o}" for d, o in NAN_CASES])
+def test_nan_fixture_chains_vs_oracle(gu, nan_fix, dtype, op):
+    """Chains of the fixture's NaN-rich operands: m = 3 fused folds and an 8-leaf tree (a compile-time program and a
+    swapped one), against the oracle, whose single steps the fixture pins."""
+    key = f"{dtype}_{op}"
+    npdt = po.NP_DTYPES[dtype]
+    raw = [nan_fix[key + "_in"], nan_fix[key + "_inout"], nan_fix[key + "_out"]]
+    ext = npdt.itemsize if dtype in ("fi", "di") else np.dtype(npdt).itemsize
+    n = raw[0].size // ext
+    rng = np.random.default_rng(7)
+    ops = [np.ascontiguousarray(raw[j % 3].reshape(n, ext)[rng.permutation(n)]).reshape(-1) for j in range(8)]
+    dt, o = NAN_DT[dtype], NAN_OP[op]
+    d = [gu.to_dev(a) for a in ops]
+    out = gu.empty_dev(ops[0].size)
+    assert ca.reduce_multi(out.data_ptr(), d[0].data_ptr(), [t.data_ptr() for t in d[1:4]], n, dt, o, gu.stream()) == 0
+    gu.sync()
+    ref = ops[0].copy().view(npdt)
+    for a in ops[1:4]:
+        po.reduce_local(a.copy().view(npdt), ref, dtype, op)
+    assert np.array_equal(out.cpu().numpy(), ref.view(np.uint8)), "m = 3"
+    for comb, swaps in (C4_TREE, SWAP_TREE):
+        assert ca.reduce_tree(out.data_ptr(), [t.data_ptr() for t in d], comb, swaps, n, dt, o, gu.stream()) == 0
+        gu.sync()
+        want = tree_ref([a.copy().view(npdt) for a in ops], comb, swaps, dtype, op)
+        assert np.array_equal(out.cpu().numpy(), want.view(np.uint8)), ("tree", swaps)

@@ -64,20 +64,40 @@ print(json.dumps({{"bad": [str(b) for b in bad]}}))
 """
 
 
-@pytest.mark.parametrize("run_kib,max_vec,hand_shift", [(4, 0, -1), (8, 0, -1), (64, 0, -1), (8, 3000, -1),
-                                                     (8, 0, 1), (0, 0, 2), (4, 3000, 3)])
-def test_xcd_run_map_covers_every_trip(run_kib, max_vec, hand_shift):
-    """max_vec > 0 also caps the vectors per launch / tree segment (CHR_REDUCE_MAX_LAUNCH_VEC), so the
-    paths that split > 32 GiB buckets into several launches and > 1 GiB trees into several segments
-    (and several flushes of 8 segments) run at these sizes, with partial trips inside a call.
-    hand_shift: the odd-XCD handover (xcd_trip_w) -- the policy's shift 6 engages at the 2^21-element
-    bucket here; shifts 1-3 hand up to half of every odd XCD's share over, on run and identity maps."""
+XCD_CONFIGS = [(4, 0, -1), (8, 0, -1), (64, 0, -1), (8, 3000, -1), (8, 0, 1), (0, 0, 2), (4, 3000, 3)]
+
+
+def test_xcd_run_map_covers_every_trip():
+    """Every (run_kib, max_vec, hand_shift) configuration in its own child process (the tuning variables are read
+    once per process), the seven children at once: each is a second of small launches behind a second or two of
+    start-up (the suite's time).  max_vec > 0 also caps the vectors per launch / tree segment
+    (CHR_REDUCE_MAX_LAUNCH_VEC), so the paths that split > 32 GiB buckets into several launches and > 1 GiB trees
+    into several segments (and several flushes of 8 segments) run at these sizes, with partial trips inside a call.
+    hand_shift: the odd-XCD handover (xcd_trip_w) -- the policy's shift 6 engages at the 2^21-element bucket here;
+    shifts 1-3 hand up to half of every odd XCD's share over, on run and identity maps."""
     code = CHILD.format(here=HERE, oracle=os.path.join(REPO, "oracle"),
                         pkg=os.path.join(REPO, "configurable-hierarchical-allreduce-algorithms_amd"))
-    env = dict(os.environ, CHR_REDUCE_NT="1", CHR_XCD_RUN_KIB=str(run_kib), CHR_REDUCE_MAX_LAUNCH_VEC=str(max_vec))
-    if hand_shift >= 0:
-        env["CHR_XCD_HAND_SHIFT"] = str(hand_shift)
-    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
-    assert out.returncode == 0, out.stderr[-3000:]
-    res = json.loads(out.stdout.strip().splitlines()[-1])
-    assert not res["bad"], res["bad"][:10]
+    procs = []
+    for run_kib, max_vec, hand_shift in XCD_CONFIGS:
+        env = dict(os.environ, CHR_REDUCE_NT="1", CHR_XCD_RUN_KIB=str(run_kib),
+                   CHR_REDUCE_MAX_LAUNCH_VEC=str(max_vec))
+        if hand_shift >= 0:
+            env["CHR_XCD_HAND_SHIFT"] = str(hand_shift)
+        procs.append(subprocess.Popen([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    failures = []
+    for cfg, p in zip(XCD_CONFIGS, procs):
+        try:
+            out, err = p.communicate(timeout=300)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, err = p.communicate()
+            failures.append((cfg, "timeout"))
+            continue
+        if p.returncode != 0:
+            failures.append((cfg, err[-3000:]))
+            continue
+        res = json.loads(out.strip().splitlines()[-1])
+        if res["bad"]:
+            failures.append((cfg, res["bad"][:10]))
+    assert not failures, failures

@@ -43,7 +43,7 @@ run() {  # run <seconds> <log> cmd...: the step's own limit; stop the script on 
 
 for step in "$@"; do
   case "$step" in
-  suite) run 1100 pytest_suite.txt $PYT --timeout 900 --durations=60 -m gpu tests/ ;;
+  suite) CHR_GPU_SUITE_BUDGET_STRICT=1 run 1100 pytest_suite.txt $PYT --timeout 900 --durations=0 -m gpu tests/ ;;
   tests) run "${TEST_LIMIT:-900}" "pytest_${TAG:-tests}.txt" python -u -m pytest -x -v --timeout-method thread --timeout 170 -m gpu ${TESTS:?set TESTS} ;;
   smoke) run 300 smoke.txt python -c "import __graft_entry__ as g; g.smoke()" ;;
   bench) run 300 bench.json python bench.py --steps 20 --warmup 5 ;;
