@@ -276,11 +276,30 @@ C2_KERNEL_SYMBOL = "void chr::k_reduce_vec<0, 0, 1, 4, true, true, 64>(chr::VecA
 
 
 TREE8_KERNEL_SYMBOL = "void chr::k_reduce_tree<0, 0, 8, 1, true, 64>(chr::TreeArgs)"
-# the flat schedule's per-chunk tree at 8 / 4 / 2 ranks (b = N): its PMC entry (tools/tree_pmc.py --leaves L) and the
-# streaming instantiation a 1 GiB call launches (reduce_tree.hpp tree_u: U = 1 / 2 / 4)
+# The kernel a flat plan's reductions run on, by the plan's own ops (reduction_pmc): a tree of L leaves -> its PMC entry
+# (tools/tree_pmc.py --leaves L) and the streaming instantiation a 1 GiB call launches (reduce_tree.hpp tree_u: U = 1 /
+# 2 / 4); a single fold of m incoming pieces -- what the N = 2 and N = 4 lines' one-node geometries compile to
+# (schedule.cpp tree_program) -- -> the bucket kernel out of place (tools/tree_pmc.py --vec m).  Round 5 bound the N = 2
+# / N = 4 lines to the 2- / 4-leaf tree entries, kernels those lines never launch.
 TREE_PMC = {8: ("tree_f32_sum_8leaves_64MiB", TREE8_KERNEL_SYMBOL),
             4: ("tree_f32_sum_4leaves_64MiB", "void chr::k_reduce_tree<0, 0, 4, 2, true, 64>(chr::TreeArgs)"),
             2: ("tree_f32_sum_2leaves_64MiB", "void chr::k_reduce_tree<0, 0, 2, 4, true, 64>(chr::TreeArgs)")}
+VEC_OOP_PMC = {1: ("reduce_f32_sum_m1_oop_128MiB", "void chr::k_reduce_vec<0, 0, 1, 4, true, true, 64>(chr::VecArgs)"),
+               3: ("reduce_f32_sum_m3_oop_64MiB", "void chr::k_reduce_vec<0, 0, 3, 2, true, true, 64>(chr::VecArgs)")}
+
+
+def reduction_pmc(plan):
+    """((pmc key, kernel symbol), None) for the reductions of a parsed plan (ca.parse_plan), or (None, why): every
+    reduction of the plan must be the same kernel shape -- trees of one leaf count, or folds of one fan-in."""
+    shapes = {("tree", len(op[4]) + 1) if op[0] == "tree" else ("reduce", len(op[4]))
+              for st in plan["steps"] for op in st["post"] if op[0] in ("tree", "reduce")}
+    if len(shapes) != 1:
+        return None, f"reductions of several shapes: {sorted(shapes)}" if shapes else "no reductions"
+    kind, width = shapes.pop()
+    entry = (TREE_PMC if kind == "tree" else VEC_OOP_PMC).get(width)
+    if entry is None:
+        return None, f"no PMC entry for {kind} width {width}"
+    return entry, None
 
 
 def pmc_ratio(kernel_key, symbol, root=REPO):
@@ -1123,16 +1142,21 @@ def bench_allreduce(args):
     if float(busiest[0]) > 0:
         ach = float(busiest[1]) / (float(busiest[0]) * 1e-3) / 1e9
         traffic, stale = None, None
-        pmc_key = None
-        if world in TREE_PMC and args.dtype == "f32":  # the flat schedule's world-leaf trees: the PMC entry's kernel
-            pmc_key, sym = TREE_PMC[world]
+        pmc_key, sym = None, None
+        # the kernel the metric's plan launches (its tuned schedule and depth)
+        mplan = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, world, rank, k, b, count,
+                                               tuned[1] if tuned else 1, tuned[0] if tuned else 2))
+        entry, why = reduction_pmc(mplan)
+        if entry is not None and args.dtype == "f32":
+            pmc_key, sym = entry
             ratio, stale = pmc_ratio(pmc_key, sym)
             traffic = None if ratio is None else round(float(busiest[1]) * ratio)
         else:
-            stale = f"no PMC entry for the {world}-rank {args.dtype} trees"
+            stale = why or f"no PMC entry for the {world}-rank {args.dtype} reductions"
         roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                    "kernel": "chr::k_reduce_tree / k_reduce_vec (fused reductions inside the collective, busiest rank)",
+                    "kernel": (sym or "chr::k_reduce_tree / k_reduce_vec") + " (fused reductions inside the collective, "
+                                                                          "busiest rank)",
                     "algorithmic_bytes_per_call": float(busiest[1]), "launches_per_call": int(busiest[2]),
                     "kernel_ms_per_call": round(float(busiest[0]), 4),
                     # one GPU's own grids (one rank per GPU): the fixed per-grid cost shows directly

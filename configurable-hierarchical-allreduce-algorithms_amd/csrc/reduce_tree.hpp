@@ -227,7 +227,7 @@ struct ScalarOp {
 // the first combine (NL * U <= 16 loads of 16 B in flight per lane).  One trip per workgroup;
 // within its segment a workgroup's trip is placed by xcd_trip (the segment's first block may sit
 // anywhere in the 8-XCD rotation: blocks of one local residue class still share one XCD).
-// ACC0 (streaming 2-leaf trees): leaf 0's first vector keeps the default policy, as the bucket kernel's ACC0 slot.
+// ACC0 (streaming trees): leaf 0's first vector keeps the default policy, as the bucket kernel's ACC0 slot.
 template <int DT, int OP, int NL, int U, bool NT, int BL, bool ACC0 = false>
 __global__ __launch_bounds__(BL) void k_reduce_tree(TreeArgs a) {
     // this workgroup's segment: one pass over the block0 table (scalar compares, no loop-carried
@@ -418,7 +418,7 @@ inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
     }
     if (grid == 0) return hipSuccess;
     const unsigned lds = NT ? nt_lds_bytes(reduce_tuning().wg_per_cu_tree, tree_wg_per_cu<NL>()) : 0;
-    if constexpr (NL == 2 && NT && !is_pair_dt<DT>() && !is_complex_dt<DT>()) {
+    if constexpr (NT && !is_pair_dt<DT>() && !is_complex_dt<DT>()) {
         if (reduce_tuning().tree_acc0 > 0) {
             hipLaunchKernelGGL((k_reduce_tree<DT, OP, NL, U, NT, BL, true>), dim3((unsigned)grid), dim3(BL), lds, s, a);
             return hipGetLastError();

@@ -104,8 +104,11 @@ int chr_reduce_multi(void* out, const void* acc, const void* const* ins, int m, 
  * operand of every step, acc = acc (op) ins[j], i.e. MPI_Reduce_local(acc, ins[j]) chained
  * the way MPICH_do_reduce does it
  * (testing/mpich_implementations/all_reduce/allreduce_recexch.cpp:147-186).  Only the floating
- * types can differ bitwise from the default order: MAX/MIN on ties of -0/+0 and NaN compares,
- * SUM/PROD on which NaN survives when two meet (inout's, as MPICH's loop keeps it). */
+ * types (and the floating-valued pairs and the complex types) can differ bitwise from the default
+ * order: MAX/MIN(LOC) on ties of -0/+0 and NaN compares, SUM/PROD on which NaN survives when two
+ * meet -- MPICH's rules on x86, pinned by its own outputs (tests/golden/nan_reduce_local.npz):
+ * inout's for float / double / bf16, in's in each part of a complex SUM, libgcc __mulsc3's operand
+ * order for a complex PROD. */
 #define CHR_REDUCE_RUNNING_FIRST 1
 int chr_reduce_multi_ex(void* out, const void* acc, const void* const* ins, int m, size_t n,
                         chr_dtype dtype, chr_op op, int flags, hipStream_t stream);

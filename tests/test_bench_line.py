@@ -210,3 +210,18 @@ def test_committed_round5_lines_meet_the_definitions():
         checked += 1
     if not files:
         pytest.skip("no round-5 bench lines committed yet")
+
+
+@pytest.mark.parametrize("n, k, b, want", [(2, 2, 2, "reduce_f32_sum_m1_oop_128MiB"), (4, 4, 4, "reduce_f32_sum_m3_oop_64MiB"),
+                                           (8, 4, 4, "tree_f32_sum_8leaves_64MiB")])
+@pytest.mark.parametrize("slices", [1, 4, 8])
+def test_roofline_binds_the_kernel_the_plan_launches(n, k, b, want, slices):
+    """The N>1 line's roofline.traffic comes from the PMC entry of the kernel the metric's plan launches: the N = 2 / N = 4
+    lines' one-node geometries compile each piece's expression to ONE fold (k_reduce_vec out of place), C4's to 8-leaf
+    trees -- read off the plan (chr_plan_describe, host only), not assumed from N."""
+    import chiara_amd as ca
+
+    plan = ca.parse_plan(ca.describe_plan(ca.MODE_ALLREDUCE, n, 0, k, b, 1 << 28, slices, ca.SCHEDULE_FLAT))
+    (key, sym), why = bench.reduction_pmc(plan)
+    assert why is None and key == want
+    assert ("k_reduce_tree<0, 0, 8," in sym) == (n == 8)

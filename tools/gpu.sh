@@ -15,7 +15,8 @@
 #   kernels    bench.py --collective-kernels (C4/C5 in-collective kernel rows) -> collective_kernels.json
 #   ranktrees  bench.py --rank-trees, plain and under rocprofv3 --kernel-trace -> rank_trees.json, rank_trees_prof/
 #   treepmc    rocprofv3 stats + FETCH_SIZE / WRITE_SIZE passes of the tree kernel alone (tools/tree_pmc.py)
-#   treepmc42  the same for the 4- and 2-leaf trees of the N = 4 / N = 2 lines
+#   treepmc42  the same for the 4- and 2-leaf trees (the tree API)
+#   vecpmc     the same for the N = 2 / N = 4 lines' out-of-place folds (k_reduce_vec m = 1 at 128 MiB, m = 3 at 64 MiB)
 #   e2e        bench.py --e2e: host-buffer (PCIe-inclusive) cost of the reference's contract -> e2e.json
 #   sweep      bench.py --sweep: 1 KiB .. 1 GiB buckets, m = 1/3/7, fp32 + bf16 (table in sweep.json.err)
 #   probe      tools/mstream_probe.py $PROBE_ARGS               -> mstream_probe.jsonl
@@ -71,7 +72,17 @@ for step in "$@"; do
       run 300 "tree_pmc_$ctr.txt" rocprofv3 --pmc $ctr --output-format csv -d "$PWD/$OUT/tree_pmc_$ctr" -o run \
         -- python3 tools/tree_pmc.py 40
     done ;;
-  treepmc42)  # the N = 4 / N = 2 lines' 4- and 2-leaf trees the same way -> tree{4,2}_prof/, tree{4,2}_pmc_*/
+  vecpmc)  # the N = 2 / N = 4 lines' out-of-place folds -> vec{1,3}_prof/, vec{1,3}_pmc_*/
+    for vm in 1 3; do
+      vmib=$([ $vm = 1 ] && echo 128 || echo 64)
+      run 300 "vec${vm}_prof.txt" rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/vec${vm}_prof" \
+        -o run -- python3 tools/tree_pmc.py 40 --vec $vm --mib $vmib
+      for ctr in FETCH_SIZE WRITE_SIZE; do
+        run 300 "vec${vm}_pmc_$ctr.txt" rocprofv3 --pmc $ctr --output-format csv -d "$PWD/$OUT/vec${vm}_pmc_$ctr" \
+          -o run -- python3 tools/tree_pmc.py 40 --vec $vm --mib $vmib
+      done
+    done ;;
+  treepmc42)  # the 4- and 2-leaf trees the same way -> tree{4,2}_prof/, tree{4,2}_pmc_*/
     for nl in 4 2; do
       run 300 "tree${nl}_prof.txt" rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/tree${nl}_prof" \
         -o run -- python3 tools/tree_pmc.py 40 --leaves $nl

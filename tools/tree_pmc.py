@@ -1,10 +1,12 @@
 #!/usr/bin/env python3
 """Launches only the fused tree kernel at C4's shape (f32, 8 leaves, 64 MiB pieces, 8 rotating
 leaf sets = 4.5 GiB, HBM-cold) for rocprofv3 --pmc passes: HBM bytes per launch vs the
-algorithmic 9 x 64 MiB (tools/pmc_summary.py ... k_reduce_tree).  `--leaves 4|2`: the N = 4 / N = 2
-lines' trees instead ((L + 1) x 64 MiB).
+algorithmic 9 x 64 MiB (tools/pmc_summary.py ... k_reduce_tree).  `--leaves 4|2`: the 4- / 2-leaf trees
+instead ((L + 1) x 64 MiB).  `--vec M --mib P`: the N = 2 / N = 4 lines' reductions instead -- one fold of M
+incoming pieces of P MiB into a separate output (chr_reduce_multi(out, acc, ins), k_reduce_vec out of place,
+(M + 2) x P MiB), over rotating sets of at least 4.5 GiB.
 
-    python3 tools/tree_pmc.py [launches] [--leaves L]"""
+    python3 tools/tree_pmc.py [launches] [--leaves L | --vec M --mib P]"""
 import argparse
 import os
 import sys
@@ -23,7 +25,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("launches", type=int, nargs="?", default=40)
     ap.add_argument("--leaves", type=int, default=8, choices=sorted(COMBS))
+    ap.add_argument("--vec", type=int, default=0)
+    ap.add_argument("--mib", type=int, default=64)
     a = ap.parse_args()
+    if a.vec:
+        return vec_oop(a)
     nl, comb = a.leaves, COMBS[a.leaves]
     dev = torch.device("cuda:0")
     s = torch.cuda.current_stream(dev)
@@ -39,6 +45,23 @@ def main():
         ca.check(ca.reduce_tree(o, lv, comb, [0] * (nl - 1), n, ca.FLOAT32, ca.SUM, s))
     torch.cuda.synchronize()
     print("tree launches done")
+
+
+def vec_oop(a):
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream(dev)
+    m, n = a.vec, (a.mib << 20) // 4
+    sets = []
+    for si in range(max(2, (9 * 64) // ((m + 2) * a.mib))):  # >= 4.5 GiB of distinct operands per rotation
+        bufs = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(m + 2)]
+        for j, t in enumerate(bufs):
+            ca.check(ca.fill(t, n, ca.FLOAT32, 0, 3, 16 * si + j, stream=s))
+        sets.append(bufs)
+    for i in range(a.launches):
+        b = sets[i % len(sets)]
+        ca.check(ca.reduce_multi(b[m + 1], b[0], b[1:m + 1], n, ca.FLOAT32, ca.SUM, s))
+    torch.cuda.synchronize()
+    print("reduce launches done")
 
 
 if __name__ == "__main__":
