@@ -275,15 +275,15 @@ def line_problems(line, rccl_library=True):
 C2_KERNEL_SYMBOL = "void chr::k_reduce_vec<0, 0, 1, 4, true, true, 64>(chr::VecArgs)"
 
 
-TREE8_KERNEL_SYMBOL = "void chr::k_reduce_tree<0, 0, 8, 1, true, 64>(chr::TreeArgs)"
+TREE8_KERNEL_SYMBOL = "void chr::k_reduce_tree<0, 0, 8, 1, true, 64, true>(chr::TreeArgs)"
 # The kernel a flat plan's reductions run on, by the plan's own ops (reduction_pmc): a tree of L leaves -> its PMC entry
 # (tools/tree_pmc.py --leaves L) and the streaming instantiation a 1 GiB call launches (reduce_tree.hpp tree_u: U = 1 /
-# 2 / 4); a single fold of m incoming pieces -- what the N = 2 and N = 4 lines' one-node geometries compile to
+# 2 / 4; the last argument: the ACC0 slot, round 6); a single fold of m incoming pieces -- what the N = 2 and N = 4 lines' one-node geometries compile to
 # (schedule.cpp tree_program) -- -> the bucket kernel out of place (tools/tree_pmc.py --vec m).  Round 5 bound the N = 2
 # / N = 4 lines to the 2- / 4-leaf tree entries, kernels those lines never launch.
 TREE_PMC = {8: ("tree_f32_sum_8leaves_64MiB", TREE8_KERNEL_SYMBOL),
-            4: ("tree_f32_sum_4leaves_64MiB", "void chr::k_reduce_tree<0, 0, 4, 2, true, 64>(chr::TreeArgs)"),
-            2: ("tree_f32_sum_2leaves_64MiB", "void chr::k_reduce_tree<0, 0, 2, 4, true, 64>(chr::TreeArgs)")}
+            4: ("tree_f32_sum_4leaves_64MiB", "void chr::k_reduce_tree<0, 0, 4, 2, true, 64, true>(chr::TreeArgs)"),
+            2: ("tree_f32_sum_2leaves_64MiB", "void chr::k_reduce_tree<0, 0, 2, 4, true, 64, true>(chr::TreeArgs)")}
 VEC_OOP_PMC = {1: ("reduce_f32_sum_m1_oop_128MiB", "void chr::k_reduce_vec<0, 0, 1, 4, true, true, 64>(chr::VecArgs)"),
                3: ("reduce_f32_sum_m3_oop_64MiB", "void chr::k_reduce_vec<0, 0, 3, 2, true, true, 64>(chr::VecArgs)")}
 

@@ -66,7 +66,6 @@ struct ReduceTuning {
     int wg_per_cu_vec;   // -1: policy
     int wg_per_cu_tree;  // -1: policy
     int xcd_hand_shift;  // -1: policy (xcd_hand in reduce_common.hpp); 0: off
-    int tree_acc0;       // CHR_TREE_ACC0: -1 policy; 0 / 1 streaming trees load leaf 0's first vector temporal
     unsigned lds_per_cu; // bytes of LDS per CU (device attribute; 160 KiB on gfx950)
     unsigned lds_per_block;  // bytes of LDS one workgroup may allocate (device attribute)
 };

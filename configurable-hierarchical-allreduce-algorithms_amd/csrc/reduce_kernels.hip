@@ -150,8 +150,6 @@ ReduceTuning& reduce_tuning() {
         r.wg_per_cu_tree = s ? std::max(0, std::atoi(s)) : -1;
         s = std::getenv("CHR_XCD_HAND_SHIFT");
         r.xcd_hand_shift = s ? std::min(31, std::max(0, std::atoi(s))) : -1;  // [0, 31]; 31 hands nothing
-        s = std::getenv("CHR_TREE_ACC0");
-        r.tree_acc0 = s ? (std::atoi(s) != 0) : -1;
         int dev = 0, lds = 0, blk = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess ||

@@ -227,7 +227,14 @@ struct ScalarOp {
 // the first combine (NL * U <= 16 loads of 16 B in flight per lane).  One trip per workgroup;
 // within its segment a workgroup's trip is placed by xcd_trip (the segment's first block may sit
 // anywhere in the 8-XCD rotation: blocks of one local residue class still share one XCD).
-// ACC0 (streaming trees): leaf 0's first vector keeps the default policy, as the bucket kernel's ACC0 slot.
+// ACC0 (streaming trees, round 6): leaf 0's first vector keeps the default policy, as the bucket kernel's ACC0 slot
+// (reduce_vec.hpp).  One GPU's own C4 / C5 grids at the in-collective cap, rocprof kernel duration per grid, off -> on
+// (bench.py --rank-trees, profiles/r06/acc0_ab/, 2 alternating rounds): C4 4 slices 0.779-0.792 -> 0.828-0.833,
+// 8 slices 0.735-0.738 -> 0.790, 8 slices after the receive copies 0.687-0.692 -> 0.732-0.735; C5 4 slices 0.769 ->
+// 0.812-0.814, 8 slices 0.737-0.766 -> 0.794-0.797, after copies 0.675-0.679 -> 0.732-0.739; 4 slices after the
+// copies tie.  The C4 tree alone over a 4.5 GiB rotation (tools/tree_pmc.py, past the translation cliff) loses 2 %
+// (0.779-0.791 -> 0.766-0.773), as the 2-leaf tree does over 3.9 GiB (tools/leaf2_ab.py: -2.5 %; +3.5-4 % at 1.9
+// GiB).  A rank's call holds ~3 GiB (send, recv, STAGE), the rows that gain.
 template <int DT, int OP, int NL, int U, bool NT, int BL, bool ACC0 = false>
 __global__ __launch_bounds__(BL) void k_reduce_tree(TreeArgs a) {
     // this workgroup's segment: one pass over the block0 table (scalar compares, no loop-carried
@@ -418,13 +425,8 @@ inline hipError_t launch_tree_vec(const TreeArgs& a_in, hipStream_t s) {
     }
     if (grid == 0) return hipSuccess;
     const unsigned lds = NT ? nt_lds_bytes(reduce_tuning().wg_per_cu_tree, tree_wg_per_cu<NL>()) : 0;
-    if constexpr (NT && !is_pair_dt<DT>() && !is_complex_dt<DT>()) {
-        if (reduce_tuning().tree_acc0 > 0) {
-            hipLaunchKernelGGL((k_reduce_tree<DT, OP, NL, U, NT, BL, true>), dim3((unsigned)grid), dim3(BL), lds, s, a);
-            return hipGetLastError();
-        }
-    }
-    hipLaunchKernelGGL((k_reduce_tree<DT, OP, NL, U, NT, BL>), dim3((unsigned)grid), dim3(BL), lds, s, a);
+    constexpr bool ACC0 = NT && !is_pair_dt<DT>() && !is_complex_dt<DT>();  // the ACC0 slot (k_reduce_tree)
+    hipLaunchKernelGGL((k_reduce_tree<DT, OP, NL, U, NT, BL, ACC0>), dim3((unsigned)grid), dim3(BL), lds, s, a);
     return hipGetLastError();
 }
 

@@ -58,12 +58,16 @@ def test_bench_reads_through_provenance(tmp_path):
     assert traffic is None and why
 
 
-def test_every_n_line_has_its_tree_entry():
-    """The N = 8 / 4 / 2 lines each read the PMC entry of the flat schedule's tree at that width (bench.TREE_PMC):
-    the key has sources registered, and the symbol is the streaming instantiation reduce_tree.hpp's tree_u ships
-    (U = 1 / 2 / 4).  Whether the committed figures are current is the bench line's own `traffic_stale`."""
+def test_every_reduction_shape_has_its_entry():
+    """Every PMC entry a bench line can bind (bench.TREE_PMC, bench.VEC_OOP_PMC; chosen off the plan by
+    bench.reduction_pmc) has sources registered, and names the streaming instantiation the library ships: trees at
+    reduce_tree.hpp's tree_u (U = 1 / 2 / 4) with the ACC0 slot, folds at reduce_vec.hpp's vec_u_nt (U = 4 / 2) with
+    theirs.  Whether the committed figures are current is the bench line's own `traffic_stale`."""
     import bench
 
-    for world, (key, sym) in bench.TREE_PMC.items():
+    for nl, (key, sym) in bench.TREE_PMC.items():
         assert key in pp.KERNEL_SOURCES
-        assert f"k_reduce_tree<0, 0, {world}, {dict([(8, 1), (4, 2), (2, 4)])[world]}, true, 64>" in sym
+        assert f"k_reduce_tree<0, 0, {nl}, {dict([(8, 1), (4, 2), (2, 4)])[nl]}, true, 64, true>" in sym
+    for m, (key, sym) in bench.VEC_OOP_PMC.items():
+        assert key in pp.KERNEL_SOURCES
+        assert f"k_reduce_vec<0, 0, {m}, {dict([(1, 4), (3, 2)])[m]}, true, true, 64>" in sym
