@@ -52,7 +52,7 @@ def vec_oop(a):
     s = torch.cuda.current_stream(dev)
     m, n = a.vec, (a.mib << 20) // 4
     sets = []
-    for si in range(max(2, (9 * 64) // ((m + 2) * a.mib))):  # >= 4.5 GiB of distinct operands per rotation
+    for si in range(max(2, -(-(9 * 8 * 64) // ((m + 2) * a.mib)))):  # >= 4.5 GiB of distinct operands per rotation
         bufs = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(m + 2)]
         for j, t in enumerate(bufs):
             ca.check(ca.fill(t, n, ca.FLOAT32, 0, 3, 16 * si + j, stream=s))
