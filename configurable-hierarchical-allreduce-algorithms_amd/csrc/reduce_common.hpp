@@ -140,10 +140,11 @@ constexpr int kMaxLocSw = 18, kMinLocSw = 19;
 
 // x86 SSE arithmetic with its NaN rules written out, for the complex types (the oracle's orc_x86f / orc_x86d):
 // two NaNs -> the FIRST operand's, quieted; one NaN -> that NaN, quieted (sign and payload kept); an invalid
-// operation on numbers (inf - inf, 0 * inf) -> x86's default NaN, sign set.  gfx950 also keeps the first
-// source's NaN, but its invalid operations give the positive canonical NaN, so the rules are spelled out as selects
-// rather than left to the instruction.  The complex kernels are not on a BASELINE path; the f32 / f64 / bf16
-// reductions keep their one-instruction combines (add_keep / mul_keep).
+// operation on numbers (inf - inf, 0 * inf) -> x86's default NaN, sign set.  gfx950's v_add / v_mul follow the same
+// three rules (tools/nan_invalid_probe.hip, profiles/r06/nan/nan_invalid.txt), but its v_sub_f32 flips the sign of a
+// NaN second operand, and the compiler picks add operand orders freely, so the complex kernels spell the rules out as
+// selects.  They are not on a BASELINE path; the f32 / f64 / bf16 reductions keep their one-instruction combines
+// (add_keep / mul_keep), whose operand order is pinned and which never subtract.
 enum { kXAdd, kXSub, kXMul };
 __device__ __forceinline__ float quiet_nan(float v) { return __uint_as_float(__float_as_uint(v) | 0x00400000u); }
 __device__ __forceinline__ double quiet_nan(double v) {
@@ -209,7 +210,8 @@ __device__ __forceinline__ void cmul(F a, F b, F c, F d, F* re, F* im) {
 
 // MPI_Reduce_local(in = x, inout = y): MPICH 3.3.2's loop is inout = OP(inout, in) with
 // MAX(p, q) = p > q ? p : q (MPIR_OP_TYPE_REDUCE_CASE, a = inoutvec, b = invec), so MAX/MIN
-// keep the accumulator on ties and NaN compares.  kMaxSw/kMinSw: the running value is the
+// take `in` on ties (-0 / +0) and whenever a NaN makes the compare false (MAXLOC / MINLOC, whose loop
+// replaces inout only by a strictly better in, keep inout there).  kMaxSw/kMinSw: the running value is the
 // `in` operand and the result takes the place of the incoming buffer: OP(x, y).
 template <int DT, int OP>
 __device__ __forceinline__ typename DTy<DT>::T apply(typename DTy<DT>::T x, typename DTy<DT>::T y) {

@@ -138,7 +138,8 @@ template <> struct StaticProgs<8> {
         tree_prog({0, 1, 1, 1, 0, 2, 1, 1}, 8),  // b = 8, k = 4
         tree_prog({0, 1, 1, 1, 1, 1, 1, 1}, 8)}; // b = 8, k >= 5: a left fold
 };
-template <> struct StaticProgs<2> {  // the 2-rank schedules (C3, the N = 2 line)
+template <> struct StaticProgs<2> {  // the tree API's 2-leaf program: no flat plan emits one (a 2-operand
+                                     // expression is one fold, k_reduce_vec; C3 and the N = 2 line fold)
     static constexpr int n = 1;
     static constexpr uint32_t v[1] = {tree_prog({0, 1, 0, 0, 0, 0, 0, 0}, 2)};
 };
@@ -347,7 +348,7 @@ constexpr int kTreeXcdHandShift = 6;
 // Two leaves move the m = 1 bucket's traffic (2 reads + 1 write) and kept the identity until focus18's
 // microbench lead for 256 KiB runs under a cap was product-verified:
 // Round 5, the product A/B focus18 asked for (tools/gpu_small_tree_ab.sh, profiles/r05/small_tree_ab/, 2
-// alternating rounds, HBM-cold, f32): the 2- and 4-leaf trees of the N = 2 / N = 4 lines take 256 KiB runs and 12
+// alternating rounds, HBM-cold, f32): the 2- and 4-leaf trees (4-rank flat plans with k < b; the tree API) take 256 KiB runs and 12
 // per CU (tree_wg_per_cu) -- alone 0.745-0.747 -> 0.765-0.766 (2 leaves, 64 MiB pieces), 0.677-0.690 -> 0.707 (two
 // trees of 16 MiB), 0.778-0.784 -> 0.791-0.800 (4 leaves, 64 MiB), 0.744-0.745 -> 0.750-0.757 (2 x 16 MiB); at
 // the in-collective cap 12 the runs add 0-1.4 %.
@@ -366,7 +367,7 @@ constexpr size_t tree_xcd_run_kib() {
 // (profiles/r02/occupancy_cap/); U = 1 with 16 per CU measured 0.751-0.763 against U = 2
 // uncapped's 0.739-0.750 on the C4 slice (2 x 8 leaves x 16 MiB, 4.5 and 1.1 GiB rotations, 2
 // rounds: microbench_focus17_tree_u_cap.txt), so trees of 5+ leaves take that shape.  The small
-// trees of the N = 2 / N = 4 flat schedules (focus18, microbench_focus18_small_trees.txt, 2 rounds,
+// trees of 2 and 4 leaves (focus18, microbench_focus18_small_trees.txt, 2 rounds,
 // 6 HBM-cold sets) showed 2 leaves at 128 MiB U = 4 uncapped 0.774-0.783 -> 0.801-0.804 with 12 per
 // CU and 256 KiB runs, and 4 leaves at 64 MiB 0.741-0.750 -> 0.774-0.781 at U = 2 with 12 per CU,
 // but the microbench over-predicted the 8-leaf change below, so trees of <= 4 leaves kept the round-1
@@ -383,8 +384,8 @@ constexpr size_t tree_xcd_run_kib() {
 // three tree waves on a SIMD leave less than the ~288 VGPRs rcclGenericKernel's waves need: an RCCL-sized kernel
 // was admitted only when the tree launch drained (median 170 us against 4 us) and the real RCCL kernel beside the
 // C4 slice took 164-165 us against 114-120 us (tools/gpu_cores_u.sh, profiles/r05/cores_u/).  U = 1 stays.
-// The same budget (<= 72 VGPRs, tests/test_kernel_resources.py) moved the streaming 3- and 4-leaf trees of the N = 4
-// flat schedule from U = 4 (104 f32 / 112 bf16 VGPRs) to U = 2 (62 / 65): beside 4-leaf f32 trees of 64 MiB
+// The same budget (<= 72 VGPRs, tests/test_kernel_resources.py) moved the streaming 3- and 4-leaf trees of 4-rank
+// flat plans with k < b from U = 4 (104 f32 / 112 bf16 VGPRs) to U = 2 (62 / 65): beside 4-leaf f32 trees of 64 MiB
 // pieces at cap 12 an RCCL-sized kernel's median workgroup was admitted after 5.5 / 17.6 us instead of ~90 us
 // (the launch drained first), the real RCCL kernel took 122-123 us instead of 129-133, and the trees ran faster
 // too, 0.770 / 0.780 vs 0.761 / 0.741 at cap 12 and 0.759 vs 0.746 at the stand-alone policy

@@ -224,7 +224,8 @@ void orc_fill(void* buf, size_t n, int dtype, int pattern, uint64_t seed, int ra
 /* MPICH 3.3.2 predefined ops (src/mpi/coll/op/opsum.c, opmax.c, ... via
  * MPIR_OP_TYPE_REDUCE_CASE): with a = inoutvec and b = invec the loop is
  * `a[i] = OP(a[i], b[i])`, OP(p, q) = p + q, p * q, (p > q ? p : q), (p < q ? p : q).  So
- * MAX/MIN keep the inout value on ties (-0/+0) and whenever a NaN makes the compare false.
+ * MAX/MIN take the in value on ties (-0/+0) and whenever a NaN makes the compare false (pinned by the
+ * ties goldens; MAXLOC / MINLOC below keep inout there).
  * Below: x = in[i], y = inout[i], result = OP(y, x). */
 #define ORC_LOOP(T, EXPR)                                     \
     do {                                                      \
