@@ -41,7 +41,7 @@ LAND, LOR, LXOR, BAND, BOR, BXOR = 4, 5, 6, 7, 8, 9
 MAXLOC, MINLOC = 10, 11
 SUCCESS = 0
 ERR_INVALID_ARG, ERR_COUNT_NOT_DIVISIBLE, ERR_BATCH_NOT_DIVISOR = 1, 2, 3
-ERR_RCCL, ERR_TIMEOUT, ERR_ABORTED = 5, 9, 10
+ERR_RCCL, ERR_UNSUPPORTED, ERR_TIMEOUT, ERR_ABORTED = 5, 8, 9, 10
 IN_PLACE = object()  # MPI_IN_PLACE analogue
 _IN_PLACE_PTR = 1     # CHR_IN_PLACE
 
@@ -110,6 +110,21 @@ def reduce_multi(out, acc, ins, count, datatype, op, stream=None):
     """Fused left-to-right reduction of len(ins) incoming buckets into acc (written to out)."""
     arr = (ctypes.c_void_p * max(1, len(ins)))(*[_addr(x) for x in ins])
     return lib().chr_reduce_multi(_addr(out), _addr(acc), arr, len(ins), count, datatype, op, _stream(stream))
+
+
+def op_create(launcher, commute=False, ctx=None):
+    """A user-defined op (chr_op_create, MPI_Op_create's analogue): `launcher` is the address of a chr_user_reduce_fn
+    -- the caller's own device code, e.g. built with include/chiara_user_op.hpp -- as an int or a ctypes function.
+    Returns the op code for every chr_reduce_* call and CHiArA's collectives."""
+    addr = ctypes.cast(launcher, ctypes.c_void_p).value if not isinstance(launcher, int) else launcher
+    op = ctypes.c_int(0)
+    check(lib().chr_op_create(addr, ctx, int(bool(commute)), ctypes.byref(op)), "chr_op_create")
+    return op.value
+
+
+def op_free(op):
+    """Release a user-defined op (chr_op_free); its code may be handed out again."""
+    return lib().chr_op_free(op)
 
 
 def fill(buf, count, datatype, pattern, seed, rank, count_for_seq=None, stream=None):

@@ -8,6 +8,7 @@
 
 #include "chr_internal.hpp"
 #include "schedule.hpp"
+#include "user_ops.hpp"
 
 // The library leaves the process environment alone.  Multi-process GPU work on this driver needs
 // dmabuf IPC (HSA_ENABLE_IPC_MODE_LEGACY=0); the entry paths that start ranks set that default
@@ -42,49 +43,49 @@ static int status(hipError_t e) {
 }
 
 int chr_reduce_local(const void* in, void* inout, size_t n, chr_dtype dtype, chr_op op, hipStream_t stream) {
-    if (!chr::valid_dtype_op(dtype, op)) return CHR_ERR_INVALID_ARG;
+    if (!chr::valid_any(dtype, op)) return CHR_ERR_INVALID_ARG;
     if (n == 0) return CHR_SUCCESS;
     if (!in || !inout) return CHR_ERR_INVALID_ARG;
     const void* ins[1] = {in};
-    return status(chr::launch_reduce(inout, inout, ins, 1, n, dtype, op, stream));
+    return chr::reduce_any(inout, inout, ins, 1, n, dtype, op, stream);
 }
 
 int chr_reduce_multi(void* out, const void* acc, const void* const* ins, int m, size_t n, chr_dtype dtype, chr_op op,
                      hipStream_t stream) {
-    if (!chr::valid_dtype_op(dtype, op) || m < 0) return CHR_ERR_INVALID_ARG;
+    if (!chr::valid_any(dtype, op) || m < 0) return CHR_ERR_INVALID_ARG;
     if (n == 0) return CHR_SUCCESS;
     if (!out || !acc || (m > 0 && !ins)) return CHR_ERR_INVALID_ARG;
     for (int j = 0; j < m; ++j)
         if (!ins[j]) return CHR_ERR_INVALID_ARG;
-    return status(chr::launch_reduce(out, acc, ins, m, n, dtype, op, stream));
+    return chr::reduce_any(out, acc, ins, m, n, dtype, op, stream);
 }
 
 int chr_reduce_multi_ex(void* out, const void* acc, const void* const* ins, int m, size_t n, chr_dtype dtype,
                         chr_op op, int flags, hipStream_t stream) {
-    if (!chr::valid_dtype_op(dtype, op) || m < 0 || (flags & ~CHR_REDUCE_RUNNING_FIRST)) return CHR_ERR_INVALID_ARG;
+    if (!chr::valid_any(dtype, op) || m < 0 || (flags & ~CHR_REDUCE_RUNNING_FIRST)) return CHR_ERR_INVALID_ARG;
     if (n == 0) return CHR_SUCCESS;
     if (!out || !acc || (m > 0 && !ins)) return CHR_ERR_INVALID_ARG;
     for (int j = 0; j < m; ++j)
         if (!ins[j]) return CHR_ERR_INVALID_ARG;
-    return status(chr::launch_reduce(out, acc, ins, m, n, dtype, op, stream, (flags & CHR_REDUCE_RUNNING_FIRST) != 0));
+    return chr::reduce_any(out, acc, ins, m, n, dtype, op, stream, (flags & CHR_REDUCE_RUNNING_FIRST) != 0);
 }
 
 int chr_reduce_tree(void* out, const void* const* leaves, int nleaves, const unsigned char* comb,
                     const unsigned char* swaps, size_t n, chr_dtype dtype, chr_op op, hipStream_t stream) {
-    if (!chr::valid_dtype_op(dtype, op) || nleaves < 1 || !comb || !leaves) return CHR_ERR_INVALID_ARG;
+    if (!chr::valid_any(dtype, op) || nleaves < 1 || !comb || !leaves) return CHR_ERR_INVALID_ARG;
     uint32_t cb = 0, sb = 0;
     if (!chr::tree_program_ok(nleaves, comb, swaps, &cb, &sb)) return CHR_ERR_UNSUPPORTED;
     if (n == 0) return CHR_SUCCESS;
     if (!out) return CHR_ERR_INVALID_ARG;
     for (int j = 0; j < nleaves; ++j)
         if (!leaves[j]) return CHR_ERR_INVALID_ARG;
-    return status(chr::launch_reduce_tree(out, leaves, nleaves, comb, swaps, n, dtype, op, stream));
+    return chr::reduce_tree_any(out, leaves, nleaves, comb, swaps, n, dtype, op, stream);
 }
 
 int chr_reduce_tree_batch(void* const* outs, const void* const* leaves, int ntrees, int nleaves,
                           const unsigned char* comb, const unsigned char* swaps, size_t n, chr_dtype dtype, chr_op op,
                           hipStream_t stream) {
-    if (!chr::valid_dtype_op(dtype, op) || ntrees < 0 || nleaves < 1 || nleaves > 8) return CHR_ERR_INVALID_ARG;
+    if (!chr::valid_any(dtype, op) || ntrees < 0 || nleaves < 1 || nleaves > 8) return CHR_ERR_INVALID_ARG;
     if (ntrees > 0 && (!outs || !leaves || !comb)) return CHR_ERR_INVALID_ARG;
     std::vector<chr::TreeJob> jobs((size_t)ntrees);
     for (int t = 0; t < ntrees; ++t) {
@@ -104,7 +105,7 @@ int chr_reduce_tree_batch(void* const* outs, const void* const* leaves, int ntre
         }
     }
     if (n == 0 || ntrees == 0) return CHR_SUCCESS;
-    return status(chr::launch_reduce_tree_multi(jobs.data(), ntrees, dtype, op, stream));
+    return chr::reduce_tree_multi_any(jobs.data(), ntrees, dtype, op, stream);
 }
 
 int chr_fill(void* buf, size_t n, chr_dtype dtype, int pattern, uint64_t seed, int rank, uint64_t count_for_seq,

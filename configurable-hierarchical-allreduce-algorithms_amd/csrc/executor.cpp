@@ -31,6 +31,7 @@
 
 #include "chr_internal.hpp"
 #include "schedule.hpp"
+#include "user_ops.hpp"
 
 namespace {
 
@@ -164,10 +165,10 @@ int run_local(const chr::LocalOp& op, const Bufs& B, int dtype, int rop, hipStre
         (void)hipEventRecord(ev.first, s);
     }
     const int rc =
-        tree ? hip_code(chr::launch_reduce_tree(B.ptr(op.dst), ins.data(), (int)ins.size(), op.comb.data(),
-                                                op.swaps.empty() ? nullptr : op.swaps.data(), op.count, dtype, rop, s))
-             : hip_code(chr::launch_reduce(B.ptr(op.dst), B.ptr(op.acc), ins.data(), (int)ins.size(), op.count, dtype,
-                                           rop, s, op.swap));
+        tree ? chr::reduce_tree_any(B.ptr(op.dst), ins.data(), (int)ins.size(), op.comb.data(),
+                                    op.swaps.empty() ? nullptr : op.swaps.data(), op.count, dtype, rop, s)
+             : chr::reduce_any(B.ptr(op.dst), B.ptr(op.acc), ins.data(), (int)ins.size(), op.count, dtype, rop, s,
+                               op.swap);
     if (timed) {
         (void)hipEventRecord(ev.second, s);
         prof->pending.push_back(ev);
@@ -238,7 +239,7 @@ int launch_tree_jobs(const std::vector<chr::TreeJob>& jobs, double bytes, int dt
         ev = prof->take();
         (void)hipEventRecord(ev.first, s);
     }
-    const int rc = hip_code(chr::launch_reduce_tree_multi(jobs.data(), (int)jobs.size(), dtype, rop, s));
+    const int rc = chr::reduce_tree_multi_any(jobs.data(), (int)jobs.size(), dtype, rop, s);
     if (timed) {
         (void)hipEventRecord(ev.second, s);
         prof->pending.push_back(ev);
@@ -928,8 +929,13 @@ int run_host_windows(chr_comm* c, int sched, int slices, int mode, const void* i
 // intra scatter) move elements of any type and ignore op.
 bool valid_args(int mode, int dtype, int op) {
     if (mode == chr::MODE_ALLGATHER || mode == chr::MODE_INTRA_SCATTER) return chr::dtype_size(dtype) != 0;
-    return chr::valid_dtype_op(dtype, op);
+    return chr::valid_any(dtype, op);
 }
+
+// The MPICH baselines branch on MPI_Op_commutative (allreduce_recursive_doubling.cpp:69,
+// allreduce_recursive_multiplying.cpp:46, allreduce_k_reduce_scatter_allgather.cpp:279), which the plans do not model:
+// they take no user op.  CHiArA's own collectives have no such branch and take any op.
+bool user_op_unsupported(int mode, int op) { return chr::is_user_op(op) && chr::is_mpich(mode); }
 
 int run_collective(chr_comm* c, int sched, int slices, int mode, const void* send, void* recv, size_t count, int dtype,
                    int op, int k, int b, bool sync) {
@@ -963,8 +969,9 @@ int run_collective(chr_comm* c, int sched, int slices, int mode, const void* sen
             return rc;
     }
     if (dev_in && dev_out) {
-        int rc = c->graphs && !c->prof.on ? launch_graph(c, p, input, recv, dtype, op)
-                                          : enqueue_rccl(c, p, input, recv, dtype, op);
+        // a user op's launcher may allocate stream-ordered scratch: never captured (chiara.h chr_op_create)
+        int rc = c->graphs && !c->prof.on && !chr::is_user_op(op) ? launch_graph(c, p, input, recv, dtype, op)
+                                                                  : enqueue_rccl(c, p, input, recv, dtype, op);
         if (rc || !sync) return rc;
         return wait_call(c);
     }
@@ -1120,6 +1127,7 @@ int collective(chr_comm* c, int mode, const void* send, void* recv, size_t count
                bool sync) {
     // allgather moves elements of any type (its op is unused)
     if (!c || !valid_args(mode, dtype, op)) return CHR_ERR_INVALID_ARG;
+    if (user_op_unsupported(mode, op)) return CHR_ERR_UNSUPPORTED;
     if (c->failed) return CHR_ERR_ABORTED;
     int sched = c->sched, slices = c->slices;
     if (sched == CHR_SCHEDULE_AUTO) {
@@ -1133,6 +1141,7 @@ int collective(chr_comm* c, int mode, const void* send, void* recv, size_t count
 int local_collective(chr_local_group* g, int mode, const void* const* sends, void* const* recvs, size_t count,
                      int dtype, int op, int k, int b) {
     if (!g || !sends || !recvs || !valid_args(mode, dtype, op)) return CHR_ERR_INVALID_ARG;
+    if (user_op_unsupported(mode, op)) return CHR_ERR_UNSUPPORTED;
     const int n = g->nranks;
     const int depth = pick_slices(g->slices, count, mode, n, b, chr::dtype_size(dtype), g->sched);
     auto key = std::make_tuple(mode, k, b, (uint64_t)count, (int)chr::dtype_size(dtype), depth, g->sched);

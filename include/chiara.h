@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define CHR_ABI_VERSION 10 /* 10: chr_comm_get_overlap; 9: chr_comm_info; 8: the stand-alone phase collectives (chr_intra_reduce_scatter_radix_batch, ...) */
+#define CHR_ABI_VERSION 11 /* 11: user-defined ops (chr_op_create); 10: chr_comm_get_overlap; 9: chr_comm_info; 8: the stand-alone phase collectives (chr_intra_reduce_scatter_radix_batch, ...) */
 
 /* Element types.  The reference is generic over MPI_Datatype (all_reduce_radix_batch.cpp:202-204,
  * sizes from MPI_Type_size at :234-277); these are the MPI predefined types MPICH's
@@ -58,7 +58,8 @@ typedef enum {
  * and on float/double (MPICH accepts those; C truth: NaN is true, -0 false); the bitwise ops on the
  * integer types only; MAXLOC/MINLOC on the five pair types only (equal values: the lower index wins,
  * the inout element is kept otherwise; NaN compares keep inout); SUM/PROD on the complex types only.
- * User ops (MPI_Op_create) are not supported (CHR_ERR_INVALID_ARG; MPI_ERR_OP through the shim). */
+ * User-defined ops: chr_op_create below (device code; codes 64..127).  MPI_Op_create's host functions stay MPI_ERR_OP
+ * through the shim. */
 typedef enum {
     CHR_SUM = 0, CHR_PROD = 1, CHR_MAX = 2, CHR_MIN = 3,
     CHR_LAND = 4, CHR_LOR = 5, CHR_LXOR = 6,  /* MPI_LAND, MPI_LOR, MPI_LXOR */
@@ -84,6 +85,28 @@ typedef enum {
 
 /* MPI_IN_PLACE analogue (all_reduce_radix_batch.cpp:234, :306-321): pass as `send`. */
 #define CHR_IN_PLACE ((const void*)(uintptr_t)1)
+
+/* ---- user-defined ops: MPI_Op_create's analogue ---------------------------------------
+ * The reference is generic over MPI_Op (all_reduce_radix_batch.cpp:202-204), user-defined ops included: its
+ * MPI_Reduce_local calls the op's function on host buffers.  Here a user op's arithmetic is the caller's own DEVICE
+ * code -- the library never runs a reduction on the host: `fn` enqueues it on `stream` and returns 0 (anything else:
+ * the op refuses the call, e.g. a type it does not implement; the library returns CHR_ERR_UNSUPPORTED).  For every
+ * element i, with MPI's user-function convention x o y = fn(invec = x, inoutvec = y):
+ *   running_first == 0:  out[i] = ins[m-1][i] o ( ... (ins[0][i] o acc[i]))    (MPI_Reduce_local(ins[j], acc) chained)
+ *   running_first != 0:  out[i] = (((acc[i] o ins[0][i]) o ins[1][i]) ...)     (MPICH_do_reduce's order)
+ * `out` may alias `acc`; m >= 0 (m == 0: out = acc).  include/chiara_user_op.hpp builds such a launcher from a device
+ * functor.  chr_op_create returns the op (codes 64..127) for every chr_reduce_* entry point and CHiArA's collectives
+ * (allreduce_radix_batch, reduce_scatter_radix_batch, the stand-alone phases, on communicators and local groups), each
+ * taking the reference's operand order for any op -- commutative or not (tests/test_gpu_user_op.py against the
+ * reference run with a user-defined non-commutative MPI_Op).  The MPICH baselines branch on MPI_Op_commutative
+ * (allreduce_recursive_doubling.cpp:69, allreduce_recursive_multiplying.cpp:46, ...), which is not modelled: with a
+ * user op they return CHR_ERR_UNSUPPORTED.  Calls with a user op are never captured into HIP graphs.  `commute` is
+ * recorded for the caller; 64 ops may be live at once.  The MPI shim still maps MPI_Op_create's host functions to
+ * MPI_ERR_OP. */
+typedef int (*chr_user_reduce_fn)(void* out, const void* acc, const void* const* ins, int m, size_t n, chr_dtype dtype,
+                                  int running_first, hipStream_t stream, void* ctx);
+int chr_op_create(chr_user_reduce_fn fn, void* ctx, int commute, chr_op* op);
+int chr_op_free(chr_op op);
 
 /* ---- kernel boundary: replaces MPI_Reduce_local --------------------------------------
  * Reference call sites (MPI_Reduce_local(in, inout, count, datatype, op)):

@@ -38,6 +38,7 @@ size_t orc_dtype_size(int dtype) {
 }
 
 int orc_valid(int dtype, int op) {
+    if (op == ORC_USER_HALFADD) return dtype == ORC_F32;
     if (!orc_dtype_size(dtype) || op < ORC_SUM || op > ORC_MINLOC) return 0;
     if (dtype >= ORC_FI && dtype <= ORC_SI) return op == ORC_MAXLOC || op == ORC_MINLOC;
     if (dtype == ORC_CF || dtype == ORC_CD) return op == ORC_SUM || op == ORC_PROD;
@@ -401,7 +402,8 @@ void orc_reduce_local(const void* in, void* inout, size_t n, int dtype, int op) 
     }
     /* MPICH 3.3.2 also takes LAND/LOR/LXOR on float and double (probed: rc 0), C truth values. */
     case ORC_F32:
-        if (op == ORC_SUM) ORC_LOOP(float, orc_x86f(y, x, ORC_XADD)); /* inout's NaN survives */
+        if (op == ORC_USER_HALFADD) ORC_LOOP(float, x * 0.5f + y); /* the user op: inout = in o inout */
+        else if (op == ORC_SUM) ORC_LOOP(float, orc_x86f(y, x, ORC_XADD)); /* inout's NaN survives */
         else if (op == ORC_PROD) ORC_LOOP(float, orc_x86f(y, x, ORC_XMUL));
         else if (op == ORC_MAX) ORC_LOOP(float, y > x ? y : x);
         else if (op == ORC_MIN) ORC_LOOP(float, y < x ? y : x);

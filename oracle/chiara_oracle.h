@@ -39,7 +39,12 @@ enum {
 enum {
     ORC_SUM = 0, ORC_PROD = 1, ORC_MAX = 2, ORC_MIN = 3,
     ORC_LAND = 4, ORC_LOR = 5, ORC_LXOR = 6, ORC_BAND = 7, ORC_BOR = 8, ORC_BXOR = 9,
-    ORC_MAXLOC = 10, ORC_MINLOC = 11
+    ORC_MAXLOC = 10, ORC_MINLOC = 11,
+    /* A user-defined, non-commutative MPI op for the user-op path (MPI_Op_create(fn, commute = 0)): MPI's user
+     * function computes inout[i] = in[i] o inout[i]; this one, on MPI_FLOAT, is in * 0.5f + inout (rounded after
+     * the multiply: no contraction).  Test infrastructure: the same function is the reference's op in
+     * oracle/ref_driver.cpp and the device op in tests/userop/halfadd_op.hip. */
+    ORC_USER_HALFADD = 12
 };
 
 /* MPICH 3.3.2's (type, op) table as MPI_Reduce_local applies it (probed; pairs and complex:

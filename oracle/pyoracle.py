@@ -16,7 +16,8 @@ LIB_PATH = os.path.join(HERE, "liboracle.so")
 DTYPES = {"f32": 0, "f64": 1, "i32": 2, "bf16": 3, "i8": 4, "u8": 5, "i16": 6, "u16": 7, "u32": 8, "i64": 9,
           "u64": 10, "fi": 11, "di": 12, "li": 13, "2i": 14, "si": 15, "cf": 16, "cd": 17}
 OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "land": 4, "lor": 5, "lxor": 6, "band": 7, "bor": 8, "bxor": 9,
-       "maxloc": 10, "minloc": 11}
+       "maxloc": 10, "minloc": 11,
+       "user_halfadd": 12}  # test user op (MPI_Op_create, non-commutative): inout = in * 0.5f + inout, f32
 
 
 def _pair(vfmt, ioff, size):

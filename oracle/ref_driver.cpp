@@ -83,6 +83,17 @@ static void bf16_user_prod(void* in, void* inout, int* len, MPI_Datatype*) {
     orc_reduce_local(in, inout, (size_t)*len, ORC_BF16, ORC_PROD);
 }
 
+// The user-defined op of the user-op path (chiara_oracle.h ORC_USER_HALFADD), written here independently of the
+// oracle: MPI's user-function contract inout[i] = in[i] o inout[i], o = in * 0.5f + inout; created non-commutative.
+static void halfadd_user_op(void* in, void* inout, int* len, MPI_Datatype*) {
+    const float* a = (const float*)in;
+    float* b = (float*)inout;
+    for (int i = 0; i < *len; ++i) {
+        const float h = a[i] * 0.5f;
+        b[i] = h + b[i];
+    }
+}
+
 static int parse_dtype(const std::string& s) {
     static const char* names[] = {"f32", "f64", "i32", "bf16", "i8", "u8", "i16", "u16", "u32", "i64", "u64",
                                   "fi",  "di",  "li",  "2i",   "si", "cf", "cd"};
@@ -92,7 +103,7 @@ static int parse_dtype(const std::string& s) {
 }
 static int parse_op(const std::string& s) {
     static const char* names[] = {"sum", "prod", "max", "min", "land", "lor", "lxor", "band", "bor", "bxor",
-                                  "maxloc", "minloc"};
+                                  "maxloc", "minloc", "user_halfadd"};
     for (int o = 0; o < (int)(sizeof(names) / sizeof(names[0])); ++o)
         if (s == names[o]) return o;
     return -1;
@@ -139,8 +150,10 @@ int main(int argc, char** argv) {
     MPI_Op_create(bf16_user_prod, 1, &bf16_ops[ORC_PROD]);
     MPI_Op_create(bf16_user_max, 1, &bf16_ops[ORC_MAX]);
     MPI_Op_create(bf16_user_min, 1, &bf16_ops[ORC_MIN]);
-    const MPI_Op std_ops[12] = {MPI_SUM,  MPI_PROD, MPI_MAX,  MPI_MIN, MPI_LAND,   MPI_LOR,
-                                MPI_LXOR, MPI_BAND, MPI_BOR,  MPI_BXOR, MPI_MAXLOC, MPI_MINLOC};
+    MPI_Op halfadd_op;
+    MPI_Op_create(halfadd_user_op, 0, &halfadd_op);  // commute = 0
+    const MPI_Op std_ops[13] = {MPI_SUM,  MPI_PROD, MPI_MAX,  MPI_MIN, MPI_LAND,   MPI_LOR,
+                                MPI_LXOR, MPI_BAND, MPI_BOR,  MPI_BXOR, MPI_MAXLOC, MPI_MINLOC, halfadd_op};
 
     std::ifstream cases(argv[1]);
     std::string line;

@@ -314,6 +314,31 @@ def phases_cases_for(n):
     return out
 
 
+def userop_cases_for(n):
+    """A user-defined, non-commutative MPI op (MPI_Op_create(halfadd, commute = 0): inout = in * 0.5f + inout on
+    MPI_FLOAT, oracle/ref_driver.cpp) through CHiArA's own collectives: the radix/batch allreduce and
+    reduce-scatter at every divisor b (in place too) and the stand-alone phases.  The reference is generic over
+    MPI_Op (all_reduce_radix_batch.cpp:202-204) and reduces with MPI_Reduce_local, which calls the user function; a
+    non-commutative op makes every operand order visible in the bits.  (The MPICH baselines branch on
+    MPI_Op_commutative -- allreduce_recursive_doubling.cpp:69, allreduce_recursive_multiplying.cpp:46,
+    allreduce_k_reduce_scatter_allgather.cpp:279 -- which the user-op path does not model: it rejects them.)"""
+    out = []
+
+    def add(mode, k, b, count, inplace):
+        cid = f"{mode}_n{n}_k{k}_b{b}_c{count}_f32_user_halfadd_p0_ip{inplace}"
+        out.append(dict(id=cid, mode=mode, n=n, k=k, b=b, count=count, dtype="f32", op="user_halfadd",
+                        pattern=pyoracle.PAT_UNIFORM, seed=SEED, inplace=inplace))
+
+    for i, b in enumerate(divisors(n)):
+        for k in (2, 3, 4):
+            add("ar", k, b, n * 16 + (n if k == 3 else 0), (i + k) % 2)
+            add("rs", k, b, 9 + k, 0)
+    for b in divisors(n):
+        add("irs", 2, b, 5, 0)
+        add("ilr", 0, b, 4, 0)
+    return out
+
+
 def run_n(n, cases, tmp):
     cf = os.path.join(tmp, f"cases_{n}.txt")
     with open(cf, "w") as f:
@@ -347,6 +372,10 @@ def main():
         for n in (2, 3, 4, 6, 8):
             all_cases += types_cases_for(n)
         prefix = "types_"
+    elif which == "userop":
+        for n in (2, 3, 4, 6, 8):
+            all_cases += userop_cases_for(n)
+        prefix = "userop_"
     elif which == "pairs":
         for n in (2, 3, 4, 5, 6, 8):
             all_cases += pairs_cases_for(n)
@@ -424,6 +453,9 @@ def main():
                 "all_reduce/{allreduce_ring,allreduce_recexch,allreduce_recursive_multiplying}.cpp, MPI pair types "
                 "(MAXLOC/MINLOC) and C complex types (SUM/PROD); ar_lib/rs_lib: MPI_Allreduce / "
                 "MPI_Reduce_scatter_block (see pairs_cases_for)" if which == "pairs" else
+                "Fugaku_experiments/{Allreduce,Reduce-scatter} + testing/custom_implementations/work_dir/"
+                "reduce_scatter/{intra_reduce_scatter_radix,inter_linear_reduce}.cpp, with a user-defined "
+                "non-commutative MPI_Op (see userop_cases_for)" if which == "userop" else
                 "testing/mpich_implementations/all_reduce/{allreduce_ring,allreduce_recursive_doubling,"
                 "allreduce_reduce_scatter_allgather,allreduce_recexch,allreduce_k_reduce_scatter_allgather,"
                 "allreduce_recursive_multiplying}.cpp" if which == "mpich" else

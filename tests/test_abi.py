@@ -34,7 +34,7 @@ def test_library_is_gfx950_code_object():
 
 
 def test_abi_basics():
-    assert ca.lib().chr_abi_version() == 10
+    assert ca.lib().chr_abi_version() == 11
     assert ca.lib().chr_error_string(2).decode().startswith("count")
     assert ca.lib().chr_error_string(0) == b"success"
 
@@ -120,3 +120,25 @@ def test_package_defaults_ipc_mode_before_torch():
     env["PYTHONPATH"] = _lib.PKG_ROOT + os.pathsep + env.get("PYTHONPATH", "")
     out = subprocess.check_output(["python3", "-c", code], env=env, cwd=REPO).decode().strip()
     assert out == "0"
+
+
+def test_user_op_registry_on_the_host():
+    """chr_op_create / chr_op_free (ABI 11) need no GPU: codes from 64 up, a NULL launcher refused, a freed code
+    reusable and refused once freed, and every slot taken after 64 live ops."""
+    import ctypes
+
+    L = ca.lib()
+    fn = ctypes.cast(L.chr_abi_version, ctypes.c_void_p).value  # any address: never called here
+    op = ctypes.c_int(-1)
+    assert L.chr_op_create(None, None, 0, ctypes.byref(op)) == ca.ERR_INVALID_ARG
+    made = []
+    for _ in range(64):
+        assert L.chr_op_create(fn, None, 0, ctypes.byref(op)) == 0
+        made.append(op.value)
+    assert sorted(made) == list(range(64, 128))
+    assert L.chr_op_create(fn, None, 1, ctypes.byref(op)) == ca.ERR_UNSUPPORTED
+    assert L.chr_op_free(made[5]) == 0 and L.chr_op_free(made[5]) == ca.ERR_INVALID_ARG
+    assert L.chr_op_create(fn, None, 1, ctypes.byref(op)) == 0 and op.value == made[5]
+    for o in made:
+        assert L.chr_op_free(o) == 0
+    assert L.chr_op_free(3) == ca.ERR_INVALID_ARG and L.chr_op_free(200) == ca.ERR_INVALID_ARG

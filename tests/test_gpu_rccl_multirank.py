@@ -717,3 +717,69 @@ def test_rccl_host_pipeline_windows_world4():
     res = _spawn(_host_pipeline_worker, 4)
     bad = [r for r in res if r[1]]
     assert not bad, bad
+
+
+def _user_op_worker(rank, world, port, q):
+    """A user-defined op (chr_op_create; tests/userop/halfadd_op.hip, non-commutative) through RCCL: each rank
+    registers the op from its own copy of the code object, then allreduce / reduce-scatter under the flat, exact and
+    reference schedules, with overlap off, graphs on (user-op calls run eagerly) and a host-buffer call: bit-exact vs
+    the oracle.  The MPICH baselines refuse it on every rank alike (no rank left waiting)."""
+    _setup(rank)
+    import ctypes
+
+    import torch
+    import torch.distributed as dist
+
+    import chiara_amd as ca
+    import pyoracle as po
+
+    comm = _init_worker(rank, world, port)
+    lib = ctypes.CDLL(os.path.join(HERE, "userop", "libhalfadd_op.so"))
+    half = ca.op_create(ctypes.cast(lib.chr_test_halfadd, ctypes.c_void_p).value)
+    bad = []
+    try:
+        comm.set_graphs(True)
+        for i, (mode, k, b, sched, overlap, host) in enumerate((
+                ("ar", 2, 2, ca.SCHEDULE_FLAT, True, False), ("ar", 4, 4, ca.SCHEDULE_FLAT, True, False),
+                ("ar", 2, 4, ca.SCHEDULE_EXACT, True, False), ("ar", 2, 1, ca.SCHEDULE_REFERENCE, False, False),
+                ("rs", 2, 2, ca.SCHEDULE_FLAT, True, False), ("rs", 4, 4, ca.SCHEDULE_EXACT, False, False),
+                ("ar", 2, 2, ca.SCHEDULE_FLAT, True, True), ("ar", 2, 2, ca.SCHEDULE_FLAT, True, False))):
+            comm.set_schedule(sched)
+            comm.set_overlap(overlap)
+            count = 65537 * world
+            in_n = count * world if mode == "rs" else count
+            allx = [po.fill(in_n, "f32", po.PAT_UNIFORM, 900 + i, r) for r in range(world)]
+            f = po.allreduce_radix_batch if mode == "ar" else po.reduce_scatter_radix_batch
+            want = f(allx, k, b, "f32", "user_halfadd")[rank]
+            fn = ca.all_reduce_radix_batch if mode == "ar" else ca.reduce_scatter_radix_batch
+            if host:
+                out = np.zeros(count, dtype=np.float32)
+                rc = fn(allx[rank], out, count, ca.FLOAT32, half, comm, k, b)
+            else:
+                dx = torch.from_numpy(allx[rank]).cuda()
+                dout = torch.zeros(count, dtype=torch.float32, device=dx.device)
+                rc = fn(dx, dout, count, ca.FLOAT32, half, comm, k, b)
+                out = dout.cpu().numpy()
+            if rc != 0 or out.tobytes() != want.tobytes():
+                bad.append((mode, k, b, sched, overlap, host, rc))
+        dx = torch.zeros(4096, dtype=torch.float32, device="cuda")
+        rc = ca.MPICH_Allreduce_ring(dx, torch.empty_like(dx), 4096, ca.FLOAT32, half, comm)
+        if rc != ca.ERR_UNSUPPORTED:
+            bad.append(("ring", rc))
+        # the communicator is still healthy after the refusal: a predefined op right after
+        rc = ca.all_reduce_radix_batch(dx, torch.empty_like(dx), 4096, ca.FLOAT32, ca.SUM, comm, 2, 2)
+        torch.cuda.synchronize()
+        if rc != 0:
+            bad.append(("sum-after-refusal", rc))
+    finally:
+        comm.set_graphs(False)
+        ca.op_free(half)
+        comm.destroy()
+        dist.destroy_process_group()
+    q.put((rank, bad))
+
+
+def test_rccl_user_op_world4():
+    res = _spawn(_user_op_worker, 4)
+    bad = [r for r in res if r[1]]
+    assert not bad, bad
