@@ -36,6 +36,7 @@ def _worker(rank, world, port, cases, q):
     try:
         for case in cases:
             (mode, k, b, count, dtype, slices), sched = case[:6], (case[6] if len(case) > 6 else None)
+            opn = case[7] if len(case) > 7 else "sum"  # "user_halfadd": non-commutative, pins every operand order
             phase = {ca.MODE_INTRA_REDUCE_SCATTER: "irs", ca.MODE_INTER_REDUCE_LINEAR: "ilr",
                      ca.MODE_INTRA_SCATTER: "isc"}.get(mode)
             if phase:  # CHiArA's stand-alone phases: count = recvcount, sizes per po.phase_sizes
@@ -47,7 +48,7 @@ def _worker(rank, world, port, cases, q):
             plan = ca.parse_plan(ca.describe_plan(mode, world, rank, k, b, count, slices, sched))
             st = plan_sim.RankState(plan, send, np.zeros(out_n, dtype=send.dtype) if phase else None, dtype)
             for op in plan["pre"]:
-                plan_sim.run_local(st, op, dtype, "sum")
+                plan_sim.run_local(st, op, dtype, opn)
             for s in plan["steps"]:
                 reqs, landing = [], []
                 for peer, ref, n in s["sends"]:
@@ -67,14 +68,14 @@ def _worker(rank, world, port, cases, q):
                     for src in range(world):
                         st.view((buf, off + src * cnt), cnt)[:] = parts[src].numpy().view(send.dtype)
                 for op in s["post"]:
-                    plan_sim.run_local(st, op, dtype, "sum")
+                    plan_sim.run_local(st, op, dtype, opn)
             out = st.buf["RECV"][:out_n]
             allsend = [po.fill(in_n, dtype, 0, 99, r) for r in range(world)]
             if phase:
-                ref = po.phase_collective(phase, allsend, dtype, "sum", k, b, count)[rank]
+                ref = po.phase_collective(phase, allsend, dtype, opn, k, b, count)[rank]
             else:
                 f = po.allreduce_radix_batch if mode == ca.MODE_ALLREDUCE else po.reduce_scatter_radix_batch
-                ref = f(allsend, k, b, dtype, "sum")[rank]
+                ref = f(allsend, k, b, dtype, opn)[rank]
             q.put((rank, mode, k, b, bool(np.array_equal(out.view(np.uint8), ref.view(np.uint8)))))
     finally:
         dist.destroy_process_group()
@@ -106,7 +107,12 @@ def test_gloo_world2():
              (ca.MODE_ALLREDUCE, 2, 2, 2 * 4096, "f32", 3, ca.SCHEDULE_FLAT_AG),
              (ca.MODE_ALLREDUCE, 2, 2, 2 * 1000, "f32", 2, ca.SCHEDULE_FLAT_1SHOT),
              (ca.MODE_INTRA_REDUCE_SCATTER, 2, 2, 300, "f32", 1), (ca.MODE_INTER_REDUCE_LINEAR, 2, 1, 300, "f32", 1),
-             (ca.MODE_INTRA_SCATTER, 2, 2, 300, "i32", 1)])
+             (ca.MODE_INTRA_SCATTER, 2, 2, 300, "i32", 1),
+             # a user-defined non-commutative op (chr_op_create; the oracle's ORC_USER_HALFADD) through the plans
+             (ca.MODE_ALLREDUCE, 2, 2, 2 * 1000, "f32", 2, ca.SCHEDULE_FLAT, "user_halfadd"),
+             (ca.MODE_ALLREDUCE, 2, 1, 2 * 1000, "f32", 1, ca.SCHEDULE_EXACT, "user_halfadd"),
+             (ca.MODE_REDUCE_SCATTER, 2, 2, 4096, "f32", 1, ca.SCHEDULE_REFERENCE, "user_halfadd"),
+             (ca.MODE_INTER_REDUCE_LINEAR, 2, 1, 300, "f32", 1, None, "user_halfadd")])
 
 
 @pytest.mark.slow
@@ -122,4 +128,9 @@ def test_gloo_world4():
              (ca.MODE_ALLREDUCE, 2, 4, 4 * 333, "f32", 1, ca.SCHEDULE_FLAT_1SHOT),
              (ca.MODE_ALLREDUCE, 4, 4, 4 * 2048, "bf16", 3, ca.SCHEDULE_FLAT_1SHOT),
              (ca.MODE_INTRA_REDUCE_SCATTER, 2, 2, 100, "f32", 1), (ca.MODE_INTRA_REDUCE_SCATTER, 3, 4, 100, "bf16", 1),
-             (ca.MODE_INTER_REDUCE_LINEAR, 2, 2, 100, "f32", 1), (ca.MODE_INTRA_SCATTER, 2, 4, 100, "i32", 1)])
+             (ca.MODE_INTER_REDUCE_LINEAR, 2, 2, 100, "f32", 1), (ca.MODE_INTRA_SCATTER, 2, 4, 100, "i32", 1),
+             (ca.MODE_ALLREDUCE, 2, 4, 4 * 333, "f32", 2, ca.SCHEDULE_FLAT, "user_halfadd"),
+             (ca.MODE_ALLREDUCE, 4, 4, 4 * 333, "f32", 1, ca.SCHEDULE_FLAT_1SHOT, "user_halfadd"),
+             (ca.MODE_ALLREDUCE, 2, 2, 4 * 333, "f32", 1, ca.SCHEDULE_EXACT, "user_halfadd"),
+             (ca.MODE_REDUCE_SCATTER, 3, 4, 60, "f32", 1, ca.SCHEDULE_BALANCED, "user_halfadd"),
+             (ca.MODE_INTRA_REDUCE_SCATTER, 3, 4, 100, "f32", 1, None, "user_halfadd")])
