@@ -75,6 +75,7 @@ def _load():
         "chr_comm_get_overlap": ([vp, ctypes.POINTER(i)], i),
         "chr_op_create": ([vp, vp, i, ctypes.POINTER(i)], i),
         "chr_op_free": ([i], i),
+        "chr_plan_describe_op": ([i, i, i, i, i, sz, i, i, i, ctypes.c_char_p, sz], ctypes.c_long),
         "chr_local_group_set_schedule": ([vp, i], i),
         "chr_plan_describe_ex": ([i, i, i, i, i, sz, i, i, ctypes.c_char_p, sz], ctypes.c_long),
         "chr_allgather_radix_batch_async": ([vp, sz, i, vp, vp, i, i], i),
@@ -134,4 +135,5 @@ EXPORTED = [
     "chr_local_reduce_scatter_mpich", "chr_local_group_set_batching",
     "chr_intra_reduce_scatter_radix_batch", "chr_inter_reduce_linear", "chr_intra_scatter_radix_batch",
     "chr_local_phase_collective", "chr_comm_info", "chr_comm_get_overlap", "chr_op_create", "chr_op_free",
+    "chr_plan_describe_op",
 ]

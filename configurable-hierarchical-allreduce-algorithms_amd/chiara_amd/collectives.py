@@ -499,13 +499,16 @@ def reduce_tree_batch(outs, leaves, comb, swaps, count, datatype, op, stream=Non
 
 # ---- plan introspection (host only) --------------------------------------------------------------
 
-def describe_plan(mode, nranks, rank, k, b, count, slices=1, schedule=None):
+def describe_plan(mode, nranks, rank, k, b, count, slices=1, schedule=None, commutative=True):
+    """Rank `rank`'s plan as text (chr_plan_describe_op); commutative=False: the plan a call with a non-commutative
+    user op runs (the MPICH baselines branch on it)."""
     bal = SCHEDULE_FLAT if schedule is None else int(schedule)
-    n = lib().chr_plan_describe_ex(mode, nranks, rank, k, b, count, slices, bal, None, 0)
+    c = int(bool(commutative))
+    n = lib().chr_plan_describe_op(mode, nranks, rank, k, b, count, slices, bal, c, None, 0)
     if n < 0:
         raise ValueError("bad plan request")
     buf = ctypes.create_string_buffer(n + 1)
-    lib().chr_plan_describe_ex(mode, nranks, rank, k, b, count, slices, bal, buf, n + 1)
+    lib().chr_plan_describe_op(mode, nranks, rank, k, b, count, slices, bal, c, buf, n + 1)
     return buf.value.decode()
 
 

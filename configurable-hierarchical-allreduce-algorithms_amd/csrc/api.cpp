@@ -124,9 +124,15 @@ long chr_plan_describe(chr_mode mode, int nranks, int rank, int k, int b, size_t
 
 long chr_plan_describe_ex(chr_mode mode, int nranks, int rank, int k, int b, size_t count, int slices, int schedule,
                           char* buf, size_t len) {
+    return chr_plan_describe_op(mode, nranks, rank, k, b, count, slices, schedule, 1, buf, len);
+}
+
+long chr_plan_describe_op(chr_mode mode, int nranks, int rank, int k, int b, size_t count, int slices, int schedule,
+                          int commutative, char* buf, size_t len) {
     if (mode < CHR_MODE_ALLREDUCE || mode > CHR_MODE_INTRA_SCATTER) return -1;
     if (!chr::plan_schedule(schedule)) return -1;
-    const std::string s = chr::describe(chr::build_plan((chr::Mode)mode, nranks, rank, k, b, count, slices, schedule));
+    const std::string s = chr::describe(
+        chr::build_plan((chr::Mode)mode, nranks, rank, k, b, count, slices, schedule, commutative != 0));
     if (buf && len) {
         const size_t c = s.size() < len - 1 ? s.size() : len - 1;
         std::memcpy(buf, s.data(), c);

@@ -307,7 +307,8 @@ bool is_device_ptr(const void* p) {
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
 }
 
-using PlanKey = std::tuple<int, int, int, int, uint64_t, int, int, int>;  // mode, rank, k, b, count, dtype size, slices, schedule
+// mode, rank, k, b, count, dtype size, slices, schedule, op commutative (the MPICH baselines branch on it)
+using PlanKey = std::tuple<int, int, int, int, uint64_t, int, int, int, bool>;
 
 // CHR_SCHEDULE = reference | balanced | flat | exact | flat_ag | flat_seq | auto (or 0 .. 6); default flat
 // CHR_OVERLAP=0: local ops on the transfer stream (no compute/xGMI overlap); default 1
@@ -503,13 +504,13 @@ struct chr_comm {
     // CHR_SCHEDULE_AUTO: (mode, count, element size, k, b, slices setting, overlap) -> (schedule, depth)
     std::map<std::tuple<int, uint64_t, int, int, int, int, int>, std::pair<int, int>> tuned;
 
-    const Plan& plan(int mode, int k, int b, uint64_t count, size_t es, int sched_, int slices_) {
+    const Plan& plan(int mode, int k, int b, uint64_t count, size_t es, int sched_, int slices_, bool commutative) {
         const int P = pick_slices(slices_, count, mode, nranks, b, es, sched_);
-        PlanKey key{mode, rank, k, b, count, (int)es, P, sched_};
+        PlanKey key{mode, rank, k, b, count, (int)es, P, sched_, commutative};
         auto it = plans.find(key);
         if (it == plans.end())
             it = plans.emplace(key, std::make_unique<Plan>(chr::build_plan((chr::Mode)mode, nranks, rank, k, b, count, P,
-                                                                           sched_)))
+                                                                           sched_, commutative)))
                      .first;
         return *it->second;
     }
@@ -527,7 +528,7 @@ struct chr_local_group {
     int sched = default_schedule() == CHR_SCHEDULE_AUTO ? (int)chr::SCHED_FLAT : default_schedule();  // no tuning
     hipStream_t stream = nullptr;
     std::vector<DevBuf> acc, stage;
-    std::map<std::tuple<int, int, int, uint64_t, int, int, int>, std::vector<Plan>> plans;
+    std::map<std::tuple<int, int, int, uint64_t, int, int, int, bool>, std::vector<Plan>> plans;
 };
 
 namespace {
@@ -890,7 +891,8 @@ int run_host_windows(chr_comm* c, int sched, int slices, int mode, const void* i
                 }
                 if ((e = hipStreamWaitEvent(c->stream, c->ev_out[i], 0)) != hipSuccess) return hip_code(e);
             }
-            const Plan& p = c->plan(mode, k, b, mode == chr::MODE_ALLREDUCE ? n * wj : wj, es, sched, slices);
+            const Plan& p = c->plan(mode, k, b, mode == chr::MODE_ALLREDUCE ? n * wj : wj, es, sched, slices,
+                                    chr::op_commutative(op));
             if (p.error) return p.error;
             int r = enqueue_rccl(c, p, c->wsend[i].p, c->wrecv[i].p, dtype, op);
             if (r) return r;
@@ -932,14 +934,9 @@ bool valid_args(int mode, int dtype, int op) {
     return chr::valid_any(dtype, op);
 }
 
-// The MPICH baselines branch on MPI_Op_commutative (allreduce_recursive_doubling.cpp:69,
-// allreduce_recursive_multiplying.cpp:46, allreduce_k_reduce_scatter_allgather.cpp:279), which the plans do not model:
-// they take no user op.  CHiArA's own collectives have no such branch and take any op.
-bool user_op_unsupported(int mode, int op) { return chr::is_user_op(op) && chr::is_mpich(mode); }
-
 int run_collective(chr_comm* c, int sched, int slices, int mode, const void* send, void* recv, size_t count, int dtype,
                    int op, int k, int b, bool sync) {
-    const Plan& p = c->plan(mode, k, b, count, chr::dtype_size(dtype), sched, slices);
+    const Plan& p = c->plan(mode, k, b, count, chr::dtype_size(dtype), sched, slices, chr::op_commutative(op));
     if (p.error) return p.error;
     if (p.g.total == 0) return CHR_SUCCESS;
     if (!recv && p.recv_elems) return CHR_ERR_INVALID_ARG;  // a rank whose plan writes no output may pass NULL
@@ -1035,7 +1032,7 @@ int tune_schedule(chr_comm* c, int mode, const void* send, void* recv, size_t co
         *slices_out = it->second.second;
         return CHR_SUCCESS;
     }
-    const Plan& p0 = c->plan(mode, k, b, count, es, chr::SCHED_FLAT, c->slices);
+    const Plan& p0 = c->plan(mode, k, b, count, es, chr::SCHED_FLAT, c->slices, chr::op_commutative(op));
     if (p0.error) return p0.error;  // a function of the arguments only: the same on every rank
     if (p0.g.total == 0) return CHR_SUCCESS;
     const bool inplace = send == CHR_IN_PLACE;
@@ -1127,7 +1124,6 @@ int collective(chr_comm* c, int mode, const void* send, void* recv, size_t count
                bool sync) {
     // allgather moves elements of any type (its op is unused)
     if (!c || !valid_args(mode, dtype, op)) return CHR_ERR_INVALID_ARG;
-    if (user_op_unsupported(mode, op)) return CHR_ERR_UNSUPPORTED;
     if (c->failed) return CHR_ERR_ABORTED;
     int sched = c->sched, slices = c->slices;
     if (sched == CHR_SCHEDULE_AUTO) {
@@ -1141,15 +1137,16 @@ int collective(chr_comm* c, int mode, const void* send, void* recv, size_t count
 int local_collective(chr_local_group* g, int mode, const void* const* sends, void* const* recvs, size_t count,
                      int dtype, int op, int k, int b) {
     if (!g || !sends || !recvs || !valid_args(mode, dtype, op)) return CHR_ERR_INVALID_ARG;
-    if (user_op_unsupported(mode, op)) return CHR_ERR_UNSUPPORTED;
     const int n = g->nranks;
+    // the MPICH baselines branch on MPI_Op_commutative (build_plan_mpich); CHiArA's own collectives take any op
+    const bool commutative = chr::op_commutative(op);
     const int depth = pick_slices(g->slices, count, mode, n, b, chr::dtype_size(dtype), g->sched);
-    auto key = std::make_tuple(mode, k, b, (uint64_t)count, (int)chr::dtype_size(dtype), depth, g->sched);
+    auto key = std::make_tuple(mode, k, b, (uint64_t)count, (int)chr::dtype_size(dtype), depth, g->sched, commutative);
     auto it = g->plans.find(key);
     if (it == g->plans.end()) {
         std::vector<Plan> v;
         for (int r = 0; r < n; ++r)
-            v.push_back(chr::build_plan((chr::Mode)mode, n, r, k, b, count, depth, g->sched));
+            v.push_back(chr::build_plan((chr::Mode)mode, n, r, k, b, count, depth, g->sched, commutative));
         it = g->plans.emplace(key, std::move(v)).first;
     }
     const std::vector<Plan>& P = it->second;

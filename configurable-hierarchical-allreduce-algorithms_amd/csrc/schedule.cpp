@@ -724,8 +724,9 @@ static void analyze_deps(Plan& p) {
     }
 }
 
-Plan build_plan(Mode mode, int n, int me, int k_in, int b, uint64_t count, int slices, int sched) {
-    Plan p = build_plan_impl(mode, n, me, k_in, b, count, slices, sched);
+Plan build_plan(Mode mode, int n, int me, int k_in, int b, uint64_t count, int slices, int sched, bool commutative) {
+    Plan p = is_mpich(mode) ? build_plan_mpich(mode, n, me, k_in, b, count, commutative)
+                            : build_plan_impl(mode, n, me, k_in, b, count, slices, sched);
     if (!p.error) {
         split_wide_reductions(p);
         analyze_deps(p);
@@ -1000,6 +1001,7 @@ struct MB {
     Plan& p;
     int n, me;
     uint64_t count;
+    bool commutative;
     Step& add(const char* label) {
         p.steps.emplace_back();
         p.steps.back().label = label;
@@ -1066,7 +1068,10 @@ void build_ring(MB& b) {  // allreduce_ring.cpp:3-104
     }
 }
 
-void build_rd(MB& b) {  // allreduce_recursive_doubling.cpp:4-101 (commutative path)
+// allreduce_recursive_doubling.cpp:4-101.  A non-commutative op keeps rank order (:69-80): the partner's buffer is
+// the left operand when the partner is the lower rank, else the running value is (reduced into tmp_buf, copied back:
+// the running-value-first combine).
+void build_rd(MB& b) {
     int pof2 = 1;
     while (pof2 <= b.n) pof2 <<= 1;
     pof2 >>= 1;
@@ -1081,6 +1086,7 @@ void build_rd(MB& b) {  // allreduce_recursive_doubling.cpp:4-101 (commutative p
         s.recvs.push_back({dst, {BUF_STAGE, 0}, b.count});
         b.need(b.count);
         b.reduce_in(s, 0, 0, b.count, 70);
+        if (!b.commutative && dst > b.me) s.post.back().swap = true;  // :75-79
     }
     mb_unfold(b, rem);
 }
@@ -1379,6 +1385,7 @@ struct RB {
     Plan& p;
     int n, me;
     uint64_t rc, total;
+    bool commutative;
     Step& add(const char* label) {
         p.steps.emplace_back();
         p.steps.back().label = label;
@@ -1480,11 +1487,12 @@ void build_rs_halving(RB& b) {
     if (newrank >= 0) s.post.push_back(make_copy({BUF_RECV, 0}, {BUF_ACC, (uint64_t)me * rc}, rc, 130));
 }
 
-// reduce_scatter_recursive_doubling.cpp:10-177 (commutative path: every predefined op, and the
-// bf16 user op, is commutative): at distance `mask` each rank exchanges every block outside its
+// reduce_scatter_recursive_doubling.cpp:10-177: at distance `mask` each rank exchanges every block outside its
 // own and its partner's subtree of `mask` ranks (two hindexed blocks each way, :58-104); for a
 // non-power-of-two size the ranks without a partner get the data relayed down the subtree
-// (:106-130); the received blocks are folded into tmp_results (:132-155).
+// (:106-130); the received blocks are folded into tmp_results (:132-155) -- as the left operand for a commutative
+// op or when the partner's subtree is the lower one, else with tmp_results as the left operand (reduced into
+// tmp_recvbuf and copied back, :158: the running-value-first combine).
 void build_rs_doubling(RB& b) {
     const int P = b.n, me = b.me;
     const uint64_t rc = b.rc, total = b.total;
@@ -1533,9 +1541,15 @@ void build_rs_doubling(RB& b) {
             }
         }
         if (received) {
-            if (r0) last->post.push_back(make_reduce({BUF_ACC, 0}, {BUF_ACC, 0}, {{BUF_STAGE, 0}}, r0, 141));
-            if (r1)
+            const bool run_first = !b.commutative && !(dtr < mtr);
+            if (r0) {
+                last->post.push_back(make_reduce({BUF_ACC, 0}, {BUF_ACC, 0}, {{BUF_STAGE, 0}}, r0, 141));
+                last->post.back().swap = run_first;
+            }
+            if (r1) {
                 last->post.push_back(make_reduce({BUF_ACC, r1off}, {BUF_ACC, r1off}, {{BUF_STAGE, r1off}}, r1, 151));
+                last->post.back().swap = run_first;
+            }
         }
     }
     Step& s = b.add("rd-out");  // :171-174
@@ -1609,7 +1623,7 @@ void build_rs_radix(RB& b, int k_in) {
 
 }  // namespace
 
-Plan build_plan_mpich(Mode mode, int n, int me, int k, int aux, uint64_t count) {
+Plan build_plan_mpich(Mode mode, int n, int me, int k, int aux, uint64_t count, bool commutative) {
     (void)aux;  // recexch single_phase_recv: buffering only, same data flow
     Plan p;
     p.mode = mode;
@@ -1617,6 +1631,15 @@ Plan build_plan_mpich(Mode mode, int n, int me, int k, int aux, uint64_t count) 
     if (n < 1 || me < 0 || me >= n || ((mode == MODE_MPICH_RECEXCH || mode == MODE_MPICH_RMULT) && k < 2)) {
         p.error = 1;
         return p;
+    }
+    if (!commutative) {  // the reference's MPI_ERR_OP, before any data moves
+        int pofk = 1;
+        while (mode == MODE_MPICH_RMULT && pofk * k <= n) pofk *= k;
+        if (mode == MODE_MPICH_KRSAG ||                     // allreduce_k_reduce_scatter_allgather.cpp:278-283
+            (mode == MODE_MPICH_RMULT && pofk < n)) {       // allreduce_recursive_multiplying.cpp:43-49
+            p.error = 8;                                    // CHR_ERR_UNSUPPORTED
+            return p;
+        }
     }
     p.g.nranks = n;
     p.g.k = k;
@@ -1630,7 +1653,7 @@ Plan build_plan_mpich(Mode mode, int n, int me, int k, int aux, uint64_t count) 
         p.send_elems = p.g.total;
         p.recv_elems = count;
         if (count == 0) return p;
-        RB rb{p, n, me, count, p.g.total};
+        RB rb{p, n, me, count, p.g.total, commutative};
         switch (mode) {
         case MODE_MPICH_RS_RADIX: build_rs_radix(rb, k); break;
         case MODE_MPICH_RS_HALVING: build_rs_halving(rb); break;
@@ -1644,7 +1667,7 @@ Plan build_plan_mpich(Mode mode, int n, int me, int k, int aux, uint64_t count) 
     if (count == 0) return p;
     // pre: recvbuf <- sendbuf (every algorithm starts with this memcpy; no-op in place)
     p.pre.push_back(make_copy({BUF_RECV, 0}, {BUF_SEND, 0}, count, 0));
-    MB b{p, n, me, count};
+    MB b{p, n, me, count, commutative};
     switch (mode) {
     case MODE_MPICH_RING: build_ring(b); break;
     case MODE_MPICH_RD: build_rd(b); break;

@@ -164,12 +164,17 @@ enum Sched : int {
 };
 // A schedule a plan can be built for (every Sched value; not CHR_SCHEDULE_AUTO).
 inline bool plan_schedule(int s) { return (s >= SCHED_REFERENCE && s <= SCHED_FLAT_SEQ) || s == SCHED_FLAT_1SHOT; }
+// `commutative`: MPI_Op_commutative of the call's op (every predefined op is; a user op as created).  Only the MPICH
+// baselines that branch on it read it (build_plan_mpich); CHiArA's own schedules take the reference's operand
+// order for any op.
 Plan build_plan(Mode mode, int nranks, int rank, int k, int b, uint64_t count, int slices = 1,
-                int sched = SCHED_FLAT);
+                int sched = SCHED_FLAT, bool commutative = true);
 int auto_slices(uint64_t irc_bytes);
 // MPICH baseline allreduces (count = elements per rank; aux = recexch single_phase_recv) and
-// reduce-scatters (count = recvcount).
-Plan build_plan_mpich(Mode mode, int nranks, int rank, int k, int aux, uint64_t count);
+// reduce-scatters (count = recvcount).  A non-commutative op takes the reference's rank-ordered branches
+// (recursive doubling, reduce-scatter recursive doubling) or its MPI_ERR_OP (error = CHR_ERR_UNSUPPORTED:
+// k-reduce-scatter-allgather, recursive multiplying at a size that is not a power of k).
+Plan build_plan_mpich(Mode mode, int nranks, int rank, int k, int aux, uint64_t count, bool commutative = true);
 Plan build_plan_allgather(int nranks, int rank, int k, int b, uint64_t sendcount);
 // The stand-alone phases (MODE_INTRA_RS / MODE_INTER_LINEAR / MODE_INTRA_SCATTER; count = recvcount).
 Plan build_plan_phase(Mode mode, int nranks, int rank, int k, int b, uint64_t recvcount);

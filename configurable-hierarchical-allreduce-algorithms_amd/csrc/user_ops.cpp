@@ -82,6 +82,11 @@ int user_tree(const UserOp& u, void* out, const void* const* leaves, int nl, con
 
 bool is_user_op(int op) { return op >= kUserOpBase && op < kUserOpBase + kMaxUserOps; }
 
+bool op_commutative(int op) {
+    UserOp u;
+    return !is_user_op(op) || (lookup(op, &u) && u.commute);
+}
+
 bool valid_any(int dtype, int op) {
     if (!is_user_op(op)) return valid_dtype_op(dtype, op);
     UserOp u;

@@ -17,6 +17,8 @@ constexpr int kUserOpBase = 64;
 constexpr int kMaxUserOps = 64;
 
 bool is_user_op(int op);
+// MPI_Op_commutative: every predefined op is commutative; a user op as chr_op_create recorded it.
+bool op_commutative(int op);
 // A live user op on a type with a size, or a (type, op) pair MPICH's table accepts (valid_dtype_op).
 bool valid_any(int dtype, int op);
 

@@ -98,11 +98,13 @@ typedef enum {
  * functor.  chr_op_create returns the op (codes 64..127) for every chr_reduce_* entry point and CHiArA's collectives
  * (allreduce_radix_batch, reduce_scatter_radix_batch, the stand-alone phases, on communicators and local groups), each
  * taking the reference's operand order for any op -- commutative or not (tests/test_gpu_user_op.py against the
- * reference run with a user-defined non-commutative MPI_Op).  The MPICH baselines branch on MPI_Op_commutative
- * (allreduce_recursive_doubling.cpp:69, allreduce_recursive_multiplying.cpp:46, ...), which is not modelled: with a
- * user op they return CHR_ERR_UNSUPPORTED.  Calls with a user op are never captured into HIP graphs.  `commute` is
- * recorded for the caller; 64 ops may be live at once.  The MPI shim still maps MPI_Op_create's host functions to
- * MPI_ERR_OP. */
+ * reference run with a user-defined non-commutative MPI_Op).  The MPICH baselines take user ops too and, as the
+ * reference's, branch on `commute` (MPI_Op_commutative): rank-ordered operands for a non-commutative op in recursive
+ * doubling (allreduce_recursive_doubling.cpp:69-80, reduce_scatter_recursive_doubling.cpp:134-160), and
+ * CHR_ERR_UNSUPPORTED where the reference returns MPI_ERR_OP (k-reduce-scatter-allgather,
+ * allreduce_k_reduce_scatter_allgather.cpp:278-283; recursive multiplying when nranks is not a power of k,
+ * allreduce_recursive_multiplying.cpp:43-49).  Calls with a user op are never captured into HIP graphs.  64 ops may
+ * be live at once.  The MPI shim still maps MPI_Op_create's host functions to MPI_ERR_OP. */
 typedef int (*chr_user_reduce_fn)(void* out, const void* acc, const void* const* ins, int m, size_t n, chr_dtype dtype,
                                   int running_first, hipStream_t stream, void* ctx);
 int chr_op_create(chr_user_reduce_fn fn, void* ctx, int commute, chr_op* op);
@@ -389,6 +391,12 @@ long chr_plan_describe(chr_mode mode, int nranks, int rank, int k, int b, size_t
 /* The same for a given CHR_SCHEDULE_* (chr_plan_describe describes CHR_SCHEDULE_FLAT). */
 long chr_plan_describe_ex(chr_mode mode, int nranks, int rank, int k, int b, size_t count,
                           int slices, int schedule, char* buf, size_t len);
+/* The plan a call with an op of the given commutativity runs (MPI_Op_commutative; commutative = 0: a user op created
+ * with commute = 0).  The MPICH baselines branch on it (recursive doubling, reduce-scatter recursive doubling) or
+ * refuse a non-commutative op (k-reduce-scatter-allgather; recursive multiplying when nranks is not a power of k),
+ * as the reference does; CHiArA's own plans do not depend on it.  (ABI 11) */
+long chr_plan_describe_op(chr_mode mode, int nranks, int rank, int k, int b, size_t count, int slices, int schedule,
+                          int commutative, char* buf, size_t len);
 
 /* ---- MPICH baseline allreduces (the ones testing/main.cpp benchmarks CHiArA against) --
  * Replace  int MPICH_Allreduce_ring(const char* sendbuf, char* recvbuf, int count,

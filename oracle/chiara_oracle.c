@@ -37,8 +37,10 @@ size_t orc_dtype_size(int dtype) {
     }
 }
 
+int orc_commutative(int op) { return op != ORC_USER_HALFADD; }
+
 int orc_valid(int dtype, int op) {
-    if (op == ORC_USER_HALFADD) return dtype == ORC_F32;
+    if (op == ORC_USER_HALFADD || op == ORC_USER_HALFADD_C) return dtype == ORC_F32;
     if (!orc_dtype_size(dtype) || op < ORC_SUM || op > ORC_MINLOC) return 0;
     if (dtype >= ORC_FI && dtype <= ORC_SI) return op == ORC_MAXLOC || op == ORC_MINLOC;
     if (dtype == ORC_CF || dtype == ORC_CD) return op == ORC_SUM || op == ORC_PROD;
@@ -402,7 +404,8 @@ void orc_reduce_local(const void* in, void* inout, size_t n, int dtype, int op) 
     }
     /* MPICH 3.3.2 also takes LAND/LOR/LXOR on float and double (probed: rc 0), C truth values. */
     case ORC_F32:
-        if (op == ORC_USER_HALFADD) ORC_LOOP(float, x * 0.5f + y); /* the user op: inout = in o inout */
+        if (op == ORC_USER_HALFADD || op == ORC_USER_HALFADD_C)
+            ORC_LOOP(float, x * 0.5f + y); /* the user op: inout = in o inout */
         else if (op == ORC_SUM) ORC_LOOP(float, orc_x86f(y, x, ORC_XADD)); /* inout's NaN survives */
         else if (op == ORC_PROD) ORC_LOOP(float, orc_x86f(y, x, ORC_XMUL));
         else if (op == ORC_MAX) ORC_LOOP(float, y > x ? y : x);
@@ -757,7 +760,8 @@ int orc_allreduce_ring(int n, size_t count, int dtype, int op, const void* const
     return 0;
 }
 
-/* MPICH_Allreduce_recursive_doubling (allreduce_recursive_doubling.cpp:4-101), commutative path */
+/* MPICH_Allreduce_recursive_doubling (allreduce_recursive_doubling.cpp:4-101).  A non-commutative op keeps rank
+ * order (:69-80): the partner's buffer is the left operand when it is the lower rank, else the right one. */
 int orc_allreduce_recursive_doubling(int n, size_t count, int dtype, int op, const void* const* send,
                                      void* const* recv) {
     size_t es = orc_dtype_size(dtype);
@@ -778,7 +782,15 @@ int orc_allreduce_recursive_doubling(int n, size_t count, int dtype, int op, con
             if (newrank < 0) continue;
             newdst = newrank ^ mask;
             dst = newdst < rem ? newdst * 2 + 1 : newdst + rem;
-            orc_reduce_local(snap + (size_t)dst * count * es, R[r], count, dtype, op); /* :70 */
+            if (orc_commutative(op) || dst < r) {
+                orc_reduce_local(snap + (size_t)dst * count * es, R[r], count, dtype, op); /* :70 */
+            } else { /* :75-79: MPI_Reduce_local(recvbuf, tmp_buf), then tmp_buf -> recvbuf */
+                char* t = (char*)malloc(count * es + 1);
+                memcpy(t, snap + (size_t)dst * count * es, count * es);
+                orc_reduce_local(R[r], t, count, dtype, op);
+                memcpy(R[r], t, count * es);
+                free(t);
+            }
         }
     }
     free(snap);
@@ -966,6 +978,7 @@ int orc_allreduce_recursive_multiplying(int n, int k, size_t count, int dtype, i
     nb = count * es;
     orc_copy_in(n, count, es, send, recv);
     while (pofk * k <= n) pofk *= k; /* :13-17 */
+    if (pofk < n && !orc_commutative(op)) return 8; /* :43-49: MPI_ERR_OP ("non pofk works only for commutative") */
     seq = (char**)calloc((size_t)(n > k ? n : k) + 1, sizeof(char*));
     if (pofk < n) /* :43-86: rank r < pofk folds r+pofk, r+2pofk, ... then its own buffer */
         for (r = 0; r < pofk; r++) {
@@ -1037,6 +1050,7 @@ int orc_allreduce_k_reduce_scatter_allgather(int n, int k_in, size_t count, int 
     char* snap;
     if (n < 1 || !es) return 1;
     if (k_in <= 1) k_in = 2; /* :273-275 */
+    if (!orc_commutative(op)) return 8; /* :278-283: MPI_ERR_OP for a non-commutative op */
     nb = count * es;
     orc_copy_in(n, count, es, send, recv);
     x = (orc_recexch_t*)calloc((size_t)n, sizeof(orc_recexch_t));
@@ -1237,7 +1251,9 @@ int orc_reduce_scatter_rec_halving(int n, size_t rc, int dtype, int op, const vo
     return 0;
 }
 
-/* reduce_scatter_recursive_doubling.cpp:10-177, commutative path. */
+/* reduce_scatter_recursive_doubling.cpp:10-177.  A non-commutative op (:132-160) reduces the received blocks as the
+ * left operand only when the partner's subtree is the lower one; otherwise tmp_results is the left operand, reduced
+ * into tmp_recvbuf and copied back (the Sendrecv-to-self at :158). */
 int orc_reduce_scatter_rec_doubling(int n, size_t rc, int dtype, int op, const void* const* send,
                                     void* const* recv) {
     const int P = n;
@@ -1293,9 +1309,21 @@ int orc_reduce_scatter_rec_doubling(int n, size_t rc, int dtype, int op, const v
             size_t r0 = rc * (size_t)(dtr < P ? dtr : P);
             size_t r1 = P - (dtr + mask) > 0 ? (size_t)(P - (dtr + mask)) * rc : 0;
             size_t r1off = r0 + rc * (size_t)(((dtr + mask) < P ? (dtr + mask) : P) - dtr);
+            const int mtr = (r >> stage) << stage;
             if (!received[r]) continue;
-            if (r0) orc_reduce_local(trecv[r], tmp[r], r0, dtype, op);
-            if (r1) orc_reduce_local(trecv[r] + r1off * es, tmp[r] + r1off * es, r1, dtype, op);
+            if (orc_commutative(op) || dtr < mtr) {
+                if (r0) orc_reduce_local(trecv[r], tmp[r], r0, dtype, op);
+                if (r1) orc_reduce_local(trecv[r] + r1off * es, tmp[r] + r1off * es, r1, dtype, op);
+            } else {
+                if (r0) {
+                    orc_reduce_local(tmp[r], trecv[r], r0, dtype, op);
+                    memcpy(tmp[r], trecv[r], r0 * es);
+                }
+                if (r1) {
+                    orc_reduce_local(tmp[r] + r1off * es, trecv[r] + r1off * es, r1, dtype, op);
+                    memcpy(tmp[r] + r1off * es, trecv[r] + r1off * es, r1 * es);
+                }
+            }
         }
     }
     for (r = 0; r < n; r++) memcpy(res[r], tmp[r] + (size_t)r * rc * es, rc * es); /* :171-174 */

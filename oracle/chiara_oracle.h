@@ -44,8 +44,15 @@ enum {
      * function computes inout[i] = in[i] o inout[i]; this one, on MPI_FLOAT, is in * 0.5f + inout (rounded after
      * the multiply: no contraction).  Test infrastructure: the same function is the reference's op in
      * oracle/ref_driver.cpp and the device op in tests/userop/halfadd_op.hip. */
-    ORC_USER_HALFADD = 12
+    ORC_USER_HALFADD = 12,
+    /* The same function created commutative (MPI_Op_create(fn, commute = 1)): identical arithmetic, but the MPICH
+     * baselines that branch on MPI_Op_commutative take their commutative paths (allreduce_recursive_doubling.cpp:69,
+     * reduce_scatter_recursive_doubling.cpp:134) -- which the non-commutative arithmetic then shows in the bits. */
+    ORC_USER_HALFADD_C = 13
 };
+
+/* MPI_Op_commutative: every predefined op is commutative; the user ops as created. */
+int orc_commutative(int op);
 
 /* MPICH 3.3.2's (type, op) table as MPI_Reduce_local applies it (probed; pairs and complex:
  * oracle/ref_pairs_probe table, tests/golden/pairs_manifest.json); bf16 takes SUM/PROD/MAX/MIN. */
@@ -144,7 +151,9 @@ int orc_reduce_scatter_radix_batch(int nranks, int k, int b, size_t recvcount, i
                                    int op, const void* const* send, void* const* recv);
 
 /* MPICH baseline allreduces driven by the reference's testing/main.cpp.
- * send[r] may be NULL (in place: recv[r] holds the input). */
+ * send[r] may be NULL (in place: recv[r] holds the input).  They follow MPI_Op_commutative (orc_commutative) where
+ * the reference branches on it; 8 = the reference's MPI_ERR_OP (k_reduce_scatter_allgather with a non-commutative
+ * op, recursive_multiplying with one at a size that is not a power of k). */
 int orc_allreduce_ring(int nranks, size_t count, int dtype, int op, const void* const* send, void* const* recv);
 int orc_allreduce_recursive_doubling(int nranks, size_t count, int dtype, int op, const void* const* send,
                                      void* const* recv);

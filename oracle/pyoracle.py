@@ -17,7 +17,9 @@ DTYPES = {"f32": 0, "f64": 1, "i32": 2, "bf16": 3, "i8": 4, "u8": 5, "i16": 6, "
           "u64": 10, "fi": 11, "di": 12, "li": 13, "2i": 14, "si": 15, "cf": 16, "cd": 17}
 OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "land": 4, "lor": 5, "lxor": 6, "band": 7, "bor": 8, "bxor": 9,
        "maxloc": 10, "minloc": 11,
-       "user_halfadd": 12}  # test user op (MPI_Op_create, non-commutative): inout = in * 0.5f + inout, f32
+       "user_halfadd": 12,  # test user op (MPI_Op_create, non-commutative): inout = in * 0.5f + inout, f32
+       "user_halfadd_c": 13}  # the same function created commutative (the baselines' commutative paths)
+ORC_ERR_OP = 8  # the oracle's MPI_ERR_OP (a baseline refusing a non-commutative op)
 
 
 def _pair(vfmt, ioff, size):
@@ -222,7 +224,7 @@ def mpich_allreduce(algo, sends, dtype, op, k=2, inplace=False):
     else:
         raise ValueError(algo)
     if rc:
-        raise ValueError(f"oracle {algo} rejected (rc={rc})")
+        raise ValueError(f"oracle {algo} rejected (rc={rc})", rc)
     return recvs
 
 
@@ -260,7 +262,7 @@ def mpich_reduce_scatter(algo, sends, dtype, op, k=2, inplace=False):
     else:
         raise ValueError(algo)
     if rc_:
-        raise ValueError(f"oracle {algo} rejected (rc={rc_})")
+        raise ValueError(f"oracle {algo} rejected (rc={rc_})", rc_)
     return [r[:rc] for r in recvs]
 
 
@@ -311,5 +313,5 @@ def phase_collective(algo, sends, dtype, op, k, b, rc, inplace=False):
     else:
         rc_ = L.orc_intra_scatter(n, k, b, rc, d, sp, rp)
     if rc_:
-        raise ValueError(f"oracle {algo} rejected (rc={rc_})")
+        raise ValueError(f"oracle {algo} rejected (rc={rc_})", rc_)
     return [r[:out_n] for r in recvs]

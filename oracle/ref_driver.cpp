@@ -103,7 +103,7 @@ static int parse_dtype(const std::string& s) {
 }
 static int parse_op(const std::string& s) {
     static const char* names[] = {"sum", "prod", "max", "min", "land", "lor", "lxor", "band", "bor", "bxor",
-                                  "maxloc", "minloc", "user_halfadd"};
+                                  "maxloc", "minloc", "user_halfadd", "user_halfadd_c"};
     for (int o = 0; o < (int)(sizeof(names) / sizeof(names[0])); ++o)
         if (s == names[o]) return o;
     return -1;
@@ -150,10 +150,11 @@ int main(int argc, char** argv) {
     MPI_Op_create(bf16_user_prod, 1, &bf16_ops[ORC_PROD]);
     MPI_Op_create(bf16_user_max, 1, &bf16_ops[ORC_MAX]);
     MPI_Op_create(bf16_user_min, 1, &bf16_ops[ORC_MIN]);
-    MPI_Op halfadd_op;
-    MPI_Op_create(halfadd_user_op, 0, &halfadd_op);  // commute = 0
-    const MPI_Op std_ops[13] = {MPI_SUM,  MPI_PROD, MPI_MAX,  MPI_MIN, MPI_LAND,   MPI_LOR,
-                                MPI_LXOR, MPI_BAND, MPI_BOR,  MPI_BXOR, MPI_MAXLOC, MPI_MINLOC, halfadd_op};
+    MPI_Op halfadd_op, halfadd_c_op;
+    MPI_Op_create(halfadd_user_op, 0, &halfadd_op);    // commute = 0
+    MPI_Op_create(halfadd_user_op, 1, &halfadd_c_op);  // the same function declared commutative
+    const MPI_Op std_ops[14] = {MPI_SUM,  MPI_PROD, MPI_MAX,  MPI_MIN,    MPI_LAND,   MPI_LOR,    MPI_LXOR,
+                                MPI_BAND, MPI_BOR,  MPI_BXOR, MPI_MAXLOC, MPI_MINLOC, halfadd_op, halfadd_c_op};
 
     std::ifstream cases(argv[1]);
     std::string line;
@@ -185,6 +186,7 @@ int main(int argc, char** argv) {
             if (in_n < out_n) in_n = out_n;  // recv is allocated with in_n elements
         }
         std::vector<char> send(in_n * es), recv(in_n * es, 0), lib(out_n * es, 0);
+        int ref_rc = 0;  // the MPICH baselines' return code (MPI_ERR_OP where they refuse the op)
         orc_fill(send.data(), in_n, dtype, pattern, seed, rank, in_n);
 
         if (phase_mode) {
@@ -223,28 +225,31 @@ int main(int argc, char** argv) {
             if (inplace) memcpy(recv.data(), send.data(), in_n * es);
             MPI_Barrier(MPI_COMM_WORLD);
             const char* sb = inplace ? (const char*)MPI_IN_PLACE : send.data();
-            if (mode == "ring") MPICH_Allreduce_ring(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
-            else if (mode == "rd") MPICH_Allreduce_recursive_doubling(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
+            if (mode == "ring") ref_rc = MPICH_Allreduce_ring(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
+            else if (mode == "rd")
+                ref_rc = MPICH_Allreduce_recursive_doubling(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
             else if (mode == "rsag")
-                MPICH_Allreduce_reduce_scatter_allgather(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
+                ref_rc = MPICH_Allreduce_reduce_scatter_allgather(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
             else if (mode == "rx")
-                MPICH_Allreduce_recursive_exchange(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD, k, b);
+                ref_rc = MPICH_Allreduce_recursive_exchange(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD, k, b);
             else if (mode == "krsag")
-                MPICH_Allreduce_k_reduce_scatter_allgather(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD, k, b);
-            else MPICH_Allreduce_recursive_multiplying(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD, k);
+                ref_rc = MPICH_Allreduce_k_reduce_scatter_allgather(sb, recv.data(), (int)count, mdt, mop,
+                                                                    MPI_COMM_WORLD, k, b);
+            else ref_rc = MPICH_Allreduce_recursive_multiplying(sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD, k);
         } else if (mode.rfind("rs_", 0) == 0) {
             MPI_Reduce_scatter_block(send.data(), lib.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
             if (inplace) memcpy(recv.data(), send.data(), in_n * es);
             MPI_Barrier(MPI_COMM_WORLD);
             const void* sb = inplace ? MPI_IN_PLACE : (const void*)send.data();
             if (mode == "rs_radix")
-                MPICH_reduce_scatter_radix(sb, recv.data(), (MPI_Aint)count, mdt, mop, MPI_COMM_WORLD, k);
+                ref_rc = MPICH_reduce_scatter_radix(sb, recv.data(), (MPI_Aint)count, mdt, mop, MPI_COMM_WORLD, k);
             else if (mode == "rs_halving")
-                MPICH_reduce_scatter_rec_halving((const char*)sb, recv.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
+                ref_rc = MPICH_reduce_scatter_rec_halving((const char*)sb, recv.data(), (int)count, mdt, mop,
+                                                          MPI_COMM_WORLD);
             else if (mode == "rs_doubling")
-                MPICH_reduce_scatter_rec_doubling(sb, recv.data(), (MPI_Aint)count, mdt, mop, MPI_COMM_WORLD);
+                ref_rc = MPICH_reduce_scatter_rec_doubling(sb, recv.data(), (MPI_Aint)count, mdt, mop, MPI_COMM_WORLD);
             else
-                MPICH_reduce_scatter_pairwise(sb, recv.data(), (MPI_Aint)count, mdt, mop, MPI_COMM_WORLD);
+                ref_rc = MPICH_reduce_scatter_pairwise(sb, recv.data(), (MPI_Aint)count, mdt, mop, MPI_COMM_WORLD);
         } else {
             MPI_Reduce_scatter_block(send.data(), lib.data(), (int)count, mdt, mop, MPI_COMM_WORLD);
             if (inplace) memcpy(recv.data(), send.data(), in_n * es);
@@ -258,6 +263,8 @@ int main(int argc, char** argv) {
                    MPI_COMM_WORLD);
         MPI_Gather(lib.data(), (int)(out_n * es), MPI_BYTE, all_lib.data(), (int)(out_n * es), MPI_BYTE, 0,
                    MPI_COMM_WORLD);
+        std::vector<int> all_rc(rank == 0 ? nprocs : 1);
+        MPI_Gather(&ref_rc, 1, MPI_INT, all_rc.data(), 1, MPI_INT, 0, MPI_COMM_WORLD);
         if (rank == 0) {
             std::string base = std::string(argv[2]) + "/" + id;
             FILE* f = fopen((base + ".out").c_str(), "wb");
@@ -265,6 +272,9 @@ int main(int argc, char** argv) {
             fclose(f);
             f = fopen((base + ".lib").c_str(), "wb");
             fwrite(all_lib.data(), 1, out_n * es * nprocs, f);
+            fclose(f);
+            f = fopen((base + ".rc").c_str(), "w");  // every rank's return code, rank order
+            for (int r = 0; r < nprocs; ++r) fprintf(f, "%d\n", all_rc[r]);
             fclose(f);
         }
     }

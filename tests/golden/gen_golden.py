@@ -319,9 +319,8 @@ def userop_cases_for(n):
     MPI_FLOAT, oracle/ref_driver.cpp) through CHiArA's own collectives: the radix/batch allreduce and
     reduce-scatter at every divisor b (in place too) and the stand-alone phases.  The reference is generic over
     MPI_Op (all_reduce_radix_batch.cpp:202-204) and reduces with MPI_Reduce_local, which calls the user function; a
-    non-commutative op makes every operand order visible in the bits.  (The MPICH baselines branch on
-    MPI_Op_commutative -- allreduce_recursive_doubling.cpp:69, allreduce_recursive_multiplying.cpp:46,
-    allreduce_k_reduce_scatter_allgather.cpp:279 -- which the user-op path does not model: it rejects them.)"""
+    non-commutative op makes every operand order visible in the bits.  (The MPICH baselines, which branch on
+    MPI_Op_commutative, have their own suite: usermpich_cases_for.)"""
     out = []
 
     def add(mode, k, b, count, inplace):
@@ -336,6 +335,39 @@ def userop_cases_for(n):
     for b in divisors(n):
         add("irs", 2, b, 5, 0)
         add("ilr", 0, b, 4, 0)
+    return out
+
+
+def usermpich_cases_for(n):
+    """The MPICH baselines (testing/mpich_implementations/{all_reduce,reduce_scatter}/) with a user-defined op: the
+    halfadd function created non-commutative (user_halfadd) and commutative (user_halfadd_c).  The baselines branch
+    on MPI_Op_commutative (allreduce_recursive_doubling.cpp:69, reduce_scatter_recursive_doubling.cpp:134,
+    allreduce_recexch.cpp:343, :378) or refuse a non-commutative op with MPI_ERR_OP
+    (allreduce_k_reduce_scatter_allgather.cpp:279-283; allreduce_recursive_multiplying.cpp:46-49 at a size that is
+    not a power of k); the arithmetic is non-commutative either way, so both paths show in the bits.  The reference's
+    return codes are recorded (ref_rc)."""
+    out = []
+
+    def add(mode, k, b, count, op, inplace):
+        cid = f"{mode}_n{n}_k{k}_b{b}_c{count}_f32_{op}_p0_ip{inplace}"
+        out.append(dict(id=cid, mode=mode, n=n, k=k, b=b, count=count, dtype="f32", op=op,
+                        pattern=pyoracle.PAT_UNIFORM, seed=SEED, inplace=inplace))
+
+    for j, op in enumerate(("user_halfadd", "user_halfadd_c")):
+        for mode in ("ring", "rd", "rsag"):
+            for i, count in enumerate((7, 3 * n + 1, 64)):
+                add(mode, 0, 0, count, op, (i + j) % 2)
+        for k in (2, 3, 4, 5):
+            for spr in (0, 1):
+                add("rx", k, spr, 33, op, (k + spr) % 2)
+        for k in (2, 3, 4):
+            add("krsag", k, 0, 33, op, 0)
+            add("rm", k, 0, 33, op, k % 2)
+        for mode in ("rs_halving", "rs_doubling", "rs_pairwise"):
+            for i, count in enumerate((1, 7, 16)):
+                add(mode, 0, 0, count, op, (i + j) % 2)
+        for k in (2, 3, 4, 5):
+            add("rs_radix", k, 0, 13, op, k % 2)
     return out
 
 
@@ -376,6 +408,10 @@ def main():
         for n in (2, 3, 4, 6, 8):
             all_cases += userop_cases_for(n)
         prefix = "userop_"
+    elif which == "usermpich":
+        for n in (1, 2, 3, 4, 5, 6, 7, 8, 9):
+            all_cases += usermpich_cases_for(n)
+        prefix = "usermpich_"
     elif which == "pairs":
         for n in (2, 3, 4, 5, 6, 8):
             all_cases += pairs_cases_for(n)
@@ -401,6 +437,8 @@ def main():
             out = open(os.path.join(tmp, c["id"] + ".out"), "rb").read()
             libb = open(os.path.join(tmp, c["id"] + ".lib"), "rb").read()
             rec = dict(c)
+            if which == "usermpich":  # every rank's return code (MPI_ERR_OP where the baseline refuses the op)
+                rec["ref_rc"] = [int(x) for x in open(os.path.join(tmp, c["id"] + ".rc")).read().split()]
             rec["sha256"] = hashlib.sha256(out).hexdigest()
             rec["sha256_lib"] = hashlib.sha256(libb).hexdigest()
             npdt = pyoracle.NP_DTYPES[c["dtype"]]
@@ -456,6 +494,8 @@ def main():
                 "Fugaku_experiments/{Allreduce,Reduce-scatter} + testing/custom_implementations/work_dir/"
                 "reduce_scatter/{intra_reduce_scatter_radix,inter_linear_reduce}.cpp, with a user-defined "
                 "non-commutative MPI_Op (see userop_cases_for)" if which == "userop" else
+                "testing/mpich_implementations/{all_reduce,reduce_scatter}/*.cpp with a user-defined MPI_Op, created "
+                "non-commutative and commutative (see usermpich_cases_for)" if which == "usermpich" else
                 "testing/mpich_implementations/all_reduce/{allreduce_ring,allreduce_recursive_doubling,"
                 "allreduce_reduce_scatter_allgather,allreduce_recexch,allreduce_k_reduce_scatter_allgather,"
                 "allreduce_recursive_multiplying}.cpp" if which == "mpich" else

@@ -12,8 +12,14 @@ import pyoracle as po
 import tree_util
 
 
-def load_plans(mode, n, k, b, count, slices=1, schedule=None):
-    return [ca.parse_plan(ca.describe_plan(mode, n, r, k, b, count, slices, schedule)) for r in range(n)]
+def load_plans(mode, n, k, b, count, slices=1, schedule=None, commutative=True):
+    return [ca.parse_plan(ca.describe_plan(mode, n, r, k, b, count, slices, schedule, commutative)) for r in range(n)]
+
+
+def commutative(op):
+    """MPI_Op_commutative of an oracle op name: every predefined op is; the test user op user_halfadd is created
+    non-commutative, user_halfadd_c commutative (chiara_oracle.c orc_commutative)."""
+    return op != "user_halfadd"
 
 
 class RankState:
@@ -124,9 +130,9 @@ def simulate(mode, sends, k, b, dtype, op, inplace=False, slices=1, schedule=Non
     n = len(sends)
     rs = mode in ca.RS_MODES
     count = sends[0].size // n if rs else sends[0].size
-    plans = load_plans(mode, n, k, b, count, slices, schedule)
+    plans = load_plans(mode, n, k, b, count, slices, schedule, commutative(op))
     if plans[0]["header"]["error"]:
-        raise ValueError(f"plan error {plans[0]['header']['error']}")
+        raise ValueError(f"plan error {plans[0]['header']['error']}", plans[0]["header"]["error"])
     outs = execute(plans, sends, dtype, op, inplace)
     if rs:
         outs = [o[:count] for o in outs]

@@ -723,7 +723,8 @@ def _user_op_worker(rank, world, port, q):
     """A user-defined op (chr_op_create; tests/userop/halfadd_op.hip, non-commutative) through RCCL: each rank
     registers the op from its own copy of the code object, then allreduce / reduce-scatter under the flat, exact and
     reference schedules, with overlap off, graphs on (user-op calls run eagerly) and a host-buffer call: bit-exact vs
-    the oracle.  The MPICH baselines refuse it on every rank alike (no rank left waiting)."""
+    the oracle.  MPICH's recursive doubling runs it in rank order; k-reduce-scatter-allgather refuses the
+    non-commutative op on every rank alike (no rank left waiting), and the communicator stays healthy."""
     _setup(rank)
     import ctypes
 
@@ -762,10 +763,17 @@ def _user_op_worker(rank, world, port, q):
                 out = dout.cpu().numpy()
             if rc != 0 or out.tobytes() != want.tobytes():
                 bad.append((mode, k, b, sched, overlap, host, rc))
-        dx = torch.zeros(4096, dtype=torch.float32, device="cuda")
-        rc = ca.MPICH_Allreduce_ring(dx, torch.empty_like(dx), 4096, ca.FLOAT32, half, comm)
+        # the MPICH baselines branch on the op's commutativity: recursive doubling keeps rank order
+        # (allreduce_recursive_doubling.cpp:69-80), k-reduce-scatter-allgather refuses it (MPI_ERR_OP)
+        allx = [po.fill(4099, "f32", po.PAT_UNIFORM, 77, r) for r in range(world)]
+        dx = torch.from_numpy(allx[rank]).cuda()
+        dout = torch.zeros_like(dx)
+        rc = ca.MPICH_Allreduce_recursive_doubling(dx, dout, 4099, ca.FLOAT32, half, comm)
+        if rc != 0 or dout.cpu().numpy().tobytes() != po.mpich_allreduce("rd", allx, "f32", "user_halfadd")[rank].tobytes():
+            bad.append(("rd", rc))
+        rc = ca.MPICH_Allreduce_k_reduce_scatter_allgather(dx, dout, 4099, ca.FLOAT32, half, comm, 2, 0)
         if rc != ca.ERR_UNSUPPORTED:
-            bad.append(("ring", rc))
+            bad.append(("krsag", rc))
         # the communicator is still healthy after the refusal: a predefined op right after
         rc = ca.all_reduce_radix_batch(dx, torch.empty_like(dx), 4096, ca.FLOAT32, ca.SUM, comm, 2, 2)
         torch.cuda.synchronize()

@@ -5,8 +5,11 @@ MPI_Op_create(halfadd, commute = 0) -- inout = in * 0.5f + inout on float, non-c
 shows in the bits -- as the caller's own device code (tests/userop/halfadd_op.hip through include/chiara_user_op.hpp).
 The collectives must reproduce the reference's outputs for the same op bit for bit (tests/golden/userop_outputs.npz:
 the reference compiled unchanged against MPICH with that MPI_Op), and every fold / tree the library evaluates must
-match the oracle's restatement (chiara_oracle.c ORC_USER_HALFADD).  The MPICH baselines branch on
-MPI_Op_commutative; they refuse user ops (CHR_ERR_UNSUPPORTED), as does a launcher that refuses the call."""
+match the oracle's restatement (chiara_oracle.c ORC_USER_HALFADD).  The MPICH baselines take user ops as the
+reference's do: branching on MPI_Op_commutative, so the same function registered commutative and non-commutative
+(tests/golden/usermpich_outputs.npz, the reference run with both) gives different bits, and refusing a
+non-commutative op where the reference returns MPI_ERR_OP (CHR_ERR_UNSUPPORTED, as for a launcher that refuses the
+call)."""
 import ctypes
 import json
 import os
@@ -24,6 +27,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 USEROP_SO = os.path.join(HERE, "userop", "libhalfadd_op.so")
 MAN = json.load(open(os.path.join(HERE, "golden", "userop_manifest.json")))
 FIX = np.load(os.path.join(HERE, "golden", "userop_outputs.npz"), allow_pickle=False)
+MMAN = json.load(open(os.path.join(HERE, "golden", "usermpich_manifest.json")))
+MFIX = np.load(os.path.join(HERE, "golden", "usermpich_outputs.npz"), allow_pickle=False)
 OPN = "user_halfadd"
 
 
@@ -36,13 +41,15 @@ def gu():
 
 @pytest.fixture(scope="module")
 def ops():
-    """(halfadd, refusing) op codes, registered from the test's own code object and freed at the end."""
+    """(halfadd, refusing, halfadd registered commutative) op codes, registered from the test's own code object and
+    freed at the end."""
     assert os.path.exists(USEROP_SO), f"{USEROP_SO} missing: make -C tests/userop (__graft_entry__.build())"
     lib = ctypes.CDLL(USEROP_SO)
     half = ca.op_create(ctypes.cast(lib.chr_test_halfadd, ctypes.c_void_p).value)
     refuse = ca.op_create(ctypes.cast(lib.chr_test_refuse, ctypes.c_void_p).value)
-    yield half, refuse
-    assert ca.op_free(half) == 0 and ca.op_free(refuse) == 0
+    half_c = ca.op_create(ctypes.cast(lib.chr_test_halfadd, ctypes.c_void_p).value, commute=True)
+    yield half, refuse, half_c
+    assert ca.op_free(half) == 0 and ca.op_free(refuse) == 0 and ca.op_free(half_c) == 0
 
 
 @pytest.fixture(scope="module")
@@ -84,7 +91,7 @@ def _chain_ref(acc, ins, running_first):
 def test_fold_matches_oracle(gu, ops, m, n):
     """chr_reduce_multi_ex with a user op: m incoming buckets into the accumulator, both operand orders, fan-in above
     the functor kernel's kMaxIns (17: two launches), out of place and in place (out = acc)."""
-    half, _ = ops
+    half = ops[0]
     acc = po.fill(n, "f32", po.PAT_UNIFORM, 21, 0)
     ins = [po.fill(n, "f32", po.PAT_UNIFORM, 21, j + 1) for j in range(m)]
     d_ins = [gu.to_dev(x) for x in ins]
@@ -101,7 +108,7 @@ def test_fold_matches_oracle(gu, ops, m, n):
 
 
 def test_reduce_local_matches_oracle(gu, ops):
-    half, _ = ops
+    half = ops[0]
     n = 77777
     x = po.fill(n, "f32", po.PAT_UNIFORM, 5, 0)
     y = po.fill(n, "f32", po.PAT_UNIFORM, 5, 1)
@@ -118,7 +125,7 @@ SWAP_TREE = ([0, 1, 1, 1, 0, 1, 1, 2], [1, 0, 1, 0, 1, 0, 1])     # running-valu
 def test_trees_match_oracle(gu, ops):
     """chr_reduce_tree with a user op: the post-order program evaluated fold by fold (user_ops.cpp user_tree), fixed
     and random programs of 1..8 leaves with random swap bits, out of place and into a leaf."""
-    half, _ = ops
+    half = ops[0]
     rng = np.random.default_rng(7)
     progs = [C4_TREE, SWAP_TREE, ([0], [])] + [random_program(rng, nl) for nl in (2, 3, 5, 6, 7, 8, 8)]
     n = 65537
@@ -134,7 +141,7 @@ def test_trees_match_oracle(gu, ops):
 
 
 def test_tree_batch_matches_oracle(gu, ops):
-    half, _ = ops
+    half = ops[0]
     rng = np.random.default_rng(9)
     n, nt, nl = 4099, 5, 6
     progs = [random_program(rng, nl) for _ in range(nt)]
@@ -181,7 +188,7 @@ def test_collectives_match_reference_golden(gu, ops, groups, schedule):
     that divides n, k = 2..4, in place and not; CHiArA's phases) bit-exact on the device.  The flat schedule evaluates
     each chunk as one expression tree, the exact one replays the reference's messages -- both must land on the
     reference's operand order."""
-    half, _ = ops
+    half = ops[0]
     bad = []
     for c in MAN["cases"]:
         g = groups(c["n"])
@@ -198,7 +205,7 @@ def test_collectives_match_reference_golden(gu, ops, groups, schedule):
 @pytest.mark.parametrize("n,k,b,slices", [(8, 4, 4, 1), (8, 2, 8, 4), (6, 3, 2, 2)])
 def test_collectives_large_vs_oracle(gu, ops, groups, n, k, b, slices):
     """MiB-sized buckets (the scratch-backed tree evaluation at size, sliced plans): bit-exact vs the oracle."""
-    half, _ = ops
+    half = ops[0]
     count = n * ((1 << 17) + 5)
     sends = [po.fill(count, "f32", po.PAT_UNIFORM, 17, r) for r in range(n)]
     g = groups(n)
@@ -219,7 +226,7 @@ def test_comm_single_rank_with_graphs(gu, ops):
     is the caller's and may not be capturable) -- then a predefined op still replays its graph."""
     import torch
 
-    half, _ = ops
+    half = ops[0]
     comm = ca.Comm(1, ca.get_unique_id(), 0, 0)
     try:
         comm.set_graphs(True)
@@ -234,19 +241,59 @@ def test_comm_single_rank_with_graphs(gu, ops):
         comm.destroy()
 
 
+MPICH_AR = {"ring": ca.MODE_MPICH_RING, "rd": ca.MODE_MPICH_RD, "rsag": ca.MODE_MPICH_RSAG,
+            "rx": ca.MODE_MPICH_RECEXCH, "krsag": ca.MODE_MPICH_KRSAG, "rm": ca.MODE_MPICH_RMULT}
+MPICH_RS = {"rs_radix": ca.MODE_MPICH_RS_RADIX, "rs_halving": ca.MODE_MPICH_RS_HALVING,
+            "rs_doubling": ca.MODE_MPICH_RS_DOUBLING, "rs_pairwise": ca.MODE_MPICH_RS_PAIRWISE}
+
+
+def test_mpich_baselines_match_reference_golden(gu, ops, groups):
+    """The ten MPICH baselines with the user op registered non-commutative and commutative: every golden case of the
+    reference (gen_golden.py usermpich) bit-exact on the device, and CHR_ERR_UNSUPPORTED wherever the reference
+    returned MPI_ERR_OP."""
+    half, _, half_c = ops
+    bad = []
+    for c in MMAN["cases"]:
+        n, count, ip = c["n"], c["count"], bool(c["inplace"])
+        op = half if c["op"] == "user_halfadd" else half_c
+        rs = c["mode"] in MPICH_RS
+        in_n = count * n if rs else count
+        sends = [po.fill(in_n, "f32", c["pattern"], c["seed"], r) for r in range(n)]
+        if ip:
+            d_recv, d_send = [gu.to_dev(s) for s in sends], [ca.IN_PLACE] * n
+        else:
+            d_recv, d_send = [gu.empty_dev(count * 4) for _ in range(n)], [gu.to_dev(s) for s in sends]
+        g = groups(n)
+        if rs:
+            rc = g.reduce_scatter_mpich(MPICH_RS[c["mode"]], d_send, d_recv, count, ca.FLOAT32, op, c["k"])
+        else:
+            rc = g.allreduce_mpich(MPICH_AR[c["mode"]], d_send, d_recv, count, ca.FLOAT32, op, c["k"], c["b"])
+        if 9 in c["ref_rc"]:  # the reference's MPI_ERR_OP
+            if rc != ca.ERR_UNSUPPORTED:
+                bad.append((c["id"], rc))
+            continue
+        got = np.concatenate([gu.from_dev(d, np.float32, count) for d in d_recv])
+        if rc != 0 or not np.array_equal(_u32(got), _u32(MFIX[c["id"]])):
+            bad.append((c["id"], rc))
+    assert not bad, f"{len(bad)} device/reference mismatches, e.g. {bad[:5]}"
+
+
 # ---- refusals ---------------------------------------------------------------------------------
 
 def test_refusals(gu, ops, groups):
-    """MPICH baselines branch on MPI_Op_commutative: user ops are CHR_ERR_UNSUPPORTED there.  A launcher that
-    refuses a call hands its verdict back (CHR_ERR_UNSUPPORTED), and a freed or never-created op code is
-    CHR_ERR_INVALID_ARG -- for the kernels and the collectives."""
-    half, refuse = ops
+    """The reference's MPI_ERR_OP for a non-commutative op (k-reduce-scatter-allgather; recursive multiplying at a
+    size that is not a power of k) is CHR_ERR_UNSUPPORTED.  A launcher that refuses a call hands its verdict back
+    (CHR_ERR_UNSUPPORTED), and a freed or never-created op code is CHR_ERR_INVALID_ARG -- for the kernels and the
+    collectives."""
+    half, refuse = ops[:2]
     n = 4
     g = groups(n)
     d = [gu.empty_dev(64 * 4) for _ in range(n)]
     dr = [gu.empty_dev(64 * 4) for _ in range(n)]
-    assert g.allreduce_mpich(ca.MODE_MPICH_RING, d, dr, 64, ca.FLOAT32, half, 2, 1) == ca.ERR_UNSUPPORTED
-    assert g.reduce_scatter_mpich(ca.MODE_MPICH_RS_HALVING, d, dr, 16, ca.FLOAT32, half) == ca.ERR_UNSUPPORTED
+    assert g.allreduce_mpich(ca.MODE_MPICH_KRSAG, d, dr, 64, ca.FLOAT32, half, 2, 0) == ca.ERR_UNSUPPORTED
+    assert groups(6).allreduce_mpich(ca.MODE_MPICH_RMULT, [gu.empty_dev(64 * 4) for _ in range(6)],
+                                     [gu.empty_dev(64 * 4) for _ in range(6)], 64, ca.FLOAT32, half, 4, 0) == \
+        ca.ERR_UNSUPPORTED  # 6 is not a power of 4
     assert g.all_reduce_radix_batch(d, dr, 64, ca.FLOAT32, refuse, 2, 2) == ca.ERR_UNSUPPORTED
     assert ca.reduce_local(d[0], d[1], 64, ca.FLOAT32, refuse, gu.stream()) == ca.ERR_UNSUPPORTED
     gu.sync()
