@@ -254,6 +254,8 @@ def line_problems(line, rccl_library=True):
             probs.append("result_check missing")
         elif not (rc.get("ranks_bit_identical") and rc.get("within_tolerance")):
             probs.append(f"result_check failed: {rc}"[:300])
+        elif rc.get("exact_known_answer") is False:
+            probs.append(f"result_check exact known answer failed: {rc}"[:300])
         if rf is not None and rf.get("traffic") is None and not rf.get("traffic_stale"):
             probs.append("roofline.traffic null without traffic_stale")
         c5 = (line.get("compare") or {}).get("c5_allreduce_bf16_k4_b4_1GiB")
@@ -264,6 +266,8 @@ def line_problems(line, rccl_library=True):
             c5rc = c5.get("result_check")
             if c5rc is not None and not (c5rc.get("ranks_bit_identical") and c5rc.get("within_tolerance")):
                 probs.append(f"c5 result_check failed: {c5rc}"[:300])
+            elif c5rc is not None and c5rc.get("exact_known_answer") is False:
+                probs.append(f"c5 result_check exact known answer failed: {c5rc}"[:300])
         if line["definitions"] != LINE_DEFINITIONS_NN:
             probs.append("definitions differ from LINE_DEFINITIONS_NN")
     cb = line["cpu_baseline"]
@@ -1125,6 +1129,11 @@ def bench_allreduce(args):
             ca.check(ca.fill(buf, count, dt, 0, SEED, r, stream=stream))
             torch.cuda.synchronize()
         check = result_check(torch, dist, recv, count, es, world, fill_rank)
+        # and bit for bit against a known answer: one more call of the same configuration on integer-valued inputs
+        check.update(exact_check(
+            torch, dist, send, recv, count, es, rank,
+            lambda: ca.check(ca.all_reduce_radix_batch(send, recv, count, dt, ca.SUM, comm, k, b)), world))
+        fill_rank(rank, send)  # the metric's inputs back for the comparison lines
     except Exception as e:  # recorded, never hidden: line_problems() flags a line without a passing check
         check = {"error": str(e)[:200]}
     torch.cuda.empty_cache()
@@ -1302,6 +1311,44 @@ def result_check(torch, dist, recv, count, es, world, fill_rank, window=1 << 26)
             "max_abs_err": max(float(t[4]) for t in allv),
             "checksum_rank0": f"{hs[0][0]:016x}:{hs[0][1]:016x}",
             "tolerance": f"|x - fp64 sum| <= (N-1) x {tol_ulp:.3g} x sum|x_i| (DESIGN §7), every element, every rank"}
+
+
+KNOWN_ANSWER_MUL, KNOWN_ANSWER_RANK = 2654435761, 40503
+
+
+def known_answer_input(torch, idx, r):
+    """Rank r's integer-valued input at positions idx (int64): in [-16, 15], so every partial sum of at most 8 ranks
+    (|.| <= 128) is exact in f32 and bf16 whatever the association -- the answer is known without the oracle."""
+    return ((idx * KNOWN_ANSWER_MUL + r * KNOWN_ANSWER_RANK) >> 7) % 32 - 16
+
+
+def exact_check(torch, dist, send, recv, count, es, rank, run, world, window=1 << 26):
+    """The reference harness's own check (Allreduce/main.cpp:55-69: known inputs, exact equality), at the metric's
+    size and configuration: every rank's send buffer gets integer-valued data (known_answer_input), `run()` makes one
+    call, and every element of every rank's output must EQUAL the sum of the N inputs -- bit for bit, on the wire and
+    in the reductions, with no tolerance.  (Association order, which exact sums cannot show, is pinned by the
+    reference's goldens and the full-size LocalGroup / RCCL-process tests.)"""
+    tdt = torch.float32 if es == 4 else torch.bfloat16
+    src = send[:count * es].view(tdt)
+    for w0 in range(0, count, window):
+        w1 = min(count, w0 + window)
+        idx = torch.arange(w0, w1, device=send.device, dtype=torch.int64)
+        src[w0:w1] = known_answer_input(torch, idx, rank).to(tdt)
+    sync = torch.cuda.synchronize if send.is_cuda else (lambda: None)
+    sync()
+    run()
+    sync()
+    out = recv[:count * es].view(tdt)
+    bad = 0
+    for w0 in range(0, count, window):
+        w1 = min(count, w0 + window)
+        idx = torch.arange(w0, w1, device=recv.device, dtype=torch.int64)
+        want = sum(known_answer_input(torch, idx, r) for r in range(world))
+        bad += int((out[w0:w1].to(torch.float64) != want.to(torch.float64)).sum())
+    t = torch.tensor([bad], dtype=torch.int64)
+    dist.all_reduce(t)
+    return {"exact_known_answer": int(t.item()) == 0, "exact_violations": int(t.item()),
+            "exact": "integer-valued inputs in [-16, 15]: every element of every rank == the sum of the N inputs"}
 
 
 def _timed_max(torch, dist, fn, steps, warmup, comm=None):
@@ -1541,6 +1588,10 @@ def baseline_configs(args, ca, torch, dist, comm, world, dev, steps, warm, late=
                     torch.cuda.synchronize()
                 ca.check(comm.synchronize())
                 row["result_check"] = result_check(torch, dist, r5, cnt, 2, world, fill5)
+                row["result_check"].update(exact_check(
+                    torch, dist, s5, r5, cnt, 2, int(os.environ["RANK"]),
+                    lambda: ca.check(ca.all_reduce_radix_batch(s5, r5, cnt, ca.BFLOAT16, ca.SUM, comm, 4, 4)), world))
+                fill5(int(os.environ["RANK"]), s5)
             except Exception as e:
                 row["result_check"] = {"error": str(e)[:200]}
             torch.cuda.empty_cache()

@@ -49,7 +49,19 @@ def _worker(rank, world, port, es, fault, q):
         def fill_rank(r, buf):
             buf.view(xs[r].dtype)[:COUNT].copy_(xs[r])
 
-        q.put((rank, bench.result_check(torch, dist, recv, COUNT, es, world, fill_rank, window=1024)))
+        res = bench.result_check(torch, dist, recv, COUNT, es, world, fill_rank, window=1024)
+        send = torch.zeros(COUNT * es, dtype=torch.uint8)
+        out = torch.zeros(COUNT * es, dtype=torch.uint8)
+
+        def run():  # an allreduce of the known-answer inputs (gloo sums integer-valued floats exactly)
+            x = send.view(xs[0].dtype).float()
+            dist.all_reduce(x)
+            if fault == "exact_off_by_one" and rank == 1:
+                x[2999] += 1
+            out.view(xs[0].dtype).copy_(x.to(xs[0].dtype))
+
+        res.update(bench.exact_check(torch, dist, send, out, COUNT, es, rank, run, world, window=1024))
+        q.put((rank, res))
     finally:
         dist.destroy_process_group()
 
@@ -78,6 +90,16 @@ def test_correct_allreduce_passes(es):
     assert out[0]["checksum_rank0"] == out[1]["checksum_rank0"]
 
 
+@pytest.mark.parametrize("es", [4, 2])
+def test_exact_known_answer(es):
+    """The known-answer call: integer-valued inputs, every element equal to the sum -- passes on a correct allreduce
+    (f32 and bf16: the partial sums stay exact), fails on one wrong element of one rank."""
+    for r, c in _run(es, None).items():
+        assert c["exact_known_answer"] and c["exact_violations"] == 0, c
+    c = _run(es, "exact_off_by_one")[0]
+    assert c["exact_known_answer"] is False and c["exact_violations"] == 1
+
+
 def test_one_rank_differing_is_caught():
     c = _run(4, "one_rank_differs")[0]
     assert c["ranks_bit_identical"] is False
@@ -97,6 +119,9 @@ def test_line_problems_flags_a_failed_check():
 
     line = _nn_line()
     assert bench.line_problems(line) == []
+    line["result_check"]["exact_known_answer"] = False
+    assert any("exact known answer failed" in p for p in bench.line_problems(line))
+    line["result_check"]["exact_known_answer"] = True
     line["result_check"]["within_tolerance"] = False
     assert any("result_check failed" in p for p in bench.line_problems(line))
     line.pop("result_check")
