@@ -270,6 +270,9 @@ def line_problems(line, rccl_library=True):
                 probs.append(f"c5 result_check exact known answer failed: {c5rc}"[:300])
         if line["definitions"] != LINE_DEFINITIONS_NN:
             probs.append("definitions differ from LINE_DEFINITIONS_NN")
+    rc1 = line.get("result_check") if line.get("n_gpus") == 1 else None
+    if rc1 is not None and not rc1.get("bit_exact_vs_torch_add"):
+        probs.append(f"result_check failed: {rc1}"[:300])
     cb = line["cpu_baseline"]
     if cb is not None:
         probs += [f"cpu_baseline.{k} missing" for k in ("value", "unit", "cores", "kind", "sample") if k not in cb]
@@ -412,6 +415,7 @@ def bench_bucket(args, cpu):
     }
     if stale:
         line["roofline"]["traffic_stale"] = stale
+    line["result_check"] = bucket_result_check(torch, ca, accs[0], ins[0], n, stream)
     if cpu:
         line["gpu_vs_cpu"] = round(line["value"] / cpu["value"], 1)
         if "all_cores" in cpu:
@@ -419,6 +423,21 @@ def bench_bucket(args, cpu):
     if args.sweep:
         line["sweep"] = sweep(ca, torch, dev, stream)
     emit(line)
+
+
+def bucket_result_check(torch, ca, acc, inc, n, stream):
+    """The metric's own output, untimed, without the oracle: one more launch on a bucket set of the timed region,
+    every element bit-compared with torch's fp32 add of the same two buckets (MPI_Reduce_local SUM on MPI_FLOAT is one
+    IEEE round-to-nearest add per element, commutative for these NaN-free inputs, so an independent implementation
+    must give the same bits)."""
+    before = acc.clone()
+    ca.check(ca.reduce_local(inc, acc, n, ca.FLOAT32, ca.SUM, stream))
+    torch.cuda.synchronize()
+    want = before + inc
+    bad = int((acc.view(torch.int32) != want.view(torch.int32)).sum())
+    del before, want
+    return {"bit_exact_vs_torch_add": bad == 0, "mismatches": bad, "elements": n,
+            "check": "one more launch on bucket set 0: every element == torch's fp32 (in + inout), bit for bit"}
 
 
 def sweep(ca, torch, dev, stream):

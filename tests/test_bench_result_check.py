@@ -126,3 +126,18 @@ def test_line_problems_flags_a_failed_check():
     assert any("result_check failed" in p for p in bench.line_problems(line))
     line.pop("result_check")
     assert any("result_check missing" in p for p in bench.line_problems(line))
+
+
+def test_line_problems_flags_a_failed_n1_check():
+    """The N = 1 line's own check (bench.bucket_result_check: one more launch, every element == torch's fp32 add):
+    absent on older lines is fine, a failed one is a problem."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    import bench
+    from test_bench_line import _n1_line
+
+    line = _n1_line()
+    assert bench.line_problems(line) == []
+    line["result_check"] = {"bit_exact_vs_torch_add": True, "mismatches": 0, "elements": 16}
+    assert bench.line_problems(line) == []
+    line["result_check"] = {"bit_exact_vs_torch_add": False, "mismatches": 3, "elements": 16}
+    assert any("result_check failed" in p for p in bench.line_problems(line))
