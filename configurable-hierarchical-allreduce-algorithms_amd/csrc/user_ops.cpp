@@ -51,30 +51,70 @@ int call(const UserOp& u, void* out, const void* acc, const void* const* ins, in
 
 // One post-order program (launch_reduce_tree's contract): push leaf j, then comb[j] combines, each popping the top
 // `in` and folding it into the value below -- MPI_Reduce_local(in, below), or with the combine's swap bit
-// MPI_Reduce_local(below, in) (MPICH_do_reduce's order), the running-value-first form of the launcher.  A combine
-// at stack position p writes scratch slot p: it reads the value below (a leaf, or slot p itself) and the top (a leaf
-// or slot p + 1), so no input is ever written.  The root is copied to `out` after the last fold.
+// MPI_Reduce_local(below, in) (MPICH_do_reduce's order), the running-value-first form of the launcher.  Consecutive
+// combines that fold leaves into the same running value in the same order are one chain -- one launcher call with
+// m inputs, as chr_reduce_multi_ex would make it -- so C4's tree ((l0 l1 l2 l3)(l4 l5 l6 l7)) is three calls, not
+// seven.  A chain's result goes to scratch slot p (its stack position; it may read slot p itself as the running
+// value, never as an input), the last one straight to `out` unless `out` is one of its inputs.
 int user_tree(const UserOp& u, void* out, const void* const* leaves, int nl, const uint8_t* comb,
               const uint8_t* swaps, size_t n, int dtype, hipStream_t s) {
     const size_t bytes = n * dtype_size(dtype);
     void* slot[8] = {};  // stack positions: at most 8 leaves (tree_program_ok)
-    std::vector<const void*> st;
-    int ci = 0, rc = CHR_SUCCESS;
+    struct Val {
+        const void* p;
+        bool leaf;
+    };
+    struct Chain {
+        int pos = -1;  // stack position of the running value; -1: none pending
+        const void* acc = nullptr;
+        std::vector<const void*> ins;
+        bool rf = false;
+    } ch;
+    std::vector<Val> st;
+    int rc = CHR_SUCCESS;
+    auto flush = [&](bool last) -> int {
+        if (ch.pos < 0) return CHR_SUCCESS;
+        void* dst = nullptr;
+        if (last) {
+            bool out_is_input = false;
+            for (const void* q : ch.ins) out_is_input |= q == out;
+            if (!out_is_input) dst = out;
+        }
+        if (!dst) {
+            if (!slot[ch.pos])
+                if (int e = hip_status(hipMallocAsync(&slot[ch.pos], bytes, s))) return e;
+            dst = slot[ch.pos];
+        }
+        const int e = call(u, dst, ch.acc, ch.ins.data(), (int)ch.ins.size(), n, dtype, ch.rf, s);
+        st[ch.pos] = {dst, false};
+        ch.pos = -1;
+        ch.ins.clear();
+        return e;
+    };
+    int ci = 0;
     for (int j = 0; j < nl && !rc; ++j) {
-        st.push_back(leaves[j]);
+        st.push_back({leaves[j], true});
         for (int c = 0; c < comb[j] && !rc; ++c, ++ci) {
-            const void* top = st.back();
+            const int p = (int)st.size() - 2;  // the running value's position; the top is at p + 1
+            const bool rf = swaps && swaps[ci];
+            if (ch.pos == p && ch.rf == rf && st.back().leaf) {  // a leaf into the pending chain's running value
+                ch.ins.push_back(st.back().p);
+                st.pop_back();
+                continue;
+            }
+            if ((rc = flush(false))) break;  // the pending chain's value lands in st[] before it is read
+            ch.pos = p;
+            ch.acc = st[p].p;
+            ch.ins.assign(1, st.back().p);
+            ch.rf = rf;
             st.pop_back();
-            const size_t p = st.size() - 1;
-            if (!slot[p] && (rc = hip_status(hipMallocAsync(&slot[p], bytes, s)))) break;
-            rc = call(u, slot[p], st.back(), &top, 1, n, dtype, swaps && swaps[ci], s);
-            st.back() = slot[p];
         }
     }
-    if (!rc && st.size() == 1 && st[0] != out)
-        rc = hip_status(hipMemcpyAsync(out, st[0], bytes, hipMemcpyDeviceToDevice, s));
-    for (void* p : slot)
-        if (p) (void)hipFreeAsync(p, s);
+    if (!rc) rc = flush(true);
+    if (!rc && st.size() == 1 && st[0].p != out)
+        rc = hip_status(hipMemcpyAsync(out, st[0].p, bytes, hipMemcpyDeviceToDevice, s));
+    for (void* q : slot)
+        if (q) (void)hipFreeAsync(q, s);
     return rc;
 }
 
