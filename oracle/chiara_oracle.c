@@ -40,7 +40,7 @@ size_t orc_dtype_size(int dtype) {
 int orc_commutative(int op) { return op != ORC_USER_HALFADD; }
 
 int orc_valid(int dtype, int op) {
-    if (op == ORC_USER_HALFADD || op == ORC_USER_HALFADD_C) return dtype == ORC_F32;
+    if (op == ORC_USER_HALFADD || op == ORC_USER_HALFADD_C) return dtype == ORC_F32 || dtype == ORC_F64 || dtype == ORC_I32;
     if (!orc_dtype_size(dtype) || op < ORC_SUM || op > ORC_MINLOC) return 0;
     if (dtype >= ORC_FI && dtype <= ORC_SI) return op == ORC_MAXLOC || op == ORC_MINLOC;
     if (dtype == ORC_CF || dtype == ORC_CD) return op == ORC_SUM || op == ORC_PROD;
@@ -415,7 +415,8 @@ void orc_reduce_local(const void* in, void* inout, size_t n, int dtype, int op) 
         else if (op == ORC_LXOR) ORC_LOOP(float, (float)(!y != !x));
         break;
     case ORC_F64:
-        if (op == ORC_SUM) ORC_LOOP(double, orc_x86d(y, x, ORC_XADD));
+        if (op == ORC_USER_HALFADD || op == ORC_USER_HALFADD_C) ORC_LOOP(double, x * 0.5 + y);
+        else if (op == ORC_SUM) ORC_LOOP(double, orc_x86d(y, x, ORC_XADD));
         else if (op == ORC_PROD) ORC_LOOP(double, orc_x86d(y, x, ORC_XMUL));
         else if (op == ORC_MAX) ORC_LOOP(double, y > x ? y : x);
         else if (op == ORC_MIN) ORC_LOOP(double, y < x ? y : x);
@@ -423,7 +424,10 @@ void orc_reduce_local(const void* in, void* inout, size_t n, int dtype, int op) 
         else if (op == ORC_LOR) ORC_LOOP(double, (double)(y || x));
         else if (op == ORC_LXOR) ORC_LOOP(double, (double)(!y != !x));
         break;
-    case ORC_I32: ORC_INT_CASE(int32_t, uint32_t, uint32_t) break;
+    case ORC_I32:
+        if (op == ORC_USER_HALFADD || op == ORC_USER_HALFADD_C) ORC_LOOP(int32_t, (int32_t)((uint32_t)x * 3u + (uint32_t)y));
+        else ORC_INT_CASE(int32_t, uint32_t, uint32_t)
+        break;
     case ORC_I8: ORC_INT_CASE(int8_t, uint8_t, uint32_t) break;
     case ORC_U8: ORC_INT_CASE(uint8_t, uint8_t, uint32_t) break;
     case ORC_I16: ORC_INT_CASE(int16_t, uint16_t, uint32_t) break;

@@ -41,9 +41,10 @@ enum {
     ORC_LAND = 4, ORC_LOR = 5, ORC_LXOR = 6, ORC_BAND = 7, ORC_BOR = 8, ORC_BXOR = 9,
     ORC_MAXLOC = 10, ORC_MINLOC = 11,
     /* A user-defined, non-commutative MPI op for the user-op path (MPI_Op_create(fn, commute = 0)): MPI's user
-     * function computes inout[i] = in[i] o inout[i]; this one, on MPI_FLOAT, is in * 0.5f + inout (rounded after
-     * the multiply: no contraction).  Test infrastructure: the same function is the reference's op in
-     * oracle/ref_driver.cpp and the device op in tests/userop/halfadd_op.hip. */
+     * function computes inout[i] = in[i] o inout[i]; this one is in * 0.5f + inout on MPI_FLOAT (rounded after the
+     * multiply: no contraction), in * 0.5 + inout on MPI_DOUBLE and 3 * in + inout (wrapping) on MPI_INT.  Test
+     * infrastructure: the same function is the reference's op in oracle/ref_driver.cpp and the device op in
+     * tests/userop/halfadd_op.hip. */
     ORC_USER_HALFADD = 12,
     /* The same function created commutative (MPI_Op_create(fn, commute = 1)): identical arithmetic, but the MPICH
      * baselines that branch on MPI_Op_commutative take their commutative paths (allreduce_recursive_doubling.cpp:69,

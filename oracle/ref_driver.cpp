@@ -84,13 +84,26 @@ static void bf16_user_prod(void* in, void* inout, int* len, MPI_Datatype*) {
 }
 
 // The user-defined op of the user-op path (chiara_oracle.h ORC_USER_HALFADD), written here independently of the
-// oracle: MPI's user-function contract inout[i] = in[i] o inout[i], o = in * 0.5f + inout; created non-commutative.
-static void halfadd_user_op(void* in, void* inout, int* len, MPI_Datatype*) {
-    const float* a = (const float*)in;
-    float* b = (float*)inout;
-    for (int i = 0; i < *len; ++i) {
-        const float h = a[i] * 0.5f;
+// oracle: MPI's user-function contract inout[i] = in[i] o inout[i], o = in * 0.5 + inout on MPI_FLOAT / MPI_DOUBLE,
+// 3 * in + inout (wrapping) on MPI_INT; created non-commutative (and, as user_halfadd_c, commutative).
+template <typename T>
+static void halfadd_loop(const void* in, void* inout, int len) {
+    const T* a = (const T*)in;
+    T* b = (T*)inout;
+    for (int i = 0; i < len; ++i) {
+        const T h = a[i] * (T)0.5;
         b[i] = h + b[i];
+    }
+}
+static void halfadd_user_op(void* in, void* inout, int* len, MPI_Datatype* dt) {
+    if (*dt == MPI_DOUBLE) {
+        halfadd_loop<double>(in, inout, *len);
+    } else if (*dt == MPI_INT) {
+        const uint32_t* a = (const uint32_t*)in;
+        uint32_t* b = (uint32_t*)inout;
+        for (int i = 0; i < *len; ++i) b[i] = a[i] * 3u + b[i];
+    } else {
+        halfadd_loop<float>(in, inout, *len);
     }
 }
 

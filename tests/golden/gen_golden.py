@@ -323,18 +323,26 @@ def userop_cases_for(n):
     MPI_Op_commutative, have their own suite: usermpich_cases_for.)"""
     out = []
 
-    def add(mode, k, b, count, inplace):
-        cid = f"{mode}_n{n}_k{k}_b{b}_c{count}_f32_user_halfadd_p0_ip{inplace}"
-        out.append(dict(id=cid, mode=mode, n=n, k=k, b=b, count=count, dtype="f32", op="user_halfadd",
+    def add(mode, k, b, count, inplace, dt="f32"):
+        cid = f"{mode}_n{n}_k{k}_b{b}_c{count}_{dt}_user_halfadd_p0_ip{inplace}"
+        out.append(dict(id=cid, mode=mode, n=n, k=k, b=b, count=count, dtype=dt, op="user_halfadd",
                         pattern=pyoracle.PAT_UNIFORM, seed=SEED, inplace=inplace))
 
     for i, b in enumerate(divisors(n)):
         for k in (2, 3, 4):
             add("ar", k, b, n * 16 + (n if k == 3 else 0), (i + k) % 2)
             add("rs", k, b, 9 + k, 0)
+        # the same function on MPI_DOUBLE (in * 0.5 + inout) and MPI_INT (3 * in + inout, wrapping): the user-op
+        # path at 8- and 4-byte integer elements
+        for j, dt in enumerate(("f64", "i32")):
+            k = (2, 3, 4)[(i + j) % 3]
+            add("ar", k, b, n * 8 + (n if j else 0), (i + j) % 2, dt)
+            add("rs", k, b, 7 + j, 0, dt)
     for b in divisors(n):
         add("irs", 2, b, 5, 0)
         add("ilr", 0, b, 4, 0)
+        add("irs", 3, b, 6, 0, "f64")
+        add("ilr", 0, b, 3, 0, "i32")
     return out
 
 

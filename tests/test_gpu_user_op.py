@@ -161,31 +161,37 @@ def test_tree_batch_matches_oracle(gu, ops):
 PHASE_MODE = {"irs": ca.MODE_INTRA_REDUCE_SCATTER, "ilr": ca.MODE_INTER_REDUCE_LINEAR}
 
 
+UDT = {"f32": ca.FLOAT32, "f64": ca.FLOAT64, "i32": ca.INT32}  # the types the test op's launcher implements
+
+
 def _run_case(gu, g, c, op):
     """Every rank's output of golden case c through the local group (rank-major, as the fixture stores them)."""
     n, k, b, count, mode, ip = c["n"], c["k"], c["b"], c["count"], c["mode"], bool(c["inplace"])
+    dt, npdt = c["dtype"], po.NP_DTYPES[c["dtype"]]
+    es = np.dtype(npdt).itemsize
     if mode in PHASE_MODE:
         in_n, out_n = po.phase_sizes(mode, n, b, count)
     else:
         in_n, out_n = (count * n if mode == "rs" else count), count
-    sends = [po.fill(in_n, "f32", c["pattern"], c["seed"], r, in_n) for r in range(n)]
+    sends = [po.fill(in_n, dt, c["pattern"], c["seed"], r, in_n) for r in range(n)]
     if ip:
         d_recv, d_send = [gu.to_dev(s) for s in sends], [ca.IN_PLACE] * n
     else:
-        d_recv, d_send = [gu.empty_dev(out_n * 4) for _ in range(n)], [gu.to_dev(s) for s in sends]
+        d_recv, d_send = [gu.empty_dev(out_n * es) for _ in range(n)], [gu.to_dev(s) for s in sends]
     if mode in PHASE_MODE:
-        rc = g.phase_collective(PHASE_MODE[mode], d_send, d_recv, count, ca.FLOAT32, op, k, b)
+        rc = g.phase_collective(PHASE_MODE[mode], d_send, d_recv, count, UDT[dt], op, k, b)
     else:
         fn = g.all_reduce_radix_batch if mode == "ar" else g.reduce_scatter_radix_batch
-        rc = fn(d_send, d_recv, count, ca.FLOAT32, op, k, b)
+        rc = fn(d_send, d_recv, count, UDT[dt], op, k, b)
     assert rc == 0, (c["id"], rc)
-    return np.concatenate([gu.from_dev(d, np.float32, out_n) for d in d_recv])
+    return np.concatenate([gu.from_dev(d, npdt, out_n) for d in d_recv])
 
 
 @pytest.mark.parametrize("schedule", ["flat", "exact"])
 def test_collectives_match_reference_golden(gu, ops, groups, schedule):
     """Every user-op golden case of the reference (radix/batch allreduce and reduce-scatter at every batch size b
-    that divides n, k = 2..4, in place and not; CHiArA's phases) bit-exact on the device.  The flat schedule evaluates
+    that divides n, k = 2..4, in place and not; CHiArA's phases; float, double and int32 through one launcher that
+    switches on the type) bit-exact on the device.  The flat schedule evaluates
     each chunk as one expression tree, the exact one replays the reference's messages -- both must land on the
     reference's operand order."""
     half = ops[0]
@@ -197,7 +203,7 @@ def test_collectives_match_reference_golden(gu, ops, groups, schedule):
             got = _run_case(gu, g, c, half)
         finally:
             g.set_schedule(ca.SCHEDULE_FLAT)
-        if not np.array_equal(_u32(got), _u32(FIX[c["id"]])):
+        if got.dtype != FIX[c["id"]].dtype or not np.array_equal(got.view(np.uint8), FIX[c["id"]].view(np.uint8)):
             bad.append(c["id"])
     assert not bad, f"{len(bad)} device/reference mismatches, e.g. {bad[:5]}"
 
@@ -296,6 +302,9 @@ def test_refusals(gu, ops, groups):
         ca.ERR_UNSUPPORTED  # 6 is not a power of 4
     assert g.all_reduce_radix_batch(d, dr, 64, ca.FLOAT32, refuse, 2, 2) == ca.ERR_UNSUPPORTED
     assert ca.reduce_local(d[0], d[1], 64, ca.FLOAT32, refuse, gu.stream()) == ca.ERR_UNSUPPORTED
+    # a type the op's launcher does not implement: its verdict, for the kernels and the collectives
+    assert ca.reduce_local(d[0], d[1], 64, ca.INT64, half, gu.stream()) == ca.ERR_UNSUPPORTED
+    assert g.all_reduce_radix_batch(d, dr, 32, ca.INT64, half, 2, 2) == ca.ERR_UNSUPPORTED
     gu.sync()
     lib = ctypes.CDLL(USEROP_SO)
     tmp = ca.op_create(ctypes.cast(lib.chr_test_halfadd, ctypes.c_void_p).value)
