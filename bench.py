@@ -1347,6 +1347,8 @@ def exact_check(torch, dist, send, recv, count, es, rank, run, world, window=1 <
     call, and every element of every rank's output must EQUAL the sum of the N inputs -- bit for bit, on the wire and
     in the reductions, with no tolerance.  (Association order, which exact sums cannot show, is pinned by the
     reference's goldens and the full-size LocalGroup / RCCL-process tests.)"""
+    if world > 16:  # |partial sums| <= 16 * world must stay within bf16's 8 significant bits
+        return {"exact_known_answer": None, "exact": f"skipped: {world} ranks, exact only up to 16"}
     tdt = torch.float32 if es == 4 else torch.bfloat16
     src = send[:count * es].view(tdt)
     for w0 in range(0, count, window):
