@@ -14,6 +14,7 @@
 // the long-double types.  The MAXLOC / MINLOC pair types and the C complex types are in the table:
 // buffers are laid out at MPI's extent (MPI_DOUBLE_INT: 16 B an element, of which 12 are data).
 // Prints one JSON line; exit status 0 = all agree.
+#include <dlfcn.h>
 #include <mpi.h>
 
 #include <cstdlib>
@@ -32,6 +33,12 @@ int MPICH_Allreduce_ring(const char* sendbuf, char* recvbuf, int count, MPI_Data
                          MPI_Comm comm);
 int allgather_radix_batch(char* sendbuf, int sendcount, MPI_Datatype datatype, char* recvbuf, MPI_Comm comm, int k,
                           int b);
+int MPICH_Allreduce_k_reduce_scatter_allgather(const char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype,
+                                               MPI_Op op, MPI_Comm comm, int k, int single_phase_recv);
+// the shim's user-op binding (csrc/shim/chiara_mpi_shim.cpp); the launcher type is chiara.h's chr_user_reduce_fn
+typedef int (*user_reduce_fn)(void*, const void*, const void* const*, int, size_t, int, int, void*, void*);
+extern "C" int chiara_shim_op_bind(MPI_Op op, user_reduce_fn fn, void* ctx);
+extern "C" int chiara_shim_op_unbind(MPI_Op op);
 
 namespace {
 
@@ -92,6 +99,18 @@ void fill(std::vector<char>& buf, int n, const TypeCase& tc, int tsize, int rank
 }
 
 void user_op(void*, void*, int*, MPI_Datatype*) {}
+
+// host twins of the test launchers in tests/userop/halfadd_op.hip (MPI's own collectives run these)
+void host_isum(void* in, void* inout, int* len, MPI_Datatype*) {
+    const uint32_t* a = (const uint32_t*)in;
+    uint32_t* b = (uint32_t*)inout;
+    for (int i = 0; i < *len; ++i) b[i] = a[i] + b[i];
+}
+void host_mix3(void* in, void* inout, int* len, MPI_Datatype*) {
+    const uint32_t* a = (const uint32_t*)in;
+    uint32_t* b = (uint32_t*)inout;
+    for (int i = 0; i < *len; ++i) b[i] = a[i] * 3u + b[i];
+}
 
 // Complex results compared by value: the parts are exact small integers, but a zero part's sign
 // depends on the association (re = ac - bd can be +0 or -0), and MPI's own collective associates
@@ -206,6 +225,56 @@ int main(int argc, char** argv) {
         if (allgather_radix_batch(a.data(), 4, MPI_DOUBLE_INT, r.data(), MPI_COMM_WORLD, 2, 1) == MPI_SUCCESS)
             fail("non-contiguous allgather type accepted");
     }
+    // user ops bound to their device launchers (chiara_shim_op_bind), when the test names the launchers' library:
+    // a commutative wrapping add against MPI_Allreduce / MPI_Reduce_scatter_block with the same host op; a
+    // non-commutative one runs the radix/batch allreduce (every rank the same bits) and is refused by
+    // k-reduce-scatter-allgather with MPI_ERR_OP, as the reference refuses it; unbound again, MPI_ERR_OP
+    int userop = 0;
+    if (const char* so = std::getenv("CHR_SHIM_USEROP_SO")) {
+        void* h = dlopen(so, RTLD_NOW | RTLD_LOCAL);
+        auto isum = h ? (user_reduce_fn)dlsym(h, "chr_test_isum") : nullptr;
+        auto mix3 = h ? (user_reduce_fn)dlsym(h, "chr_test_halfadd") : nullptr;
+        if (!isum || !mix3) {
+            fail(std::string("user-op launchers not found in ") + so);
+        } else {
+            MPI_Op sop, nop;
+            MPI_Op_create(host_isum, 1, &sop);
+            MPI_Op_create(host_mix3, 0, &nop);
+            const int per = 1001, cnt = per * n;
+            TypeCase ti{MPI_INT, "MPI_INT", 0};
+            std::vector<char> send, r((size_t)cnt * 4), lib((size_t)cnt * 4), rs((size_t)per * 4),
+                rs_lib((size_t)per * 4);
+            fill(send, cnt, ti, 4, rank, 9999);
+            if (chiara_shim_op_bind(sop, isum, nullptr) != MPI_SUCCESS) fail("bind commutative user op");
+            if (chiara_shim_op_bind(MPI_SUM, isum, nullptr) == MPI_SUCCESS) fail("a predefined op was bound");
+            int rc = all_reduce_radix_batch(send.data(), r.data(), cnt, MPI_INT, sop, MPI_COMM_WORLD, 2, n % 2 ? 1 : 2);
+            MPI_Allreduce(send.data(), lib.data(), cnt, MPI_INT, sop, MPI_COMM_WORLD);
+            if (rc != MPI_SUCCESS || r != lib) fail("bound user op allreduce rc=" + std::to_string(rc));
+            rc = reduce_scatter_radix_batch(send.data(), rs.data(), per, MPI_INT, sop, MPI_COMM_WORLD, 2, 1);
+            MPI_Reduce_scatter_block(send.data(), rs_lib.data(), per, MPI_INT, sop, MPI_COMM_WORLD);
+            if (rc != MPI_SUCCESS || rs != rs_lib) fail("bound user op reduce_scatter rc=" + std::to_string(rc));
+            std::vector<char> ring((size_t)cnt * 4);
+            rc = MPICH_Allreduce_ring(send.data(), ring.data(), cnt, MPI_INT, sop, MPI_COMM_WORLD);
+            if (rc != MPI_SUCCESS || ring != lib) fail("bound user op ring rc=" + std::to_string(rc));
+            if (chiara_shim_op_bind(nop, mix3, nullptr) != MPI_SUCCESS) fail("bind non-commutative user op");
+            rc = all_reduce_radix_batch(send.data(), r.data(), cnt, MPI_INT, nop, MPI_COMM_WORLD, 2, n % 2 ? 1 : 2);
+            std::vector<char> all((size_t)cnt * 4 * n);
+            MPI_Allgather(r.data(), cnt * 4, MPI_BYTE, all.data(), cnt * 4, MPI_BYTE, MPI_COMM_WORLD);
+            bool same_all = true;
+            for (int q = 1; q < n; ++q) same_all &= std::memcmp(all.data(), all.data() + (size_t)q * cnt * 4, cnt * 4) == 0;
+            if (rc != MPI_SUCCESS || !same_all) fail("non-commutative bound op allreduce rc=" + std::to_string(rc));
+            rc = MPICH_Allreduce_k_reduce_scatter_allgather(send.data(), r.data(), cnt, MPI_INT, nop, MPI_COMM_WORLD,
+                                                            2, 0);
+            if (rc != MPI_ERR_OP) fail("k_reduce_scatter_allgather with a non-commutative op rc=" + std::to_string(rc));
+            if (chiara_shim_op_unbind(sop) != MPI_SUCCESS || chiara_shim_op_unbind(nop) != MPI_SUCCESS)
+                fail("unbind");
+            rc = all_reduce_radix_batch(send.data(), r.data(), cnt, MPI_INT, sop, MPI_COMM_WORLD, 2, 1);
+            if (rc != MPI_ERR_OP) fail("unbound user op rc=" + std::to_string(rc));
+            MPI_Op_free(&sop);
+            MPI_Op_free(&nop);
+            userop = 1;
+        }
+    }
     // allgather moves any contiguous type as bytes (the reference sizes it with MPI_Type_size)
     {
         MPI_Datatype tri;
@@ -222,8 +291,8 @@ int main(int argc, char** argv) {
     int all_bad = 0;
     MPI_Allreduce(&bad, &all_bad, 1, MPI_INT, MPI_SUM, MPI_COMM_WORLD);
     if (rank == 0)
-        std::printf("{\"pairs\": %d, \"supported_by_mpich\": %d, \"failures\": %d, \"first\": \"%s\"}\n", pairs,
-                    supported, all_bad, failures.c_str());
+        std::printf("{\"pairs\": %d, \"supported_by_mpich\": %d, \"failures\": %d, \"userop\": %d, \"first\": \"%s\"}\n",
+                    pairs, supported, all_bad, userop, failures.c_str());
     MPI_Finalize();
     return all_bad ? 1 : 0;
 }

@@ -29,6 +29,12 @@
 // MPI_Bcast, device = node-local rank mod visible GPUs) and cached as an MPI attribute.
 // Buffers are the reference's host buffers: libchiara stages them through HBM.
 //
+// User-defined ops: MPI_Op_create's function is host code the device cannot call.  A caller that has the same
+// arithmetic as device code (a chr_user_reduce_fn, include/chiara_user_op.hpp) binds it to its MPI_Op once,
+//   chiara_shim_op_bind(op, launcher, ctx)      (commutativity from MPI_Op_commutative, as the reference reads it)
+// and every entry point below then takes that MPI_Op; an unbound user op stays MPI_ERR_OP.  A baseline that refuses
+// a non-commutative op returns MPI_ERR_OP, as the reference's do.
+//
 // CHR_SHIM_TRACE=1: at exit, every process writes one line to stderr,
 //   [chiara-shim] rank R calls: <entry point>=<count> ...
 // the positive marker that a reference main really ran these definitions (and not its own file's
@@ -159,8 +165,26 @@ bool map_type(MPI_Datatype d, chr_dtype* out) {
     return true;
 }
 
-// MPI predefined ops.  MPI_REPLACE/NO_OP and user ops (MPI_Op_create: a host function pointer the
-// device cannot call) are MPI_ERR_OP.
+// User ops bound to a device launcher (chiara_shim_op_bind): MPI_Op handle -> chr_op code.
+constexpr int kMaxBound = 64;
+struct BoundOp {
+    MPI_Op mpi;
+    chr_op op;
+};
+BoundOp g_bound[kMaxBound];
+int g_nbound = 0;
+
+bool bound_op(MPI_Op o, chr_op* out) {
+    for (int i = 0; i < g_nbound; ++i)
+        if (g_bound[i].mpi == o) {
+            *out = g_bound[i].op;
+            return true;
+        }
+    return false;
+}
+
+// MPI predefined ops.  MPI_REPLACE/NO_OP and unbound user ops (MPI_Op_create: a host function pointer
+// the device cannot call) are MPI_ERR_OP.
 bool map_op(MPI_Op o, chr_op* out) {
     if (o == MPI_SUM) *out = CHR_SUM;
     else if (o == MPI_PROD) *out = CHR_PROD;
@@ -183,6 +207,7 @@ bool map_op(MPI_Op o, chr_op* out) {
 // extension of MPI-3.1 §5.9.2) but not the bitwise ones; 0 or the MPI error class to return.
 int map_pair(MPI_Datatype d, MPI_Op o, chr_dtype* dt, chr_op* op) {
     if (!map_type(d, dt)) return MPI_ERR_TYPE;
+    if (bound_op(o, op)) return 0;  // a user op: its launcher decides which types it implements
     if (!map_op(o, op)) return MPI_ERR_OP;
     const bool bitwise = *op == CHR_BAND || *op == CHR_BOR || *op == CHR_BXOR;
     const bool logical = *op == CHR_LAND || *op == CHR_LOR || *op == CHR_LXOR;
@@ -202,10 +227,44 @@ int to_mpi(int rc) {
     if (rc == CHR_SUCCESS) return MPI_SUCCESS;
     if (rc == CHR_ERR_COUNT_NOT_DIVISIBLE) return MPI_ERR_COUNT;
     if (rc == CHR_ERR_BATCH_NOT_DIVISOR || rc == CHR_ERR_INVALID_ARG) return MPI_ERR_ARG;
+    if (rc == CHR_ERR_UNSUPPORTED) return MPI_ERR_OP;  // a user op refused (by its launcher, or a baseline)
     return MPI_ERR_OTHER;  // HIP / RCCL errors, timeouts and aborted communicators
 }
 
 }  // namespace
+
+// Binds a user-defined MPI_Op to the device launcher with its arithmetic (chr_op_create, with MPI_Op_commutative's
+// answer as `commute`).  Binding the same MPI_Op again replaces the launcher.  MPI_SUCCESS, or MPI_ERR_OP.
+extern "C" int chiara_shim_op_bind(MPI_Op op, chr_user_reduce_fn fn, void* ctx) {
+    chr_op code;
+    if (!fn || op == MPI_OP_NULL || map_op(op, &code)) return MPI_ERR_OP;  // predefined ops stay the library's
+    int commute = 0;
+    if (MPI_Op_commutative(op, &commute) != MPI_SUCCESS) return MPI_ERR_OP;
+    if (chr_op_create(fn, ctx, commute, &code) != CHR_SUCCESS) return MPI_ERR_OP;
+    for (int i = 0; i < g_nbound; ++i)
+        if (g_bound[i].mpi == op) {
+            chr_op_free(g_bound[i].op);
+            g_bound[i].op = code;
+            return MPI_SUCCESS;
+        }
+    if (g_nbound == kMaxBound) {
+        chr_op_free(code);
+        return MPI_ERR_OP;
+    }
+    g_bound[g_nbound++] = {op, code};
+    return MPI_SUCCESS;
+}
+
+// Drops a binding (before MPI_Op_free); the MPI_Op is MPI_ERR_OP again.
+extern "C" int chiara_shim_op_unbind(MPI_Op op) {
+    for (int i = 0; i < g_nbound; ++i)
+        if (g_bound[i].mpi == op) {
+            chr_op_free(g_bound[i].op);
+            g_bound[i] = g_bound[--g_nbound];
+            return MPI_SUCCESS;
+        }
+    return MPI_ERR_OP;
+}
 
 int all_reduce_radix_batch(char* sendbuf, char* recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
                            MPI_Comm comm, int k, int b) {

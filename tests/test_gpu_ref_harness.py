@@ -15,6 +15,7 @@ from plot_pipeline import COLUMNS, per_algo_medians, plotter_frame
 
 pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+USEROP_SO = os.path.join(REPO, "tests", "userop", "libhalfadd_op.so")  # the user-op tests' device launchers
 MPIEXEC = "/opt/conda/bin/mpiexec"
 
 
@@ -166,7 +167,9 @@ def test_shim_over_mpi_datatype_op_table(tmp_path):
     MPI_Allreduce's / MPI_Reduce_scatter_block's result through all_reduce_radix_batch,
     reduce_scatter_radix_batch and MPICH_Allreduce_ring (complex by value: a zero part's sign follows
     the association); pairs it rejects, user ops, the long-double types and non-contiguous allgather
-    types come back as MPI error classes (shim_types_main.cpp)."""
+    types come back as MPI error classes (shim_types_main.cpp).  User ops bound to device launchers
+    (chiara_shim_op_bind, tests/userop/libhalfadd_op.so): a commutative one equals MPI's own collectives, a
+    non-commutative one is refused by k-reduce-scatter-allgather with MPI_ERR_OP, as the reference refuses it."""
     import json
 
     exe = os.path.join(REPO, *BIN, "chiara_shim_types")
@@ -177,7 +180,7 @@ def test_shim_over_mpi_datatype_op_table(tmp_path):
         if r:
             cmd.append(":")
         cmd += ["-n", "1", "-env", "NCCL_HOSTID", f"chiara-shim-types-{r}", "-env", "NCCL_SOCKET_IFNAME", "lo",
-                "-env", "NCCL_IB_DISABLE", "1", exe]
+                "-env", "NCCL_IB_DISABLE", "1", "-env", "CHR_SHIM_USEROP_SO", USEROP_SO, exe]
     out = subprocess.run(cmd, cwd=tmp_path, capture_output=True, text=True, timeout=400)
     line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert line, out.stdout[-2000:] + out.stderr[-2000:]
@@ -186,6 +189,8 @@ def test_shim_over_mpi_datatype_op_table(tmp_path):
     # 31 types x 12 ops; MPICH accepts 226 of the pairs (the MAXLOC / MINLOC pair types and the C
     # complex types included)
     assert res["pairs"] == 372 and res["supported_by_mpich"] >= 226, res
+    # user ops bound to their device launchers through the shim (chiara_shim_op_bind): checked
+    assert res["userop"] == 1, res
 
 
 # One geometry per self-test main (each run starts n MPI processes, each with HIP and an RCCL

@@ -38,6 +38,13 @@ extern "C" int chr_test_halfadd(void* out, const void* acc, const void* const* i
     }
 }
 
+// A commutative, associative user op (int32 wrapping add): any schedule gives MPI's own collective's bits, so the
+// MPI-signature shim's binding can be checked against MPI_Allreduce (csrc/harness/shim_types_main.cpp).
+struct IAdd {
+    __device__ int32_t operator()(int32_t in, int32_t inout) const { return (int32_t)((uint32_t)in + (uint32_t)inout); }
+};
+CHR_DEFINE_USER_OP(chr_test_isum, int32_t, IAdd)
+
 // A launcher that refuses every call: the library must hand its verdict back (CHR_ERR_UNSUPPORTED).
 extern "C" int chr_test_refuse(void*, const void*, const void* const*, int, size_t, chr_dtype, int, hipStream_t,
                                void*) {
