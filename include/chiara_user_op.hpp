@@ -145,3 +145,12 @@ int launch_fold(void* out, const void* acc, const void* const* ins, int m, size_
                         int running_first, hipStream_t stream, void*) {                                           \
         return chr_user::launch_fold<T, F>(out, acc, ins, m, n, running_first, stream);                           \
     }
+
+/* The same for one chr_dtype: a call on any other type is refused (the library returns CHR_ERR_UNSUPPORTED), as an
+ * MPI user function may reject a datatype it does not implement. */
+#define CHR_DEFINE_USER_OP_FOR(name, T, F, DTYPE)                                                                     \
+    extern "C" int name(void* out, const void* acc, const void* const* ins, int m, size_t n, chr_dtype dt,          \
+                        int running_first, hipStream_t stream, void*) {                                           \
+        if (dt != (DTYPE)) return 1;                                                                                 \
+        return chr_user::launch_fold<T, F>(out, acc, ins, m, n, running_first, stream);                           \
+    }

@@ -313,6 +313,18 @@ def test_refusals(gu, ops, groups):
     assert ca.reduce_local(d[0], d[1], 64, ca.FLOAT32, tmp, gu.stream()) == ca.ERR_INVALID_ARG
     assert g.all_reduce_radix_batch(d, dr, 64, ca.FLOAT32, tmp, 2, 2) == ca.ERR_INVALID_ARG
     assert ca.reduce_local(d[0], d[1], 64, ca.FLOAT32, 127, gu.stream()) == ca.ERR_INVALID_ARG
+    # a launcher defined for one type (CHR_DEFINE_USER_OP_FOR): that type runs, any other is refused
+    isum = ca.op_create(ctypes.cast(lib.chr_test_isum, ctypes.c_void_p).value, commute=True)
+    try:
+        x = np.arange(-500, 500, dtype=np.int32)
+        y = (np.arange(1000, dtype=np.int32) * 7919).astype(np.int32)
+        dx, dy = gu.to_dev(x), gu.to_dev(y)
+        assert ca.reduce_local(dx, dy, 1000, ca.INT32, isum, gu.stream()) == 0
+        assert ca.reduce_local(dx, dy, 250, ca.FLOAT32, isum, gu.stream()) == ca.ERR_UNSUPPORTED
+        gu.sync()
+        np.testing.assert_array_equal(gu.from_dev(dy, np.int32, 1000), x + y)
+    finally:
+        ca.op_free(isum)
     # the registry hands the freed code out again, still live for the next call
     again = ca.op_create(ctypes.cast(lib.chr_test_halfadd, ctypes.c_void_p).value)
     try:

@@ -43,7 +43,7 @@ extern "C" int chr_test_halfadd(void* out, const void* acc, const void* const* i
 struct IAdd {
     __device__ int32_t operator()(int32_t in, int32_t inout) const { return (int32_t)((uint32_t)in + (uint32_t)inout); }
 };
-CHR_DEFINE_USER_OP(chr_test_isum, int32_t, IAdd)
+CHR_DEFINE_USER_OP_FOR(chr_test_isum, int32_t, IAdd, CHR_INT32)
 
 // A launcher that refuses every call: the library must hand its verdict back (CHR_ERR_UNSUPPORTED).
 extern "C" int chr_test_refuse(void*, const void*, const void* const*, int, size_t, chr_dtype, int, hipStream_t,
