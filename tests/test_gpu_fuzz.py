@@ -41,11 +41,20 @@ MPICH = {{"ring": ca.MODE_MPICH_RING, "rd": ca.MODE_MPICH_RD, "rsag": ca.MODE_MP
 MPICH_RS = {{"rs_radix": ca.MODE_MPICH_RS_RADIX, "rs_halving": ca.MODE_MPICH_RS_HALVING,
             "rs_doubling": ca.MODE_MPICH_RS_DOUBLING, "rs_pairwise": ca.MODE_MPICH_RS_PAIRWISE}}
 
+if {userops}:  # user-defined ops (chr_op_create): the test launcher registered non-commutative and commutative
+    import ctypes
+    _lib = ctypes.CDLL({userop_so!r})
+    _fn = ctypes.cast(_lib.chr_test_halfadd, ctypes.c_void_p).value
+    OP["user_halfadd"] = ca.op_create(_fn, commute=False)
+    OP["user_halfadd_c"] = ca.op_create(_fn, commute=True)
+    PAIRS = [("f32", "user_halfadd"), ("f32", "user_halfadd"), ("f64", "user_halfadd"), ("i32", "user_halfadd"),
+             ("f32", "user_halfadd_c"), ("i32", "user_halfadd_c")]
 rng = np.random.default_rng({seed})
 groups = {{}}
 bad, done = [], 0
 for case in range({ncases}):
-    fam = rng.choice(["ar", "ar", "rs", "rs", "ag", "mpich", "mpich_rs", "phase"])
+    fam = rng.choice(["ar", "ar", "rs", "rs", "mpich", "mpich_rs", "phase"] if {userops} else
+                     ["ar", "ar", "rs", "rs", "ag", "mpich", "mpich_rs", "phase"])
     n = int(rng.integers(1, 13))
     divs = [d for d in range(1, n + 1) if n % d == 0]
     b = int(rng.choice(divs))
@@ -53,7 +62,7 @@ for case in range({ncases}):
     dtype, op = PAIRS[int(rng.integers(len(PAIRS)))]
     if fam == "ag":
         op = "sum"
-    algo = str(rng.choice(["irs", "ilr", "isc"])) if fam == "phase" else None
+    algo = str(rng.choice(["irs", "ilr"] if {userops} else ["irs", "ilr", "isc"])) if fam == "phase" else None
     if algo == "isc":
         op = "sum"
     rc_ = int(rng.choice([1, 3, 17, 255, 256, 1000, 4097, 12345, 40000]))
@@ -82,7 +91,13 @@ for case in range({ncases}):
                 algo = str(rng.choice(list(MPICH)))
                 tag["algo"] = algo
                 rc = g.allreduce_mpich(MPICH[algo], d_sendp, d_recv, count, DT[dtype], OP[op], k, 0)
-                want = po.mpich_allreduce(algo, sends, dtype, op, k=k, inplace=inplace)
+                try:
+                    want = po.mpich_allreduce(algo, sends, dtype, op, k=k, inplace=inplace)
+                except ValueError as e:  # the reference's MPI_ERR_OP for a non-commutative op: refused alike
+                    if not (len(e.args) > 1 and e.args[1] == po.ORC_ERR_OP and rc == ca.ERR_UNSUPPORTED):
+                        raise
+                    done += 1
+                    continue
             outc = count
         elif fam in ("rs", "mpich_rs"):
             sends = [po.fill(rc_ * n, dtype, pat, seed, r) for r in range(n)]
@@ -143,10 +158,11 @@ print(json.dumps({{"done": done, "bad": bad[:20], "nbad": len(bad)}}))
 """
 
 
-def _run(seed, ncases, env_extra):
+def _run(seed, ncases, env_extra, userops=False):
     code = CHILD.format(here=HERE, oracle=os.path.join(REPO, "oracle"),
                         pkg=os.path.join(REPO, "configurable-hierarchical-allreduce-algorithms_amd"),
-                        seed=seed, ncases=ncases)
+                        seed=seed, ncases=ncases, userops=userops,
+                        userop_so=os.path.join(HERE, "userop", "libhalfadd_op.so"))
     env = dict(os.environ, **env_extra)
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=900)
     assert out.returncode == 0, out.stderr[-3000:]
@@ -164,3 +180,12 @@ def test_fuzz_collectives_streaming_kernels_forced():
     assert res["nbad"] == 0, res["bad"]
     assert res["done"] == 400
 
+
+
+def test_fuzz_collectives_user_ops():
+    """User-defined ops through every family but allgather (no op): the test launcher registered non-commutative
+    and commutative, float / double / int32, every schedule and depth, the MPICH baselines' refusals of a
+    non-commutative op included -- bit for bit against the oracle's restatement (ORC_USER_HALFADD)."""
+    res = _run(606, 600, {}, userops=True)
+    assert res["nbad"] == 0, res["bad"]
+    assert res["done"] == 600
