@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--leaves", type=int, default=8, choices=sorted(COMBS))
     ap.add_argument("--vec", type=int, default=0)
     ap.add_argument("--mib", type=int, default=64)
+    ap.add_argument("--rot-gib", type=float, default=4.5,
+                    help="distinct operand bytes per rotation (4.5: past the translation cliff, the PMC runs' "
+                         "setting; 1.9: C2's side of it, DESIGN §4.1)")
     a = ap.parse_args()
     if a.vec:
         return vec_oop(a)
@@ -35,7 +38,8 @@ def main():
     s = torch.cuda.current_stream(dev)
     n = (64 << 20) // 4
     sets = []
-    for si in range(max(8, 64 // (nl + 1))):  # >= 4.5 GiB of distinct operands per rotation
+    nsets = max(8, 64 // (nl + 1)) if a.rot_gib >= 4.5 else max(1, int(a.rot_gib * 16 // (nl + 1)))
+    for si in range(nsets):  # >= 4.5 GiB of distinct operands per rotation by default
         leaves = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(nl)]
         for j, t in enumerate(leaves):
             ca.check(ca.fill(t, n, ca.FLOAT32, 0, 3, 8 * si + j, stream=s))
@@ -52,7 +56,9 @@ def vec_oop(a):
     s = torch.cuda.current_stream(dev)
     m, n = a.vec, (a.mib << 20) // 4
     sets = []
-    for si in range(max(2, -(-(9 * 8 * 64) // ((m + 2) * a.mib)))):  # >= 4.5 GiB of distinct operands per rotation
+    nsets = (max(2, -(-(9 * 8 * 64) // ((m + 2) * a.mib))) if a.rot_gib >= 4.5
+             else max(1, int(a.rot_gib * 1024 // ((m + 2) * a.mib))))
+    for si in range(nsets):  # >= 4.5 GiB of distinct operands per rotation by default
         bufs = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(m + 2)]
         for j, t in enumerate(bufs):
             ca.check(ca.fill(t, n, ca.FLOAT32, 0, 3, 16 * si + j, stream=s))
