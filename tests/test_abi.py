@@ -2,6 +2,7 @@
 declares (no compute calls without a GPU)."""
 import os
 import re
+import shutil
 import subprocess
 
 import pytest
@@ -142,3 +143,15 @@ def test_user_op_registry_on_the_host():
     for o in made:
         assert L.chr_op_free(o) == 0
     assert L.chr_op_free(3) == ca.ERR_INVALID_ARG and L.chr_op_free(200) == ca.ERR_INVALID_ARG
+
+
+def test_shim_exports_the_user_op_binding():
+    """The MPI-signature shim (linked into the harness executables) defines chiara_shim_op_bind / _unbind: a user
+    MPI_Op gets its device twin there (csrc/shim/chiara_mpi_shim.cpp); exercised under mpiexec by
+    test_gpu_ref_harness.py::test_shim_over_mpi_datatype_op_table."""
+    exe = os.path.join(REPO, "configurable-hierarchical-allreduce-algorithms_amd", "bin", "chiara_shim_types")
+    if not os.path.exists(exe) or not shutil.which("nm"):
+        pytest.skip("shim harness not built here")
+    syms = subprocess.check_output(["nm", "-C", exe]).decode()
+    for name in ("chiara_shim_op_bind", "chiara_shim_op_unbind", "all_reduce_radix_batch(char*"):
+        assert f" T {name}" in syms, name
