@@ -290,7 +290,8 @@ TREE8_KERNEL_SYMBOL = "void chr::k_reduce_tree<0, 0, 8, 1, true, 64, true>(chr::
 # / N = 4 lines to the 2- / 4-leaf tree entries, kernels those lines never launch.
 TREE_PMC = {8: ("tree_f32_sum_8leaves_64MiB", TREE8_KERNEL_SYMBOL),
             4: ("tree_f32_sum_4leaves_64MiB", "void chr::k_reduce_tree<0, 0, 4, 2, true, 64, true>(chr::TreeArgs)"),
-            2: ("tree_f32_sum_2leaves_64MiB", "void chr::k_reduce_tree<0, 0, 2, 4, true, 64, true>(chr::TreeArgs)")}
+            # a streaming 2-leaf tree runs as one out-of-place fold on the bucket kernel (reduce_tree.hip, round 6)
+            2: ("tree_f32_sum_2leaves_64MiB", "void chr::k_reduce_vec<0, 0, 1, 4, true, true, 64>(chr::VecArgs)")}
 VEC_OOP_PMC = {1: ("reduce_f32_sum_m1_oop_128MiB", "void chr::k_reduce_vec<0, 0, 1, 4, true, true, 64>(chr::VecArgs)"),
                3: ("reduce_f32_sum_m3_oop_64MiB", "void chr::k_reduce_vec<0, 0, 3, 2, true, true, 64>(chr::VecArgs)")}
 

@@ -13,7 +13,9 @@ $P "$D/vec1_pmc_FETCH_SIZE" "$D/vec1_pmc_WRITE_SIZE" reduce_f32_sum_m1_oop_128Mi
 $P "$D/vec3_pmc_FETCH_SIZE" "$D/vec3_pmc_WRITE_SIZE" reduce_f32_sum_m3_oop_64MiB 335544320 - "k_reduce_vec<0, 0, 3," > /dev/null
 for nl in 4 2; do
   if [ -d "$D/tree${nl}_pmc_FETCH_SIZE" ]; then
-    $P "$D/tree${nl}_pmc_FETCH_SIZE" "$D/tree${nl}_pmc_WRITE_SIZE" "tree_f32_sum_${nl}leaves_64MiB" $(( (nl + 1) * 64 * 1048576 )) - k_reduce_tree > /dev/null
+    # a streaming 2-leaf tree runs on the bucket kernel (reduce_tree.hip routes it, round 6)
+    k=k_reduce_tree; [ $nl = 2 ] && k="k_reduce_vec<0, 0, 1,"
+    $P "$D/tree${nl}_pmc_FETCH_SIZE" "$D/tree${nl}_pmc_WRITE_SIZE" "tree_f32_sum_${nl}leaves_64MiB" $(( (nl + 1) * 64 * 1048576 )) - "$k" > /dev/null
   fi
 done
 python3 -c "

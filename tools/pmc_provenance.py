@@ -19,9 +19,10 @@ KERNEL_SOURCES = {
     "tree_f32_sum_8leaves_64MiB": [f"{CSRC}/reduce_tree.hpp", f"{CSRC}/reduce_common.hpp", f"{CSRC}/reduce_tree.hip",
                                    f"{CSRC}/chr_internal.hpp"],
 }
-# the 4- and 2-leaf trees (the tree API; no flat plan of a bench line launches them) come from the same sources
+# the 4-leaf tree (the tree API; no flat plan of a bench line launches it) comes from the same sources; a streaming
+# 2-leaf tree runs on the bucket kernel, routed there by reduce_tree.hip (round 6)
 KERNEL_SOURCES["tree_f32_sum_4leaves_64MiB"] = KERNEL_SOURCES["tree_f32_sum_8leaves_64MiB"]
-KERNEL_SOURCES["tree_f32_sum_2leaves_64MiB"] = KERNEL_SOURCES["tree_f32_sum_8leaves_64MiB"]
+KERNEL_SOURCES["tree_f32_sum_2leaves_64MiB"] = KERNEL_SOURCES["reduce_f32_sum_m1_64MiB"] + [f"{CSRC}/reduce_tree.hip"]
 # the N = 2 / N = 4 lines' reductions: one fold per piece, out of place (recv = send (op) stage...), on the bucket
 # kernel (schedule.cpp tree_program: a single fold is one k_reduce_vec launch)
 KERNEL_SOURCES["reduce_f32_sum_m1_oop_128MiB"] = KERNEL_SOURCES["reduce_f32_sum_m1_64MiB"]

@@ -2,7 +2,7 @@
 """Launches only the fused tree kernel at C4's shape (f32, 8 leaves, 64 MiB pieces, 8 rotating
 leaf sets = 4.5 GiB, HBM-cold) for rocprofv3 --pmc passes: HBM bytes per launch vs the
 algorithmic 9 x 64 MiB (tools/pmc_summary.py ... k_reduce_tree).  `--leaves 4|2`: the 4- / 2-leaf trees
-instead ((L + 1) x 64 MiB).  `--vec M --mib P`: the N = 2 / N = 4 lines' reductions instead -- one fold of M
+instead ((L + 1) x 64 MiB; a streaming 2-leaf tree runs on the bucket kernel, reduce_tree.hip).  `--vec M --mib P`: the N = 2 / N = 4 lines' reductions instead -- one fold of M
 incoming pieces of P MiB into a separate output (chr_reduce_multi(out, acc, ins), k_reduce_vec out of place,
 (M + 2) x P MiB), over rotating sets of at least 4.5 GiB.
 
