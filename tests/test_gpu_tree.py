@@ -102,6 +102,17 @@ def test_out_aliases_leaf(gu):
         _run(gu, "f32", "sum", *C4_TREE, 70001, inplace_leaf=leaf)
 
 
+@pytest.mark.parametrize("dtype,op", [("f32", "sum"), ("f32", "max"), ("bf16", "sum"), ("i32", "prod"), ("f64", "min")])
+def test_streaming_two_leaf_tree_runs_as_a_fold(gu, dtype, op):
+    """A streaming 2-leaf tree is one out-of-place fold on the bucket kernel (reduce_tree.hip): both operand orders
+    (swap bit), out separate, out = the running value, and out = the fold's input (kept on the tree kernel), on TIES
+    data where the order shows -- bit-exact vs the oracle's tree evaluation."""
+    n = (24 << 20) // np.dtype(po.NP_DTYPES[dtype]).itemsize + 5  # 3 x 24 MiB per call: past the 40 MiB threshold
+    for swaps in ([0], [1]):
+        for leaf in (None, 0, 1):
+            _run(gu, dtype, op, [0, 1], swaps, n, pattern=2 if op in ("max", "min") else 0, inplace_leaf=leaf)
+
+
 def test_large_nt_path(gu):
     """>= 64 MiB streamed per call takes the non-temporal instantiation."""
     _run(gu, "f32", "sum", *C4_TREE, (16 << 20) + 7)
